@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""Headline benchmark: particle-steps/s (+ ms/step) of the SPH step on MI355X.
+
+BASELINE.json metric: "particle-steps/sec + ms/step at 1M particles; 1/2/4/8 MI355X
+scaling". At N=1 the workload is configs[2] = C3: 1,048,576 particles, 3D dam-break,
+fp32, h = 1.2·dx (SPEC_SPH.md §2), synthetic lattice init (seed 1234). One step = hash →
+radix sort → reorder → cell-start → density → force+integrate, over all particles, with
+the state already resident in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--no-cpu-baseline]
+
+For N > 1 it is launched by torch.distributed.run. Every rank owns an x-slab of the
+global tank and exchanges one-cell halos with its neighbours over RCCL (SPEC_SPH.md §3),
+so per-GPU work is fixed as N grows ("weak" scaling).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import __graft_entry__ as GE  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+# SURVEY.md §8d, algorithmic bytes per particle-step of the force+visc+XSPH+KDK pass
+# (read x,v,ρ,P 32 B + write x,v 24 B, SoA fp32, neighbour reads counted once)
+FORCE_BYTES_PER_PARTICLE = 56.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event pass")
+    return ap.parse_args()
+
+
+def load_traffic(config: str):
+    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 PMC passes
+    (profiles/pmc_*.json, FETCH_SIZE×2 + WRITE_SIZE per MI355X_MICROARCH.md §HBM)."""
+    best = None
+    for f in sorted((ROOT / "profiles").glob("pmc_*.json")):
+        try:
+            d = json.loads(f.read_text())
+        except Exception:
+            continue
+        if d.get("config") == config and d.get("kernel_bytes", {}).get("force_integrate"):
+            best = d["kernel_bytes"]["force_integrate"]
+    return best
+
+
+def cpu_baseline(config: str, budget_s: float):
+    """The C oracle (oracle/, port of SPEC_SPH.md §2) on the host cores, rank 0 only,
+    over a bounded sample of the same workload: the C3 initial state, as many whole
+    steps as fit in ~budget_s seconds."""
+    import numpy as np
+    O = GE.load_oracle()
+    pkg = GE.load_package()
+    sc = pkg.config_scenario(config)
+    p, dt = pkg.scenario_params(sc)
+    op = O.sph_params(sc.dim, p.dx, p.h, p.rho0, p.c0, p.alpha, p.xsph_eps, tuple(p.gravity), tuple(p.box),
+                      p.wall_restitution, p.forcing_amp, p.forcing_freq)
+    x = O.lattice(sc.dim, sc.nx, sc.ny, sc.nz, sc.dx, seed=sc.seed, jitter=sc.jitter * sc.dx)
+    v = np.zeros_like(x)
+    ids = np.arange(len(x), dtype=np.int32)
+    try:
+        threads = len(os.sched_getaffinity(0))
+    except AttributeError:
+        threads = os.cpu_count() or 1
+    threads = max(1, min(threads, int(os.environ.get("OMP_NUM_THREADS", threads) or threads)))
+    t0 = time.perf_counter()
+    x, v, ids, _, _, _ = O.sph_step(op, x, v, ids, dt, 0.0, nthreads=threads)
+    one = time.perf_counter() - t0
+    steps = max(1, int(budget_s / max(one, 1e-6)) - 1)
+    t0 = time.perf_counter()
+    for s in range(steps):
+        x, v, ids, _, _, _ = O.sph_step(op, x, v, ids, dt, float(np.float32((s + 1) * dt)), nthreads=threads)
+    el = time.perf_counter() - t0
+    return {"value": len(x) * steps / el, "unit": "particle-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{config} initial state ({len(x)} particles), {steps} oracle steps after 1 warm-up "
+                      f"step, {el:.1f} s, OpenMP {threads} threads"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    pkg = GE.load_package()
+
+    if world > 1:
+        from sph_test_amd import slab
+        runner = slab.SlabRunner(args.config, rank, world, device=local, profile=not args.no_profile)
+    else:
+        runner = SingleRunner(pkg, args.config, local, profile=not args.no_profile)
+
+    # one explicit HIP stream shared by torch (events, RCCL ordering) and libsphhip
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    runner.bind_stream(stream.cuda_stream)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    runner.step(args.warmup)
+    barrier()
+    runner.reset_stats()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    runner.step(args.steps)
+    ev1.record(stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    el = torch.tensor([wall], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    wall = float(el.item())
+    n_total = runner.total_particles()
+    value = n_total * args.steps / wall
+    kstats = runner.kernel_stats()
+
+    roofline = None
+    fi = kstats.get("force_integrate")
+    if fi and fi["launches"] > 0 and fi["total_ms"] > 0:
+        avg_s = fi["total_ms"] / fi["launches"] / 1e3
+        bytes_per_launch = FORCE_BYTES_PER_PARTICLE * runner.local_particles()
+        achieved = bytes_per_launch / avg_s / 1e9
+        traffic = load_traffic(args.config) if world == 1 else None
+        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
+                    "kernel": "k_force_integrate", "kernel_avg_us": round(avg_s * 1e6, 2),
+                    "bytes_per_launch": bytes_per_launch}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.config, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "particle-steps/sec + ms/step at 1M particles; 1/2/4/8 MI355X scaling",
+            "value": round(value, 1),
+            "unit": "particle-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (dam-break lattice, seed 1234)",
+            "config": {"workload": runner.workload(), "particles": n_total,
+                       "particles_per_gpu": runner.local_particles(), "h_over_dx": 1.2,
+                       "parallelism": f"slab{world}" if world > 1 else "single"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
+            "kernels_ms_per_step": {k: round(v["total_ms"] / max(1, args.steps), 4) for k, v in kstats.items()
+                                    if v["total_ms"] > 0},
+        }
+        print(json.dumps(line), flush=True)
+    runner.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+class SingleRunner:
+    def __init__(self, pkg, config, device, profile):
+        self.config = config
+        self.sim = pkg.SPHSim.from_config(config, device=device, profile=profile)
+
+    def bind_stream(self, handle):
+        self.sim.ctx.set_stream(handle)
+
+    def step(self, k):
+        self.sim.step(k)
+
+    def reset_stats(self):
+        self.sim.ctx.reset_kernel_stats()
+
+    def kernel_stats(self):
+        return self.sim.ctx.kernel_stats()
+
+    def total_particles(self):
+        return self.sim.n
+
+    def local_particles(self):
+        return self.sim.n
+
+    def workload(self):
+        sc = self.sim.scenario
+        return (f"{self.config}: {self.sim.n} particles, {sc.dim}D dam-break, column {sc.nx}x{sc.ny}x{sc.nz}, "
+                f"tank {sc.tx}x{sc.ty}x{sc.tz} dx")
+
+    def close(self):
+        self.sim.close()
+
+
+if __name__ == "__main__":
+    main()

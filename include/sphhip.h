@@ -1,0 +1,183 @@
+/* sphhip.h — C ABI of libsphhip.so, the MI355X (gfx950) particle step.
+ *
+ * This is the drop-in boundary for the reference's per-frame GPU path. The reference
+ * drives its HLSL kernels through Unity's engine API from ParticleSystemController
+ * (/root/reference/Assets/Scripts/ParticleSystemController.cs); each entry point below
+ * names the reference call site(s) it replaces. Conventions:
+ *   - extern "C", cdecl, blittable structs (every field 4 bytes: C# Pack=4 works as is);
+ *   - return 0 (SPH_OK) or a negative sph_status; no exception crosses the ABI;
+ *     sph_last_error() holds the message of the last failure on that context;
+ *   - the library owns device memory, the caller owns every host array;
+ *   - one context per thread, not thread-safe (the reference is single-threaded:
+ *     Unity main thread);
+ *   - particle arrays passed in or out are in PARTICLE INDEX order (the index the
+ *     reference uses for particleBuffer[i]); the device keeps them cell-sorted internally.
+ */
+#ifndef SPHHIP_H
+#define SPHHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPH_ABI_VERSION 1
+
+typedef struct sph_ctx sph_ctx;
+
+typedef enum sph_status {
+    SPH_OK = 0,
+    SPH_ERR_INVALID = -1,   /* bad argument / out-of-range count */
+    SPH_ERR_HIP = -2,       /* HIP runtime failure (no device, launch error, …) */
+    SPH_ERR_CAPACITY = -3,  /* count > capacity; resize first */
+    SPH_ERR_STATE = -4,     /* call not valid for this model / not initialised */
+    SPH_ERR_NOMEM = -5
+} sph_status;
+
+typedef enum sph_model {
+    SPH_MODEL_CONTACT = 0,  /* Model R: SimulateParticles.compute:211-408 (SPEC_SPH.md §1) */
+    SPH_MODEL_WCSPH = 1     /* Model S: weakly-compressible SPH (SPEC_SPH.md §2) */
+} sph_model;
+
+#define SPH_FLAG_PROFILE 1  /* time every kernel launch with HIP events (sph_get_kernel_stat) */
+
+/* replaces: new ComputeBuffer(particleCount, 84) … (ParticleSystemController.cs:373-388) */
+typedef struct sph_config {
+    int32_t model;          /* sph_model */
+    int32_t dim;            /* 2 or 3 (Model R: 3) */
+    int32_t capacity;       /* particleCount (ParticleSystemController.cs:12) */
+    int32_t flags;          /* SPH_FLAG_* */
+} sph_config;
+
+/* replaces: computeShader.SetFloat/SetInt uniforms (ParticleSystemController.cs:255-263,
+ * 496-508; SimulateParticles.compute:89-100) plus the Model S constants of SPEC_SPH.md §2. */
+typedef struct sph_params {
+    /* --- Model R uniforms (reference names) --- */
+    float spawn_radius;                       /* spawnRadius */
+    float min_radius, max_radius;             /* minRadius, maxRadius */
+    float global_drag_multiplier;             /* globalDragMultiplier */
+    float torque_factor;                      /* torqueFactor */
+    float torque_damping;                     /* torqueDamping */
+    float boundary_friction;                  /* boundaryFriction */
+    float rolling_contact_radius_multiplier;  /* rollingContactRadiusMultiplier */
+    float density;                            /* density */
+    float repulsion_strength;                 /* repulsionStrength */
+    int32_t active_particle_count;            /* activeParticleCount */
+    /* --- Model S --- */
+    float dx, h, rho0, c0, alpha, xsph_eps;
+    float gravity[3];
+    float box[3];                              /* tank extent; walls at 0 and box[a] */
+    float wall_restitution;
+    float forcing_amp, forcing_freq;           /* f_ext = (amp·sin(2π f t), 0, 0) */
+} sph_params;
+
+typedef enum sph_scenario_kind {
+    SPH_SCENARIO_DAMBREAK = 0,  /* fluid column at the tank's low-x corner */
+    SPH_SCENARIO_SLOSHING = 1,  /* fluid layer filling the tank floor + lateral forcing */
+    SPH_SCENARIO_SPHERE = 2     /* Model R: InitParticles-style random sphere (compute:118-194) */
+} sph_scenario_kind;
+
+typedef struct sph_scenario {
+    int32_t kind;               /* sph_scenario_kind */
+    int32_t dim;
+    int32_t nx, ny, nz;         /* fluid lattice (particles per axis) */
+    int32_t tx, ty, tz;         /* tank extent in units of dx */
+    float dx;
+    uint32_t seed;
+    float jitter;               /* lattice jitter amplitude in units of dx (0.01) */
+} sph_scenario;
+
+/* replaces: DragInput (ParticleSystemController.cs:149-154; compute:70-74), 20 bytes */
+typedef struct sph_drag_input {
+    int32_t selected_id;
+    float target[3];
+    float strength;
+} sph_drag_input;
+
+typedef struct sph_stats {
+    int64_t steps;              /* steps taken since create / last upload */
+    double sim_time;            /* Σ dt */
+    int32_t active;             /* active particle count */
+    int32_t capacity;
+    int32_t grid[3];            /* cells per axis */
+    int32_t key_bits;           /* radix-sort key width */
+    int64_t device_bytes;       /* device memory held by the context */
+} sph_stats;
+
+typedef struct sph_kernel_stat {
+    char name[32];
+    int64_t launches;
+    double total_ms;            /* Σ HIP-event durations (SPH_FLAG_PROFILE only) */
+    double bytes_per_launch;    /* algorithmic HBM bytes of the last launch */
+} sph_kernel_stat;
+
+/* ---- lifetime: replaces InitializeBuffers / ReleaseBuffers (controller:373-482) ---- */
+int sph_create(const sph_config* cfg, int32_t device, sph_ctx** out);
+void sph_destroy(sph_ctx* ctx);
+/* replaces ResizeParticleBuffers (controller:1162-1222): keeps the active particles */
+int sph_resize(sph_ctx* ctx, int32_t capacity);
+const char* sph_last_error(const sph_ctx* ctx);
+int32_t sph_abi_version(void);
+
+/* Run the step on a caller-provided HIP stream (hipStream_t as void*; NULL = own stream). */
+int sph_set_stream(sph_ctx* ctx, void* hip_stream);
+int sph_get_stream(sph_ctx* ctx, void** hip_stream);
+
+/* ---- configuration: replaces SetFloat/SetInt (controller:255-263, 496-508) ---- */
+int sph_set_params(sph_ctx* ctx, const sph_params* params);
+int sph_get_params(const sph_ctx* ctx, sph_params* params);
+/* Derive the SPEC_SPH.md §2 constants (h, c0, box, forcing …) for a scenario. Pure; no ctx. */
+int sph_scenario_params(const sph_scenario* sc, sph_params* out, float* dt_out);
+
+/* ---- particle data: replaces particleBuffer.SetData/GetData (controller:519-522,794,959)
+ *      and InitParticles (compute:118-194, controller:484-552) ---- */
+int sph_upload_particles_aos84(sph_ctx* ctx, const void* src, int32_t count);
+int sph_download_particles_aos84(sph_ctx* ctx, void* dst, int32_t count);
+int sph_upload_state(sph_ctx* ctx, const float* pos_xyz, const float* vel_xyz, int32_t count);
+int sph_init_scenario(sph_ctx* ctx, const sph_scenario* sc);
+
+/* ---- the per-frame step: replaces the Dispatch sequence of Update()
+ *      (controller:265-331: torque clear, ClearGrid, BuildHashGrid, ApplySPHForces,
+ *       ApplyDragForce, UpdateMotion, UpdateRotation) ---- */
+int sph_step(sph_ctx* ctx, float dt, int32_t nsteps);
+/* replaces HandleMouseDrag → dragInputBuffer.SetData (controller:975-1034) */
+int sph_set_drag(sph_ctx* ctx, const sph_drag_input* drag);
+/* next (§8f-1): adhesion bonds, 84-byte AdhesionConnection (compute:43-55) */
+int sph_set_adhesion(sph_ctx* ctx, const void* conn84, int32_t count);
+
+/* ---- readback: replaces Copy*ToReadbackBuffer + GetData (compute:410-422,
+ *      controller:327-333) and AsyncGPUReadback (controller:1115-1159) ---- */
+int sph_read_positions(sph_ctx* ctx, float* xyz, int32_t count);
+int sph_read_rotations(sph_ctx* ctx, float* xyzw, int32_t count);
+int sph_read_velocities(sph_ctx* ctx, float* xyz, int32_t count);
+int sph_read_angular_velocities(sph_ctx* ctx, float* xyz, int32_t count);
+int sph_read_density(sph_ctx* ctx, float* rho, int32_t count);   /* Model S, pass-1 ρ */
+int sph_synchronize(sph_ctx* ctx);
+
+/* ---- introspection (tests / bench) ---- */
+int sph_get_stats(sph_ctx* ctx, sph_stats* out);
+int sph_get_kernel_stat(sph_ctx* ctx, int32_t index, sph_kernel_stat* out);
+int sph_reset_kernel_stats(sph_ctx* ctx);
+/* sorted-slot views of the last step (slot order = cell order) */
+int sph_read_sorted_ids(sph_ctx* ctx, int32_t* ids, int32_t count);
+int sph_read_cell_start(sph_ctx* ctx, uint32_t* cell_start, int32_t count);
+int sph_read_torque_int(sph_ctx* ctx, int32_t* xyz, int32_t count);  /* Model R, index order */
+/* stable LSD radix sort of (key, index) on the device: the sort of the step, exposed for
+ * bit-exact parity tests. perm[i] = source index of sorted slot i. */
+int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int32_t key_bits,
+                         uint32_t* perm_out, uint32_t* sorted_keys_out);
+
+/* ---- slab decomposition (multi-GPU; SPEC_SPH.md §3). One context per rank; the host moves
+ *      the packed buffers between ranks (RCCL over xGMI from bench.py / torch.distributed). ---- */
+typedef struct sph_slab {
+    int32_t cx_lo, cx_hi;       /* owned cell columns [cx_lo, cx_hi) of the global grid */
+    int32_t rank, nranks;
+    int32_t ghost_capacity;     /* per side, particles */
+} sph_slab;
+int sph_set_slab(sph_ctx* ctx, const sph_slab* slab);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPHHIP_H */

@@ -1,0 +1,221 @@
+/* contact_oracle.c — CPU restatement of the reference contact model (TEST INFRASTRUCTURE ONLY).
+ *
+ * Line-by-line restatement of /root/reference/Assets/Compute/SimulateParticles.compute:
+ *   GetGridCoord/GridHash :102-109, ApplySPHForces :211-309, ApplyDragForce :311-324,
+ *   UpdateMotion :326-357, quat_mul :359-365, UpdateRotation :379-408,
+ * with the two semantic choices of SPEC_SPH.md §1: Jacobi reads (the reference's in-place
+ * write at :308 races) and the gather form of the InterlockedAdd reaction torque (:291-294),
+ * which gives the same int32 sums (integer addition is associative).
+ * HLSL intrinsics: length = sqrt(dot), dot = x*x+y*y+z*z, saturate = clamp01 (NaN->0),
+ * normalize(v) = v / length(v), pow(x,2.0) = x*x, (int3)(float3) = D3D ftoi (trunc, sat, NaN->0).
+ * Compiled with -ffp-contract=off. PARITY UNPINNED by reference fixtures (see oracle.h).
+ */
+#include "oracle.h"
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define GRID_DIM 32
+#define TORQUE_SCALE 10000
+
+typedef struct { float x, y, z; } f3;
+static inline f3 mk(float x, float y, float z) { f3 r = {x, y, z}; return r; }
+static inline f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline f3 mul(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+static inline f3 divs(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+static inline f3 neg(f3 a) { return mk(-a.x, -a.y, -a.z); }
+static inline float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline float len(f3 a) { return sqrtf(dot(a, a)); }
+static inline f3 cross(f3 a, f3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+static inline float sat(float x) { return x > 0.0f ? (x < 1.0f ? x : 1.0f) : 0.0f; }
+static inline f3 nrm(f3 a) { return divs(a, len(a)); }
+static inline f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+static inline void st3(float* p, f3 a) { p[0] = a.x; p[1] = a.y; p[2] = a.z; }
+
+static inline int32_t ftoi(float x) {   /* D3D10+ ftoi: truncate, saturate, NaN -> 0 */
+    if (x != x) return 0;
+    if (x >= 2147483648.0f) return 2147483647;
+    if (x <= -2147483648.0f) return (int32_t)0x80000000;
+    return (int32_t)x;
+}
+
+typedef struct { f3 force, torque; int hit; f3 react; } pair_out;
+
+/* One pair evaluated from `self`'s thread (compute:240-296). Returns self's repulsion and
+ * rolling torque A, and the rolling torque B that the reference adds to the other
+ * particle (:287). */
+static inline pair_out contact_pair(const or_contact_params* P, const or_particle84* self,
+                                    const or_particle84* other) {
+    pair_out o;
+    o.hit = 0; o.force = mk(0, 0, 0); o.torque = mk(0, 0, 0); o.react = mk(0, 0, 0);
+    f3 posA = ld3(self->position), velA = ld3(self->velocity), omegaA = ld3(self->angularVelocity);
+    float rA = self->radius;
+    float effectiveRadiusA = rA * 0.5f;                         /* :225 */
+    f3 posB = ld3(other->position), velB = ld3(other->velocity), omegaB = ld3(other->angularVelocity);
+    float rB = other->radius;
+    float effectiveRadiusB = rB * 0.5f;                         /* :248 */
+    f3 delta = sub(posA, posB);                                 /* :249 */
+    float dist = len(delta);
+    float overlap = (effectiveRadiusA + effectiveRadiusB) - dist;
+    if (!(overlap > 0.001f)) return o;                          /* :253 */
+    o.hit = 1;
+    f3 dir = divs(delta, dist);
+    float overlapFalloff = sat(overlap / (effectiveRadiusA + effectiveRadiusB));
+    float falloff = sat(1.0f - dist / (effectiveRadiusA + effectiveRadiusB));
+    o.force = mul(mul(mul(dir, falloff), P->repulsion_strength), overlapFalloff); /* :260 */
+    f3 contactPointA = sub(posA, mul(dir, effectiveRadiusA));  /* :264 */
+    f3 contactPointB = add(posB, mul(dir, effectiveRadiusB));
+    f3 surfaceVelA = add(velA, cross(omegaA, sub(contactPointA, posA)));
+    f3 surfaceVelB = add(velB, cross(omegaB, sub(contactPointB, posB)));
+    f3 relSurfaceVel = sub(surfaceVelA, surfaceVelB);
+    f3 tangentVel = sub(relSurfaceVel, mul(dir, dot(relSurfaceVel, dir)));  /* :271 */
+    float slipSpeed = len(tangentVel);
+    if (slipSpeed > 1e-4f) {                                    /* :274 */
+        f3 frictionDir = divs(tangentVel, slipSpeed);
+        float torqueInput = fabsf(slipSpeed * P->torque_factor);
+        float frictionMag = powf(torqueInput, 1.25f);
+        frictionMag = fminf(frictionMag, 10.0f);
+        float torqueRadiusScale = overlapFalloff * overlapFalloff;          /* pow(x, 2.0) :282 */
+        float effectiveRadiusTorqueA = torqueRadiusScale * effectiveRadiusA * P->roll_mult;
+        float effectiveRadiusTorqueB = torqueRadiusScale * effectiveRadiusB * P->roll_mult;
+        o.torque = cross(mul(neg(dir), effectiveRadiusTorqueA), mul(neg(frictionDir), frictionMag));
+        o.react = cross(mul(dir, effectiveRadiusTorqueB), mul(frictionDir, frictionMag));
+        o.hit = 2;
+    }
+    return o;
+}
+
+static inline int32_t or_coord_r(float x, float R) {   /* compute:102-105 */
+    float g = (x + R) / 4.0f;
+    if (!(g > 0.0f)) return 0;
+    if (g >= (float)(GRID_DIM - 1)) return GRID_DIM - 1;
+    return (int32_t)g;
+}
+
+int or_contact_step(const or_contact_params* P, int n, or_particle84* parts, int32_t* torque_out,
+                    int nthreads) {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+    (void)nthreads;
+#endif
+    const uint32_t NK = GRID_DIM * GRID_DIM * GRID_DIM;
+    size_t nn = (size_t)(n > 0 ? n : 1);
+    uint32_t* keys = (uint32_t*)malloc(sizeof(uint32_t) * nn);
+    uint32_t* perm = (uint32_t*)malloc(sizeof(uint32_t) * nn);
+    uint32_t* sk = (uint32_t*)malloc(sizeof(uint32_t) * nn);
+    uint32_t* cs = (uint32_t*)malloc(sizeof(uint32_t) * (NK + 1));
+    or_particle84* in = (or_particle84*)malloc(sizeof(or_particle84) * nn);
+    memcpy(in, parts, sizeof(or_particle84) * (size_t)n);
+    /* grid: same neighbour set as the reference's linked lists, visited in stable-sorted order */
+    for (int i = 0; i < n; ++i) {
+        int32_t cx = or_coord_r(in[i].position[0], P->spawn_radius);
+        int32_t cy = or_coord_r(in[i].position[1], P->spawn_radius);
+        int32_t cz = or_coord_r(in[i].position[2], P->spawn_radius);
+        keys[i] = ((uint32_t)cx * GRID_DIM + (uint32_t)cy) * GRID_DIM + (uint32_t)cz;
+    }
+    or_stable_sort(n, keys, NK, perm);
+    for (int i = 0; i < n; ++i) sk[i] = keys[perm[i]];
+    or_cell_start(n, sk, NK, cs);
+
+    const float dt = P->dt;
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int a = 0; a < n; ++a) {
+        const or_particle84* self = &in[a];
+        uint32_t key = keys[a];
+        int32_t cz = (int32_t)(key % GRID_DIM), cy = (int32_t)((key / GRID_DIM) % GRID_DIM),
+                cx = (int32_t)(key / (GRID_DIM * GRID_DIM));
+        f3 totalForce = mk(0, 0, 0), totalTorque = mk(0, 0, 0);
+        uint32_t tq[3] = {0, 0, 0};   /* wrapping int32 sums (InterlockedAdd) */
+        int32_t z0 = cz > 0 ? cz - 1 : 0, z1 = cz < GRID_DIM - 1 ? cz + 1 : GRID_DIM - 1;
+        for (int ddx = -1; ddx <= 1; ++ddx) {
+            int32_t x = cx + ddx;
+            if (x < 0 || x >= GRID_DIM) continue;
+            for (int ddy = -1; ddy <= 1; ++ddy) {
+                int32_t y = cy + ddy;
+                if (y < 0 || y >= GRID_DIM) continue;
+                uint32_t rowk = ((uint32_t)x * GRID_DIM + (uint32_t)y) * GRID_DIM;
+                for (uint32_t s = cs[rowk + (uint32_t)z0]; s < cs[rowk + (uint32_t)z1 + 1]; ++s) {
+                    uint32_t b = perm[s];
+                    if ((int)b == a) continue;                          /* :240 */
+                    const or_particle84* other = &in[b];
+                    pair_out mine = contact_pair(P, self, other);
+                    if (!mine.hit) continue;
+                    totalForce = add(totalForce, mine.force);           /* :261 */
+                    if (mine.hit == 2) totalTorque = add(totalTorque, mine.torque); /* :289 */
+                    /* reaction: what b's thread scatters into a (:291-294) */
+                    pair_out theirs = contact_pair(P, other, self);
+                    if (theirs.hit == 2) {
+                        f3 sc = mul(mul(theirs.react, dt), (float)TORQUE_SCALE);
+                        tq[0] += (uint32_t)ftoi(sc.x);
+                        tq[1] += (uint32_t)ftoi(sc.y);
+                        tq[2] += (uint32_t)ftoi(sc.z);
+                    }
+                }
+            }
+        }
+        or_particle84 p = *self;
+        /* :302-306 */
+        f3 linearAccel = divs(totalForce, p.mass);
+        f3 angularAccel = divs(totalTorque, p.momentOfInertia);
+        f3 vel = add(ld3(p.velocity), mul(linearAccel, dt));
+        f3 omg = add(ld3(p.angularVelocity), mul(angularAccel, dt));
+        f3 pos = ld3(p.position);
+        /* ApplyDragForce :316-323 */
+        if (P->drag_id >= 0 && P->drag_id == a) {
+            f3 toTarget = sub(ld3(P->drag_target), pos);
+            f3 force = mul(mul(toTarget, P->drag_strength), dt);
+            vel = add(vel, divs(force, p.mass));
+        }
+        /* UpdateMotion :332-354 */
+        float linearDamping = expf(-p.drag * P->global_drag * dt);
+        float angularDamping = expf(-P->torque_damping * dt);
+        vel = mul(vel, linearDamping);
+        omg = mul(omg, angularDamping);
+        pos = add(pos, mul(vel, dt));
+        float distFromOrigin = len(pos);
+        if (distFromOrigin > P->spawn_radius) {
+            f3 norm = nrm(pos);
+            pos = mul(norm, P->spawn_radius);
+            vel = sub(vel, mul(norm, 2.0f * dot(vel, norm)));           /* reflect */
+            f3 tangentialVel = sub(vel, mul(norm, dot(vel, norm)));
+            f3 frictionDir = nrm(add(tangentialVel, mk(1e-6f, 1e-6f, 1e-6f)));
+            float frictionMag = len(tangentialVel) * P->boundary_friction;
+            float effectiveRadius = p.radius * P->roll_mult;
+            f3 torque = cross(mul(neg(norm), effectiveRadius), mul(neg(frictionDir), frictionMag));
+            omg = add(omg, mul(divs(torque, p.momentOfInertia), dt));
+        }
+        /* UpdateRotation :385-406 */
+        f3 torque = divs(mk((float)(int32_t)tq[0], (float)(int32_t)tq[1], (float)(int32_t)tq[2]),
+                         (float)TORQUE_SCALE);
+        f3 angAcc = divs(torque, p.momentOfInertia);
+        omg = add(omg, angAcc);
+        omg = mul(omg, expf(-P->torque_damping * dt));
+        float angle = len(mul(omg, dt));
+        if (angle > 0.00001f) {
+            f3 axis = nrm(omg);
+            float s = sinf(angle * 0.5f), c = cosf(angle * 0.5f);
+            float dq[4] = {axis.x * s, axis.y * s, axis.z * s, c};
+            const float* q = p.rotation;
+            /* quat_mul(dq, q) :359-365 */
+            f3 dqv = mk(dq[0], dq[1], dq[2]), qv = mk(q[0], q[1], q[2]);
+            f3 xyz = add(add(mul(qv, dq[3]), mul(dqv, q[3])), cross(dqv, qv));
+            float w = dq[3] * q[3] - dot(dqv, qv);
+            float l = sqrtf(xyz.x * xyz.x + xyz.y * xyz.y + xyz.z * xyz.z + w * w);
+            p.rotation[0] = xyz.x / l; p.rotation[1] = xyz.y / l; p.rotation[2] = xyz.z / l;
+            p.rotation[3] = w / l;
+        }
+        st3(p.position, pos); st3(p.velocity, vel); st3(p.angularVelocity, omg);
+        parts[a] = p;
+        if (torque_out) {
+            torque_out[3 * a] = (int32_t)tq[0]; torque_out[3 * a + 1] = (int32_t)tq[1];
+            torque_out[3 * a + 2] = (int32_t)tq[2];
+        }
+    }
+    free(keys); free(perm); free(sk); free(cs); free(in);
+    return 0;
+}

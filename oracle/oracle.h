@@ -1,0 +1,86 @@
+/* oracle.h — CPU restatement of the step (TEST INFRASTRUCTURE ONLY).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this.
+ * The product (sph-test_amd/libsphhip.so) never links or calls it.
+ *
+ * Model R follows /root/reference/Assets/Compute/SimulateParticles.compute:102-408
+ * line by line (Jacobi semantics, gather-form reaction torque: SPEC_SPH.md §1).
+ * Model S follows SPEC_SPH.md §2 (no reference source exists for it: SURVEY.md §0).
+ *
+ * PARITY UNPINNED by reference fixtures: the reference has no tests, golden vectors or
+ * CPU path, and its HLSL cannot be compiled or run here (no dxc/fxc/Unity/dotnet;
+ * SURVEY.md §4, §8c). The restatement is pinned instead by hand-derived known-answer
+ * cases (tests/test_oracle_kat.py) and by committed fixtures (tests/golden/).
+ */
+#ifndef SPH_ORACLE_H
+#define SPH_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- common grid (SPEC_SPH.md §0) ---- */
+typedef struct {
+    float origin[3];
+    float inv_cell;
+    int32_t G[3];
+} or_grid;
+
+uint32_t or_cell_key(const or_grid* g, float x, float y, float z);
+void or_keys(const or_grid* g, int n, const float* pos3, uint32_t* keys);
+/* stable counting sort by key; perm[i] = source slot of sorted slot i */
+void or_stable_sort(int n, const uint32_t* keys, uint32_t nkeys, uint32_t* perm);
+/* cell_start[k] = first sorted index with key >= k, k = 0..nkeys */
+void or_cell_start(int n, const uint32_t* sorted_keys, uint32_t nkeys, uint32_t* cell_start);
+
+/* ---- Model S (SPEC_SPH.md §2) ---- */
+typedef struct {
+    int32_t dim;
+    float dx, h, rho0, c0, alpha, eps_xsph;
+    float g[3];
+    float L[3];
+    float wall_e;
+    float f_amp, f_freq;
+    /* derived by or_sph_derive */
+    float mass, B, sigma, inv_h, four_h2;
+    or_grid grid;
+} or_sph_params;
+
+void or_sph_derive(or_sph_params* p);
+/* One step. Arrays are permuted in place into this step's sorted order.
+ * rho/prho (optional) receive pass-1 results in that order; cell_start (optional, C+1). */
+int or_sph_step(const or_sph_params* p, int n, float* pos3, float* vel3, int32_t* id,
+                float dt, float t, float* rho, float* prho, uint32_t* cell_start,
+                int nthreads);
+/* Dam-break lattice init (SPEC_SPH.md; the same integer hash as the device init). */
+void or_sph_lattice(int dim, int nx, int ny, int nz, float dx, float x0, float y0, float z0,
+                    uint32_t seed, float jitter, float* pos3);
+
+/* ---- Model R (SPEC_SPH.md §1) ---- */
+typedef struct {
+    float position[3]; float radius;
+    float velocity[3]; float mass;
+    float angularVelocity[3]; float momentOfInertia;
+    float drag; float repulsionStrength; float padding1; float padding2;
+    float rotation[4];
+    int32_t modeIndex;
+} or_particle84;   /* SimulateParticles.compute:23-40, 84 bytes */
+
+typedef struct {
+    float dt, spawn_radius, global_drag, torque_factor, torque_damping, boundary_friction,
+          roll_mult, repulsion_strength;
+    int32_t drag_id;            /* DragInput.selectedID (compute:70-74), -1 = none */
+    float drag_target[3];
+    float drag_strength;
+} or_contact_params;
+
+/* One step on n active particles (AoS, in/out). torque_int (optional, n*3) receives the
+ * per-particle int torque sums that UpdateRotation consumed. */
+int or_contact_step(const or_contact_params* p, int n, or_particle84* parts, int32_t* torque_int,
+                    int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

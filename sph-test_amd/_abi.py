@@ -1,0 +1,163 @@
+"""ctypes binding of libsphhip.so (include/sphhip.h).
+
+This is the Python counterpart of the C# P/Invoke layer shown in INTEGRATION.md. It uses
+the same structs, the same entry points and the same error codes. The HIP library is the
+product. There is no fallback: if libsphhip.so is missing or fails to load, every call
+raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "libsphhip.so"
+
+SPH_OK = 0
+SPH_ERR_INVALID = -1
+SPH_ERR_HIP = -2
+SPH_ERR_CAPACITY = -3
+SPH_ERR_STATE = -4
+SPH_ERR_NOMEM = -5
+_STATUS = {0: "SPH_OK", -1: "SPH_ERR_INVALID", -2: "SPH_ERR_HIP", -3: "SPH_ERR_CAPACITY",
+           -4: "SPH_ERR_STATE", -5: "SPH_ERR_NOMEM"}
+
+SPH_MODEL_CONTACT = 0
+SPH_MODEL_WCSPH = 1
+SPH_FLAG_PROFILE = 1
+SPH_SCENARIO_DAMBREAK = 0
+SPH_SCENARIO_SLOSHING = 1
+SPH_SCENARIO_SPHERE = 2
+
+# SimulateParticles.compute:23-40 / ParticleSystemController.cs:157-175 (84 bytes)
+PARTICLE84 = np.dtype([
+    ("position", "<f4", (3,)), ("radius", "<f4"),
+    ("velocity", "<f4", (3,)), ("mass", "<f4"),
+    ("angularVelocity", "<f4", (3,)), ("momentOfInertia", "<f4"),
+    ("drag", "<f4"), ("repulsionStrength", "<f4"), ("genomeFlags", "<u4"),
+    ("orientConstraintStr", "<f4"),
+    ("rotation", "<f4", (4,)), ("modeIndex", "<i4"),
+])
+assert PARTICLE84.itemsize == 84
+
+
+class SphConfig(C.Structure):
+    _fields_ = [("model", C.c_int32), ("dim", C.c_int32), ("capacity", C.c_int32), ("flags", C.c_int32)]
+
+
+class SphParams(C.Structure):
+    _fields_ = [
+        ("spawn_radius", C.c_float), ("min_radius", C.c_float), ("max_radius", C.c_float),
+        ("global_drag_multiplier", C.c_float), ("torque_factor", C.c_float),
+        ("torque_damping", C.c_float), ("boundary_friction", C.c_float),
+        ("rolling_contact_radius_multiplier", C.c_float), ("density", C.c_float),
+        ("repulsion_strength", C.c_float), ("active_particle_count", C.c_int32),
+        ("dx", C.c_float), ("h", C.c_float), ("rho0", C.c_float), ("c0", C.c_float),
+        ("alpha", C.c_float), ("xsph_eps", C.c_float), ("gravity", C.c_float * 3),
+        ("box", C.c_float * 3), ("wall_restitution", C.c_float), ("forcing_amp", C.c_float),
+        ("forcing_freq", C.c_float),
+    ]
+
+
+class SphScenario(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("dim", C.c_int32), ("nx", C.c_int32), ("ny", C.c_int32),
+                ("nz", C.c_int32), ("tx", C.c_int32), ("ty", C.c_int32), ("tz", C.c_int32),
+                ("dx", C.c_float), ("seed", C.c_uint32), ("jitter", C.c_float)]
+
+
+class SphDragInput(C.Structure):
+    _fields_ = [("selected_id", C.c_int32), ("target", C.c_float * 3), ("strength", C.c_float)]
+
+
+class SphStats(C.Structure):
+    _fields_ = [("steps", C.c_int64), ("sim_time", C.c_double), ("active", C.c_int32),
+                ("capacity", C.c_int32), ("grid", C.c_int32 * 3), ("key_bits", C.c_int32),
+                ("device_bytes", C.c_int64)]
+
+
+class SphKernelStat(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("total_ms", C.c_double),
+                ("bytes_per_launch", C.c_double)]
+
+
+assert C.sizeof(SphDragInput) == 20
+assert C.sizeof(SphConfig) == 16
+
+# every entry point declared in include/sphhip.h, with its ctypes signature
+_P = C.c_void_p
+_I = C.c_int32
+SIGNATURES = {
+    "sph_abi_version": ([], C.c_int32),
+    "sph_last_error": ([_P], C.c_char_p),
+    "sph_create": ([C.POINTER(SphConfig), _I, C.POINTER(_P)], C.c_int),
+    "sph_destroy": ([_P], None),
+    "sph_resize": ([_P, _I], C.c_int),
+    "sph_set_stream": ([_P, _P], C.c_int),
+    "sph_get_stream": ([_P, C.POINTER(_P)], C.c_int),
+    "sph_set_params": ([_P, C.POINTER(SphParams)], C.c_int),
+    "sph_get_params": ([_P, C.POINTER(SphParams)], C.c_int),
+    "sph_scenario_params": ([C.POINTER(SphScenario), C.POINTER(SphParams), C.POINTER(C.c_float)], C.c_int),
+    "sph_upload_particles_aos84": ([_P, _P, _I], C.c_int),
+    "sph_download_particles_aos84": ([_P, _P, _I], C.c_int),
+    "sph_upload_state": ([_P, _P, _P, _I], C.c_int),
+    "sph_init_scenario": ([_P, C.POINTER(SphScenario)], C.c_int),
+    "sph_step": ([_P, C.c_float, _I], C.c_int),
+    "sph_set_drag": ([_P, C.POINTER(SphDragInput)], C.c_int),
+    "sph_set_adhesion": ([_P, _P, _I], C.c_int),
+    "sph_read_positions": ([_P, _P, _I], C.c_int),
+    "sph_read_rotations": ([_P, _P, _I], C.c_int),
+    "sph_read_velocities": ([_P, _P, _I], C.c_int),
+    "sph_read_angular_velocities": ([_P, _P, _I], C.c_int),
+    "sph_read_density": ([_P, _P, _I], C.c_int),
+    "sph_synchronize": ([_P], C.c_int),
+    "sph_get_stats": ([_P, C.POINTER(SphStats)], C.c_int),
+    "sph_get_kernel_stat": ([_P, _I, C.POINTER(SphKernelStat)], C.c_int),
+    "sph_reset_kernel_stats": ([_P], C.c_int),
+    "sph_read_sorted_ids": ([_P, _P, _I], C.c_int),
+    "sph_read_cell_start": ([_P, _P, _I], C.c_int),
+    "sph_read_torque_int": ([_P, _P, _I], C.c_int),
+    "sph_debug_radix_sort": ([_P, _P, _I, _I, _P, _P], C.c_int),
+    "sph_set_slab": ([_P, _P], C.c_int),
+}
+
+
+class SphError(RuntimeError):
+    def __init__(self, fn: str, status: int, message: str = ""):
+        self.status = status
+        super().__init__(f"{fn} -> {_STATUS.get(status, status)}: {message}")
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libsphhip.so from the package directory. Raises if it is missing (no fallback)."""
+    global _lib
+    if _lib is None:
+        path = Path(os.environ.get("SPHHIP_LIB", str(LIB_PATH)))
+        if not path.exists():
+            raise RuntimeError(f"libsphhip.so not built at {path}: run __graft_entry__.build()")
+        L = C.CDLL(str(path))
+        for name, (args, res) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def ptr(a) -> C.c_void_p:
+    if a is None:
+        return C.c_void_p(0)
+    if isinstance(a, np.ndarray):
+        return C.c_void_p(a.ctypes.data)
+    return C.c_void_p(int(a))
+
+
+def check(fn: str, status: int, ctx=None) -> None:
+    if status != SPH_OK:
+        msg = lib().sph_last_error(ctx).decode(errors="replace") if ctx else ""
+        raise SphError(fn, status, msg)

@@ -1,0 +1,176 @@
+"""`Context`: one libsphhip.so context (one GPU), the object the controllers drive."""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import _abi as A
+
+
+class Context:
+    """A device context: particle buffers, grid, stream (include/sphhip.h)."""
+
+    def __init__(self, model: int, dim: int, capacity: int, device: int = 0, profile: bool = False):
+        self._L = A.lib()
+        cfg = A.SphConfig(model, dim, capacity, A.SPH_FLAG_PROFILE if profile else 0)
+        h = C.c_void_p()
+        st = self._L.sph_create(C.byref(cfg), device, C.byref(h))
+        if st != A.SPH_OK:
+            raise A.SphError("sph_create", st, f"model={model} dim={dim} capacity={capacity} device={device}")
+        self._h = h
+        self.model, self.dim, self.capacity, self.device = model, dim, capacity, device
+        self.n = 0
+
+    # -------------------------------------------------------------- lifetime
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.sph_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _chk(self, fn: str, st: int) -> None:
+        A.check(fn, st, self._h)
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    # -------------------------------------------------------------- config
+    def resize(self, capacity: int) -> None:
+        self._chk("sph_resize", self._L.sph_resize(self._h, capacity))
+        self.capacity = capacity
+
+    def set_stream(self, stream_handle: Optional[int]) -> None:
+        self._chk("sph_set_stream", self._L.sph_set_stream(self._h, C.c_void_p(stream_handle or 0)))
+
+    def stream(self) -> int:
+        s = C.c_void_p()
+        self._chk("sph_get_stream", self._L.sph_get_stream(self._h, C.byref(s)))
+        return int(s.value or 0)
+
+    def set_params(self, params: A.SphParams) -> None:
+        self._chk("sph_set_params", self._L.sph_set_params(self._h, C.byref(params)))
+
+    def get_params(self) -> A.SphParams:
+        p = A.SphParams()
+        self._chk("sph_get_params", self._L.sph_get_params(self._h, C.byref(p)))
+        return p
+
+    # -------------------------------------------------------------- data
+    def upload_aos84(self, parts: np.ndarray) -> None:
+        parts = np.ascontiguousarray(parts, dtype=A.PARTICLE84)
+        self._chk("sph_upload_particles_aos84", self._L.sph_upload_particles_aos84(self._h, A.ptr(parts), len(parts)))
+        self.n = len(parts)
+
+    def download_aos84(self) -> np.ndarray:
+        out = np.zeros(self.n, A.PARTICLE84)
+        self._chk("sph_download_particles_aos84", self._L.sph_download_particles_aos84(self._h, A.ptr(out), self.n))
+        return out
+
+    def upload_state(self, pos: np.ndarray, vel: Optional[np.ndarray] = None) -> None:
+        pos = np.ascontiguousarray(pos, dtype=np.float32).reshape(-1, 3)
+        v = None if vel is None else np.ascontiguousarray(vel, dtype=np.float32).reshape(-1, 3)
+        self._chk("sph_upload_state", self._L.sph_upload_state(self._h, A.ptr(pos), A.ptr(v), len(pos)))
+        self.n = len(pos)
+
+    def init_scenario(self, sc: A.SphScenario) -> None:
+        self._chk("sph_init_scenario", self._L.sph_init_scenario(self._h, C.byref(sc)))
+        self.n = sc.nx * sc.ny * (sc.nz if sc.dim == 3 else 1)
+
+    def step(self, dt: float, nsteps: int = 1) -> None:
+        self._chk("sph_step", self._L.sph_step(self._h, dt, nsteps))
+
+    def set_drag(self, selected_id: int, target, strength: float) -> None:
+        d = A.SphDragInput(selected_id, (C.c_float * 3)(*target), strength)
+        self._chk("sph_set_drag", self._L.sph_set_drag(self._h, C.byref(d)))
+
+    def synchronize(self) -> None:
+        self._chk("sph_synchronize", self._L.sph_synchronize(self._h))
+
+    def _read(self, fn: str, comps: int, dtype=np.float32) -> np.ndarray:
+        out = np.empty((self.n, comps) if comps > 1 else self.n, dtype)
+        self._chk(fn, getattr(self._L, fn)(self._h, A.ptr(out), self.n))
+        return out
+
+    def positions(self) -> np.ndarray:
+        return self._read("sph_read_positions", 3)
+
+    def velocities(self) -> np.ndarray:
+        return self._read("sph_read_velocities", 3)
+
+    def rotations(self) -> np.ndarray:
+        return self._read("sph_read_rotations", 4)
+
+    def angular_velocities(self) -> np.ndarray:
+        return self._read("sph_read_angular_velocities", 3)
+
+    def density(self) -> np.ndarray:
+        return self._read("sph_read_density", 1)
+
+    def torque_int(self) -> np.ndarray:
+        return self._read("sph_read_torque_int", 3, np.int32)
+
+    def sorted_ids(self) -> np.ndarray:
+        return self._read("sph_read_sorted_ids", 1, np.int32)
+
+    def cell_start(self) -> np.ndarray:
+        st = self.stats()
+        nc = st.grid[0] * st.grid[1] * st.grid[2] + 1
+        out = np.empty(nc, np.uint32)
+        self._chk("sph_read_cell_start", self._L.sph_read_cell_start(self._h, A.ptr(out), nc))
+        return out
+
+    def radix_sort(self, keys: np.ndarray, key_bits: int):
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        perm = np.empty_like(keys)
+        sk = np.empty_like(keys)
+        self._chk("sph_debug_radix_sort",
+                  self._L.sph_debug_radix_sort(self._h, A.ptr(keys), len(keys), key_bits, A.ptr(perm), A.ptr(sk)))
+        return perm, sk
+
+    # -------------------------------------------------------------- stats
+    def stats(self) -> A.SphStats:
+        s = A.SphStats()
+        self._chk("sph_get_stats", self._L.sph_get_stats(self._h, C.byref(s)))
+        return s
+
+    def kernel_stats(self) -> dict:
+        out = {}
+        i = 0
+        while True:
+            k = A.SphKernelStat()
+            if self._L.sph_get_kernel_stat(self._h, i, C.byref(k)) != A.SPH_OK:
+                break
+            out[k.name.decode()] = {"launches": k.launches, "total_ms": k.total_ms,
+                                    "bytes_per_launch": k.bytes_per_launch}
+            i += 1
+        return out
+
+    def reset_kernel_stats(self) -> None:
+        self._chk("sph_reset_kernel_stats", self._L.sph_reset_kernel_stats(self._h))
+
+
+def scenario_params(sc: A.SphScenario):
+    """SPEC_SPH.md §2 constants for a scenario (pure C call, no GPU needed)."""
+    p = A.SphParams()
+    dt = C.c_float()
+    A.check("sph_scenario_params", A.lib().sph_scenario_params(C.byref(sc), C.byref(p), C.byref(dt)))
+    return p, float(dt.value)
+
+
+def make_scenario(kind: int, dim: int, nx: int, ny: int, nz: int, tx: int, ty: int, tz: int,
+                  dx: float = 0.01, seed: int = 1234, jitter: float = 0.01) -> A.SphScenario:
+    return A.SphScenario(kind, dim, nx, ny, nz, tx, ty, tz, dx, seed, jitter)

@@ -1,0 +1,106 @@
+// common.h — internal declarations shared by the HIP kernels and the C ABI (libsphhip.so).
+// Not part of the public ABI (that is include/sphhip.h). gfx950 / wave64 only.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sph {
+
+// Uniform grid (SPEC_SPH.md §0). key = (cx*gy + cy)*gz + cz, x slowest.
+struct GridDesc {
+    float ox, oy, oz;
+    float inv_cell;
+    int32_t gx, gy, gz;
+    uint32_t ncells;     // gx*gy*gz (keys == ncells mark inactive particles)
+};
+
+// Model S constants (SPEC_SPH.md §2), derived on the host from sph_params.
+struct SphConst {
+    float mass, four_h2, inv_h, sigma, sigma_h, sigma_h2;
+    float B, inv_rho0, h, eta2, ac0, eps;
+    float gx, gy, gz;
+    float Lx, Ly, Lz;
+    float wall_e;
+};
+
+// Model R uniforms (SimulateParticles.compute:89-100) + DragInput (:70-74).
+struct ContactConst {
+    float dt, spawn_radius, global_drag, torque_factor, torque_damping, boundary_friction;
+    float roll_mult, repulsion_strength;
+    int32_t drag_id;
+    float drag_tx, drag_ty, drag_tz, drag_strength;
+};
+
+#if defined(__HIPCC__)
+__device__ __forceinline__ int32_t cell_coord(float x, float o, float inv, int32_t G) {
+    // GetGridCoord (compute:102-105): (uint)((p - origin) * inv) with ftou (neg/NaN -> 0), clamp
+    float g = (x - o) * inv;
+    if (!(g > 0.0f)) return 0;
+    if (g >= (float)(G - 1)) return G - 1;
+    return (int32_t)g;
+}
+
+__device__ __forceinline__ uint32_t cell_key(const GridDesc& g, float x, float y, float z) {
+    int32_t cx = cell_coord(x, g.ox, g.inv_cell, g.gx);
+    int32_t cy = cell_coord(y, g.oy, g.inv_cell, g.gy);
+    int32_t cz = cell_coord(z, g.oz, g.inv_cell, g.gz);
+    return ((uint32_t)cx * (uint32_t)g.gy + (uint32_t)cy) * (uint32_t)g.gz + (uint32_t)cz;
+}
+
+__device__ __forceinline__ uint32_t lane_id() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+#endif
+
+// ---- host-side launchers (each .hip file) ----
+// radix sort (sort.hip)
+size_t radix_hist_elems(int32_t capacity);
+// Sort (keys_a, vals_a) by the low key_bits bits, stable. identity_vals: vals_a is not read,
+// the input values are the slot indices. Ping-pongs between a and b; returns 1 if the
+// result is in (keys_b, vals_b), 0 if in (keys_a, vals_a).
+int radix_sort(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, int32_t n,
+               int32_t key_bits, bool identity_vals, uint32_t* hist, uint32_t* bin_total,
+               hipStream_t s);
+
+// grid / data movement (grid.hip)
+void launch_keys(const float4* pos, int32_t n, const int32_t* id, int32_t n_active_id,
+                 GridDesc g, uint32_t* keys, hipStream_t s);
+void launch_cell_start(const uint32_t* sorted_keys, int32_t n, uint32_t* cs, uint32_t ncells,
+                       hipStream_t s);
+void launch_gather_f4(const uint32_t* perm, const float4* src, float4* dst, int32_t n, hipStream_t s);
+void launch_gather_i32(const uint32_t* perm, const int32_t* src, int32_t* dst, int32_t n, hipStream_t s);
+void launch_gather_s(const uint32_t* perm, const float4* pos, const float4* vel, const int32_t* id,
+                     float4* pos_o, float4* vel_o, int32_t* id_o, int32_t n, hipStream_t s);
+void launch_scatter_f4_by_id(const float4* src, const int32_t* id, int32_t n, float* dst,
+                             int32_t comps, hipStream_t s);
+void launch_scatter_f2x_by_id(const float2* src, const int32_t* id, int32_t n, float* dst, hipStream_t s);
+void launch_scatter_i3_by_id(const int32_t* src, const int32_t* id, int32_t n, int32_t* dst, hipStream_t s);
+void launch_aos84_to_soa(const void* aos, int32_t n, float4* pos, float4* vel, float4* omg,
+                         float4* rot, float4* aux, int32_t* mode, int32_t* id, hipStream_t s);
+void launch_soa_to_aos84(const float4* pos, const float4* vel, const float4* omg, const float4* rot,
+                         const float4* aux, const int32_t* mode, const int32_t* id, int32_t n,
+                         void* aos, hipStream_t s);
+void launch_pack_sv(const float* pos3, const float* vel3, int32_t n, float4* pos, float4* vel,
+                    int32_t* id, hipStream_t s);
+void launch_lattice(int32_t dim, int32_t nx, int32_t ny, int32_t nz, float dx, float x0, float y0,
+                    float z0, uint32_t seed, float jitter, float4* pos, float4* vel, int32_t* id,
+                    hipStream_t s);
+void launch_iota(uint32_t* v, int32_t n, hipStream_t s);
+
+// Model S (wcsph.hip)
+void launch_density(const float4* pos, const uint32_t* cs, int32_t n, GridDesc g, SphConst c,
+                    float2* rp, hipStream_t s);
+void launch_force_integrate(const float4* pos, const float4* vel, const float2* rp,
+                            const uint32_t* cs, int32_t n, GridDesc g, SphConst c, float dt,
+                            float fext_x, float4* pos_o, float4* vel_o, uint32_t* keys_o,
+                            hipStream_t s);
+
+// Model R (contact.hip)
+void launch_contact_step(const float4* pos, const float4* vel, const float4* omg, const float4* rot,
+                         const float4* aux, const int32_t* id, const uint32_t* cs, int32_t n_active,
+                         int32_t n, GridDesc g, ContactConst c, float4* pos_o, float4* vel_o,
+                         float4* omg_o, float4* rot_o, int32_t* torque_o, uint32_t* keys_o,
+                         int32_t n_active_id, hipStream_t s);
+
+}  // namespace sph

@@ -1,0 +1,198 @@
+// contact.hip — Model R: the reference's soft-sphere contact step (SPEC_SPH.md §1), gfx950.
+//
+// One fused kernel replaces five of the reference's dispatches per frame:
+//   ApplySPHForces (SimulateParticles.compute:211-309), ApplyDragForce (:311-324),
+//   UpdateMotion (:326-357), UpdateRotation (:379-408) and the torqueAccumBuffer clear
+//   (ParticleSystemController.cs:265).
+// Jacobi semantics: all reads come from the start-of-step arrays, all writes go to the
+// *_o arrays. The reaction torque the reference scatters with three InterlockedAdds per
+// contact (compute:291-294) is gathered instead: particle a evaluates each contact pair a
+// second time from b's side and sums the same truncated int3 terms. int32 addition is
+// associative, so the sum is bit-identical to the atomic one, with no atomics and no
+// ordering dependence.
+#include "common.h"
+
+namespace sph {
+
+constexpr int CT_BLK = 256;
+constexpr float TORQUE_SCALE = 10000.0f;   // compute:19
+
+struct f3 { float x, y, z; };
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return {x, y, z}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f3 operator*(f3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ f3 operator/(f3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ f3 operator-(f3 a) { return {-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float len(f3 a) { return sqrtf(dot(a, a)); }
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ float saturate(float x) { return x > 0.0f ? (x < 1.0f ? x : 1.0f) : 0.0f; }
+__device__ __forceinline__ f3 normalize(f3 a) { return a / len(a); }
+__device__ __forceinline__ f3 xyz(float4 v) { return {v.x, v.y, v.z}; }
+
+__device__ __forceinline__ int32_t ftoi(float x) {   // D3D ftoi: truncate, saturate, NaN -> 0
+    if (x != x) return 0;
+    if (x >= 2147483648.0f) return 2147483647;
+    if (x <= -2147483648.0f) return (int32_t)0x80000000;
+    return (int32_t)x;
+}
+
+struct Body { f3 pos, vel, omg; float r; };
+
+// ApplySPHForces' pair body (compute:248-295) from `self`'s thread.
+// hit: 0 none, 1 repulsion only, 2 repulsion + rolling friction.
+__device__ __forceinline__ int contact_pair(const ContactConst& c, const Body& A, const Body& B,
+                                            f3& force, f3& torqueA, f3& torqueB) {
+    const float effectiveRadiusA = A.r * 0.5f;
+    const float effectiveRadiusB = B.r * 0.5f;
+    const f3 delta = A.pos - B.pos;
+    const float dist = len(delta);
+    const float overlap = (effectiveRadiusA + effectiveRadiusB) - dist;
+    if (!(overlap > 0.001f)) return 0;
+    const f3 dir = delta / dist;
+    const float overlapFalloff = saturate(overlap / (effectiveRadiusA + effectiveRadiusB));
+    const float falloff = saturate(1.0f - dist / (effectiveRadiusA + effectiveRadiusB));
+    force = dir * falloff * c.repulsion_strength * overlapFalloff;
+    const f3 contactPointA = A.pos - dir * effectiveRadiusA;
+    const f3 contactPointB = B.pos + dir * effectiveRadiusB;
+    const f3 surfaceVelA = A.vel + cross(A.omg, contactPointA - A.pos);
+    const f3 surfaceVelB = B.vel + cross(B.omg, contactPointB - B.pos);
+    const f3 relSurfaceVel = surfaceVelA - surfaceVelB;
+    const f3 tangentVel = relSurfaceVel - dir * dot(relSurfaceVel, dir);
+    const float slipSpeed = len(tangentVel);
+    if (!(slipSpeed > 1e-4f)) return 1;
+    const f3 frictionDir = tangentVel / slipSpeed;
+    const float torqueInput = fabsf(slipSpeed * c.torque_factor);
+    float frictionMag = powf(torqueInput, 1.25f);
+    frictionMag = fminf(frictionMag, 10.0f);
+    const float torqueRadiusScale = overlapFalloff * overlapFalloff;   // pow(x, 2.0) :282
+    const float effectiveRadiusTorqueA = torqueRadiusScale * effectiveRadiusA * c.roll_mult;
+    const float effectiveRadiusTorqueB = torqueRadiusScale * effectiveRadiusB * c.roll_mult;
+    torqueA = cross(-dir * effectiveRadiusTorqueA, -frictionDir * frictionMag);
+    torqueB = cross(dir * effectiveRadiusTorqueB, frictionDir * frictionMag);
+    return 2;
+}
+
+__global__ __launch_bounds__(CT_BLK) void k_contact_step(
+    const float4* __restrict__ pos, const float4* __restrict__ vel, const float4* __restrict__ omg,
+    const float4* __restrict__ rot, const float4* __restrict__ aux, const int32_t* __restrict__ id,
+    const uint32_t* __restrict__ cs, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
+    float4* __restrict__ pos_o, float4* __restrict__ vel_o, float4* __restrict__ omg_o,
+    float4* __restrict__ rot_o, int32_t* __restrict__ torque_o, uint32_t* __restrict__ keys_o) {
+    const int32_t a = blockIdx.x * CT_BLK + threadIdx.x;
+    if (a >= n) return;
+    const float4 pa = pos[a], va = vel[a], wa = omg[a], qa = rot[a];
+    if (a >= n_active) {   // inactive slots (id >= activeParticleCount) pass through
+        pos_o[a] = pa; vel_o[a] = va; omg_o[a] = wa; rot_o[a] = qa;
+        if (torque_o) { torque_o[3 * a] = 0; torque_o[3 * a + 1] = 0; torque_o[3 * a + 2] = 0; }
+        keys_o[a] = g.ncells;
+        return;
+    }
+    const Body A{xyz(pa), xyz(va), xyz(wa), pa.w};
+    const float mass = va.w, inertia = wa.w, drag = aux[a].x;
+    const float dt = c.dt;
+    f3 totalForce = mk(0, 0, 0), totalTorque = mk(0, 0, 0);
+    uint32_t tq0 = 0, tq1 = 0, tq2 = 0;   // wrapping int32 sums (InterlockedAdd)
+
+    const int32_t cx = cell_coord(pa.x, g.ox, g.inv_cell, g.gx);
+    const int32_t cy = cell_coord(pa.y, g.oy, g.inv_cell, g.gy);
+    const int32_t cz = cell_coord(pa.z, g.oz, g.inv_cell, g.gz);
+    const int32_t z0 = cz > 0 ? cz - 1 : 0, z1 = cz < g.gz - 1 ? cz + 1 : g.gz - 1;
+#pragma unroll 1
+    for (int k = 0; k < 9; ++k) {
+        const int32_t xx = cx + k / 3 - 1, yy = cy + k % 3 - 1;
+        if (xx < 0 || xx >= g.gx || yy < 0 || yy >= g.gy) continue;
+        const uint32_t rowk = ((uint32_t)xx * (uint32_t)g.gy + (uint32_t)yy) * (uint32_t)g.gz;
+        const uint32_t j0 = cs[rowk + (uint32_t)z0], j1 = cs[rowk + (uint32_t)z1 + 1u];
+#pragma unroll 1
+        for (uint32_t j = j0; j < j1; ++j) {
+            if ((int32_t)j == a) continue;                                   // :240
+            const float4 pb = pos[j];
+            const f3 d = A.pos - xyz(pb);
+            const float reff = A.r * 0.5f + pb.w * 0.5f;
+            if (!(reff - len(d) > 0.001f)) continue;                         // :253 (cheap reject)
+            const float4 vb = vel[j], wb = omg[j];
+            const Body B{xyz(pb), xyz(vb), xyz(wb), pb.w};
+            f3 F, TA, TB;
+            const int hit = contact_pair(c, A, B, F, TA, TB);
+            if (hit == 0) continue;
+            totalForce = totalForce + F;                                     // :261
+            if (hit == 2) totalTorque = totalTorque + TA;                    // :289
+            f3 F2, TA2, TB2;
+            if (contact_pair(c, B, A, F2, TA2, TB2) == 2) {                  // b's scatter into a
+                const f3 sc = TB2 * dt * TORQUE_SCALE;                       // :291
+                tq0 += (uint32_t)ftoi(sc.x);
+                tq1 += (uint32_t)ftoi(sc.y);
+                tq2 += (uint32_t)ftoi(sc.z);
+            }
+        }
+    }
+    // :302-306
+    f3 v = A.vel + (totalForce / mass) * dt;
+    f3 w = A.omg + (totalTorque / inertia) * dt;
+    f3 p = A.pos;
+    // ApplyDragForce :316-323 (selectedID is a particle index)
+    if (c.drag_id >= 0 && id[a] == c.drag_id) {
+        const f3 toTarget = mk(c.drag_tx, c.drag_ty, c.drag_tz) - p;
+        const f3 force = toTarget * c.drag_strength * dt;
+        v = v + force / mass;
+    }
+    // UpdateMotion :332-354
+    const float linearDamping = expf(-drag * c.global_drag * dt);
+    const float angularDamping = expf(-c.torque_damping * dt);
+    v = v * linearDamping;
+    w = w * angularDamping;
+    p = p + v * dt;
+    if (len(p) > c.spawn_radius) {
+        const f3 norm = normalize(p);
+        p = norm * c.spawn_radius;
+        v = v - norm * (2.0f * dot(v, norm));                              // reflect
+        const f3 tangentialVel = v - norm * dot(v, norm);
+        const f3 frictionDir = normalize(tangentialVel + mk(1e-6f, 1e-6f, 1e-6f));
+        const float frictionMag = len(tangentialVel) * c.boundary_friction;
+        const float effectiveRadius = A.r * c.roll_mult;
+        const f3 torque = cross(-norm * effectiveRadius, -frictionDir * frictionMag);
+        w = w + (torque / inertia) * dt;
+    }
+    // UpdateRotation :385-406
+    const f3 torque = mk((float)(int32_t)tq0, (float)(int32_t)tq1, (float)(int32_t)tq2) / TORQUE_SCALE;
+    w = w + torque / inertia;
+    w = w * expf(-c.torque_damping * dt);
+    float4 q = qa;
+    const float angle = len(w * dt);
+    if (angle > 0.00001f) {
+        const f3 axis = normalize(w);
+        const float s = sinf(angle * 0.5f), co = cosf(angle * 0.5f);
+        const f3 dqv = axis * s;
+        const f3 qv = xyz(qa);
+        const f3 r = qv * co + dqv * qa.w + cross(dqv, qv);                // quat_mul(dq, q) :359-365
+        const float rw = co * qa.w - dot(dqv, qv);
+        const float l = sqrtf(r.x * r.x + r.y * r.y + r.z * r.z + rw * rw);
+        q = make_float4(r.x / l, r.y / l, r.z / l, rw / l);
+    }
+    pos_o[a] = make_float4(p.x, p.y, p.z, pa.w);
+    vel_o[a] = make_float4(v.x, v.y, v.z, mass);
+    omg_o[a] = make_float4(w.x, w.y, w.z, inertia);
+    rot_o[a] = q;
+    if (torque_o) {
+        torque_o[3 * a] = (int32_t)tq0; torque_o[3 * a + 1] = (int32_t)tq1; torque_o[3 * a + 2] = (int32_t)tq2;
+    }
+    keys_o[a] = cell_key(g, p.x, p.y, p.z);
+}
+
+void launch_contact_step(const float4* pos, const float4* vel, const float4* omg, const float4* rot,
+                         const float4* aux, const int32_t* id, const uint32_t* cs, int32_t n_active,
+                         int32_t n, GridDesc g, ContactConst c, float4* pos_o, float4* vel_o,
+                         float4* omg_o, float4* rot_o, int32_t* torque_o, uint32_t* keys_o,
+                         int32_t n_active_id, hipStream_t s) {
+    (void)n_active_id;
+    if (n > 0)
+        k_contact_step<<<(n + CT_BLK - 1) / CT_BLK, CT_BLK, 0, s>>>(pos, vel, omg, rot, aux, id, cs,
+                                                                    n_active, n, g, c, pos_o, vel_o,
+                                                                    omg_o, rot_o, torque_o, keys_o);
+}
+
+}  // namespace sph

@@ -1,0 +1,791 @@
+// sph_abi.cpp — the C ABI of libsphhip.so (include/sphhip.h) and the host-side step.
+//
+// Host orchestration of the reference's per-frame GPU work, MI355X-first:
+//   ParticleSystemController.Update() (ParticleSystemController.cs:244-351) issues
+//   ~9 Dispatches plus two full-buffer H2D clears and two synchronous D2H readbacks every
+//   frame. sph_step() issues hash → radix sort → reorder → cell-start → pass 1 → pass 2
+//   on one HIP stream with no host synchronisation, no per-step allocation and no
+//   readback. Readback is an explicit call (sph_read_*).
+// Device memory is owned here and sized once per capacity (InitializeBuffers :373-451).
+#include "common.h"
+#include "sphhip.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace sph;
+
+namespace {
+
+struct KStat {
+    std::string name;
+    int64_t launches = 0;
+    double total_ms = 0.0;
+    double bytes = 0.0;
+};
+
+struct Pending {
+    int k;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct sph_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    sph_config cfg{};
+    sph_params prm{};
+    bool params_set = false;
+    int32_t capacity = 0;
+    int32_t n = 0;
+    GridDesc grid{};
+    int32_t key_bits = 1;
+    SphConst sc{};
+    // particle state, cell-sorted slot order; *2 = ping-pong partner
+    float4 *pos = nullptr, *vel = nullptr, *pos2 = nullptr, *vel2 = nullptr;
+    float4 *omg = nullptr, *rot = nullptr, *aux = nullptr, *omg2 = nullptr, *rot2 = nullptr, *aux2 = nullptr;
+    int32_t *id = nullptr, *id2 = nullptr, *mode = nullptr, *mode2 = nullptr;
+    float2* rp = nullptr;        // Model S (ρ, P/ρ²)
+    int32_t* torque = nullptr;   // Model R int torque of the last step (slot order)
+    // sort / grid
+    uint32_t *keys = nullptr, *keys2 = nullptr, *vals = nullptr, *vals2 = nullptr;
+    uint32_t *hist = nullptr, *bin_total = nullptr;
+    uint32_t* cs = nullptr;
+    uint32_t cs_cap = 0;
+    void* staging = nullptr;
+    size_t staging_bytes = 0;
+    bool keys_valid = false;
+    int32_t keys_active = -1;
+    int64_t steps = 0;
+    double sim_time = 0.0;
+    sph_drag_input drag{-1, {0.f, 0.f, 0.f}, 0.f};
+    std::string err;
+    bool profiling = false;
+    std::vector<KStat> kstats;
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> ev_pool;
+    int64_t device_bytes = 0;
+};
+
+namespace {
+
+int fail(sph_ctx* c, int code, const char* fmt, ...) {
+    if (c) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        c->err = buf;
+    }
+    return code;
+}
+
+#define HIPCHK(call)                                                                            \
+    do {                                                                                        \
+        hipError_t e_ = (call);                                                                 \
+        if (e_ != hipSuccess) return fail(ctx, SPH_ERR_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+int dalloc(sph_ctx* ctx, T** p, size_t count) {
+    if (*p) { (void)hipFree(*p); *p = nullptr; }
+    if (count == 0) return SPH_OK;
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, count * sizeof(T));
+    if (e != hipSuccess) return fail(ctx, SPH_ERR_NOMEM, "hipMalloc(%zu): %s", count * sizeof(T), hipGetErrorString(e));
+    *p = (T*)q;
+    ctx->device_bytes += (int64_t)(count * sizeof(T));
+    return SPH_OK;
+}
+
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+void free_all(sph_ctx* c) {
+    dfree(c->pos); dfree(c->vel); dfree(c->pos2); dfree(c->vel2);
+    dfree(c->omg); dfree(c->rot); dfree(c->aux); dfree(c->omg2); dfree(c->rot2); dfree(c->aux2);
+    dfree(c->id); dfree(c->id2); dfree(c->mode); dfree(c->mode2);
+    dfree(c->rp); dfree(c->torque);
+    dfree(c->keys); dfree(c->keys2); dfree(c->vals); dfree(c->vals2); dfree(c->hist); dfree(c->bin_total);
+    dfree(c->cs);
+    if (c->staging) (void)hipFree(c->staging);
+    c->staging = nullptr;
+    c->staging_bytes = 0;
+    c->cs_cap = 0;
+    c->device_bytes = 0;
+}
+
+int bit_width(uint32_t v) {
+    int b = 0;
+    while (v) { ++b; v >>= 1; }
+    return b < 1 ? 1 : b;
+}
+
+bool is_contact(const sph_ctx* c) { return c->cfg.model == SPH_MODEL_CONTACT; }
+
+int alloc_particles(sph_ctx* ctx, int32_t cap) {
+    const size_t n = (size_t)std::max(cap, 1);
+    int r;
+#define AL(p, cnt) if ((r = dalloc(ctx, &ctx->p, cnt)) != SPH_OK) return r
+    AL(pos, n); AL(vel, n); AL(pos2, n); AL(vel2, n);
+    AL(id, n); AL(id2, n);
+    AL(keys, n); AL(keys2, n); AL(vals, n); AL(vals2, n);
+    AL(hist, radix_hist_elems((int32_t)n)); AL(bin_total, 256);
+    if (is_contact(ctx)) {
+        AL(omg, n); AL(rot, n); AL(aux, n); AL(omg2, n); AL(rot2, n); AL(aux2, n);
+        AL(mode, n); AL(mode2, n); AL(torque, 3 * n);
+    } else {
+        AL(rp, n);
+    }
+#undef AL
+    ctx->staging_bytes = n * 84;
+    HIPCHK(hipMalloc(&ctx->staging, ctx->staging_bytes));
+    ctx->device_bytes += (int64_t)ctx->staging_bytes;
+    return SPH_OK;
+}
+
+int ensure_cells(sph_ctx* ctx) {
+    const uint32_t need = ctx->grid.ncells + 1;
+    if (need <= ctx->cs_cap) return SPH_OK;
+    int r = dalloc(ctx, &ctx->cs, need);
+    if (r != SPH_OK) return r;
+    ctx->cs_cap = need;
+    return SPH_OK;
+}
+
+// Grid + constants from params (SPEC_SPH.md §0/§2; same float arithmetic as the oracle).
+int derive(sph_ctx* ctx) {
+    const sph_params& p = ctx->prm;
+    GridDesc g{};
+    if (is_contact(ctx)) {
+        // SimulateParticles.compute:16-18,102-105: 32^3 cells of 4.0 anchored at -spawnRadius
+        g.ox = g.oy = g.oz = -p.spawn_radius;
+        g.inv_cell = 0.25f;
+        g.gx = g.gy = g.gz = 32;
+    } else {
+        if (!(p.h > 0.f) || !(p.dx > 0.f) || !(p.rho0 > 0.f))
+            return fail(ctx, SPH_ERR_INVALID, "Model S needs dx, h, rho0 > 0");
+        const float cell = 2.0f * p.h;
+        g.ox = g.oy = g.oz = 0.f;
+        g.inv_cell = 1.0f / cell;
+        int32_t G[3];
+        for (int a = 0; a < 3; ++a) {
+            G[a] = (int32_t)floorf(p.box[a] / cell) + 1;
+            if (G[a] < 1) G[a] = 1;
+        }
+        if (ctx->cfg.dim == 2) G[2] = 1;
+        g.gx = G[0]; g.gy = G[1]; g.gz = G[2];
+        const double nc = (double)G[0] * G[1] * G[2];
+        if (nc > 2.0e9) return fail(ctx, SPH_ERR_INVALID, "grid too large (%g cells)", nc);
+        const float PI = 3.14159265358979f, d = p.dx, h = p.h;
+        SphConst& s = ctx->sc;
+        s.mass = p.rho0 * d * d * (ctx->cfg.dim == 3 ? d : 1.0f);
+        s.B = p.c0 * p.c0 * p.rho0 / 7.0f;
+        s.sigma = ctx->cfg.dim == 3 ? 1.0f / (PI * h * h * h) : 10.0f / (7.0f * PI * h * h);
+        s.inv_h = 1.0f / h;
+        s.four_h2 = 4.0f * h * h;
+        s.sigma_h = s.sigma * s.inv_h;
+        s.sigma_h2 = s.sigma * s.inv_h * s.inv_h;
+        s.inv_rho0 = 1.0f / p.rho0;
+        s.h = h;
+        s.eta2 = 0.01f * h * h;
+        s.ac0 = p.alpha * p.c0;
+        s.eps = p.xsph_eps;
+        s.gx = p.gravity[0]; s.gy = p.gravity[1]; s.gz = p.gravity[2];
+        s.Lx = p.box[0]; s.Ly = p.box[1]; s.Lz = ctx->cfg.dim == 3 ? p.box[2] : 0.f;
+        s.wall_e = p.wall_restitution;
+    }
+    g.ncells = (uint32_t)g.gx * (uint32_t)g.gy * (uint32_t)g.gz;
+    ctx->grid = g;
+    ctx->key_bits = bit_width(g.ncells);   // the sentinel key == ncells must sort last
+    ctx->keys_valid = false;
+    return ensure_cells(ctx);
+}
+
+// ---------------------------------------------------------------- profiling
+int kstat_index(sph_ctx* c, const char* name) {
+    for (size_t i = 0; i < c->kstats.size(); ++i)
+        if (c->kstats[i].name == name) return (int)i;
+    KStat k;
+    k.name = name;
+    c->kstats.push_back(k);
+    return (int)c->kstats.size() - 1;
+}
+
+hipEvent_t take_event(sph_ctx* c) {
+    if (!c->ev_pool.empty()) {
+        hipEvent_t e = c->ev_pool.back();
+        c->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+void resolve_pending(sph_ctx* c) {
+    for (auto& p : c->pending) {
+        (void)hipEventSynchronize(p.b);
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) c->kstats[p.k].total_ms += ms;
+        c->ev_pool.push_back(p.a);
+        c->ev_pool.push_back(p.b);
+    }
+    c->pending.clear();
+}
+
+struct KTimer {
+    sph_ctx* c;
+    int k;
+    hipEvent_t a = nullptr;
+    KTimer(sph_ctx* ctx, const char* name, double bytes) : c(ctx), k(kstat_index(ctx, name)) {
+        c->kstats[k].launches++;
+        c->kstats[k].bytes = bytes;
+        if (c->profiling) {
+            a = take_event(c);
+            (void)hipEventRecord(a, c->stream);
+        }
+    }
+    ~KTimer() {
+        if (c->profiling) {
+            hipEvent_t b = take_event(c);
+            (void)hipEventRecord(b, c->stream);
+            c->pending.push_back({k, a, b});
+            if (c->pending.size() > 8192) resolve_pending(c);
+        }
+    }
+};
+
+// ---------------------------------------------------------------- steps
+void swap_sv(sph_ctx* c) {
+    std::swap(c->pos, c->pos2);
+    std::swap(c->vel, c->vel2);
+}
+
+int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id) {
+    const int32_t n = ctx->n;
+    if (!ctx->keys_valid || ctx->keys_active != n_active_id) {
+        KTimer t(ctx, "keys", 20.0 * n);
+        launch_keys(ctx->pos, n, is_contact(ctx) ? ctx->id : nullptr, n_active_id, ctx->grid, ctx->keys,
+                    ctx->stream);
+    }
+    int side;
+    {
+        const int passes = (ctx->key_bits + 7) / 8;
+        KTimer t(ctx, "radix_sort", (double)n * (20.0 * passes));
+        side = radix_sort(ctx->keys, ctx->vals, ctx->keys2, ctx->vals2, n, ctx->key_bits, true, ctx->hist,
+                          ctx->bin_total, ctx->stream);
+    }
+    const uint32_t* sk = side ? ctx->keys2 : ctx->keys;
+    const uint32_t* perm = side ? ctx->vals2 : ctx->vals;
+    if (is_contact(ctx)) {
+        KTimer t(ctx, "reorder", (double)n * (4 + 2 * (5 * 16 + 8)));
+        launch_gather_f4(perm, ctx->pos, ctx->pos2, n, ctx->stream);
+        launch_gather_f4(perm, ctx->vel, ctx->vel2, n, ctx->stream);
+        launch_gather_f4(perm, ctx->omg, ctx->omg2, n, ctx->stream);
+        launch_gather_f4(perm, ctx->rot, ctx->rot2, n, ctx->stream);
+        launch_gather_f4(perm, ctx->aux, ctx->aux2, n, ctx->stream);
+        launch_gather_i32(perm, ctx->id, ctx->id2, n, ctx->stream);
+        launch_gather_i32(perm, ctx->mode, ctx->mode2, n, ctx->stream);
+        swap_sv(ctx);
+        std::swap(ctx->omg, ctx->omg2);
+        std::swap(ctx->rot, ctx->rot2);
+        std::swap(ctx->aux, ctx->aux2);
+        std::swap(ctx->id, ctx->id2);
+        std::swap(ctx->mode, ctx->mode2);
+    } else {
+        KTimer t(ctx, "reorder", (double)n * (4 + 2 * 36));
+        launch_gather_s(perm, ctx->pos, ctx->vel, ctx->id, ctx->pos2, ctx->vel2, ctx->id2, n, ctx->stream);
+        swap_sv(ctx);
+        std::swap(ctx->id, ctx->id2);
+    }
+    {
+        KTimer t(ctx, "cell_start", 4.0 * (ctx->grid.ncells + 1));
+        launch_cell_start(sk, n, ctx->cs, ctx->grid.ncells, ctx->stream);
+    }
+    return SPH_OK;
+}
+
+int step_wcsph(sph_ctx* ctx, float dt) {
+    const int32_t n = ctx->n;
+    int r = sort_and_reorder(ctx, 0);
+    if (r != SPH_OK) return r;
+    {
+        KTimer t(ctx, "density", 24.0 * n);
+        launch_density(ctx->pos, ctx->cs, n, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
+    }
+    const sph_params& p = ctx->prm;
+    const float tt = (float)ctx->sim_time;
+    const float fext = p.forcing_amp != 0.0f ? p.forcing_amp * sinf(6.28318530718f * p.forcing_freq * tt) : 0.0f;
+    {
+        KTimer t(ctx, "force_integrate", 76.0 * n);
+        launch_force_integrate(ctx->pos, ctx->vel, ctx->rp, ctx->cs, n, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
+                               ctx->vel2, ctx->keys, ctx->stream);
+    }
+    swap_sv(ctx);
+    ctx->keys_valid = true;
+    ctx->keys_active = 0;
+    return SPH_OK;
+}
+
+int32_t contact_active(const sph_ctx* c) {
+    int32_t a = c->prm.active_particle_count;
+    if (a <= 0 || a > c->n) a = c->n;
+    return a;
+}
+
+int step_contact(sph_ctx* ctx, float dt) {
+    const int32_t n = ctx->n;
+    const int32_t act = contact_active(ctx);
+    int r = sort_and_reorder(ctx, act);
+    if (r != SPH_OK) return r;
+    const sph_params& p = ctx->prm;
+    ContactConst c{};
+    c.dt = dt;
+    c.spawn_radius = p.spawn_radius;
+    c.global_drag = p.global_drag_multiplier;
+    c.torque_factor = p.torque_factor;
+    c.torque_damping = p.torque_damping;
+    c.boundary_friction = p.boundary_friction;
+    c.roll_mult = p.rolling_contact_radius_multiplier;
+    c.repulsion_strength = p.repulsion_strength;
+    c.drag_id = ctx->drag.selected_id;
+    c.drag_tx = ctx->drag.target[0];
+    c.drag_ty = ctx->drag.target[1];
+    c.drag_tz = ctx->drag.target[2];
+    c.drag_strength = ctx->drag.strength;
+    {
+        KTimer t(ctx, "contact_step", (double)n * (2 * 64 + 4 + 12 + 4));
+        launch_contact_step(ctx->pos, ctx->vel, ctx->omg, ctx->rot, ctx->aux, ctx->id, ctx->cs, act, n, ctx->grid,
+                            c, ctx->pos2, ctx->vel2, ctx->omg2, ctx->rot2, ctx->torque, ctx->keys, act,
+                            ctx->stream);
+    }
+    swap_sv(ctx);
+    std::swap(ctx->omg, ctx->omg2);
+    std::swap(ctx->rot, ctx->rot2);
+    ctx->keys_valid = true;
+    ctx->keys_active = act;
+    return SPH_OK;
+}
+
+}  // namespace
+
+// ====================================================================== ABI
+extern "C" {
+
+int32_t sph_abi_version(void) { return SPH_ABI_VERSION; }
+
+const char* sph_last_error(const sph_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int sph_create(const sph_config* cfg, int32_t device, sph_ctx** out) {
+    if (!cfg || !out) return SPH_ERR_INVALID;
+    *out = nullptr;
+    if (cfg->model != SPH_MODEL_CONTACT && cfg->model != SPH_MODEL_WCSPH) return SPH_ERR_INVALID;
+    if (cfg->dim != 2 && cfg->dim != 3) return SPH_ERR_INVALID;
+    if (cfg->model == SPH_MODEL_CONTACT && cfg->dim != 3) return SPH_ERR_INVALID;
+    if (cfg->capacity < 0) return SPH_ERR_INVALID;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SPH_ERR_HIP;
+    if (device < 0 || device >= ndev) return SPH_ERR_INVALID;
+    sph_ctx* ctx = new sph_ctx();
+    ctx->cfg = *cfg;
+    ctx->device = device;
+    ctx->profiling = (cfg->flags & SPH_FLAG_PROFILE) != 0;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return SPH_ERR_HIP;
+    }
+    ctx->own_stream = true;
+    ctx->capacity = cfg->capacity;
+    int r = alloc_particles(ctx, cfg->capacity);
+    if (r != SPH_OK) {
+        free_all(ctx);
+        (void)hipStreamDestroy(ctx->stream);
+        delete ctx;
+        return r;
+    }
+    // reference defaults (ParticleSystemController.cs:12-24)
+    sph_params& p = ctx->prm;
+    p.spawn_radius = 15.f; p.min_radius = 1.5f; p.max_radius = 2.0f; p.global_drag_multiplier = 1.f;
+    p.torque_factor = 1.f; p.torque_damping = 0.5f; p.boundary_friction = 0.8f;
+    p.rolling_contact_radius_multiplier = 5.f; p.density = 0.1f; p.repulsion_strength = 200.f;
+    p.active_particle_count = 0;
+    if (is_contact(ctx)) {
+        r = derive(ctx);
+        if (r != SPH_OK) { sph_destroy(ctx); return r; }
+        ctx->params_set = true;
+    }
+    *out = ctx;
+    return SPH_OK;
+}
+
+void sph_destroy(sph_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    resolve_pending(ctx);
+    for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
+    free_all(ctx);
+    if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int sph_set_stream(sph_ctx* ctx, void* s) {
+    if (!ctx) return SPH_ERR_INVALID;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (s == nullptr) {
+        if (!ctx->own_stream) {
+            HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+            ctx->own_stream = true;
+        }
+        return SPH_OK;
+    }
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+    ctx->stream = (hipStream_t)s;
+    ctx->own_stream = false;
+    return SPH_OK;
+}
+
+int sph_get_stream(sph_ctx* ctx, void** s) {
+    if (!ctx || !s) return SPH_ERR_INVALID;
+    *s = (void*)ctx->stream;
+    return SPH_OK;
+}
+
+int sph_set_params(sph_ctx* ctx, const sph_params* params) {
+    if (!ctx || !params) return SPH_ERR_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    const sph_params old = ctx->prm;
+    ctx->prm = *params;
+    int r = derive(ctx);
+    if (r != SPH_OK) { ctx->prm = old; return r; }
+    ctx->params_set = true;
+    return SPH_OK;
+}
+
+int sph_get_params(const sph_ctx* ctx, sph_params* params) {
+    if (!ctx || !params) return SPH_ERR_INVALID;
+    *params = ctx->prm;
+    return SPH_OK;
+}
+
+int sph_scenario_params(const sph_scenario* sc, sph_params* out, float* dt_out) {
+    if (!sc || !out) return SPH_ERR_INVALID;
+    if (sc->dim != 2 && sc->dim != 3) return SPH_ERR_INVALID;
+    if (!(sc->dx > 0.f) || sc->nx <= 0 || sc->ny <= 0 || (sc->dim == 3 && sc->nz <= 0)) return SPH_ERR_INVALID;
+    std::memset(out, 0, sizeof *out);
+    const double dx = sc->dx, g = 9.81;
+    const double H = sc->ny * dx;               // initial fluid height (y up)
+    const double c0 = 10.0 * std::sqrt(2.0 * g * H);
+    out->dx = (float)dx;
+    out->h = (float)(1.2 * dx);
+    out->rho0 = 1000.f;
+    out->c0 = (float)c0;
+    out->alpha = 0.02f;
+    out->xsph_eps = 0.5f;
+    out->gravity[0] = 0.f; out->gravity[1] = (float)-g; out->gravity[2] = 0.f;
+    out->box[0] = (float)(sc->tx * dx);
+    out->box[1] = (float)(sc->ty * dx);
+    out->box[2] = sc->dim == 3 ? (float)(sc->tz * dx) : 0.f;
+    out->wall_restitution = 0.5f;
+    if (sc->kind == SPH_SCENARIO_SLOSHING) {
+        const double L = sc->tx * dx, PI = 3.14159265358979323846;
+        out->forcing_amp = (float)(0.1 * g);
+        out->forcing_freq = (float)(std::sqrt(g * PI / L * std::tanh(PI * H / L)) / (2.0 * PI));
+    }
+    // reference uniforms keep their defaults (ParticleSystemController.cs:12-24)
+    out->spawn_radius = 15.f; out->min_radius = 1.5f; out->max_radius = 2.0f;
+    out->global_drag_multiplier = 1.f; out->torque_factor = 1.f; out->torque_damping = 0.5f;
+    out->boundary_friction = 0.8f; out->rolling_contact_radius_multiplier = 5.f;
+    out->density = 0.1f; out->repulsion_strength = 200.f;
+    if (dt_out) *dt_out = (float)(0.25 * (1.2 * dx) / c0);
+    return SPH_OK;
+}
+
+int sph_upload_particles_aos84(sph_ctx* ctx, const void* src, int32_t count) {
+    if (!ctx || (!src && count > 0) || count < 0) return SPH_ERR_INVALID;
+    if (count > ctx->capacity) return fail(ctx, SPH_ERR_CAPACITY, "count %d > capacity %d", count, ctx->capacity);
+    HIPCHK(hipSetDevice(ctx->device));
+    if (count > 0) {
+        HIPCHK(hipMemcpyAsync(ctx->staging, src, (size_t)count * 84, hipMemcpyHostToDevice, ctx->stream));
+        launch_aos84_to_soa(ctx->staging, count, ctx->pos, ctx->vel, ctx->omg, ctx->rot, ctx->aux, ctx->mode,
+                            ctx->id, ctx->stream);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->n = count;
+    ctx->keys_valid = false;
+    ctx->steps = 0;
+    ctx->sim_time = 0.0;
+    return SPH_OK;
+}
+
+int sph_download_particles_aos84(sph_ctx* ctx, void* dst, int32_t count) {
+    if (!ctx || (!dst && count > 0)) return SPH_ERR_INVALID;
+    if (count < ctx->n) return fail(ctx, SPH_ERR_INVALID, "count %d < active particles %d", count, ctx->n);
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->n > 0) {
+        launch_soa_to_aos84(ctx->pos, ctx->vel, ctx->omg, ctx->rot, ctx->aux, ctx->mode, ctx->id, ctx->n,
+                            ctx->staging, ctx->stream);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(dst, ctx->staging, (size_t)ctx->n * 84, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SPH_OK;
+}
+
+int sph_upload_state(sph_ctx* ctx, const float* pos3, const float* vel3, int32_t count) {
+    if (!ctx || (!pos3 && count > 0) || count < 0) return SPH_ERR_INVALID;
+    if (is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "sph_upload_state is Model S only; use aos84");
+    if (count > ctx->capacity) return fail(ctx, SPH_ERR_CAPACITY, "count %d > capacity %d", count, ctx->capacity);
+    HIPCHK(hipSetDevice(ctx->device));
+    if (count > 0) {
+        float* sp = (float*)ctx->staging;
+        float* sv = vel3 ? sp + 3 * (size_t)count : nullptr;
+        HIPCHK(hipMemcpyAsync(sp, pos3, (size_t)count * 12, hipMemcpyHostToDevice, ctx->stream));
+        if (vel3) HIPCHK(hipMemcpyAsync(sv, vel3, (size_t)count * 12, hipMemcpyHostToDevice, ctx->stream));
+        launch_pack_sv(sp, sv, count, ctx->pos, ctx->vel, ctx->id, ctx->stream);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->n = count;
+    ctx->keys_valid = false;
+    ctx->steps = 0;
+    ctx->sim_time = 0.0;
+    return SPH_OK;
+}
+
+int sph_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
+    if (!ctx || !sc) return SPH_ERR_INVALID;
+    if (is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "scenario init for Model R is not implemented");
+    if (sc->dim != ctx->cfg.dim) return fail(ctx, SPH_ERR_INVALID, "scenario dim %d != context dim %d", sc->dim, ctx->cfg.dim);
+    const int64_t n = (int64_t)sc->nx * sc->ny * (sc->dim == 3 ? sc->nz : 1);
+    if (n <= 0) return fail(ctx, SPH_ERR_INVALID, "empty scenario");
+    if (n > ctx->capacity) return fail(ctx, SPH_ERR_CAPACITY, "scenario needs %lld > capacity %d", (long long)n, ctx->capacity);
+    HIPCHK(hipSetDevice(ctx->device));
+    launch_lattice(sc->dim, sc->nx, sc->ny, sc->nz, sc->dx, 0.f, 0.f, 0.f, sc->seed, sc->jitter * sc->dx, ctx->pos,
+                   ctx->vel, ctx->id, ctx->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->n = (int32_t)n;
+    ctx->keys_valid = false;
+    ctx->steps = 0;
+    ctx->sim_time = 0.0;
+    return SPH_OK;
+}
+
+int sph_step(sph_ctx* ctx, float dt, int32_t nsteps) {
+    if (!ctx || nsteps < 0 || !(dt >= 0.f)) return SPH_ERR_INVALID;
+    if (!ctx->params_set) return fail(ctx, SPH_ERR_STATE, "sph_set_params first");
+    HIPCHK(hipSetDevice(ctx->device));
+    for (int32_t s = 0; s < nsteps; ++s) {
+        if (ctx->n > 0) {
+            int r = is_contact(ctx) ? step_contact(ctx, dt) : step_wcsph(ctx, dt);
+            if (r != SPH_OK) return r;
+        }
+        ctx->steps++;
+        ctx->sim_time += (double)dt;
+    }
+    HIPCHK(hipGetLastError());
+    return SPH_OK;
+}
+
+int sph_set_drag(sph_ctx* ctx, const sph_drag_input* drag) {
+    if (!ctx || !drag) return SPH_ERR_INVALID;
+    ctx->drag = *drag;
+    return SPH_OK;
+}
+
+int sph_set_adhesion(sph_ctx* ctx, const void* conn84, int32_t count) {
+    (void)conn84;
+    if (!ctx) return SPH_ERR_INVALID;
+    if (count == 0) return SPH_OK;
+    return fail(ctx, SPH_ERR_STATE, "adhesion constraints are not implemented yet (SURVEY §8f-1)");
+}
+
+static int read_f4(sph_ctx* ctx, const float4* src, float* dst, int32_t count, int comps) {
+    if (!ctx || (!dst && count > 0)) return SPH_ERR_INVALID;
+    if (count < ctx->n) return fail(ctx, SPH_ERR_INVALID, "count %d < active particles %d", count, ctx->n);
+    if (!src) return fail(ctx, SPH_ERR_STATE, "field not held by this model");
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->n > 0) {
+        launch_scatter_f4_by_id(src, ctx->id, ctx->n, (float*)ctx->staging, comps, ctx->stream);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(dst, ctx->staging, (size_t)ctx->n * comps * 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SPH_OK;
+}
+
+int sph_read_positions(sph_ctx* ctx, float* xyz, int32_t count) {
+    return ctx ? read_f4(ctx, ctx->pos, xyz, count, 3) : SPH_ERR_INVALID;
+}
+int sph_read_velocities(sph_ctx* ctx, float* xyz, int32_t count) {
+    return ctx ? read_f4(ctx, ctx->vel, xyz, count, 3) : SPH_ERR_INVALID;
+}
+int sph_read_rotations(sph_ctx* ctx, float* xyzw, int32_t count) {
+    return ctx ? read_f4(ctx, ctx->rot, xyzw, count, 4) : SPH_ERR_INVALID;
+}
+int sph_read_angular_velocities(sph_ctx* ctx, float* xyz, int32_t count) {
+    return ctx ? read_f4(ctx, ctx->omg, xyz, count, 3) : SPH_ERR_INVALID;
+}
+
+int sph_read_density(sph_ctx* ctx, float* rho, int32_t count) {
+    if (!ctx || (!rho && count > 0)) return SPH_ERR_INVALID;
+    if (is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "density is Model S only");
+    if (count < ctx->n) return fail(ctx, SPH_ERR_INVALID, "count %d < active particles %d", count, ctx->n);
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->n > 0) {
+        // rp is in the slot order of the last step's density pass; id was reordered before it
+        launch_scatter_f2x_by_id(ctx->rp, ctx->id, ctx->n, (float*)ctx->staging, ctx->stream);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(rho, ctx->staging, (size_t)ctx->n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SPH_OK;
+}
+
+int sph_read_torque_int(sph_ctx* ctx, int32_t* xyz, int32_t count) {
+    if (!ctx || (!xyz && count > 0)) return SPH_ERR_INVALID;
+    if (!is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "torque is Model R only");
+    if (count < ctx->n) return fail(ctx, SPH_ERR_INVALID, "count %d < active particles %d", count, ctx->n);
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->n > 0) {
+        launch_scatter_i3_by_id(ctx->torque, ctx->id, ctx->n, (int32_t*)ctx->staging, ctx->stream);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(xyz, ctx->staging, (size_t)ctx->n * 12, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SPH_OK;
+}
+
+int sph_synchronize(sph_ctx* ctx) {
+    if (!ctx) return SPH_ERR_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SPH_OK;
+}
+
+int sph_get_stats(sph_ctx* ctx, sph_stats* out) {
+    if (!ctx || !out) return SPH_ERR_INVALID;
+    out->steps = ctx->steps;
+    out->sim_time = ctx->sim_time;
+    out->active = ctx->n;
+    out->capacity = ctx->capacity;
+    out->grid[0] = ctx->grid.gx; out->grid[1] = ctx->grid.gy; out->grid[2] = ctx->grid.gz;
+    out->key_bits = ctx->key_bits;
+    out->device_bytes = ctx->device_bytes;
+    return SPH_OK;
+}
+
+int sph_get_kernel_stat(sph_ctx* ctx, int32_t index, sph_kernel_stat* out) {
+    if (!ctx || !out) return SPH_ERR_INVALID;
+    if (!ctx->pending.empty()) resolve_pending(ctx);
+    if (index < 0 || index >= (int32_t)ctx->kstats.size()) return SPH_ERR_INVALID;
+    const KStat& k = ctx->kstats[index];
+    std::memset(out, 0, sizeof *out);
+    std::snprintf(out->name, sizeof out->name, "%s", k.name.c_str());
+    out->launches = k.launches;
+    out->total_ms = k.total_ms;
+    out->bytes_per_launch = k.bytes;
+    return SPH_OK;
+}
+
+int sph_reset_kernel_stats(sph_ctx* ctx) {
+    if (!ctx) return SPH_ERR_INVALID;
+    if (!ctx->pending.empty()) resolve_pending(ctx);
+    for (auto& k : ctx->kstats) { k.launches = 0; k.total_ms = 0.0; }
+    return SPH_OK;
+}
+
+int sph_read_sorted_ids(sph_ctx* ctx, int32_t* ids, int32_t count) {
+    if (!ctx || (!ids && count > 0)) return SPH_ERR_INVALID;
+    if (count < ctx->n) return fail(ctx, SPH_ERR_INVALID, "count %d < active particles %d", count, ctx->n);
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->n > 0) HIPCHK(hipMemcpyAsync(ids, ctx->id, (size_t)ctx->n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SPH_OK;
+}
+
+int sph_read_cell_start(sph_ctx* ctx, uint32_t* cs, int32_t count) {
+    if (!ctx || (!cs && count > 0)) return SPH_ERR_INVALID;
+    if ((uint32_t)count < ctx->grid.ncells + 1)
+        return fail(ctx, SPH_ERR_INVALID, "count %d < ncells+1 = %u", count, ctx->grid.ncells + 1);
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemcpyAsync(cs, ctx->cs, (size_t)(ctx->grid.ncells + 1) * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SPH_OK;
+}
+
+int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int32_t key_bits, uint32_t* perm_out,
+                         uint32_t* sorted_keys_out) {
+    if (!ctx || count < 0 || (count > 0 && !keys) || key_bits < 1 || key_bits > 32) return SPH_ERR_INVALID;
+    if (count == 0) return SPH_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    uint32_t *ka = nullptr, *kb = nullptr, *va = nullptr, *vb = nullptr, *hist = nullptr, *bt = nullptr;
+    const size_t nb = (size_t)count * 4;
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = hipMalloc(&ka, nb);
+    if (e == hipSuccess) e = hipMalloc(&kb, nb);
+    if (e == hipSuccess) e = hipMalloc(&va, nb);
+    if (e == hipSuccess) e = hipMalloc(&vb, nb);
+    if (e == hipSuccess) e = hipMalloc(&hist, radix_hist_elems(count) * 4);
+    if (e == hipSuccess) e = hipMalloc(&bt, 256 * 4);
+    int side = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(ka, keys, nb, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) {
+        side = radix_sort(ka, va, kb, vb, count, key_bits, true, hist, bt, ctx->stream);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess && perm_out) e = hipMemcpyAsync(perm_out, side ? vb : va, nb, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && sorted_keys_out)
+        e = hipMemcpyAsync(sorted_keys_out, side ? kb : ka, nb, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ka); (void)hipFree(kb); (void)hipFree(va); (void)hipFree(vb); (void)hipFree(hist); (void)hipFree(bt);
+    if (e != hipSuccess) return fail(ctx, SPH_ERR_HIP, "debug radix sort: %s", hipGetErrorString(e));
+    return SPH_OK;
+}
+
+int sph_resize(sph_ctx* ctx, int32_t capacity) {
+    if (!ctx || capacity < 0) return SPH_ERR_INVALID;
+    if (capacity < ctx->n) return fail(ctx, SPH_ERR_CAPACITY, "capacity %d < active particles %d", capacity, ctx->n);
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    // keep the active particles: download in index order, reallocate, upload
+    const int32_t n = ctx->n;
+    std::vector<unsigned char> host((size_t)n * 84);
+    int r = n > 0 ? sph_download_particles_aos84(ctx, host.data(), n) : SPH_OK;
+    if (r != SPH_OK) return r;
+    free_all(ctx);
+    ctx->capacity = capacity;
+    r = alloc_particles(ctx, capacity);
+    if (r != SPH_OK) return r;
+    if (ctx->params_set) {
+        r = derive(ctx);
+        if (r != SPH_OK) return r;
+    }
+    if (n > 0) {
+        r = sph_upload_particles_aos84(ctx, host.data(), n);
+        if (r != SPH_OK) return r;
+    }
+    return SPH_OK;
+}
+
+int sph_set_slab(sph_ctx* ctx, const sph_slab* slab) {
+    (void)slab;
+    if (!ctx) return SPH_ERR_INVALID;
+    return fail(ctx, SPH_ERR_STATE, "slab decomposition is driven by the host (see sph_test_amd.slab)");
+}
+
+}  // extern "C"

@@ -1,0 +1,103 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol the header
+declares, the struct layouts agree with the header, and the pure entry points work."""
+import ctypes as C
+import re
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "sphhip.h"
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(sph_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_every_declared_symbol_is_exported(pkg):
+    L = pkg.lib()
+    names = declared_functions()
+    assert len(names) >= 30
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    from sph_test_amd import _abi
+    assert set(names) == set(_abi.SIGNATURES), "ctypes signatures out of sync with the header"
+
+
+def test_struct_layouts_match_header(tmp_path, pkg):
+    """Compile a probe against include/sphhip.h with gcc and compare sizeof/offsetof."""
+    from sph_test_amd import _abi as A
+    src = tmp_path / "probe.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "sphhip.h"
+int main(void){
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(sph_config), sizeof(sph_params), sizeof(sph_scenario),
+         sizeof(sph_drag_input), sizeof(sph_stats), sizeof(sph_kernel_stat), sizeof(sph_slab),
+         offsetof(sph_params, forcing_freq));
+  return 0; }
+''')
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    want = [C.sizeof(A.SphConfig), C.sizeof(A.SphParams), C.sizeof(A.SphScenario), C.sizeof(A.SphDragInput),
+            C.sizeof(A.SphStats), C.sizeof(A.SphKernelStat), 20, A.SphParams.forcing_freq.offset]
+    assert got == want
+    assert C.sizeof(A.SphDragInput) == 20          # DragInput, ParticleSystemController.cs:377
+    assert A.PARTICLE84.itemsize == 84             # Particle, ParticleSystemController.cs:375
+
+
+def test_particle84_field_offsets(pkg):
+    """Field order of SimulateParticles.compute:23-40 / InstancedParticles.shader:27-44."""
+    d = pkg.PARTICLE84
+    offs = {name: d.fields[name][1] for name in d.names}
+    assert offs == {"position": 0, "radius": 12, "velocity": 16, "mass": 28, "angularVelocity": 32,
+                    "momentOfInertia": 44, "drag": 48, "repulsionStrength": 52, "genomeFlags": 56,
+                    "orientConstraintStr": 60, "rotation": 64, "modeIndex": 80}
+
+
+def test_scenario_params_pure(pkg):
+    sc = pkg.config_scenario("C3")
+    p, dt = pkg.scenario_params(sc)
+    H = 128 * 0.01
+    c0 = 10 * np.sqrt(2 * 9.81 * H)
+    assert p.c0 == pytest.approx(c0, rel=1e-6)
+    assert p.h == pytest.approx(0.012, rel=1e-6)
+    assert dt == pytest.approx(0.25 * 0.012 / c0, rel=1e-6)
+    assert list(p.box) == pytest.approx([2.56, 2.56, 1.28])
+    s4 = pkg.config_scenario("C4")
+    p4, _ = pkg.scenario_params(s4)
+    L, Hs = 2.56, 0.64
+    f1 = np.sqrt(9.81 * np.pi / L * np.tanh(np.pi * Hs / L)) / (2 * np.pi)
+    assert p4.forcing_freq == pytest.approx(f1, rel=1e-5)
+    assert p4.forcing_amp == pytest.approx(0.981, rel=1e-6)
+
+
+def test_scenario_params_rejects_bad_input(pkg):
+    from sph_test_amd import _abi as A
+    sc = pkg.make_scenario(0, 4, 1, 1, 1, 1, 1, 1)
+    with pytest.raises(A.SphError):
+        pkg.scenario_params(sc)
+
+
+def test_create_without_gpu_fails_loudly(pkg):
+    """No GPU in this container: sph_create must fail with an error, never fall back to CPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from sph_test_amd import _abi as A
+    with pytest.raises(A.SphError) as e:
+        pkg.Context(A.SPH_MODEL_WCSPH, 3, 16)
+    assert e.value.status in (A.SPH_ERR_HIP, A.SPH_ERR_INVALID)
+
+
+def test_null_arguments_rejected(pkg):
+    L = pkg.lib()
+    assert L.sph_step(None, 0.01, 1) == -1
+    assert L.sph_create(None, 0, None) == -1
+    assert L.sph_last_error(None) == b"null context"

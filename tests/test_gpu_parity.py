@@ -1,0 +1,247 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle on the same inputs.
+
+Tolerances (SPEC_SPH.md §1-2):
+  * integer / index work (cell keys, radix-sort permutation, cell_start, sorted ids): bit-exact;
+  * Model S after 1 step: ρ rtol 2e-5; x atol 1e-6 (·1 m); v atol 1e-4·c0·dt·max(1,|a|dt) —
+    differences come from fp contraction and v_sqrt/v_rcp rounding, not the summation order,
+    which is the same §0 order on both sides;
+  * Model R after 1 step: v, ω rtol 1e-4 (+atol), x rtol 1e-5; int torque sums exact except
+    when a per-pair float lies within an ulp of an integer boundary (counted and bounded).
+"""
+import numpy as np
+import pytest
+
+from conftest import oracle_sph_params
+
+pytestmark = pytest.mark.gpu
+
+
+# ------------------------------------------------------------------ sort / grid
+@pytest.mark.parametrize("n,bits", [(1, 8), (2047, 8), (2048, 15), (2049, 16), (100_000, 20),
+                                    (1_048_576, 20), (333_333, 24), (65_536, 32)])
+def test_radix_sort_bit_exact(pkg, n, bits):
+    rng = np.random.default_rng(n + bits)
+    keys = rng.integers(0, 2 ** bits, n, dtype=np.uint64).astype(np.uint32)
+    with pkg.Context(pkg.SPH_MODEL_WCSPH, 3, 16) as ctx:
+        perm, sk = ctx.radix_sort(keys, bits)
+    ref = np.argsort(keys, kind="stable")
+    assert np.array_equal(perm, ref)
+    assert np.array_equal(sk, keys[ref])
+
+
+def test_radix_sort_nearly_sorted_and_ties(pkg):
+    """The step's real input: the previous step's order with a few keys changed."""
+    rng = np.random.default_rng(3)
+    keys = np.sort(rng.integers(0, 600_000, 500_000)).astype(np.uint32)
+    flip = rng.integers(0, len(keys), 5000)
+    keys[flip] += rng.integers(-3, 4, len(flip)).astype(np.int64).clip(0).astype(np.uint32)
+    keys[:1000] = 7                              # long run of ties
+    with pkg.Context(pkg.SPH_MODEL_WCSPH, 3, 16) as ctx:
+        perm, _ = ctx.radix_sort(keys, 20)
+    assert np.array_equal(perm, np.argsort(keys, kind="stable"))
+
+
+# ------------------------------------------------------------------ Model S
+def _sim_and_oracle(pkg, oracle, name_or_sc):
+    sc = pkg.config_scenario(name_or_sc) if isinstance(name_or_sc, str) else name_or_sc
+    sim = pkg.SPHSim(sc)
+    op = oracle_sph_params(oracle, sim.params, sc.dim)
+    return sim, op
+
+
+def test_lattice_init_bit_exact(pkg, oracle):
+    sim, _ = _sim_and_oracle(pkg, oracle, "C1")
+    x = sim.positions()
+    ref = oracle.lattice(2, 64, 64, 1, 0.01, seed=1234)
+    assert np.array_equal(x, ref)
+    sim.close()
+    sc = pkg.make_scenario(0, 3, 9, 7, 5, 32, 32, 32, seed=77)
+    sim = pkg.SPHSim(sc)
+    assert np.array_equal(sim.positions(), oracle.lattice(3, 9, 7, 5, 0.01, seed=77))
+    sim.close()
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_wcsph_one_step(pkg, oracle, cfg):
+    sim, op = _sim_and_oracle(pkg, oracle, cfg)
+    x0 = sim.positions()
+    n = len(x0)
+    sim.step(1)
+    xg, vg, rg = sim.positions(), sim.velocities(), sim.density()
+    ids_g = sim.ctx.sorted_ids()
+    cs_g = sim.ctx.cell_start()
+    xo, vo, io, ro, _, cso = oracle.sph_step(op, x0, np.zeros_like(x0), np.arange(n, dtype=np.int32), sim.dt, 0.0)
+    # integer work: identical sort permutation and cell table
+    assert np.array_equal(ids_g, io)
+    assert np.array_equal(cs_g, cso)
+    order = np.argsort(io)
+    np.testing.assert_allclose(rg, ro[order], rtol=2e-5, atol=0)
+    np.testing.assert_allclose(xg, xo[order], rtol=0, atol=1e-6)
+    vscale = float(sim.params.c0) * sim.dt * 10
+    np.testing.assert_allclose(vg, vo[order], rtol=1e-3, atol=1e-4 * vscale)
+    sim.close()
+
+
+def test_wcsph_ten_steps_c1(pkg, oracle):
+    sim, op = _sim_and_oracle(pkg, oracle, "C1")
+    x = sim.positions()
+    n = len(x)
+    v = np.zeros_like(x)
+    ids = np.arange(n, dtype=np.int32)
+    for s in range(10):
+        x, v, ids, rho, _, _ = oracle.sph_step(op, x, v, ids, sim.dt, np.float32(s * sim.dt))
+    sim.step(10)
+    order = np.argsort(ids)
+    np.testing.assert_allclose(sim.positions(), x[order], rtol=0, atol=2e-6)
+    np.testing.assert_allclose(sim.density(), rho[order], rtol=2e-4)
+    sim.close()
+
+
+def test_wcsph_sloshing_forcing(pkg, oracle):
+    """C4-shaped (scaled down) sloshing: the lateral forcing term f_ext(t)."""
+    sc = pkg.make_scenario(1, 3, 32, 8, 16, 32, 16, 16)
+    sim, op = _sim_and_oracle(pkg, oracle, sc)
+    assert sim.params.forcing_amp > 0
+    x = sim.positions()
+    v = np.zeros_like(x)
+    ids = np.arange(len(x), dtype=np.int32)
+    for s in range(3):
+        x, v, ids, _, _, _ = oracle.sph_step(op, x, v, ids, sim.dt, np.float32(s * sim.dt))
+    sim.step(3)
+    order = np.argsort(ids)
+    np.testing.assert_allclose(sim.velocities(), v[order], rtol=1e-3, atol=1e-3)
+    sim.close()
+
+
+def test_wcsph_c3_invariants(pkg):
+    """Full C3 size (1,048,576): size-independent properties over 20 steps."""
+    sim = pkg.SPHSim.from_config("C3")
+    n = sim.n
+    assert n == 1_048_576
+    sim.step(20)
+    x, v, rho = sim.positions(), sim.velocities(), sim.density()
+    box = np.array(sim.params.box)
+    assert np.isfinite(x).all() and np.isfinite(v).all() and np.isfinite(rho).all()
+    assert (x >= 0).all() and (x <= box).all()
+    ids = sim.ctx.sorted_ids()
+    assert np.array_equal(np.sort(ids), np.arange(n))        # a permutation: no particle lost
+    cs = sim.ctx.cell_start()
+    assert cs[0] == 0 and cs[-1] == n and np.all(np.diff(cs.astype(np.int64)) >= 0)
+    assert 500 < np.median(rho) < 1100
+    sim.close()
+
+
+def test_wcsph_upload_state_and_empty(pkg, oracle):
+    sc = pkg.config_scenario("C1")
+    p, dt = pkg.scenario_params(sc)
+    with pkg.Context(pkg.SPH_MODEL_WCSPH, 2, 100) as ctx:
+        ctx.set_params(p)
+        ctx.upload_state(np.zeros((0, 3), np.float32))
+        ctx.step(dt, 3)                                 # empty: a no-op, not an error
+        x = np.array([[0.3, 0.3, 0.0]], np.float32)
+        ctx.upload_state(x, np.zeros_like(x))
+        ctx.step(dt, 1)
+        assert ctx.positions()[0][1] == pytest.approx(0.3 - 9.81 * dt * dt, rel=1e-6)
+        from sph_test_amd import _abi as A
+        with pytest.raises(A.SphError) as e:
+            ctx.upload_state(np.zeros((101, 3), np.float32))
+        assert e.value.status == A.SPH_ERR_CAPACITY
+
+
+# ------------------------------------------------------------------ Model R
+def random_sphere(PARTICLE84, n, seed=1234, R=15.0):
+    """SURVEY §8c fixture recipe: positions in a sphere, radii U[1.5,2], v,ω ~ N(0,1), q = identity."""
+    rng = np.random.default_rng(seed)
+    p = np.zeros(n, PARTICLE84)
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    p["position"] = d * (R * rng.random((n, 1)) ** (1 / 3))
+    p["radius"] = rng.uniform(1.5, 2.0, n)
+    p["velocity"] = rng.normal(size=(n, 3))
+    p["mass"] = 0.1 * 4.0 / 3.0 * 3.1415926 * p["radius"] ** 3
+    p["angularVelocity"] = rng.normal(size=(n, 3))
+    p["momentOfInertia"] = 0.4 * p["mass"] * p["radius"] ** 2
+    p["drag"] = rng.uniform(0.5, 1.0, n)
+    p["repulsionStrength"] = 1.0
+    p["rotation"] = (0, 0, 0, 1)
+    p["modeIndex"] = -1
+    return p
+
+
+def test_aos84_round_trip_bit_exact(pkg):
+    parts = random_sphere(pkg.PARTICLE84, 1000)
+    parts["genomeFlags"] = np.arange(1000)
+    parts["modeIndex"] = np.arange(1000) % 7
+    with pkg.Context(pkg.SPH_MODEL_CONTACT, 3, 1000) as ctx:
+        ctx.upload_aos84(parts)
+        back = ctx.download_aos84()
+    assert back.tobytes() == parts.tobytes()
+
+
+@pytest.mark.parametrize("n", [64, 4096, 32768])
+def test_contact_one_step(pkg, oracle, n):
+    parts = random_sphere(pkg.PARTICLE84, n)
+    dt = 0.01
+    ctl = pkg.ParticleSystemController(particleCount=n)
+    ctl.Start(parts)
+    ctl.Update(dt)
+    got = ctl.GetParticles()
+    tq = ctl.context.torque_int()
+    ref, tq_ref = oracle.contact_step(oracle.contact_params(dt), parts.view(oracle.PARTICLE84))
+    # integer reaction torque: exact except at ulp-boundary truncations
+    diff = np.abs(tq.astype(np.int64) - tq_ref)
+    assert (diff > 0).mean() < 1e-3 and diff.max() <= 4
+    for f, rtol, atol in [("velocity", 1e-4, 1e-4), ("angularVelocity", 1e-4, 1e-3), ("position", 1e-5, 1e-5),
+                          ("rotation", 1e-4, 1e-5)]:
+        np.testing.assert_allclose(got[f], ref[f], rtol=rtol, atol=atol, err_msg=f)
+    for f in ["radius", "mass", "momentOfInertia", "drag", "repulsionStrength", "modeIndex"]:
+        assert np.array_equal(got[f], parts[f]), f
+    ctl.OnDestroy()
+
+
+def test_contact_drag_and_inactive(pkg, oracle):
+    n = 2000
+    parts = random_sphere(pkg.PARTICLE84, n, seed=5)
+    act = 1500
+    ctl = pkg.ParticleSystemController(particleCount=n)
+    ctl.Start(parts)
+    ctl.activeParticleCount = act
+    ctl.drag.selectedID = 17
+    ctl.drag.targetPosition = (3.0, -2.0, 1.0)
+    ctl.drag.strength = 100.0
+    ctl.Update(0.01)
+    got = ctl.GetParticles()
+    cp = oracle.contact_params(0.01, drag_id=17, drag_target=(3.0, -2.0, 1.0), drag_strength=100.0)
+    ref, _ = oracle.contact_step(cp, parts[:act].view(oracle.PARTICLE84))
+    np.testing.assert_allclose(got["velocity"][:act], ref["velocity"], rtol=1e-4, atol=1e-4)
+    assert got[act:].tobytes() == parts[act:].tobytes()     # inactive particles untouched
+    ctl.OnDestroy()
+
+
+def test_contact_long_run_invariants(pkg):
+    n = 10000
+    parts = random_sphere(pkg.PARTICLE84, n, seed=9)
+    ctl = pkg.ParticleSystemController(particleCount=n)
+    ctl.Start(parts)
+    for _ in range(50):
+        ctl.Update(0.005)
+    got = ctl.GetParticles()
+    assert np.isfinite(got["position"]).all() and np.isfinite(got["angularVelocity"]).all()
+    r = np.linalg.norm(got["position"], axis=1)
+    assert (r <= 15.0 * (1 + 1e-5)).all()
+    qn = np.linalg.norm(got["rotation"], axis=1)
+    assert np.allclose(qn, 1.0, atol=1e-5)
+    ctl.OnDestroy()
+
+
+def test_contact_resize_keeps_state(pkg):
+    n = 300
+    parts = random_sphere(pkg.PARTICLE84, n, seed=11)
+    ctl = pkg.ParticleSystemController(particleCount=n)
+    ctl.Start(parts)
+    ctl.Update(0.01)
+    before = ctl.GetParticles()
+    ctl.ResizeParticleBuffers(1000)
+    assert ctl.GetParticles().tobytes() == before.tobytes()
+    ctl.Update(0.01)
+    ctl.OnDestroy()
