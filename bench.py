@@ -70,7 +70,7 @@ def cpu_baseline(config: str, budget_s: float):
     p, dt = pkg.scenario_params(sc)
     op = O.sph_params(sc.dim, p.dx, p.h, p.rho0, p.c0, p.alpha, p.xsph_eps, tuple(p.gravity), tuple(p.box),
                       p.wall_restitution, p.forcing_amp, p.forcing_freq)
-    x = O.lattice(sc.dim, sc.nx, sc.ny, sc.nz, sc.dx, seed=sc.seed, jitter=sc.jitter * sc.dx)
+    x = O.lattice(sc.dim, sc.nx, sc.ny, sc.nz, sc.dx, seed=sc.seed, jitter_frac=sc.jitter)
     v = np.zeros_like(x)
     ids = np.arange(len(x), dtype=np.int32)
     try:

@@ -118,9 +118,9 @@ def sph_step(p: OrSphParams, pos, vel, ids, dt, t=0.0, nthreads=0):
     return pos, vel, ids, rho, prho, cs
 
 
-def lattice(dim, nx, ny, nz, dx, origin=(0.0, 0.0, 0.0), seed=1234, jitter=None):
-    if jitter is None:
-        jitter = 0.01 * dx
+def lattice(dim, nx, ny, nz, dx, origin=(0.0, 0.0, 0.0), seed=1234, jitter_frac=0.01):
+    """Dam-break lattice; jitter amplitude = jitter_frac·dx as ONE fp32 product (as the library)."""
+    jitter = float(np.float32(jitter_frac) * np.float32(dx))
     n = nx * ny * (nz if dim == 3 else 1)
     out = np.empty((n, 3), np.float32)
     lib().or_sph_lattice(dim, nx, ny, nz, dx, origin[0], origin[1], origin[2], seed, jitter, _ptr(out))

@@ -96,6 +96,13 @@ void launch_force_integrate(const float4* pos, const float4* vel, const float2* 
                             float fext_x, float4* pos_o, float4* vel_o, uint32_t* keys_o,
                             hipStream_t s);
 
+// Model S, LDS-tiled (wcsph_tiled.hip)
+void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t n, GridDesc g, SphConst c,
+                          float2* rp, hipStream_t s);
+void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs,
+                        int32_t n, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o,
+                        float4* vel_o, uint32_t* keys_o, hipStream_t s);
+
 // Model R (contact.hip)
 void launch_contact_step(const float4* pos, const float4* vel, const float4* omg, const float4* rot,
                          const float4* aux, const int32_t* id, const uint32_t* cs, int32_t n_active,

@@ -165,7 +165,7 @@ __device__ __forceinline__ float lattice_jitter(uint32_t seed_mix, uint32_t id, 
                                                 float jitter) {
     const uint32_t u = mix32(seed_mix ^ (3u * id + axis));
     const float r = (float)(u >> 8) * (1.0f / 16777216.0f);
-    return __fmul_rn(2.0f * r - 1.0f, jitter);   // no contraction into the caller's add
+    return (2.0f * r - 1.0f) * jitter;
 }
 
 __global__ __launch_bounds__(BLK) void k_lattice(int32_t dim, int32_t nx, int32_t ny, int32_t n,
@@ -173,14 +173,14 @@ __global__ __launch_bounds__(BLK) void k_lattice(int32_t dim, int32_t nx, int32_
                                                  uint32_t seed_mix, float jitter,
                                                  float4* __restrict__ pos, float4* __restrict__ vel,
                                                  int32_t* __restrict__ id) {
+#pragma clang fp contract(off)   // the oracle's roundings: one fma, one multiply, one add
     const int32_t p = blockIdx.x * BLK + threadIdx.x;
     if (p >= n) return;
     const int32_t ix = p % nx, iy = (p / nx) % ny, iz = p / (nx * ny);
     const uint32_t u = (uint32_t)p;
-    // same roundings as oracle/sph_oracle.c: one fma, one multiply, one add
-    const float x = __fadd_rn(fmaf((float)ix + 0.5f, dx, x0), lattice_jitter(seed_mix, u, 0, jitter));
-    const float y = __fadd_rn(fmaf((float)iy + 0.5f, dx, y0), lattice_jitter(seed_mix, u, 1, jitter));
-    const float z = dim == 3 ? __fadd_rn(fmaf((float)iz + 0.5f, dx, z0), lattice_jitter(seed_mix, u, 2, jitter)) : 0.0f;
+    const float x = fmaf((float)ix + 0.5f, dx, x0) + lattice_jitter(seed_mix, u, 0, jitter);
+    const float y = fmaf((float)iy + 0.5f, dx, y0) + lattice_jitter(seed_mix, u, 1, jitter);
+    const float z = dim == 3 ? fmaf((float)iz + 0.5f, dx, z0) + lattice_jitter(seed_mix, u, 2, jitter) : 0.0f;
     pos[p] = make_float4(x, y, z, 0.f);
     vel[p] = make_float4(0.f, 0.f, 0.f, 0.f);
     id[p] = p;

@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -72,6 +73,7 @@ struct sph_ctx {
     std::vector<Pending> pending;
     std::vector<hipEvent_t> ev_pool;
     int64_t device_bytes = 0;
+    int nb_variant = 1;          // neighbour passes: 0 direct (L1/L2 gathers), 1 LDS-tiled
 };
 
 namespace {
@@ -323,14 +325,21 @@ int step_wcsph(sph_ctx* ctx, float dt) {
     if (r != SPH_OK) return r;
     {
         KTimer t(ctx, "density", 24.0 * n);
-        launch_density(ctx->pos, ctx->cs, n, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
+        if (ctx->nb_variant == 0)
+            launch_density(ctx->pos, ctx->cs, n, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
+        else
+            launch_density_tiled(ctx->pos, ctx->cs, n, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
     }
     const sph_params& p = ctx->prm;
     const float tt = (float)ctx->sim_time;
     const float fext = p.forcing_amp != 0.0f ? p.forcing_amp * sinf(6.28318530718f * p.forcing_freq * tt) : 0.0f;
     {
         KTimer t(ctx, "force_integrate", 76.0 * n);
-        launch_force_integrate(ctx->pos, ctx->vel, ctx->rp, ctx->cs, n, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
+        if (ctx->nb_variant == 0)
+            launch_force_integrate(ctx->pos, ctx->vel, ctx->rp, ctx->cs, n, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
+                                   ctx->vel2, ctx->keys, ctx->stream);
+        else
+            launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, n, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
                                ctx->vel2, ctx->keys, ctx->stream);
     }
     swap_sv(ctx);
@@ -402,6 +411,7 @@ int sph_create(const sph_config* cfg, int32_t device, sph_ctx** out) {
     ctx->cfg = *cfg;
     ctx->device = device;
     ctx->profiling = (cfg->flags & SPH_FLAG_PROFILE) != 0;
+    if (const char* v = std::getenv("SPH_NB_VARIANT")) ctx->nb_variant = std::atoi(v);
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return SPH_ERR_HIP;

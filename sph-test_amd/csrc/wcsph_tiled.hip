@@ -1,0 +1,258 @@
+// wcsph_tiled.hip — LDS-tiled Model S neighbour passes (SPEC_SPH.md §2), gfx950.
+//
+// A workgroup owns 256 consecutive cell-sorted targets. Their keys span [kf, kl]. For each of
+// the 9 (dx,dy) row offsets `off`, the block's candidates are the ONE contiguous sorted
+// interval of keys [kf+off-1, kl+off+1], and every target's own row range lies inside it
+// (SPEC_SPH.md §0). The interval is staged into LDS with coalesced loads (chunks of TT_CH),
+// and every target walks its own sub-range out of LDS. Lanes of one cell read the same LDS
+// address (broadcast). The visit order is the §0 order.
+//
+// Scan: 4 candidates per iteration, branchless (clamped LDS reads, predicated
+// accumulation), so four ds_reads are in flight per lane instead of one.
+// Force pass: only ~16% of candidates are within 2h. Running the ~50-op pair body under a
+// divergent mask would cost every candidate the full body. So the scan appends hits (u16
+// LDS index) to a per-lane LDS list (unconditional store, predicated increment), and a
+// wave-uniform flush runs the body over the lists with nearly full lanes.
+// A block whose targets span many sparse rows gets huge intervals. If an interval exceeds
+// TT_FALLBACK candidates, that offset is gathered directly from global memory instead.
+#include "common.h"
+
+namespace sph {
+
+constexpr int TT_BLK = 256;        // targets per workgroup
+constexpr int TT_CH = 512;         // candidates per LDS chunk
+constexpr int TT_CAP = 32;         // per-lane hit list (force)
+constexpr int TT_FALLBACK = 4 * TT_CH;
+
+struct BlockRows {
+    int64_t kf, kl;           // key range of the block's targets
+    int32_t cx, cy, z0, z1;   // this lane's cell (x, y) and z window
+};
+
+__device__ __forceinline__ BlockRows block_rows(const GridDesc& g, const float4* __restrict__ pos, int32_t i0,
+                                                int32_t ilast, float4 pi) {
+    BlockRows b;
+    const float4 pf = pos[i0], pl = pos[ilast];
+    b.kf = cell_key(g, pf.x, pf.y, pf.z);
+    b.kl = cell_key(g, pl.x, pl.y, pl.z);
+    b.cx = cell_coord(pi.x, g.ox, g.inv_cell, g.gx);
+    b.cy = cell_coord(pi.y, g.oy, g.inv_cell, g.gy);
+    const int32_t cz = cell_coord(pi.z, g.oz, g.inv_cell, g.gz);
+    b.z0 = cz > 0 ? cz - 1 : 0;
+    b.z1 = cz < g.gz - 1 ? cz + 1 : g.gz - 1;
+    return b;
+}
+
+// Interval of row offset k for the block ([c0,c1) sorted indices) and this lane's row [r0,r1).
+__device__ __forceinline__ void offset_ranges(const GridDesc& g, const uint32_t* __restrict__ cs,
+                                              const BlockRows& b, bool valid, int k, int32_t& c0, int32_t& c1,
+                                              int32_t& r0, int32_t& r1) {
+    const int32_t dxk = k / 3 - 1, dyk = k % 3 - 1;
+    const int64_t off = ((int64_t)dxk * g.gy + dyk) * g.gz;
+    int64_t ka = b.kf + off - 1, kb = b.kl + off + 1;
+    const int64_t last = (int64_t)g.ncells - 1;
+    if (kb < 0 || ka > last) {
+        c0 = c1 = 0;
+    } else {
+        ka = ka < 0 ? 0 : ka;
+        kb = kb > last ? last : kb;
+        c0 = (int32_t)cs[ka];
+        c1 = (int32_t)cs[kb + 1];
+    }
+    const int32_t xx = b.cx + dxk, yy = b.cy + dyk;
+    r0 = r1 = 0;
+    if (valid && xx >= 0 && xx < g.gx && yy >= 0 && yy < g.gy) {
+        const uint32_t rowk = ((uint32_t)xx * (uint32_t)g.gy + (uint32_t)yy) * (uint32_t)g.gz;
+        r0 = (int32_t)cs[rowk + (uint32_t)b.z0];
+        r1 = (int32_t)cs[rowk + (uint32_t)b.z1 + 1u];
+    }
+}
+
+__device__ __forceinline__ float dist2(float4 a, float4 b) {
+    const float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
+    return dx * dx + dy * dy + dz * dz;
+}
+
+// Unnormalised cubic spline w(q) (W = σ·w) for r² < 4h², else 0; branchless.
+__device__ __forceinline__ float spline_w(const SphConst& c, float r2) {
+    const float q = __builtin_amdgcn_sqrtf(r2) * c.inv_h;
+    const float t = 2.0f - q;
+    const float w = q < 1.0f ? 1.0f + q * q * (-1.5f + 0.75f * q) : 0.25f * t * t * t;
+    return r2 < c.four_h2 ? w : 0.0f;
+}
+
+__global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restrict__ pos,
+                                                          const uint32_t* __restrict__ cs, int32_t n,
+                                                          GridDesc g, SphConst c, float2* __restrict__ rp) {
+    __shared__ float4 sp[TT_CH + 4];
+    const int tid = threadIdx.x;
+    const int32_t i0 = blockIdx.x * TT_BLK;
+    const int32_t i = i0 + tid;
+    const bool valid = i < n;
+    const int32_t ilast = min(i0 + TT_BLK, n) - 1;
+    const float4 pi = pos[valid ? i : ilast];
+    const BlockRows b = block_rows(g, pos, i0, ilast, pi);
+    float s = 0.0f;
+#pragma unroll 1
+    for (int k = 0; k < 9; ++k) {
+        int32_t c0, c1, r0, r1;
+        offset_ranges(g, cs, b, valid, k, c0, c1, r0, r1);
+        if (c1 - c0 > TT_FALLBACK) {           // sparse block: gather this row directly
+            for (int32_t j = r0; j < r1; ++j) s += spline_w(c, dist2(pi, pos[j]));
+            continue;
+        }
+#pragma unroll 1
+        for (int32_t base = c0; base < c1; base += TT_CH) {
+            const int32_t len = min(TT_CH, c1 - base);
+            __syncthreads();
+            for (int t = tid; t < len; t += TT_BLK) sp[t] = pos[base + t];
+            __syncthreads();
+            const int32_t lo = max(r0, base) - base;
+            const int32_t ln = max(min(r1, base + len) - base - lo, 0);
+            int32_t t = 0;
+            for (; t + 4 <= ln; t += 4) {
+                const float4 a = sp[lo + t], bb = sp[lo + t + 1], cc = sp[lo + t + 2], d = sp[lo + t + 3];
+                s += spline_w(c, dist2(pi, a));
+                s += spline_w(c, dist2(pi, bb));
+                s += spline_w(c, dist2(pi, cc));
+                s += spline_w(c, dist2(pi, d));
+            }
+            for (; t < ln; ++t) s += spline_w(c, dist2(pi, sp[lo + t]));
+        }
+    }
+    if (!valid) return;
+    const float d = c.mass * (c.sigma * s);
+    const float tr = d * c.inv_rho0;
+    const float t2 = tr * tr, t4 = t2 * t2;
+    const float P = c.B * (t4 * t2 * tr - 1.0f);
+    rp[i] = make_float2(d, P / (d * d));
+}
+
+struct ForceAcc {
+    float ax, ay, az, sx, sy, sz;
+};
+
+// Pair body (SPEC_SPH.md §2). pj = (x, y, z, ρ_j), vj = (u, v, w, P_j/ρ_j²). Branchless.
+__device__ __forceinline__ void pair_force(const SphConst& c, float4 pi, float4 vi, float rhoi, float prhoi,
+                                           float4 pj, float4 vj, ForceAcc& a) {
+    const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+    const float r2 = dx * dx + dy * dy + dz * dz;
+    const float r = __builtin_amdgcn_sqrtf(r2);
+    const float q = r * c.inv_h;
+    const float t = 2.0f - q;
+    const bool inner = q < 1.0f;
+    const float W = c.sigma * (inner ? 1.0f + q * q * (-1.5f + 0.75f * q) : 0.25f * t * t * t);
+    const float F = inner ? c.sigma_h2 * (-3.0f + 2.25f * q) : -c.sigma_h * 0.75f * t * t * __builtin_amdgcn_rcpf(r);
+    const float du = vi.x - vj.x, dv = vi.y - vj.y, dw = vi.z - vj.z;
+    const float vr = du * dx + dv * dy + dw * dz;
+    const float inv_rbar = __builtin_amdgcn_rcpf(0.5f * (rhoi + pj.w));
+    const float mu = c.h * vr * __builtin_amdgcn_rcpf(r2 + c.eta2);
+    const float pij = vr < 0.0f ? -c.ac0 * mu * inv_rbar : 0.0f;
+    const float cf = -c.mass * (prhoi + vj.w + pij) * F;
+    a.ax += cf * dx; a.ay += cf * dy; a.az += cf * dz;
+    const float cx = c.eps * c.mass * inv_rbar * W;
+    a.sx -= cx * du; a.sy -= cx * dv; a.sz -= cx * dw;
+}
+
+__global__ __launch_bounds__(TT_BLK) void k_force_tiled(
+    const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
+    const uint32_t* __restrict__ cs, int32_t n, GridDesc g, SphConst c, float dt, float fext_x,
+    float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o) {
+    __shared__ float4 sp[TT_CH + 4];     // (x, y, z, ρ)
+    __shared__ float4 sv[TT_CH + 4];     // (u, v, w, P/ρ²)
+    __shared__ uint16_t lst[TT_CAP][TT_BLK];
+    const int tid = threadIdx.x;
+    const int32_t i0 = blockIdx.x * TT_BLK;
+    const int32_t i = i0 + tid;
+    const bool valid = i < n;
+    const int32_t ilast = min(i0 + TT_BLK, n) - 1;
+    const int32_t ii = valid ? i : ilast;
+    const float4 pi = pos[ii], vi = vel[ii];
+    const float2 ri = rp[ii];
+    const BlockRows b = block_rows(g, pos, i0, ilast, pi);
+    ForceAcc acc{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int cnt = 0;
+    auto flush = [&]() {
+        for (int q = 0; __any(q < cnt); ++q) {
+            if (q < cnt) {
+                const int lj = lst[q][tid];
+                pair_force(c, pi, vi, ri.x, ri.y, sp[lj], sv[lj], acc);
+            }
+        }
+        cnt = 0;
+    };
+#pragma unroll 1
+    for (int k = 0; k < 9; ++k) {
+        int32_t c0, c1, r0, r1;
+        offset_ranges(g, cs, b, valid, k, c0, c1, r0, r1);
+        if (c1 - c0 > TT_FALLBACK) {           // sparse block: gather this row directly
+            for (int32_t j = r0; j < r1; ++j) {
+                const float4 pj = pos[j];
+                if (j != i && dist2(pi, pj) < c.four_h2) {
+                    const float4 vj = vel[j];
+                    const float2 rj = rp[j];
+                    pair_force(c, pi, vi, ri.x, ri.y, make_float4(pj.x, pj.y, pj.z, rj.x),
+                               make_float4(vj.x, vj.y, vj.z, rj.y), acc);
+                }
+            }
+            continue;
+        }
+#pragma unroll 1
+        for (int32_t base = c0; base < c1; base += TT_CH) {
+            const int32_t len = min(TT_CH, c1 - base);
+            __syncthreads();
+            for (int t = tid; t < len; t += TT_BLK) {
+                const float4 p = pos[base + t], v = vel[base + t];
+                const float2 r = rp[base + t];
+                sp[t] = make_float4(p.x, p.y, p.z, r.x);
+                sv[t] = make_float4(v.x, v.y, v.z, r.y);
+            }
+            __syncthreads();
+            const int32_t lo = max(r0, base) - base;
+            const int32_t ln = max(min(r1, base + len) - base - lo, 0);
+            const int32_t self = i - base - lo;     // self's position in my sub-range
+            for (int t = 0; __any(t < ln); t += 4) {
+                // four candidates per iteration; reads past ln hit the padded tail (masked)
+                const int32_t j = min(lo + t, TT_CH);   // lanes past their range stay in the array
+                const float4 a = sp[j], bb = sp[j + 1], cc = sp[j + 2], d = sp[j + 3];
+                const bool h0 = t < ln && t != self && dist2(pi, a) < c.four_h2;
+                const bool h1 = t + 1 < ln && t + 1 != self && dist2(pi, bb) < c.four_h2;
+                const bool h2 = t + 2 < ln && t + 2 != self && dist2(pi, cc) < c.four_h2;
+                const bool h3 = t + 3 < ln && t + 3 != self && dist2(pi, d) < c.four_h2;
+                lst[cnt][tid] = (uint16_t)j;       cnt += h0;
+                lst[cnt][tid] = (uint16_t)(j + 1); cnt += h1;
+                lst[cnt][tid] = (uint16_t)(j + 2); cnt += h2;
+                lst[cnt][tid] = (uint16_t)(j + 3); cnt += h3;
+                if (__any(cnt > TT_CAP - 4)) flush();
+            }
+            flush();
+        }
+    }
+    if (!valid) return;
+    float nv[3] = {vi.x + (acc.ax + c.gx + fext_x) * dt, vi.y + (acc.ay + c.gy) * dt, vi.z + (acc.az + c.gz) * dt};
+    float np[3] = {pi.x + (nv[0] + acc.sx) * dt, pi.y + (nv[1] + acc.sy) * dt, pi.z + (nv[2] + acc.sz) * dt};
+    const float L[3] = {c.Lx, c.Ly, c.Lz};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (np[a] < 0.0f) { np[a] = 0.0f; if (nv[a] < 0.0f) nv[a] = -c.wall_e * nv[a]; }
+        if (np[a] > L[a]) { np[a] = L[a]; if (nv[a] > 0.0f) nv[a] = -c.wall_e * nv[a]; }
+    }
+    pos_o[i] = make_float4(np[0], np[1], np[2], 0.f);
+    vel_o[i] = make_float4(nv[0], nv[1], nv[2], 0.f);
+    keys_o[i] = cell_key(g, np[0], np[1], np[2]);
+}
+
+void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t n, GridDesc g, SphConst c, float2* rp,
+                          hipStream_t s) {
+    if (n > 0) k_density_tiled<<<(n + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, cs, n, g, c, rp);
+}
+
+void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t n,
+                        GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o,
+                        uint32_t* keys_o, hipStream_t s) {
+    if (n > 0)
+        k_force_tiled<<<(n + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, vel, rp, cs, n, g, c, dt, fext_x, pos_o,
+                                                                   vel_o, keys_o);
+}
+
+}  // namespace sph
