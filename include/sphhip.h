@@ -168,14 +168,35 @@ int sph_read_torque_int(sph_ctx* ctx, int32_t* xyz, int32_t count);  /* Model R,
 int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int32_t key_bits,
                          uint32_t* perm_out, uint32_t* sorted_keys_out);
 
-/* ---- slab decomposition (multi-GPU; SPEC_SPH.md §3). One context per rank; the host moves
- *      the packed buffers between ranks (RCCL over xGMI from bench.py / torch.distributed). ---- */
+/* ---- slab decomposition (multi-GPU; SPEC_SPH.md §3). New capability: the reference is one
+ *      GPU. One context per rank owns global cell columns [cx_lo, cx_hi)
+ *      plus one halo column per side. The HOST moves the packed device buffers between ranks
+ *      (RCCL over xGMI: sph_test_amd.slab / bench.py). Per step:
+ *        count_sends → pack_send(0/1) → [exchange] → assemble → ranges → density →
+ *        pack_rho(0/1) → [exchange] → force(interior) ∥ [rho in flight] → unpack_rho → force(boundary)
+ *        → finish_step.
+ *      Particle records are 32 bytes: (x, y, z, id-bits, u, v, w, 0). ---- */
 typedef struct sph_slab {
-    int32_t cx_lo, cx_hi;       /* owned cell columns [cx_lo, cx_hi) of the global grid */
-    int32_t rank, nranks;
-    int32_t ghost_capacity;     /* per side, particles */
+    int32_t cx_lo, cx_hi;       /* owned columns of the global grid; neighbours exist iff
+                                   cx_lo > 0 / cx_hi < columns */
 } sph_slab;
-int sph_set_slab(sph_ctx* ctx, const sph_slab* slab);
+#define SPH_SLAB_RECORD_BYTES 32
+/* ranges[]: ghost-left [0,1), owned [2,3), ghost-right [4,5), boundary column cx_lo [6,7),
+ * boundary column cx_hi-1 [8,9), all as sorted-slot index ranges [begin, end). */
+int sph_slab_set(sph_ctx* ctx, const sph_slab* slab);
+int sph_slab_init_scenario(sph_ctx* ctx, const sph_scenario* sc);
+int sph_slab_count_sends(sph_ctx* ctx, int32_t counts[2]);
+int sph_slab_pack_send(sph_ctx* ctx, int32_t side, void* dev_records, int32_t capacity);
+int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t n_left, const void* dev_right,
+                      int32_t n_right);
+int sph_slab_ranges(sph_ctx* ctx, int32_t ranges[10]);
+int sph_slab_density(sph_ctx* ctx);
+int sph_slab_pack_rho(sph_ctx* ctx, int32_t side, void* dev_rho_prho, int32_t capacity);
+int sph_slab_unpack_rho(sph_ctx* ctx, int32_t side, const void* dev_rho_prho, int32_t count);
+int sph_slab_force(sph_ctx* ctx, float dt, int32_t part);   /* 0 all, 1 interior, 2 boundary */
+int sph_slab_finish_step(sph_ctx* ctx, float dt);
+/* owned particles as 8-float records (x, y, z, u, v, w, id-bits, ρ); count >= owned */
+int sph_slab_read_owned(sph_ctx* ctx, float* records, int32_t count, int32_t* n_owned);
 
 #ifdef __cplusplus
 }

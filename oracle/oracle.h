@@ -53,6 +53,13 @@ void or_sph_derive(or_sph_params* p);
 int or_sph_step(const or_sph_params* p, int n, float* pos3, float* vel3, int32_t* id,
                 float dt, float t, float* rho, float* prho, uint32_t* cell_start,
                 int nthreads);
+/* Phases of or_sph_step over sorted arrays (sk = sorted keys, cs = cell start), used by the
+ * slab-decomposition tests: targets [i0, i1); neighbours may be any sorted slot (ghosts). */
+void or_sph_density_range(const or_sph_params* p, const float* pos3, const uint32_t* sk, const uint32_t* cs,
+                          int i0, int i1, float* rho, float* prho, int nthreads);
+void or_sph_force_range(const or_sph_params* p, const float* pos3, const float* vel3, const float* rho,
+                        const float* prho, const uint32_t* sk, const uint32_t* cs, int i0, int i1, float dt,
+                        float t, float* pos_out, float* vel_out, int nthreads);
 /* Dam-break lattice init (SPEC_SPH.md; the same integer hash as the device init). */
 void or_sph_lattice(int dim, int nx, int ny, int nz, float dx, float x0, float y0, float z0,
                     uint32_t seed, float jitter, float* pos3);

@@ -80,6 +80,11 @@ def lib():
         L.or_stable_sort.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p]
         L.or_cell_start.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p]
         L.or_keys.argtypes = [P(OrGrid), C.c_int, C.c_void_p, C.c_void_p]
+        L.or_sph_density_range.argtypes = [P(OrSphParams), C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                           C.c_void_p, C.c_void_p, C.c_int]
+        L.or_sph_force_range.argtypes = [P(OrSphParams), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_float,
+                                         C.c_void_p, C.c_void_p, C.c_int]
         _lib = L
     return _lib
 
@@ -116,6 +121,17 @@ def sph_step(p: OrSphParams, pos, vel, ids, dt, t=0.0, nthreads=0):
     lib().or_sph_step(C.byref(p), n, _ptr(pos), _ptr(vel), _ptr(ids), dt, t, _ptr(rho), _ptr(prho),
                       _ptr(cs), nthreads)
     return pos, vel, ids, rho, prho, cs
+
+
+def density_range(p: OrSphParams, pos, sk, cs, i0, i1, rho, prho, nthreads=0):
+    """Pass 1 for sorted targets [i0, i1) (in place into rho/prho)."""
+    lib().or_sph_density_range(C.byref(p), _ptr(pos), _ptr(sk), _ptr(cs), i0, i1, _ptr(rho), _ptr(prho), nthreads)
+
+
+def force_range(p: OrSphParams, pos, vel, rho, prho, sk, cs, i0, i1, dt, t, pos_out, vel_out, nthreads=0):
+    """Pass 2 + integrate for sorted targets [i0, i1) (in place into pos_out/vel_out)."""
+    lib().or_sph_force_range(C.byref(p), _ptr(pos), _ptr(vel), _ptr(rho), _ptr(prho), _ptr(sk), _ptr(cs), i0, i1,
+                             dt, t, _ptr(pos_out), _ptr(vel_out), nthreads)
 
 
 def lattice(dim, nx, ny, nz, dx, origin=(0.0, 0.0, 0.0), seed=1234, jitter_frac=0.01):

@@ -133,40 +133,18 @@ static int neighbour_rows(const or_grid* g, const uint32_t* cs, uint32_t key, ui
     return nr;
 }
 
-int or_sph_step(const or_sph_params* p, int n, float* pos, float* vel, int32_t* id,
-                float dt, float t, float* rho_out, float* prho_out, uint32_t* cs_out, int nthreads) {
+/* pass 1 over sorted targets [i0, i1): density + Tait EOS (SPEC_SPH.md §2) */
+void or_sph_density_range(const or_sph_params* p, const float* p2, const uint32_t* sk, const uint32_t* cs,
+                          int i0, int i1, float* rho, float* prho, int nthreads) {
     const or_grid* g = &p->grid;
-    uint32_t nk = (uint32_t)g->G[0] * (uint32_t)g->G[1] * (uint32_t)g->G[2];
-    uint32_t* keys = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));
-    uint32_t* perm = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));
-    uint32_t* sk = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));
-    uint32_t* cs = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)nk + 1));
-    float* p2 = (float*)malloc(sizeof(float) * 3 * (size_t)(n > 0 ? n : 1));
-    float* v2 = (float*)malloc(sizeof(float) * 3 * (size_t)(n > 0 ? n : 1));
-    int32_t* id2 = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
-    float* rho = (float*)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
-    float* prho = (float*)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
+    const float m = p->mass, four_h2 = p->four_h2, inv_rho0 = 1.0f / p->rho0;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #else
     (void)nthreads;
 #endif
-    /* hash + stable sort + reorder + cell start */
-    or_keys(g, n, pos, keys);
-    or_stable_sort(n, keys, nk, perm);
-    for (int i = 0; i < n; ++i) {
-        uint32_t s = perm[i];
-        sk[i] = keys[s];
-        memcpy(p2 + 3 * (size_t)i, pos + 3 * (size_t)s, 12);
-        memcpy(v2 + 3 * (size_t)i, vel + 3 * (size_t)s, 12);
-        id2[i] = id[s];
-    }
-    or_cell_start(n, sk, nk, cs);
-
-    const float m = p->mass, four_h2 = p->four_h2, inv_rho0 = 1.0f / p->rho0;
-    /* pass 1: density + Tait EOS */
 #pragma omp parallel for schedule(dynamic, 1024)
-    for (int i = 0; i < n; ++i) {
+    for (int i = i0; i < i1; ++i) {
         uint32_t rg[9][2];
         int nr = neighbour_rows(g, cs, sk[i], rg);
         float xi = p2[3 * i], yi = p2[3 * i + 1], zi = p2[3 * i + 2];
@@ -188,11 +166,24 @@ int or_sph_step(const or_sph_params* p, int n, float* pos, float* vel, int32_t* 
         rho[i] = d;
         prho[i] = P / (d * d);
     }
-    /* pass 2: pressure force + artificial viscosity + XSPH + leapfrog kick-drift + walls */
+}
+
+/* pass 2 over sorted targets [i0, i1): pressure + viscosity + XSPH + kick-drift + walls.
+ * Reads p2/v2/rho/prho (all sorted slots, ghosts included), writes pos_out/vel_out[i]. */
+void or_sph_force_range(const or_sph_params* p, const float* p2, const float* v2, const float* rho,
+                        const float* prho, const uint32_t* sk, const uint32_t* cs, int i0, int i1, float dt,
+                        float t, float* pos_out, float* vel_out, int nthreads) {
+    const or_grid* g = &p->grid;
+    const float m = p->mass, four_h2 = p->four_h2;
     const float h = p->h, eta2 = 0.01f * h * h, ac0 = p->alpha * p->c0, eps = p->eps_xsph;
     const float fx = p->f_amp != 0.0f ? p->f_amp * sinf(6.28318530718f * p->f_freq * t) : 0.0f;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+    (void)nthreads;
+#endif
 #pragma omp parallel for schedule(dynamic, 1024)
-    for (int i = 0; i < n; ++i) {
+    for (int i = i0; i < i1; ++i) {
         uint32_t rg[9][2];
         int nr = neighbour_rows(g, cs, sk[i], rg);
         float xi = p2[3 * i], yi = p2[3 * i + 1], zi = p2[3 * i + 2];
@@ -223,20 +214,45 @@ int or_sph_step(const or_sph_params* p, int n, float* pos, float* vel, int32_t* 
         float nu = ui + (ax + p->g[0] + fx) * dt;
         float nv = vi + (ay + p->g[1]) * dt;
         float nw = wi + (az + p->g[2]) * dt;
-        float nxp = xi + (nu + sx) * dt;
-        float nyp = yi + (nv + sy) * dt;
-        float nzp = zi + (nw + sz) * dt;
-        float npos[3] = {nxp, nyp, nzp}, nvel[3] = {nu, nv, nw};
-        int na = p->dim;
-        for (int a = 0; a < na; ++a) {
+        float npos[3] = {xi + (nu + sx) * dt, yi + (nv + sy) * dt, zi + (nw + sz) * dt};
+        float nvel[3] = {nu, nv, nw};
+        for (int a = 0; a < p->dim; ++a) {
             if (npos[a] < 0.0f) { npos[a] = 0.0f; if (nvel[a] < 0.0f) nvel[a] = -p->wall_e * nvel[a]; }
             if (npos[a] > p->L[a]) { npos[a] = p->L[a]; if (nvel[a] > 0.0f) nvel[a] = -p->wall_e * nvel[a]; }
         }
         if (p->dim == 2) { npos[2] = 0.0f; nvel[2] = 0.0f; }
-        /* write into the outgoing arrays at sorted slot i */
-        pos[3 * (size_t)i] = npos[0]; pos[3 * (size_t)i + 1] = npos[1]; pos[3 * (size_t)i + 2] = npos[2];
-        vel[3 * (size_t)i] = nvel[0]; vel[3 * (size_t)i + 1] = nvel[1]; vel[3 * (size_t)i + 2] = nvel[2];
+        pos_out[3 * (size_t)i] = npos[0]; pos_out[3 * (size_t)i + 1] = npos[1]; pos_out[3 * (size_t)i + 2] = npos[2];
+        vel_out[3 * (size_t)i] = nvel[0]; vel_out[3 * (size_t)i + 1] = nvel[1]; vel_out[3 * (size_t)i + 2] = nvel[2];
     }
+}
+
+int or_sph_step(const or_sph_params* p, int n, float* pos, float* vel, int32_t* id,
+                float dt, float t, float* rho_out, float* prho_out, uint32_t* cs_out, int nthreads) {
+    const or_grid* g = &p->grid;
+    uint32_t nk = (uint32_t)g->G[0] * (uint32_t)g->G[1] * (uint32_t)g->G[2];
+    size_t nn = (size_t)(n > 0 ? n : 1);
+    uint32_t* keys = (uint32_t*)malloc(sizeof(uint32_t) * nn);
+    uint32_t* perm = (uint32_t*)malloc(sizeof(uint32_t) * nn);
+    uint32_t* sk = (uint32_t*)malloc(sizeof(uint32_t) * nn);
+    uint32_t* cs = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)nk + 1));
+    float* p2 = (float*)malloc(sizeof(float) * 3 * nn);
+    float* v2 = (float*)malloc(sizeof(float) * 3 * nn);
+    int32_t* id2 = (int32_t*)malloc(sizeof(int32_t) * nn);
+    float* rho = (float*)malloc(sizeof(float) * nn);
+    float* prho = (float*)malloc(sizeof(float) * nn);
+    /* hash + stable sort + reorder + cell start */
+    or_keys(g, n, pos, keys);
+    or_stable_sort(n, keys, nk, perm);
+    for (int i = 0; i < n; ++i) {
+        uint32_t s = perm[i];
+        sk[i] = keys[s];
+        memcpy(p2 + 3 * (size_t)i, pos + 3 * (size_t)s, 12);
+        memcpy(v2 + 3 * (size_t)i, vel + 3 * (size_t)s, 12);
+        id2[i] = id[s];
+    }
+    or_cell_start(n, sk, nk, cs);
+    or_sph_density_range(p, p2, sk, cs, 0, n, rho, prho, nthreads);
+    or_sph_force_range(p, p2, v2, rho, prho, sk, cs, 0, n, dt, t, pos, vel, nthreads);
     memcpy(id, id2, sizeof(int32_t) * (size_t)n);
     if (rho_out) memcpy(rho_out, rho, sizeof(float) * (size_t)n);
     if (prho_out) memcpy(prho_out, prho, sizeof(float) * (size_t)n);

@@ -83,6 +83,12 @@ class SphKernelStat(C.Structure):
                 ("bytes_per_launch", C.c_double)]
 
 
+class SphSlab(C.Structure):
+    _fields_ = [("cx_lo", C.c_int32), ("cx_hi", C.c_int32)]
+
+
+SPH_SLAB_RECORD_BYTES = 32
+
 assert C.sizeof(SphDragInput) == 20
 assert C.sizeof(SphConfig) == 16
 
@@ -120,7 +126,18 @@ SIGNATURES = {
     "sph_read_cell_start": ([_P, _P, _I], C.c_int),
     "sph_read_torque_int": ([_P, _P, _I], C.c_int),
     "sph_debug_radix_sort": ([_P, _P, _I, _I, _P, _P], C.c_int),
-    "sph_set_slab": ([_P, _P], C.c_int),
+    "sph_slab_set": ([_P, C.POINTER(SphSlab)], C.c_int),
+    "sph_slab_init_scenario": ([_P, C.POINTER(SphScenario)], C.c_int),
+    "sph_slab_count_sends": ([_P, C.POINTER(C.c_int32)], C.c_int),
+    "sph_slab_pack_send": ([_P, _I, _P, _I], C.c_int),
+    "sph_slab_assemble": ([_P, _P, _I, _P, _I], C.c_int),
+    "sph_slab_ranges": ([_P, C.POINTER(C.c_int32)], C.c_int),
+    "sph_slab_density": ([_P], C.c_int),
+    "sph_slab_pack_rho": ([_P, _I, _P, _I], C.c_int),
+    "sph_slab_unpack_rho": ([_P, _I, _P, _I], C.c_int),
+    "sph_slab_force": ([_P, C.c_float, _I], C.c_int),
+    "sph_slab_finish_step": ([_P, C.c_float], C.c_int),
+    "sph_slab_read_owned": ([_P, _P, _I, C.POINTER(C.c_int32)], C.c_int),
 }
 
 
@@ -137,6 +154,14 @@ def lib() -> C.CDLL:
     """Load libsphhip.so from the package directory. Raises if it is missing (no fallback)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same SONAME as
+        # ROCm's) and whichever loads first serves both. Load torch's first when torch is
+        # installed, so torch streams/RCCL and this library share one runtime and stream
+        # handles are valid across them.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         path = Path(os.environ.get("SPHHIP_LIB", str(LIB_PATH)))
         if not path.exists():
             raise RuntimeError(f"libsphhip.so not built at {path}: run __graft_entry__.build()")

@@ -8,11 +8,16 @@
 namespace sph {
 
 // Uniform grid (SPEC_SPH.md §0). key = (cx*gy + cy)*gz + cz, x slowest.
+// A context may hold an x-window [cx0, cx0+gx) of a global grid of gx_all columns (slab
+// decomposition, SPEC_SPH.md §3). The column is computed globally then shifted, so all
+// ranks agree bit for bit on which column a particle is in.
 struct GridDesc {
     float ox, oy, oz;
     float inv_cell;
     int32_t gx, gy, gz;
     uint32_t ncells;     // gx*gy*gz (keys == ncells mark inactive particles)
+    int32_t cx0;         // first global column held (0 without decomposition)
+    int32_t gx_all;      // global column count (== gx without decomposition)
 };
 
 // Model S constants (SPEC_SPH.md §2), derived on the host from sph_params.
@@ -41,8 +46,14 @@ __device__ __forceinline__ int32_t cell_coord(float x, float o, float inv, int32
     return (int32_t)g;
 }
 
+// local x column of a position (global column - cx0, clamped to the held window)
+__device__ __forceinline__ int32_t cell_cx(const GridDesc& g, float x) {
+    const int32_t c = cell_coord(x, g.ox, g.inv_cell, g.gx_all) - g.cx0;
+    return c < 0 ? 0 : (c >= g.gx ? g.gx - 1 : c);
+}
+
 __device__ __forceinline__ uint32_t cell_key(const GridDesc& g, float x, float y, float z) {
-    int32_t cx = cell_coord(x, g.ox, g.inv_cell, g.gx);
+    int32_t cx = cell_cx(g, x);
     int32_t cy = cell_coord(y, g.oy, g.inv_cell, g.gy);
     int32_t cz = cell_coord(z, g.oz, g.inv_cell, g.gz);
     return ((uint32_t)cx * (uint32_t)g.gy + (uint32_t)cy) * (uint32_t)g.gz + (uint32_t)cz;
@@ -88,20 +99,42 @@ void launch_lattice(int32_t dim, int32_t nx, int32_t ny, int32_t nz, float dx, f
                     hipStream_t s);
 void launch_iota(uint32_t* v, int32_t n, hipStream_t s);
 
-// Model S (wcsph.hip)
-void launch_density(const float4* pos, const uint32_t* cs, int32_t n, GridDesc g, SphConst c,
-                    float2* rp, hipStream_t s);
+// Model S (wcsph.hip): targets are the sorted slots [ib, ie)
+void launch_density(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g,
+                    SphConst c, float2* rp, hipStream_t s);
 void launch_force_integrate(const float4* pos, const float4* vel, const float2* rp,
-                            const uint32_t* cs, int32_t n, GridDesc g, SphConst c, float dt,
-                            float fext_x, float4* pos_o, float4* vel_o, uint32_t* keys_o,
+                            const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
+                            float dt, float fext_x, float4* pos_o, float4* vel_o, uint32_t* keys_o,
                             hipStream_t s);
 
 // Model S, LDS-tiled (wcsph_tiled.hip)
-void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t n, GridDesc g, SphConst c,
-                          float2* rp, hipStream_t s);
+void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g,
+                          SphConst c, float2* rp, hipStream_t s);
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs,
-                        int32_t n, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o,
-                        float4* vel_o, uint32_t* keys_o, hipStream_t s);
+                        int32_t ib, int32_t ie, GridDesc g, SphConst c, float dt, float fext_x,
+                        float4* pos_o, float4* vel_o, uint32_t* keys_o, hipStream_t s);
+
+// slab decomposition (slab.hip)
+// Order-preserving compaction of the sorted slots [b, e) whose key column satisfies
+// col <= col_le (side 0) / col >= col_ge (side 1) into 32-byte records (x,y,z,id | u,v,w,0).
+int32_t slab_compact_blocks(int32_t b, int32_t e);
+void launch_slab_count(const uint32_t* keys, int32_t b, int32_t e, uint32_t gyz, int32_t col_le,
+                       int32_t col_ge, uint32_t* blk /*[2][nblk]*/, uint32_t* totals /*[2]*/,
+                       hipStream_t s);
+void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
+                      int32_t b, int32_t e, uint32_t gyz, int32_t side, int32_t col_le, int32_t col_ge,
+                      const uint32_t* blk, float4* out, hipStream_t s);
+void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, int32_t* id,
+                        hipStream_t s);
+void launch_pick(const uint32_t* cs, const int32_t* idx, int32_t m, uint32_t* out, hipStream_t s);
+// owned slots [o0, o0+n) -> records of 8 floats (x,y,z,u,v,w,id-bits,ρ)
+void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, const float2* rp,
+                       int32_t o0, int32_t n, float* out, hipStream_t s);
+// keep the particles of global columns [lo, hi) (order-preserving) — slab init
+void launch_slab_select_columns(const float4* pos, const float4* vel, const int32_t* id, int32_t n,
+                                GridDesc gglobal, int32_t lo, int32_t hi, uint32_t* blk,
+                                uint32_t* total, float4* pos_o, float4* vel_o, int32_t* id_o,
+                                hipStream_t s);
 
 // Model R (contact.hip)
 void launch_contact_step(const float4* pos, const float4* vel, const float4* omg, const float4* rot,

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step(
     f3 totalForce = mk(0, 0, 0), totalTorque = mk(0, 0, 0);
     uint32_t tq0 = 0, tq1 = 0, tq2 = 0;   // wrapping int32 sums (InterlockedAdd)
 
-    const int32_t cx = cell_coord(pa.x, g.ox, g.inv_cell, g.gx);
+    const int32_t cx = cell_cx(g, pa.x);
     const int32_t cy = cell_coord(pa.y, g.oy, g.inv_cell, g.gy);
     const int32_t cz = cell_coord(pa.z, g.oz, g.inv_cell, g.gz);
     const int32_t z0 = cz > 0 ? cz - 1 : 0, z1 = cz < g.gz - 1 ? cz + 1 : g.gz - 1;

@@ -1,0 +1,220 @@
+// slab.hip — device side of the x-slab decomposition (SPEC_SPH.md §3), gfx950.
+//
+// The reference is single-GPU. Here a rank owns global cell columns
+// [cx_lo, cx_hi) and holds one halo column on each side. Keys are x-slowest, so every column
+// is a contiguous run of sorted slots. Send lists are filtered runs, and the order of those
+// runs is load-bearing: both ranks must sort a shared column into the same order.
+// So every compaction here is ORDER-PRESERVING: per-block counts, one exclusive scan, then
+// a scatter whose in-block ranks come from wave64 ballots + mbcnt and per-wave prefixes in
+// LDS. No atomics, no dependence on block scheduling.
+#include "common.h"
+
+namespace sph {
+
+constexpr int SL_BLK = 256;
+constexpr int SL_WAVES = SL_BLK / 64;
+
+int32_t slab_compact_blocks(int32_t b, int32_t e) { return e > b ? (e - b + SL_BLK - 1) / SL_BLK : 1; }
+
+__device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {   // set lanes below this lane
+    return (uint32_t)__popcll(mask & ((1ull << lane_id()) - 1ull));
+}
+
+// Block-wide count of a predicate -> per-wave counts in LDS; returns the block total.
+__device__ __forceinline__ uint32_t block_ballot_count(bool pred, uint32_t* wcnt, uint32_t& wave_base) {
+    const int w = threadIdx.x >> 6;
+    const uint64_t m = __ballot(pred);
+    if ((threadIdx.x & 63) == 0) wcnt[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < SL_WAVES; ++k) {
+        base += k < w ? wcnt[k] : 0u;
+        tot += wcnt[k];
+    }
+    wave_base = base;
+    return tot;
+}
+
+__global__ __launch_bounds__(SL_BLK) void k_slab_count(const uint32_t* __restrict__ keys, int32_t b, int32_t e,
+                                                       uint32_t gyz, int32_t col_le, int32_t col_ge,
+                                                       uint32_t* __restrict__ blk, int32_t nblk) {
+    __shared__ uint32_t wl[SL_WAVES], wr[SL_WAVES];
+    const int32_t i = b + blockIdx.x * SL_BLK + threadIdx.x;
+    const bool in = i < e;
+    const int32_t col = in ? (int32_t)(keys[i] / gyz) : 0;
+    uint32_t bl, br;
+    const uint32_t tl = block_ballot_count(in && col <= col_le, wl, bl);
+    const uint32_t tr = block_ballot_count(in && col >= col_ge, wr, br);
+    if (threadIdx.x == 0) {
+        blk[blockIdx.x] = tl;
+        blk[nblk + blockIdx.x] = tr;
+    }
+}
+
+// one workgroup: exclusive scan of both count rows in place, totals[2]
+__global__ __launch_bounds__(SL_BLK) void k_slab_scan(uint32_t* __restrict__ blk, int32_t nblk,
+                                                      uint32_t* __restrict__ totals) {
+    __shared__ uint32_t ws[SL_WAVES];
+    for (int side = 0; side < 2; ++side) {
+        uint32_t* row = blk + side * nblk;
+        uint32_t carry = 0;
+        for (int32_t base = 0; base < nblk; base += SL_BLK) {
+            const int32_t i = base + threadIdx.x;
+            const uint32_t v = i < nblk ? row[i] : 0u;
+            uint32_t inc = v;
+            const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(inc, o, 64);
+                if (lane >= o) inc += t;
+            }
+            if (lane == 63) ws[w] = inc;
+            __syncthreads();
+            uint32_t pre = 0, tot = 0;
+#pragma unroll
+            for (int k = 0; k < SL_WAVES; ++k) {
+                pre += k < w ? ws[k] : 0u;
+                tot += ws[k];
+            }
+            __syncthreads();
+            if (i < nblk) row[i] = carry + pre + inc - v;
+            carry += tot;
+        }
+        if (threadIdx.x == 0) totals[side] = carry;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(SL_BLK) void k_slab_pack(const uint32_t* __restrict__ keys,
+                                                      const float4* __restrict__ pos,
+                                                      const float4* __restrict__ vel,
+                                                      const int32_t* __restrict__ id, int32_t b, int32_t e,
+                                                      uint32_t gyz, int32_t side, int32_t col_le, int32_t col_ge,
+                                                      const uint32_t* __restrict__ blk, int32_t nblk,
+                                                      float4* __restrict__ out) {
+    __shared__ uint32_t wc[SL_WAVES];
+    const int32_t i = b + blockIdx.x * SL_BLK + threadIdx.x;
+    const bool in = i < e;
+    const int32_t col = in ? (int32_t)(keys[i] / gyz) : 0;
+    const bool pred = in && (side == 0 ? col <= col_le : col >= col_ge);
+    uint32_t wave_base;
+    block_ballot_count(pred, wc, wave_base);
+    if (!pred) return;
+    const uint32_t r = blk[side * nblk + blockIdx.x] + wave_base + lane_prefix(__ballot(pred));
+    const float4 p = pos[i], v = vel[i];
+    out[2 * (size_t)r] = make_float4(p.x, p.y, p.z, __int_as_float(id[i]));
+    out[2 * (size_t)r + 1] = make_float4(v.x, v.y, v.z, 0.f);
+}
+
+__global__ __launch_bounds__(SL_BLK) void k_slab_unpack(const float4* __restrict__ rec, int32_t n,
+                                                        float4* __restrict__ pos, float4* __restrict__ vel,
+                                                        int32_t* __restrict__ id) {
+    const int32_t i = blockIdx.x * SL_BLK + threadIdx.x;
+    if (i >= n) return;
+    const float4 a = rec[2 * (size_t)i], v = rec[2 * (size_t)i + 1];
+    pos[i] = make_float4(a.x, a.y, a.z, 0.f);
+    vel[i] = make_float4(v.x, v.y, v.z, 0.f);
+    id[i] = __float_as_int(a.w);
+}
+
+// ---- init-time selection of owned columns (global grid in `g`)
+__global__ __launch_bounds__(SL_BLK) void k_sel_count(const float4* __restrict__ pos, int32_t n, GridDesc g,
+                                                      int32_t lo, int32_t hi, uint32_t* __restrict__ blk) {
+    __shared__ uint32_t wc[SL_WAVES];
+    const int32_t i = blockIdx.x * SL_BLK + threadIdx.x;
+    bool pred = false;
+    if (i < n) {
+        const int32_t c = cell_cx(g, pos[i].x);
+        pred = c >= lo && c < hi;
+    }
+    uint32_t wb;
+    const uint32_t t = block_ballot_count(pred, wc, wb);
+    if (threadIdx.x == 0) blk[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(SL_BLK) void k_sel_scatter(const float4* __restrict__ pos,
+                                                        const float4* __restrict__ vel,
+                                                        const int32_t* __restrict__ id, int32_t n, GridDesc g,
+                                                        int32_t lo, int32_t hi, const uint32_t* __restrict__ blk,
+                                                        float4* __restrict__ pos_o, float4* __restrict__ vel_o,
+                                                        int32_t* __restrict__ id_o) {
+    __shared__ uint32_t wc[SL_WAVES];
+    const int32_t i = blockIdx.x * SL_BLK + threadIdx.x;
+    bool pred = false;
+    if (i < n) {
+        const int32_t c = cell_cx(g, pos[i].x);
+        pred = c >= lo && c < hi;
+    }
+    uint32_t wb;
+    block_ballot_count(pred, wc, wb);
+    if (!pred) return;
+    const uint32_t r = blk[blockIdx.x] + wb + lane_prefix(__ballot(pred));
+    pos_o[r] = pos[i];
+    vel_o[r] = vel[i];
+    id_o[r] = id[i];
+}
+
+struct Pick10 {
+    int32_t idx[10];
+};
+
+__global__ void k_pick(const uint32_t* __restrict__ cs, Pick10 p, int32_t m, uint32_t* __restrict__ out) {
+    const int t = threadIdx.x;
+    if (t < m) out[t] = cs[p.idx[t]];
+}
+
+__global__ __launch_bounds__(SL_BLK) void k_pack_owned(const float4* __restrict__ pos, const float4* __restrict__ vel,
+                                                       const int32_t* __restrict__ id,
+                                                       const float2* __restrict__ rp, int32_t o0, int32_t n,
+                                                       float* __restrict__ out) {
+    const int32_t i = blockIdx.x * SL_BLK + threadIdx.x;
+    if (i >= n) return;
+    const float4 p = pos[o0 + i], v = vel[o0 + i];
+    float* q = out + 8 * (size_t)i;
+    q[0] = p.x; q[1] = p.y; q[2] = p.z; q[3] = v.x; q[4] = v.y; q[5] = v.z;
+    q[6] = __int_as_float(id[o0 + i]);
+    q[7] = rp ? rp[o0 + i].x : 0.f;
+}
+
+void launch_pick(const uint32_t* cs, const int32_t* idx, int32_t m, uint32_t* out, hipStream_t s) {
+    Pick10 p{};
+    for (int k = 0; k < m && k < 10; ++k) p.idx[k] = idx[k];
+    k_pick<<<1, 64, 0, s>>>(cs, p, m, out);
+}
+
+void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, const float2* rp, int32_t o0,
+                       int32_t n, float* out, hipStream_t s) {
+    if (n > 0) k_pack_owned<<<(n + SL_BLK - 1) / SL_BLK, SL_BLK, 0, s>>>(pos, vel, id, rp, o0, n, out);
+}
+
+void launch_slab_count(const uint32_t* keys, int32_t b, int32_t e, uint32_t gyz, int32_t col_le, int32_t col_ge,
+                       uint32_t* blk, uint32_t* totals, hipStream_t s) {
+    const int32_t nb = slab_compact_blocks(b, e);
+    k_slab_count<<<nb, SL_BLK, 0, s>>>(keys, b, e, gyz, col_le, col_ge, blk, nb);
+    k_slab_scan<<<1, SL_BLK, 0, s>>>(blk, nb, totals);
+}
+
+void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id, int32_t b,
+                      int32_t e, uint32_t gyz, int32_t side, int32_t col_le, int32_t col_ge, const uint32_t* blk,
+                      float4* out, hipStream_t s) {
+    const int32_t nb = slab_compact_blocks(b, e);
+    if (e > b) k_slab_pack<<<nb, SL_BLK, 0, s>>>(keys, pos, vel, id, b, e, gyz, side, col_le, col_ge, blk, nb, out);
+}
+
+void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, int32_t* id, hipStream_t s) {
+    if (n > 0) k_slab_unpack<<<(n + SL_BLK - 1) / SL_BLK, SL_BLK, 0, s>>>(rec, n, pos, vel, id);
+}
+
+void launch_slab_select_columns(const float4* pos, const float4* vel, const int32_t* id, int32_t n, GridDesc g,
+                                int32_t lo, int32_t hi, uint32_t* blk, uint32_t* total, float4* pos_o,
+                                float4* vel_o, int32_t* id_o, hipStream_t s) {
+    const int32_t nb = slab_compact_blocks(0, n);
+    k_sel_count<<<nb, SL_BLK, 0, s>>>(pos, n, g, lo, hi, blk);
+    // reuse the two-row scan: row 1 is a dummy of zeros
+    (void)hipMemsetAsync(blk + nb, 0, sizeof(uint32_t) * nb, s);
+    k_slab_scan<<<1, SL_BLK, 0, s>>>(blk, nb, total);
+    if (n > 0 && pos_o != nullptr) k_sel_scatter<<<nb, SL_BLK, 0, s>>>(pos, vel, id, n, g, lo, hi, blk, pos_o, vel_o, id_o);
+}
+
+}  // namespace sph

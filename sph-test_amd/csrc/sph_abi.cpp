@@ -74,6 +74,16 @@ struct sph_ctx {
     std::vector<hipEvent_t> ev_pool;
     int64_t device_bytes = 0;
     int nb_variant = 1;          // neighbour passes: 0 direct (L1/L2 gathers), 1 LDS-tiled
+    // slab decomposition (SPEC_SPH.md §3)
+    bool slab = false;
+    sph_slab sl{};
+    bool has_left = false, has_right = false;
+    GridDesc gglobal{};
+    int32_t o0 = 0, o1 = 0;      // owned sorted slots
+    int32_t rng[10] = {0};
+    int32_t send_counts[2] = {0, 0};
+    uint32_t* sblk = nullptr;    // compaction block counts [2][nblk]
+    uint32_t* sdev = nullptr;    // small device scratch (totals, picks)
 };
 
 namespace {
@@ -121,6 +131,7 @@ void free_all(sph_ctx* c) {
     dfree(c->rp); dfree(c->torque);
     dfree(c->keys); dfree(c->keys2); dfree(c->vals); dfree(c->vals2); dfree(c->hist); dfree(c->bin_total);
     dfree(c->cs);
+    dfree(c->sblk); dfree(c->sdev);
     if (c->staging) (void)hipFree(c->staging);
     c->staging = nullptr;
     c->staging_bytes = 0;
@@ -144,6 +155,7 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
     AL(id, n); AL(id2, n);
     AL(keys, n); AL(keys2, n); AL(vals, n); AL(vals2, n);
     AL(hist, radix_hist_elems((int32_t)n)); AL(bin_total, 256);
+    AL(sblk, 2 * (size_t)slab_compact_blocks(0, (int32_t)n) + 2); AL(sdev, 16);
     if (is_contact(ctx)) {
         AL(omg, n); AL(rot, n); AL(aux, n); AL(omg2, n); AL(rot2, n); AL(aux2, n);
         AL(mode, n); AL(mode2, n); AL(torque, 3 * n);
@@ -208,6 +220,8 @@ int derive(sph_ctx* ctx) {
         s.Lx = p.box[0]; s.Ly = p.box[1]; s.Lz = ctx->cfg.dim == 3 ? p.box[2] : 0.f;
         s.wall_e = p.wall_restitution;
     }
+    g.cx0 = 0;
+    g.gx_all = g.gx;
     g.ncells = (uint32_t)g.gx * (uint32_t)g.gy * (uint32_t)g.gz;
     ctx->grid = g;
     ctx->key_bits = bit_width(g.ncells);   // the sentinel key == ncells must sort last
@@ -326,9 +340,9 @@ int step_wcsph(sph_ctx* ctx, float dt) {
     {
         KTimer t(ctx, "density", 24.0 * n);
         if (ctx->nb_variant == 0)
-            launch_density(ctx->pos, ctx->cs, n, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
+            launch_density(ctx->pos, ctx->cs, 0, n, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
         else
-            launch_density_tiled(ctx->pos, ctx->cs, n, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
+            launch_density_tiled(ctx->pos, ctx->cs, 0, n, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
     }
     const sph_params& p = ctx->prm;
     const float tt = (float)ctx->sim_time;
@@ -336,10 +350,10 @@ int step_wcsph(sph_ctx* ctx, float dt) {
     {
         KTimer t(ctx, "force_integrate", 76.0 * n);
         if (ctx->nb_variant == 0)
-            launch_force_integrate(ctx->pos, ctx->vel, ctx->rp, ctx->cs, n, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
-                                   ctx->vel2, ctx->keys, ctx->stream);
+            launch_force_integrate(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, n, ctx->grid, ctx->sc, dt, fext,
+                                   ctx->pos2, ctx->vel2, ctx->keys, ctx->stream);
         else
-            launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, n, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
+            launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, n, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
                                ctx->vel2, ctx->keys, ctx->stream);
     }
     swap_sv(ctx);
@@ -389,6 +403,8 @@ int step_contact(sph_ctx* ctx, float dt) {
 }
 
 }  // namespace
+
+static int slab_local_grid(sph_ctx* ctx);
 
 // ====================================================================== ABI
 extern "C" {
@@ -481,6 +497,10 @@ int sph_set_params(sph_ctx* ctx, const sph_params* params) {
     int r = derive(ctx);
     if (r != SPH_OK) { ctx->prm = old; return r; }
     ctx->params_set = true;
+    if (ctx->slab) {                 // keep the slab's window of the (new) global grid
+        ctx->gglobal = ctx->grid;
+        return slab_local_grid(ctx);
+    }
     return SPH_OK;
 }
 
@@ -597,6 +617,7 @@ int sph_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
 
 int sph_step(sph_ctx* ctx, float dt, int32_t nsteps) {
     if (!ctx || nsteps < 0 || !(dt >= 0.f)) return SPH_ERR_INVALID;
+    if (ctx->slab) return fail(ctx, SPH_ERR_STATE, "slab mode: the host drives sph_slab_* phases");
     if (!ctx->params_set) return fail(ctx, SPH_ERR_STATE, "sph_set_params first");
     HIPCHK(hipSetDevice(ctx->device));
     for (int32_t s = 0; s < nsteps; ++s) {
@@ -626,6 +647,7 @@ int sph_set_adhesion(sph_ctx* ctx, const void* conn84, int32_t count) {
 
 static int read_f4(sph_ctx* ctx, const float4* src, float* dst, int32_t count, int comps) {
     if (!ctx || (!dst && count > 0)) return SPH_ERR_INVALID;
+    if (ctx->slab) return fail(ctx, SPH_ERR_STATE, "slab mode: use sph_slab_read_owned");
     if (count < ctx->n) return fail(ctx, SPH_ERR_INVALID, "count %d < active particles %d", count, ctx->n);
     if (!src) return fail(ctx, SPH_ERR_STATE, "field not held by this model");
     HIPCHK(hipSetDevice(ctx->device));
@@ -654,6 +676,7 @@ int sph_read_angular_velocities(sph_ctx* ctx, float* xyz, int32_t count) {
 int sph_read_density(sph_ctx* ctx, float* rho, int32_t count) {
     if (!ctx || (!rho && count > 0)) return SPH_ERR_INVALID;
     if (is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "density is Model S only");
+    if (ctx->slab) return fail(ctx, SPH_ERR_STATE, "slab mode: use sph_slab_read_owned");
     if (count < ctx->n) return fail(ctx, SPH_ERR_INVALID, "count %d < active particles %d", count, ctx->n);
     HIPCHK(hipSetDevice(ctx->device));
     if (ctx->n > 0) {
@@ -792,10 +815,287 @@ int sph_resize(sph_ctx* ctx, int32_t capacity) {
     return SPH_OK;
 }
 
-int sph_set_slab(sph_ctx* ctx, const sph_slab* slab) {
-    (void)slab;
+// ---------------------------------------------------------------- slab decomposition
+static int slab_local_grid(sph_ctx* ctx) {
+    const GridDesc& G = ctx->gglobal;
+    GridDesc g = G;
+    ctx->has_left = ctx->sl.cx_lo > 0;
+    ctx->has_right = ctx->sl.cx_hi < G.gx;
+    g.cx0 = ctx->sl.cx_lo - (ctx->has_left ? 1 : 0);
+    g.gx = ctx->sl.cx_hi + (ctx->has_right ? 1 : 0) - g.cx0;
+    g.gx_all = G.gx;
+    g.ncells = (uint32_t)g.gx * (uint32_t)g.gy * (uint32_t)g.gz;
+    ctx->grid = g;
+    ctx->key_bits = bit_width(g.ncells);
+    ctx->keys_valid = false;
+    return ensure_cells(ctx);
+}
+
+static inline int32_t col_start(const sph_ctx* c, int32_t local_col) {
+    return local_col * c->grid.gy * c->grid.gz;
+}
+
+int sph_slab_set(sph_ctx* ctx, const sph_slab* slab) {
+    if (!ctx || !slab) return SPH_ERR_INVALID;
+    if (is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "slab decomposition is Model S only");
+    if (!ctx->params_set) return fail(ctx, SPH_ERR_STATE, "sph_set_params first");
+    HIPCHK(hipSetDevice(ctx->device));
+    if (!ctx->slab) ctx->gglobal = ctx->grid;
+    const int32_t GX = ctx->gglobal.gx;
+    if (slab->cx_lo < 0 || slab->cx_hi > GX || slab->cx_lo >= slab->cx_hi)
+        return fail(ctx, SPH_ERR_INVALID, "slab [%d,%d) outside 0..%d", slab->cx_lo, slab->cx_hi, GX);
+    ctx->slab = true;
+    ctx->sl = *slab;
+    ctx->n = ctx->o0 = ctx->o1 = 0;
+    return slab_local_grid(ctx);
+}
+
+int sph_slab_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
+    if (!ctx || !sc) return SPH_ERR_INVALID;
+    if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "sph_slab_set first");
+    const int64_t N = (int64_t)sc->nx * sc->ny * (sc->dim == 3 ? sc->nz : 1);
+    if (N <= 0 || N > 0x7fffffff) return fail(ctx, SPH_ERR_INVALID, "bad scenario size");
+    HIPCHK(hipSetDevice(ctx->device));
+    float4 *gp = nullptr, *gv = nullptr;
+    int32_t* gi = nullptr;
+    uint32_t* blk = nullptr;
+    const int32_t nb = slab_compact_blocks(0, (int32_t)N);
+    hipError_t e = hipMalloc(&gp, N * sizeof(float4));
+    if (e == hipSuccess) e = hipMalloc(&gv, N * sizeof(float4));
+    if (e == hipSuccess) e = hipMalloc(&gi, N * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&blk, (2 * (size_t)nb + 2) * sizeof(uint32_t));
+    uint32_t total = 0;
+    if (e == hipSuccess) {
+        launch_lattice(sc->dim, sc->nx, sc->ny, sc->nz, sc->dx, 0.f, 0.f, 0.f, sc->seed, sc->jitter * sc->dx, gp, gv,
+                       gi, ctx->stream);
+        // count first: the owned part must fit the context
+        launch_slab_select_columns(gp, gv, gi, (int32_t)N, ctx->gglobal, ctx->sl.cx_lo, ctx->sl.cx_hi, blk,
+                                   ctx->sdev, nullptr, nullptr, nullptr, ctx->stream);
+        e = hipMemcpyAsync(&total, ctx->sdev, 4, hipMemcpyDeviceToHost, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    }
+    if (e == hipSuccess && (int64_t)total > ctx->capacity) {
+        (void)hipFree(gp); (void)hipFree(gv); (void)hipFree(gi); (void)hipFree(blk);
+        return fail(ctx, SPH_ERR_CAPACITY, "slab owns %u particles > capacity %d", total, ctx->capacity);
+    }
+    if (e == hipSuccess) {
+        launch_slab_select_columns(gp, gv, gi, (int32_t)N, ctx->gglobal, ctx->sl.cx_lo, ctx->sl.cx_hi, blk,
+                                   ctx->sdev, ctx->pos, ctx->vel, ctx->id, ctx->stream);
+        e = hipStreamSynchronize(ctx->stream);
+    }
+    (void)hipFree(gp); (void)hipFree(gv); (void)hipFree(gi); (void)hipFree(blk);
+    if (e != hipSuccess) return fail(ctx, SPH_ERR_HIP, "slab init: %s", hipGetErrorString(e));
+    ctx->n = ctx->o1 = (int32_t)total;
+    ctx->o0 = 0;
+    ctx->keys_valid = false;
+    ctx->steps = 0;
+    ctx->sim_time = 0.0;
+    return SPH_OK;
+}
+
+int sph_slab_count_sends(sph_ctx* ctx, int32_t counts[2]) {
+    if (!ctx || !counts) return SPH_ERR_INVALID;
+    if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
+    HIPCHK(hipSetDevice(ctx->device));
+    const int32_t no = ctx->o1 - ctx->o0;
+    if (!ctx->keys_valid && no > 0) {
+        KTimer t(ctx, "keys", 20.0 * no);
+        launch_keys(ctx->pos + ctx->o0, no, nullptr, 0, ctx->grid, ctx->keys + ctx->o0, ctx->stream);
+        ctx->keys_valid = true;
+    }
+    const uint32_t gyz = (uint32_t)ctx->grid.gy * (uint32_t)ctx->grid.gz;
+    const int32_t col_le = ctx->has_left ? ctx->sl.cx_lo - ctx->grid.cx0 : -1;
+    const int32_t col_ge = ctx->has_right ? ctx->sl.cx_hi - 1 - ctx->grid.cx0 : 0x7fffffff;
+    uint32_t tot[2] = {0, 0};
+    {
+        KTimer t(ctx, "slab_count", 4.0 * no);
+        launch_slab_count(ctx->keys, ctx->o0, ctx->o1, gyz, col_le, col_ge, ctx->sblk, ctx->sdev, ctx->stream);
+    }
+    HIPCHK(hipMemcpyAsync(tot, ctx->sdev, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    counts[0] = ctx->send_counts[0] = (int32_t)tot[0];
+    counts[1] = ctx->send_counts[1] = (int32_t)tot[1];
+    return SPH_OK;
+}
+
+int sph_slab_pack_send(sph_ctx* ctx, int32_t side, void* dev_records, int32_t capacity) {
+    if (!ctx || side < 0 || side > 1) return SPH_ERR_INVALID;
+    if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
+    if (ctx->send_counts[side] == 0) return SPH_OK;
+    if (!dev_records || capacity < ctx->send_counts[side])
+        return fail(ctx, SPH_ERR_CAPACITY, "send buffer %d < %d records", capacity, ctx->send_counts[side]);
+    HIPCHK(hipSetDevice(ctx->device));
+    const uint32_t gyz = (uint32_t)ctx->grid.gy * (uint32_t)ctx->grid.gz;
+    const int32_t col_le = ctx->has_left ? ctx->sl.cx_lo - ctx->grid.cx0 : -1;
+    const int32_t col_ge = ctx->has_right ? ctx->sl.cx_hi - 1 - ctx->grid.cx0 : 0x7fffffff;
+    KTimer t(ctx, "slab_pack", 36.0 * ctx->send_counts[side]);
+    launch_slab_pack(ctx->keys, ctx->pos, ctx->vel, ctx->id, ctx->o0, ctx->o1, gyz, side, col_le, col_ge, ctx->sblk,
+                     (float4*)dev_records, ctx->stream);
+    HIPCHK(hipGetLastError());
+    return SPH_OK;
+}
+
+int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void* dev_right, int32_t nr) {
+    if (!ctx || nl < 0 || nr < 0 || (nl > 0 && !dev_left) || (nr > 0 && !dev_right)) return SPH_ERR_INVALID;
+    if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
+    HIPCHK(hipSetDevice(ctx->device));
+    const int32_t no = ctx->o1 - ctx->o0;
+    const int64_t n = (int64_t)nl + no + nr;
+    if (n > ctx->capacity) return fail(ctx, SPH_ERR_CAPACITY, "slab needs %lld slots > capacity %d", (long long)n, ctx->capacity);
+    hipStream_t s = ctx->stream;
+    // canonical pre-sort order [from left | own | from right]: both ranks sharing a column then
+    // break key ties identically (SPEC_SPH.md §3)
+    {
+        KTimer t(ctx, "slab_assemble", 64.0 * (double)n);
+        launch_slab_unpack((const float4*)dev_left, nl, ctx->pos2, ctx->vel2, ctx->id2, s);
+        if (no > 0) {
+            HIPCHK(hipMemcpyAsync(ctx->pos2 + nl, ctx->pos + ctx->o0, (size_t)no * 16, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(ctx->vel2 + nl, ctx->vel + ctx->o0, (size_t)no * 16, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(ctx->id2 + nl, ctx->id + ctx->o0, (size_t)no * 4, hipMemcpyDeviceToDevice, s));
+        }
+        launch_slab_unpack((const float4*)dev_right, nr, ctx->pos2 + nl + no, ctx->vel2 + nl + no, ctx->id2 + nl + no, s);
+        launch_keys(ctx->pos2, (int32_t)n, nullptr, 0, ctx->grid, ctx->keys, s);
+    }
+    int side;
+    {
+        const int passes = (ctx->key_bits + 7) / 8;
+        KTimer t(ctx, "radix_sort", (double)n * (20.0 * passes));
+        side = radix_sort(ctx->keys, ctx->vals, ctx->keys2, ctx->vals2, (int32_t)n, ctx->key_bits, true, ctx->hist,
+                          ctx->bin_total, s);
+    }
+    const uint32_t* sk = side ? ctx->keys2 : ctx->keys;
+    const uint32_t* perm = side ? ctx->vals2 : ctx->vals;
+    {
+        KTimer t(ctx, "reorder", (double)n * (4 + 2 * 36));
+        launch_gather_s(perm, ctx->pos2, ctx->vel2, ctx->id2, ctx->pos, ctx->vel, ctx->id, (int32_t)n, s);
+    }
+    {
+        KTimer t(ctx, "cell_start", 4.0 * (ctx->grid.ncells + 1));
+        launch_cell_start(sk, (int32_t)n, ctx->cs, ctx->grid.ncells, s);
+    }
+    // ranges from the cell table at column starts
+    const int32_t lc_lo = ctx->sl.cx_lo - ctx->grid.cx0, lc_hi = ctx->sl.cx_hi - ctx->grid.cx0;
+    const int32_t idx[6] = {col_start(ctx, 0), col_start(ctx, lc_lo), col_start(ctx, lc_lo + 1),
+                            col_start(ctx, lc_hi - 1), col_start(ctx, lc_hi), col_start(ctx, ctx->grid.gx)};
+    uint32_t v[6];
+    launch_pick(ctx->cs, idx, 6, ctx->sdev, s);
+    HIPCHK(hipMemcpyAsync(v, ctx->sdev, sizeof v, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    int32_t* r = ctx->rng;
+    r[0] = (int32_t)v[0]; r[1] = (int32_t)v[1];                          // ghost left
+    r[2] = (int32_t)v[1]; r[3] = (int32_t)v[4];                          // owned
+    r[4] = (int32_t)v[4]; r[5] = (int32_t)v[5];                          // ghost right
+    r[6] = (int32_t)v[1]; r[7] = (int32_t)v[2];                          // boundary column cx_lo
+    r[8] = (int32_t)v[3]; r[9] = (int32_t)v[4];                          // boundary column cx_hi-1
+    if (r[5] != (int32_t)n)
+        return fail(ctx, SPH_ERR_STATE, "slab assemble: %d particles fall outside the held columns", (int32_t)n - r[5]);
+    ctx->n = (int32_t)n;
+    ctx->o0 = r[2];
+    ctx->o1 = r[3];
+    ctx->keys_valid = false;
+    return SPH_OK;
+}
+
+int sph_slab_ranges(sph_ctx* ctx, int32_t ranges[10]) {
+    if (!ctx || !ranges) return SPH_ERR_INVALID;
+    std::memcpy(ranges, ctx->rng, sizeof ctx->rng);
+    return SPH_OK;
+}
+
+int sph_slab_density(sph_ctx* ctx) {
     if (!ctx) return SPH_ERR_INVALID;
-    return fail(ctx, SPH_ERR_STATE, "slab decomposition is driven by the host (see sph_test_amd.slab)");
+    if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
+    HIPCHK(hipSetDevice(ctx->device));
+    KTimer t(ctx, "density", 24.0 * (ctx->o1 - ctx->o0));
+    if (ctx->nb_variant == 0)
+        launch_density(ctx->pos, ctx->cs, ctx->o0, ctx->o1, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
+    else
+        launch_density_tiled(ctx->pos, ctx->cs, ctx->o0, ctx->o1, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
+    HIPCHK(hipGetLastError());
+    return SPH_OK;
+}
+
+int sph_slab_pack_rho(sph_ctx* ctx, int32_t side, void* dev, int32_t capacity) {
+    if (!ctx || side < 0 || side > 1) return SPH_ERR_INVALID;
+    const int32_t b = ctx->rng[6 + 2 * side], e = ctx->rng[7 + 2 * side];
+    if (e == b) return SPH_OK;
+    if (!dev || capacity < e - b) return fail(ctx, SPH_ERR_CAPACITY, "rho buffer %d < %d", capacity, e - b);
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemcpyAsync(dev, ctx->rp + b, (size_t)(e - b) * sizeof(float2), hipMemcpyDeviceToDevice, ctx->stream));
+    return SPH_OK;
+}
+
+int sph_slab_unpack_rho(sph_ctx* ctx, int32_t side, const void* dev, int32_t count) {
+    if (!ctx || side < 0 || side > 1) return SPH_ERR_INVALID;
+    const int32_t b = ctx->rng[4 * side], e = ctx->rng[4 * side + 1];
+    if (count != e - b)
+        return fail(ctx, SPH_ERR_STATE, "ghost column %d holds %d particles but %d densities arrived", side, e - b, count);
+    if (count == 0) return SPH_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemcpyAsync(ctx->rp + b, dev, (size_t)count * sizeof(float2), hipMemcpyDeviceToDevice, ctx->stream));
+    return SPH_OK;
+}
+
+static void slab_force_range(sph_ctx* ctx, float dt, int32_t b, int32_t e) {
+    if (e <= b) return;
+    const sph_params& p = ctx->prm;
+    const float tt = (float)ctx->sim_time;
+    const float fext = p.forcing_amp != 0.0f ? p.forcing_amp * sinf(6.28318530718f * p.forcing_freq * tt) : 0.0f;
+    KTimer t(ctx, "force_integrate", 76.0 * (e - b));
+    if (ctx->nb_variant == 0)
+        launch_force_integrate(ctx->pos, ctx->vel, ctx->rp, ctx->cs, b, e, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
+                               ctx->vel2, ctx->keys, ctx->stream);
+    else
+        launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, b, e, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
+                           ctx->vel2, ctx->keys, ctx->stream);
+}
+
+int sph_slab_force(sph_ctx* ctx, float dt, int32_t part) {
+    if (!ctx || part < 0 || part > 2) return SPH_ERR_INVALID;
+    if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
+    HIPCHK(hipSetDevice(ctx->device));
+    const int32_t* r = ctx->rng;
+    // interior = owned slots whose neighbourhood holds no ghost
+    const int32_t ib = ctx->has_left ? r[7] : r[2];
+    const int32_t ie = ctx->has_right ? r[8] : r[3];
+    if (part == 0) {
+        slab_force_range(ctx, dt, r[2], r[3]);
+    } else if (part == 1) {
+        slab_force_range(ctx, dt, ib, std::max(ib, ie));
+    } else {
+        if (ie < ib) {                  // one-column slab: boundary columns coincide
+            slab_force_range(ctx, dt, r[2], r[3]);
+        } else {
+            slab_force_range(ctx, dt, r[2], ib);
+            slab_force_range(ctx, dt, ie, r[3]);
+        }
+    }
+    HIPCHK(hipGetLastError());
+    return SPH_OK;
+}
+
+int sph_slab_finish_step(sph_ctx* ctx, float dt) {
+    if (!ctx) return SPH_ERR_INVALID;
+    swap_sv(ctx);
+    ctx->keys_valid = true;
+    ctx->steps++;
+    ctx->sim_time += (double)dt;
+    return SPH_OK;
+}
+
+int sph_slab_read_owned(sph_ctx* ctx, float* rec, int32_t count, int32_t* n_owned) {
+    if (!ctx || !n_owned) return SPH_ERR_INVALID;
+    const int32_t no = ctx->o1 - ctx->o0;
+    *n_owned = no;
+    if (count < no || (no > 0 && !rec)) return fail(ctx, SPH_ERR_INVALID, "count %d < owned %d", count, no);
+    HIPCHK(hipSetDevice(ctx->device));
+    if (no > 0) {
+        launch_pack_owned(ctx->pos, ctx->vel, ctx->id, ctx->rp, ctx->o0, no, (float*)ctx->staging, ctx->stream);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(rec, ctx->staging, (size_t)no * 32, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SPH_OK;
 }
 
 }  // extern "C"

@@ -23,7 +23,7 @@ struct RowIter {
 
 __device__ __forceinline__ RowIter row_iter(const GridDesc& g, float x, float y, float z) {
     RowIter it;
-    it.cx = cell_coord(x, g.ox, g.inv_cell, g.gx);
+    it.cx = cell_cx(g, x);
     it.cy = cell_coord(y, g.oy, g.inv_cell, g.gy);
     const int32_t cz = cell_coord(z, g.oz, g.inv_cell, g.gz);
     it.z0 = cz > 0 ? cz - 1 : 0;
@@ -57,9 +57,9 @@ __device__ __forceinline__ void spline(const SphConst& c, float r2, float& W, fl
 }
 
 __global__ __launch_bounds__(NB_BLK) void k_density(const float4* __restrict__ pos,
-                                                    const uint32_t* __restrict__ cs, int32_t n,
+                                                    const uint32_t* __restrict__ cs, int32_t ib, int32_t n,
                                                     GridDesc g, SphConst c, float2* __restrict__ rp) {
-    const int32_t i = blockIdx.x * NB_BLK + threadIdx.x;
+    const int32_t i = ib + blockIdx.x * NB_BLK + threadIdx.x;
     if (i >= n) return;
     const float4 pi = pos[i];
     const RowIter it = row_iter(g, pi.x, pi.y, pi.z);
@@ -91,9 +91,9 @@ __global__ __launch_bounds__(NB_BLK) void k_density(const float4* __restrict__ p
 
 __global__ __launch_bounds__(NB_BLK) void k_force_integrate(
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
-    const uint32_t* __restrict__ cs, int32_t n, GridDesc g, SphConst c, float dt, float fext_x,
+    const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, float dt, float fext_x,
     float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o) {
-    const int32_t i = blockIdx.x * NB_BLK + threadIdx.x;
+    const int32_t i = ib + blockIdx.x * NB_BLK + threadIdx.x;
     if (i >= n) return;
     const float4 pi = pos[i];
     const float4 vi = vel[i];
@@ -141,17 +141,17 @@ __global__ __launch_bounds__(NB_BLK) void k_force_integrate(
     keys_o[i] = cell_key(g, np[0], np[1], np[2]);
 }
 
-void launch_density(const float4* pos, const uint32_t* cs, int32_t n, GridDesc g, SphConst c,
+void launch_density(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
                     float2* rp, hipStream_t s) {
-    if (n > 0) k_density<<<(n + NB_BLK - 1) / NB_BLK, NB_BLK, 0, s>>>(pos, cs, n, g, c, rp);
+    if (ie > ib) k_density<<<(ie - ib + NB_BLK - 1) / NB_BLK, NB_BLK, 0, s>>>(pos, cs, ib, ie, g, c, rp);
 }
 
-void launch_force_integrate(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs,
-                            int32_t n, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o,
+void launch_force_integrate(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,
+                            int32_t ie, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o,
                             float4* vel_o, uint32_t* keys_o, hipStream_t s) {
-    if (n > 0)
-        k_force_integrate<<<(n + NB_BLK - 1) / NB_BLK, NB_BLK, 0, s>>>(pos, vel, rp, cs, n, g, c, dt,
-                                                                       fext_x, pos_o, vel_o, keys_o);
+    if (ie > ib)
+        k_force_integrate<<<(ie - ib + NB_BLK - 1) / NB_BLK, NB_BLK, 0, s>>>(pos, vel, rp, cs, ib, ie, g, c, dt,
+                                                                             fext_x, pos_o, vel_o, keys_o);
 }
 
 }  // namespace sph

@@ -35,7 +35,7 @@ __device__ __forceinline__ BlockRows block_rows(const GridDesc& g, const float4*
     const float4 pf = pos[i0], pl = pos[ilast];
     b.kf = cell_key(g, pf.x, pf.y, pf.z);
     b.kl = cell_key(g, pl.x, pl.y, pl.z);
-    b.cx = cell_coord(pi.x, g.ox, g.inv_cell, g.gx);
+    b.cx = cell_cx(g, pi.x);
     b.cy = cell_coord(pi.y, g.oy, g.inv_cell, g.gy);
     const int32_t cz = cell_coord(pi.z, g.oz, g.inv_cell, g.gz);
     b.z0 = cz > 0 ? cz - 1 : 0;
@@ -82,11 +82,11 @@ __device__ __forceinline__ float spline_w(const SphConst& c, float r2) {
 }
 
 __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restrict__ pos,
-                                                          const uint32_t* __restrict__ cs, int32_t n,
+                                                          const uint32_t* __restrict__ cs, int32_t ib, int32_t n,
                                                           GridDesc g, SphConst c, float2* __restrict__ rp) {
     __shared__ float4 sp[TT_CH + 4];
     const int tid = threadIdx.x;
-    const int32_t i0 = blockIdx.x * TT_BLK;
+    const int32_t i0 = ib + blockIdx.x * TT_BLK;
     const int32_t i = i0 + tid;
     const bool valid = i < n;
     const int32_t ilast = min(i0 + TT_BLK, n) - 1;
@@ -156,13 +156,13 @@ __device__ __forceinline__ void pair_force(const SphConst& c, float4 pi, float4 
 
 __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
-    const uint32_t* __restrict__ cs, int32_t n, GridDesc g, SphConst c, float dt, float fext_x,
+    const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, float dt, float fext_x,
     float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o) {
     __shared__ float4 sp[TT_CH + 4];     // (x, y, z, ρ)
     __shared__ float4 sv[TT_CH + 4];     // (u, v, w, P/ρ²)
     __shared__ uint16_t lst[TT_CAP][TT_BLK];
     const int tid = threadIdx.x;
-    const int32_t i0 = blockIdx.x * TT_BLK;
+    const int32_t i0 = ib + blockIdx.x * TT_BLK;
     const int32_t i = i0 + tid;
     const bool valid = i < n;
     const int32_t ilast = min(i0 + TT_BLK, n) - 1;
@@ -242,17 +242,17 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     keys_o[i] = cell_key(g, np[0], np[1], np[2]);
 }
 
-void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t n, GridDesc g, SphConst c, float2* rp,
-                          hipStream_t s) {
-    if (n > 0) k_density_tiled<<<(n + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, cs, n, g, c, rp);
+void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
+                          float2* rp, hipStream_t s) {
+    if (ie > ib) k_density_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, cs, ib, ie, g, c, rp);
 }
 
-void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t n,
-                        GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o,
+void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,
+                        int32_t ie, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o,
                         uint32_t* keys_o, hipStream_t s) {
-    if (n > 0)
-        k_force_tiled<<<(n + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, vel, rp, cs, n, g, c, dt, fext_x, pos_o,
-                                                                   vel_o, keys_o);
+    if (ie > ib)
+        k_force_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, vel, rp, cs, ib, ie, g, c, dt, fext_x,
+                                                                         pos_o, vel_o, keys_o);
 }
 
 }  // namespace sph

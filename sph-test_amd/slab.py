@@ -1,0 +1,290 @@
+"""Multi-GPU slab decomposition of the Model S step (SPEC_SPH.md §3).
+
+There is one process per GPU. Rank r owns the global cell columns [cx_lo, cx_hi) of the
+x-slowest grid and holds one halo column on each side. Particles move between ranks, and
+halos are exchanged, over `torch.distributed` point-to-point ops. With the "nccl" backend
+that is RCCL over xGMI, ordered on the same HIP stream as libsphhip's kernels. Per step:
+
+  1. count_sends / pack_send: owned particles now in column <= cx_lo go left, those in
+     column >= cx_hi-1 go right (ballot/scan compaction, order preserved) — one exchange
+     carries both the migrants and the position/velocity halo;
+  2. assemble: [from left | own | from right] -> keys -> radix sort -> cell start;
+  3. density on the owned slots;
+  4. ρ, P/ρ² of the two boundary columns -> neighbours' ghost columns, in flight while the
+     interior columns' force pass runs; then the boundary columns' force pass;
+  5. finish_step.
+
+The backend is libsphhip.so (GpuSlabBackend). The tests drive the same SlabRunner with a CPU
+backend over gloo to check the decomposition against the single-domain oracle.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from . import _abi as A
+from .context import Context, make_scenario, scenario_params
+
+REC_FLOATS = A.SPH_SLAB_RECORD_BYTES // 4     # 8 floats per particle record
+
+
+def weak_scenario(config: str, world: int, dx: float = 0.01, seed: int = 1234) -> A.SphScenario:
+    """Weak-scaling scenario: `config`'s fluid column and tank stretched ×world along x
+    (the slab axis), so every rank owns the same number of particles as one C-config GPU."""
+    from .controllers import CONFIGS
+    kind, dim, nx, ny, nz, tx, ty, tz = CONFIGS[config]
+    return make_scenario(kind, dim, nx * world, ny, nz, tx * world, ty, tz, dx=dx, seed=seed)
+
+
+def balanced_cuts(sc: A.SphScenario, params: A.SphParams, world: int) -> List[Tuple[int, int]]:
+    """Column cuts with equal initial particle counts (the lattice is uniform in y and z, so
+    counts per column come from the x lattice index alone; jitter is ignored, cuts only need
+    to be identical on every rank)."""
+    cell = np.float32(2.0) * np.float32(params.h)
+    inv = np.float32(1.0) / cell
+    G = int(np.floor(np.float32(params.box[0]) / cell)) + 1
+    x = (np.arange(sc.nx, dtype=np.float32) + np.float32(0.5)) * np.float32(sc.dx)
+    col = np.clip(np.floor(x * inv).astype(np.int64), 0, G - 1)
+    per_col = np.bincount(col, minlength=G).astype(np.float64)
+    cum = np.cumsum(per_col)
+    total = cum[-1]
+    cuts = [0]
+    for r in range(1, world):
+        c = int(np.searchsorted(cum, total * r / world, side="left")) + 1
+        c = max(c, cuts[-1] + 1)
+        c = min(c, G - (world - r))
+        cuts.append(c)
+    cuts.append(G)
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+class GpuSlabBackend:
+    """One rank's libsphhip.so context in slab mode."""
+
+    def __init__(self, sc: A.SphScenario, params: A.SphParams, cut: Tuple[int, int], capacity: int,
+                 device: int = 0, profile: bool = False):
+        import torch
+        self.torch = torch
+        self.device = torch.device("cuda", device)
+        self.ctx = Context(A.SPH_MODEL_WCSPH, sc.dim, capacity, device=device, profile=profile)
+        self.ctx.set_params(params)
+        L, h = self.ctx._L, self.ctx.handle
+        A.check("sph_slab_set", L.sph_slab_set(h, C.byref(A.SphSlab(cut[0], cut[1]))), h)
+        A.check("sph_slab_init_scenario", L.sph_slab_init_scenario(h, C.byref(sc)), h)
+        self._L, self._h = L, h
+
+    def _chk(self, fn, st):
+        A.check(fn, st, self._h)
+
+    def bind_stream(self, handle: int) -> None:
+        self.ctx.set_stream(handle)
+
+    def empty(self, n: int, width: int):
+        return self.torch.empty((max(n, 1), width), dtype=self.torch.float32, device=self.device)
+
+    def count_sends(self) -> Tuple[int, int]:
+        c = (C.c_int32 * 2)()
+        self._chk("sph_slab_count_sends", self._L.sph_slab_count_sends(self._h, c))
+        return int(c[0]), int(c[1])
+
+    def pack_send(self, side: int, buf, n: int) -> None:
+        self._chk("sph_slab_pack_send", self._L.sph_slab_pack_send(self._h, side, A.ptr(buf.data_ptr()), n))
+
+    def assemble(self, left, nl: int, right, nr: int) -> None:
+        self._chk("sph_slab_assemble", self._L.sph_slab_assemble(self._h, A.ptr(left.data_ptr() if nl else 0), nl,
+                                                                 A.ptr(right.data_ptr() if nr else 0), nr))
+
+    def ranges(self) -> List[int]:
+        r = (C.c_int32 * 10)()
+        self._chk("sph_slab_ranges", self._L.sph_slab_ranges(self._h, r))
+        return list(r)
+
+    def density(self) -> None:
+        self._chk("sph_slab_density", self._L.sph_slab_density(self._h))
+
+    def pack_rho(self, side: int, buf, n: int) -> None:
+        self._chk("sph_slab_pack_rho", self._L.sph_slab_pack_rho(self._h, side, A.ptr(buf.data_ptr()), n))
+
+    def unpack_rho(self, side: int, buf, n: int) -> None:
+        self._chk("sph_slab_unpack_rho", self._L.sph_slab_unpack_rho(self._h, side, A.ptr(buf.data_ptr() if n else 0), n))
+
+    def force(self, dt: float, part: int) -> None:
+        self._chk("sph_slab_force", self._L.sph_slab_force(self._h, dt, part))
+
+    def finish(self, dt: float) -> None:
+        self._chk("sph_slab_finish_step", self._L.sph_slab_finish_step(self._h, dt))
+
+    def read_owned(self) -> np.ndarray:
+        """(n, 8) records: x, y, z, u, v, w, id (as int32 bits), ρ."""
+        cap = self.ctx.capacity
+        out = np.empty((cap, 8), np.float32)
+        n = C.c_int32()
+        self._chk("sph_slab_read_owned", self._L.sph_slab_read_owned(self._h, A.ptr(out), cap, C.byref(n)))
+        return out[: n.value].copy()
+
+    def kernel_stats(self) -> dict:
+        return self.ctx.kernel_stats()
+
+    def reset_stats(self) -> None:
+        self.ctx.reset_kernel_stats()
+
+    def close(self) -> None:
+        self.ctx.close()
+
+
+class _StagedWork:
+    """gloo transport of device tensors through host copies (one-GPU test boxes)."""
+
+    def __init__(self, dist, sends, recvs):
+        self.recvs = recvs
+        self.host = [t.new_empty(t.shape, device="cpu") for t, _ in recvs]
+        ops = [dist.P2POp(dist.isend, t.cpu(), p) for t, p in sends]
+        ops += [dist.P2POp(dist.irecv, h, p) for h, (_, p) in zip(self.host, recvs)]
+        self.works = dist.batch_isend_irecv(ops)
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        for h, (t, _) in zip(self.host, self.recvs):
+            t.copy_(h)
+
+
+class SlabRunner:
+    """Drives one rank's backend through the decomposed step (see module doc)."""
+
+    def __init__(self, config: str, rank: int, world: int, device: int = 0, profile: bool = False,
+                 backend=None, scenario: Optional[A.SphScenario] = None, capacity_factor: float = 1.5):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.config, self.rank, self.world = config, rank, world
+        self.scenario = scenario if scenario is not None else weak_scenario(config, world)
+        self.params, self.dt = scenario_params(self.scenario)
+        self.cuts = balanced_cuts(self.scenario, self.params, world)
+        sc = self.scenario
+        self.n_global = sc.nx * sc.ny * (sc.nz if sc.dim == 3 else 1)
+        if backend is None:
+            cap = int(self.n_global / world * capacity_factor) + 4096
+            backend = GpuSlabBackend(sc, self.params, self.cuts[rank], cap, device=device, profile=profile)
+        elif callable(backend) and not hasattr(backend, "count_sends"):
+            backend = backend(self.cuts[rank])          # factory: cut -> backend
+        self.be = backend
+        # gloo moves CPU tensors only: stage device buffers through the host (tests on one GPU)
+        probe = self.be.empty(1, 1)
+        self.host_staging = probe.is_cuda and dist.is_initialized() and dist.get_backend() == "gloo"
+        self.left = rank - 1 if rank > 0 else None
+        self.right = rank + 1 if rank + 1 < world else None
+        self.ranges = None
+        self._owned = None
+
+    # ----------------------------------------------------------------- plumbing
+    def bind_stream(self, handle: int) -> None:
+        self.be.bind_stream(handle)
+
+    def _p2p(self, sends, recvs):
+        """sends/recvs: lists of (tensor, peer). Returns the works (async)."""
+        if self.host_staging:
+            return [_StagedWork(self.dist, sends, recvs)] if (sends or recvs) else []
+        ops = [self.dist.P2POp(self.dist.isend, t, p) for t, p in sends]
+        ops += [self.dist.P2POp(self.dist.irecv, t, p) for t, p in recvs]
+        return self.dist.batch_isend_irecv(ops) if ops else []
+
+    def _exchange_counts(self, nl: int, nr: int) -> Tuple[int, int]:
+        dev = self.be.empty(1, 1).device
+        sends, recvs = [], []
+        out_l = self.torch.zeros(1, dtype=self.torch.int64, device=dev)
+        out_r = self.torch.zeros(1, dtype=self.torch.int64, device=dev)
+        if self.left is not None:
+            sends.append((self.torch.tensor([nl], dtype=self.torch.int64, device=dev), self.left))
+            recvs.append((out_l, self.left))
+        if self.right is not None:
+            sends.append((self.torch.tensor([nr], dtype=self.torch.int64, device=dev), self.right))
+            recvs.append((out_r, self.right))
+        for w in self._p2p(sends, recvs):
+            w.wait()
+        return int(out_l.item()), int(out_r.item())
+
+    # ----------------------------------------------------------------- step
+    def step(self, k: int = 1) -> None:
+        for _ in range(k):
+            self._one_step()
+
+    def _one_step(self) -> None:
+        be, dt = self.be, self.dt
+        # 1. migrants + x,v halo in one exchange
+        nl, nr = be.count_sends()
+        if self.left is None:
+            nl = 0
+        if self.right is None:
+            nr = 0
+        bl, br = be.empty(nl, REC_FLOATS), be.empty(nr, REC_FLOATS)
+        if nl:
+            be.pack_send(0, bl, nl)
+        if nr:
+            be.pack_send(1, br, nr)
+        il, ir = self._exchange_counts(nl, nr)
+        rl, rr = be.empty(il, REC_FLOATS), be.empty(ir, REC_FLOATS)
+        sends = [(bl[:nl], self.left)] if nl else []
+        sends += [(br[:nr], self.right)] if nr else []
+        recvs = [(rl[:il], self.left)] if il else []
+        recvs += [(rr[:ir], self.right)] if ir else []
+        for w in self._p2p(sends, recvs):
+            w.wait()
+        # 2. rebuild + sort; 3. density
+        be.assemble(rl, il, rr, ir)
+        r = be.ranges()
+        self.ranges = r
+        be.density()
+        # 4. ρ halo: boundary columns out, ghost columns in; interior force meanwhile
+        nbl, nbr = r[7] - r[6], r[9] - r[8]
+        ngl, ngr = r[1] - r[0], r[5] - r[4]
+        sends, recvs = [], []
+        if self.left is not None and nbl:
+            sl = be.empty(nbl, 2)
+            be.pack_rho(0, sl, nbl)
+            sends.append((sl[:nbl], self.left))
+        if self.right is not None and nbr:
+            sr = be.empty(nbr, 2)
+            be.pack_rho(1, sr, nbr)
+            sends.append((sr[:nbr], self.right))
+        gl, gr = be.empty(ngl, 2), be.empty(ngr, 2)
+        if ngl:
+            recvs.append((gl[:ngl], self.left))
+        if ngr:
+            recvs.append((gr[:ngr], self.right))
+        works = self._p2p(sends, recvs)
+        be.force(dt, 1)
+        for w in works:
+            w.wait()
+        be.unpack_rho(0, gl, ngl)
+        be.unpack_rho(1, gr, ngr)
+        be.force(dt, 2)
+        be.finish(dt)
+
+    # ----------------------------------------------------------------- reporting
+    def total_particles(self) -> int:
+        return self.n_global
+
+    def local_particles(self) -> int:
+        if self.ranges is None:
+            return self.n_global // self.world
+        return self.ranges[3] - self.ranges[2]
+
+    def owned(self) -> np.ndarray:
+        return self.be.read_owned()
+
+    def reset_stats(self) -> None:
+        self.be.reset_stats()
+
+    def kernel_stats(self) -> dict:
+        return self.be.kernel_stats()
+
+    def workload(self) -> str:
+        sc = self.scenario
+        return (f"{self.config}x{self.world} weak: {self.n_global} particles, {sc.dim}D dam-break, column "
+                f"{sc.nx}x{sc.ny}x{sc.nz}, tank {sc.tx}x{sc.ty}x{sc.tz} dx, x-slabs {self.cuts}")
+
+    def close(self) -> None:
+        self.be.close()

@@ -46,7 +46,7 @@ int main(void){
     subprocess.run(["gcc", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = [C.sizeof(A.SphConfig), C.sizeof(A.SphParams), C.sizeof(A.SphScenario), C.sizeof(A.SphDragInput),
-            C.sizeof(A.SphStats), C.sizeof(A.SphKernelStat), 20, A.SphParams.forcing_freq.offset]
+            C.sizeof(A.SphStats), C.sizeof(A.SphKernelStat), C.sizeof(A.SphSlab), A.SphParams.forcing_freq.offset]
     assert got == want
     assert C.sizeof(A.SphDragInput) == 20          # DragInput, ParticleSystemController.cs:377
     assert A.PARTICLE84.itemsize == 84             # Particle, ParticleSystemController.cs:375

@@ -1,0 +1,97 @@
+"""Slab decomposition on the GPU (SPEC_SPH.md §3).
+
+* world 1: the slab path (no neighbours) must reproduce the single-context step bit for bit;
+* world 2: two ranks share the one GPU of the test box (gloo transport staged through the
+  host; bench.py uses RCCL between GPUs), compared with the single-context step.
+"""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parent.parent
+STEPS = 8
+
+
+def _scenario(pkg):
+    return pkg.make_scenario(0, 3, 48, 32, 32, 120, 48, 32, dx=0.01, seed=99)
+
+
+def _single(pkg, sc):
+    sim = pkg.SPHSim(sc)
+    sim.step(STEPS)
+    x, v = sim.positions(), sim.velocities()
+    sim.close()
+    return x, v
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as GE
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    pkg = GE.load_package()
+    from sph_test_amd import slab
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
+    runner = slab.SlabRunner("C3", rank, world, device=0, scenario=_scenario(pkg))
+    runner.bind_stream(s.cuda_stream)
+    runner.step(STEPS)
+    torch.cuda.synchronize()
+    np.save(os.path.join(outdir, f"rank{rank}.npy"), runner.owned())
+    runner.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_slab_world1_bitwise(pkg):
+    import torch
+    import torch.distributed as dist
+    from sph_test_amd import slab
+    sc = _scenario(pkg)
+    xs, vs = _single(pkg, sc)
+    runner = slab.SlabRunner("C3", 0, 1, device=0, scenario=sc)
+    assert runner.cuts == [(0, runner.cuts[0][1])]
+    runner.step(STEPS)
+    rec = runner.owned()
+    runner.close()
+    ids = rec[:, 6].view(np.int32)
+    order = np.argsort(ids)
+    assert np.array_equal(ids[order], np.arange(len(xs)))
+    assert np.array_equal(rec[order, 0:3], xs)
+    assert np.array_equal(rec[order, 3:6], vs)
+
+
+def test_slab_world2_matches_single(pkg, tmp_path):
+    import multiprocessing as mp
+    sc = _scenario(pkg)
+    xs, vs = _single(pkg, sc)
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=400)
+        assert p.exitcode == 0, f"rank exited with {p.exitcode}"
+    rec = np.concatenate([np.load(tmp_path / f"rank{r}.npy") for r in range(2)])
+    ids = rec[:, 6].view(np.int32)
+    assert np.array_equal(np.sort(ids), np.arange(len(xs)))
+    order = np.argsort(ids)
+    np.testing.assert_allclose(rec[order, 0:3], xs, rtol=0, atol=2e-6)
+    np.testing.assert_allclose(rec[order, 3:6], vs, rtol=1e-3, atol=2e-3)
