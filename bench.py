@@ -99,10 +99,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL over xGMI between GPUs; SPH_DIST_BACKEND=gloo rehearses N ranks on one GPU
+    backend = os.environ.get("SPH_DIST_BACKEND", "nccl")
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     pkg = GE.load_package()
@@ -136,7 +142,7 @@ def main():
     barrier()
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
-    el = torch.tensor([wall], dtype=torch.float64, device="cuda")
+    el = torch.tensor([wall], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     wall = float(el.item())

@@ -245,3 +245,33 @@ def test_contact_resize_keeps_state(pkg):
     assert ctl.GetParticles().tobytes() == before.tobytes()
     ctl.Update(0.01)
     ctl.OnDestroy()
+
+
+# ------------------------------------------------------------------ committed fixtures
+def test_gpu_vs_golden_wcsph_c1(pkg):
+    from pathlib import Path
+    d = np.load(Path(__file__).resolve().parent / "golden" / "wcsph_c1_s10.npz")
+    sim = pkg.SPHSim.from_config("C1")
+    assert np.array_equal(sim.positions(), d["x0"])
+    sim.step(10)
+    np.testing.assert_allclose(sim.positions(), d["x"], rtol=0, atol=2e-6)
+    np.testing.assert_allclose(sim.density(), d["rho"], rtol=2e-4)
+    sim.close()
+
+
+def test_gpu_vs_golden_contact_n4096(pkg):
+    from pathlib import Path
+    d = np.load(Path(__file__).resolve().parent / "golden" / "contact_n4096_s1.npz")
+    inp = d["input"].view(pkg.PARTICLE84)
+    ref = d["output"].view(pkg.PARTICLE84)
+    ctl = pkg.ParticleSystemController(particleCount=len(inp))
+    ctl.globalDragMultiplier = 10.0
+    ctl.Start(inp)
+    ctl.Update(0.01)
+    got = ctl.GetParticles()
+    tq = ctl.context.torque_int()
+    diff = np.abs(tq.astype(np.int64) - d["torque"])
+    assert (diff > 0).mean() < 1e-3 and diff.max() <= 4
+    np.testing.assert_allclose(got["velocity"], ref["velocity"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(got["position"], ref["position"], rtol=1e-5, atol=1e-5)
+    ctl.OnDestroy()
