@@ -23,8 +23,10 @@ extern "C" {
 /* ---- common grid (SPEC_SPH.md §0) ---- */
 typedef struct {
     float origin[3];
-    float inv_cell;
-    int32_t G[3];
+    float inv_cell;     /* x, y */
+    float inv_cell_z;   /* z sub-cells: cell / zsub */
+    int32_t G[3];       /* G[2] counts z sub-cells */
+    int32_t zwin;       /* neighbour z window in sub-cells (zsub + 1) */
 } or_grid;
 
 uint32_t or_cell_key(const or_grid* g, float x, float y, float z);

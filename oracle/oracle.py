@@ -31,7 +31,8 @@ assert PARTICLE84.itemsize == 84
 
 
 class OrGrid(C.Structure):
-    _fields_ = [("origin", C.c_float * 3), ("inv_cell", C.c_float), ("G", C.c_int32 * 3)]
+    _fields_ = [("origin", C.c_float * 3), ("inv_cell", C.c_float), ("inv_cell_z", C.c_float),
+                ("G", C.c_int32 * 3), ("zwin", C.c_int32)]
 
 
 class OrSphParams(C.Structure):

@@ -25,7 +25,7 @@ static inline int32_t or_coord(float x, float origin, float inv_cell, int32_t G)
 uint32_t or_cell_key(const or_grid* g, float x, float y, float z) {
     int32_t cx = or_coord(x, g->origin[0], g->inv_cell, g->G[0]);
     int32_t cy = or_coord(y, g->origin[1], g->inv_cell, g->G[1]);
-    int32_t cz = or_coord(z, g->origin[2], g->inv_cell, g->G[2]);
+    int32_t cz = or_coord(z, g->origin[2], g->inv_cell_z, g->G[2]);
     return ((uint32_t)cx * (uint32_t)g->G[1] + (uint32_t)cy) * (uint32_t)g->G[2] + (uint32_t)cz;
 }
 
@@ -59,11 +59,16 @@ void or_sph_derive(or_sph_params* p) {
     p->sigma = p->dim == 3 ? 1.0f / (PI * p->h * p->h * p->h) : 10.0f / (7.0f * PI * p->h * p->h);
     p->inv_h = 1.0f / p->h;
     p->four_h2 = 4.0f * p->h * p->h;
+    /* SPEC_SPH.md §0: cells 2h in x, y; z split into zsub = 4 sub-cells (3D) */
     float cell = 2.0f * p->h;
+    int32_t zsub = p->dim == 3 ? 4 : 1;
+    float cz = cell / (float)zsub;
     p->grid.inv_cell = 1.0f / cell;
+    p->grid.inv_cell_z = 1.0f / cz;
+    p->grid.zwin = zsub + 1;
     for (int a = 0; a < 3; ++a) {
         p->grid.origin[a] = 0.0f;
-        int32_t G = (int32_t)floorf(p->L[a] / cell) + 1;
+        int32_t G = (int32_t)floorf(p->L[a] / (a == 2 ? cz : cell)) + 1;
         if (a == 2 && p->dim == 2) G = 1;
         p->grid.G[a] = G < 1 ? 1 : G;
     }
@@ -110,13 +115,16 @@ static inline void kernel_wf(const or_sph_params* p, float r2, float* W, float* 
 
 typedef struct { int n; int lo, hi; } row_range;
 
-/* the 9 (3D) / 3 (2D) contiguous neighbour rows of SPEC_SPH.md §0, in visit order */
+/* the 9 contiguous neighbour rows of SPEC_SPH.md §0, in visit order, each over the z
+ * sub-cell window [cz - zwin, cz + zwin] (a superset of every row's trimmed window) */
 static int neighbour_rows(const or_grid* g, const uint32_t* cs, uint32_t key, uint32_t ranges[9][2]) {
     int32_t GY = g->G[1], GZ = g->G[2];
     int32_t cz = (int32_t)(key % (uint32_t)GZ);
     int32_t cy = (int32_t)((key / (uint32_t)GZ) % (uint32_t)GY);
     int32_t cx = (int32_t)(key / ((uint32_t)GZ * (uint32_t)GY));
-    int32_t z0 = cz > 0 ? cz - 1 : 0, z1 = cz < GZ - 1 ? cz + 1 : GZ - 1;
+    int32_t z0 = cz - g->zwin, z1 = cz + g->zwin;
+    if (z0 < 0) z0 = 0;
+    if (z1 > GZ - 1) z1 = GZ - 1;
     int nr = 0;
     for (int ddx = -1; ddx <= 1; ++ddx) {
         int32_t x = cx + ddx;

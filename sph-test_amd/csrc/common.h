@@ -11,13 +11,18 @@ namespace sph {
 // A context may hold an x-window [cx0, cx0+gx) of a global grid of gx_all columns (slab
 // decomposition, SPEC_SPH.md §3). The column is computed globally then shifted, so all
 // ranks agree bit for bit on which column a particle is in.
+// Model S splits z into zsub sub-cells (cells 2h × 2h × 2h/zsub, SPEC_SPH.md §0): each of the
+// 9 neighbour rows is then walked over a z window trimmed to the row's xy distance.
 struct GridDesc {
     float ox, oy, oz;
-    float inv_cell;
-    int32_t gx, gy, gz;
+    float inv_cell;      // 1 / cell (x, y)
+    float inv_cz;        // 1 / (cell / zsub) (z)
+    int32_t gx, gy, gz;  // gz counts z sub-cells
     uint32_t ncells;     // gx*gy*gz (keys == ncells mark inactive particles)
     int32_t cx0;         // first global column held (0 without decomposition)
     int32_t gx_all;      // global column count (== gx without decomposition)
+    int32_t zsub;        // z sub-cells per cell (Model S 4, Model R 1)
+    int32_t zwin;        // max |Δ z sub-cell| of a neighbour (zsub + 1; Model R 1)
 };
 
 // Model S constants (SPEC_SPH.md §2), derived on the host from sph_params.
@@ -55,8 +60,33 @@ __device__ __forceinline__ int32_t cell_cx(const GridDesc& g, float x) {
 __device__ __forceinline__ uint32_t cell_key(const GridDesc& g, float x, float y, float z) {
     int32_t cx = cell_cx(g, x);
     int32_t cy = cell_coord(y, g.oy, g.inv_cell, g.gy);
-    int32_t cz = cell_coord(z, g.oz, g.inv_cell, g.gz);
+    int32_t cz = cell_coord(z, g.oz, g.inv_cz, g.gz);
     return ((uint32_t)cx * (uint32_t)g.gy + (uint32_t)cy) * (uint32_t)g.gz + (uint32_t)cz;
+}
+
+// One of the 9 neighbour rows of a Model S particle (SPEC_SPH.md §0): the z sub-cell window
+// [zlo, zhi] of row (cx+dx, cy+dy) that can hold a particle within 2h, or false when the
+// row's column is ≥ 2h away in xy. fx, fy: the particle's position inside its cell, in [0,1].
+__device__ __forceinline__ bool row_window(const GridDesc& g, float fx, float fy, float gzf, int dx, int dy,
+                                           int32_t& zlo, int32_t& zhi) {
+    const float gxg = dx < 0 ? fx : (dx > 0 ? 1.0f - fx : 0.0f);
+    const float gyg = dy < 0 ? fy : (dy > 0 ? 1.0f - fy : 0.0f);
+    const float d2 = gxg * gxg + gyg * gyg;
+    if (!(d2 < 1.0f)) return false;
+    const float hz = __builtin_amdgcn_sqrtf(1.0f - d2) * (float)g.zsub + 1e-3f;
+    const float a = gzf - hz, b = gzf + hz;
+    zlo = a > 0.0f ? (int32_t)a : 0;
+    zhi = b < (float)(g.gz - 1) ? (int32_t)b : g.gz - 1;
+    if (zhi < 0) zhi = 0;
+    return true;
+}
+
+// The particle's in-cell fractions (x, y) and z sub-cell coordinate for row_window.
+__device__ __forceinline__ void cell_fracs(const GridDesc& g, float x, float y, float z, int32_t cx, int32_t cy,
+                                           float& fx, float& fy, float& gzf) {
+    fx = fminf(fmaxf((x - g.ox) * g.inv_cell - (float)(cx + g.cx0), 0.0f), 1.0f);
+    fy = fminf(fmaxf((y - g.oy) * g.inv_cell - (float)cy, 0.0f), 1.0f);
+    gzf = (z - g.oz) * g.inv_cz;
 }
 
 __device__ __forceinline__ uint32_t lane_id() {
@@ -77,8 +107,11 @@ int radix_sort(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* v
 // grid / data movement (grid.hip)
 void launch_keys(const float4* pos, int32_t n, const int32_t* id, int32_t n_active_id,
                  GridDesc g, uint32_t* keys, hipStream_t s);
+// cell_start[k] = lower_bound(sorted keys, k) for k = 0..ncells, every cell written once:
+// each particle boundary fills the cells up to its key; gaps longer than CS_SHORT cells are
+// queued (gap list + counter, zeroed by the call) and filled by whole workgroups.
 void launch_cell_start(const uint32_t* sorted_keys, int32_t n, uint32_t* cs, uint32_t ncells,
-                       hipStream_t s);
+                       uint4* gaps, uint32_t* gap_count, hipStream_t s);
 void launch_gather_f4(const uint32_t* perm, const float4* src, float4* dst, int32_t n, hipStream_t s);
 void launch_gather_i32(const uint32_t* perm, const int32_t* src, int32_t* dst, int32_t n, hipStream_t s);
 void launch_gather_s(const uint32_t* perm, const float4* pos, const float4* vel, const int32_t* id,

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step(
 
     const int32_t cx = cell_cx(g, pa.x);
     const int32_t cy = cell_coord(pa.y, g.oy, g.inv_cell, g.gy);
-    const int32_t cz = cell_coord(pa.z, g.oz, g.inv_cell, g.gz);
+    const int32_t cz = cell_coord(pa.z, g.oz, g.inv_cz, g.gz);
     const int32_t z0 = cz > 0 ? cz - 1 : 0, z1 = cz < g.gz - 1 ? cz + 1 : g.gz - 1;
 #pragma unroll 1
     for (int k = 0; k < 9; ++k) {

@@ -28,16 +28,39 @@ __global__ __launch_bounds__(BLK) void k_keys(const float4* __restrict__ pos, in
     keys[i] = k;
 }
 
+constexpr uint32_t CS_SHORT = 32;
+constexpr uint32_t CS_CHUNK = 8192;   // long gaps are queued in chunks so no workgroup fills more
+
+// thread i in [0, n]: cells (key[i-1], key[i]] start at slot i (key[-1] = -1, key[n] = ncells)
 __global__ __launch_bounds__(BLK) void k_cell_start(const uint32_t* __restrict__ sk, int32_t n,
-                                                    uint32_t* __restrict__ cs, uint32_t ncells) {
-    const uint32_t k = blockIdx.x * BLK + threadIdx.x;
-    if (k > ncells) return;
-    int32_t lo = 0, hi = n;
-    while (lo < hi) {                      // lower_bound: first index with key >= k
-        const int32_t mid = (lo + hi) >> 1;
-        if (sk[mid] < k) lo = mid + 1; else hi = mid;
+                                                    uint32_t* __restrict__ cs, uint32_t ncells,
+                                                    uint4* __restrict__ gaps, uint32_t* __restrict__ gap_count) {
+    const int32_t i = blockIdx.x * BLK + threadIdx.x;
+    if (i > n) return;
+    const int64_t kp = i > 0 ? (int64_t)sk[i - 1] : -1;
+    const int64_t kc = i < n ? (int64_t)sk[i] : (int64_t)ncells;
+    if (kc <= kp) return;
+    if (kc - kp <= CS_SHORT) {
+        for (int64_t k = kp + 1; k <= kc; ++k) cs[k] = (uint32_t)i;
+    } else {
+        const uint32_t nch = (uint32_t)((kc - kp + CS_CHUNK - 1) / CS_CHUNK);
+        const uint32_t slot = atomicAdd(gap_count, nch);
+        for (uint32_t c = 0; c < nch; ++c) {
+            const int64_t a = kp + 1 + (int64_t)c * CS_CHUNK;
+            const int64_t b = a + CS_CHUNK - 1 < kc ? a + CS_CHUNK - 1 : kc;
+            gaps[slot + c] = make_uint4((uint32_t)a, (uint32_t)b, (uint32_t)i, 0u);
+        }
     }
-    cs[k] = (uint32_t)lo;
+}
+
+__global__ __launch_bounds__(BLK) void k_cell_start_gaps(const uint4* __restrict__ gaps,
+                                                         const uint32_t* __restrict__ gap_count,
+                                                         uint32_t* __restrict__ cs) {
+    const uint32_t ng = *gap_count;
+    for (uint32_t gi = blockIdx.x; gi < ng; gi += gridDim.x) {
+        const uint4 gp = gaps[gi];
+        for (uint32_t k = gp.x + threadIdx.x; k <= gp.y; k += BLK) cs[k] = gp.z;
+    }
 }
 
 __global__ __launch_bounds__(BLK) void k_gather_f4(const uint32_t* __restrict__ perm,
@@ -196,8 +219,11 @@ void launch_keys(const float4* pos, int32_t n, const int32_t* id, int32_t n_acti
                  uint32_t* keys, hipStream_t s) {
     if (n > 0) k_keys<<<nblk(n), BLK, 0, s>>>(pos, n, id, n_active_id, g, keys);
 }
-void launch_cell_start(const uint32_t* sk, int32_t n, uint32_t* cs, uint32_t ncells, hipStream_t s) {
-    k_cell_start<<<nblk((int64_t)ncells + 1), BLK, 0, s>>>(sk, n, cs, ncells);
+void launch_cell_start(const uint32_t* sk, int32_t n, uint32_t* cs, uint32_t ncells, uint4* gaps,
+                       uint32_t* gap_count, hipStream_t s) {
+    (void)hipMemsetAsync(gap_count, 0, sizeof(uint32_t), s);
+    k_cell_start<<<nblk((int64_t)n + 1), BLK, 0, s>>>(sk, n, cs, ncells, gaps, gap_count);
+    k_cell_start_gaps<<<1024, BLK, 0, s>>>(gaps, gap_count, cs);
 }
 void launch_gather_f4(const uint32_t* perm, const float4* src, float4* dst, int32_t n, hipStream_t s) {
     if (n > 0) k_gather_f4<<<nblk(n), BLK, 0, s>>>(perm, src, dst, n);

@@ -21,6 +21,8 @@
 
 using namespace sph;
 
+static const int32_t SPH_ZSUB = 4;   // z sub-cells per 2h cell (SPEC_SPH.md §0)
+
 namespace {
 
 struct KStat {
@@ -60,6 +62,8 @@ struct sph_ctx {
     uint32_t *hist = nullptr, *bin_total = nullptr;
     uint32_t* cs = nullptr;
     uint32_t cs_cap = 0;
+    uint4* gaps = nullptr;       // cell-start long-gap queue
+    uint32_t gaps_cap = 0;
     void* staging = nullptr;
     size_t staging_bytes = 0;
     bool keys_valid = false;
@@ -130,7 +134,8 @@ void free_all(sph_ctx* c) {
     dfree(c->id); dfree(c->id2); dfree(c->mode); dfree(c->mode2);
     dfree(c->rp); dfree(c->torque);
     dfree(c->keys); dfree(c->keys2); dfree(c->vals); dfree(c->vals2); dfree(c->hist); dfree(c->bin_total);
-    dfree(c->cs);
+    dfree(c->cs); dfree(c->gaps);
+    c->gaps_cap = 0;
     dfree(c->sblk); dfree(c->sdev);
     if (c->staging) (void)hipFree(c->staging);
     c->staging = nullptr;
@@ -171,10 +176,19 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
 
 int ensure_cells(sph_ctx* ctx) {
     const uint32_t need = ctx->grid.ncells + 1;
-    if (need <= ctx->cs_cap) return SPH_OK;
-    int r = dalloc(ctx, &ctx->cs, need);
-    if (r != SPH_OK) return r;
-    ctx->cs_cap = need;
+    if (need > ctx->cs_cap) {
+        int r = dalloc(ctx, &ctx->cs, need);
+        if (r != SPH_OK) return r;
+        ctx->cs_cap = need;
+    }
+    // queued chunks: one per long gap (> 32 cells, so at most (ncells+1)/33) plus one per
+    // 8192 cells of gap length
+    const uint32_t g = (ctx->grid.ncells + 1) / 33 + (ctx->grid.ncells + 1) / 8192 + 4;
+    if (g > ctx->gaps_cap) {
+        int r = dalloc(ctx, &ctx->gaps, g);
+        if (r != SPH_OK) return r;
+        ctx->gaps_cap = g;
+    }
     return SPH_OK;
 }
 
@@ -186,16 +200,24 @@ int derive(sph_ctx* ctx) {
         // SimulateParticles.compute:16-18,102-105: 32^3 cells of 4.0 anchored at -spawnRadius
         g.ox = g.oy = g.oz = -p.spawn_radius;
         g.inv_cell = 0.25f;
+        g.inv_cz = 0.25f;
         g.gx = g.gy = g.gz = 32;
+        g.zsub = 1;
+        g.zwin = 1;
     } else {
         if (!(p.h > 0.f) || !(p.dx > 0.f) || !(p.rho0 > 0.f))
             return fail(ctx, SPH_ERR_INVALID, "Model S needs dx, h, rho0 > 0");
         const float cell = 2.0f * p.h;
+        const int32_t zsub = ctx->cfg.dim == 3 ? SPH_ZSUB : 1;
+        const float cz = cell / (float)zsub;
         g.ox = g.oy = g.oz = 0.f;
         g.inv_cell = 1.0f / cell;
+        g.inv_cz = 1.0f / cz;
+        g.zsub = zsub;
+        g.zwin = zsub + 1;
         int32_t G[3];
         for (int a = 0; a < 3; ++a) {
-            G[a] = (int32_t)floorf(p.box[a] / cell) + 1;
+            G[a] = (int32_t)floorf(p.box[a] / (a == 2 ? cz : cell)) + 1;
             if (G[a] < 1) G[a] = 1;
         }
         if (ctx->cfg.dim == 2) G[2] = 1;
@@ -328,9 +350,25 @@ int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id) {
     }
     {
         KTimer t(ctx, "cell_start", 4.0 * (ctx->grid.ncells + 1));
-        launch_cell_start(sk, n, ctx->cs, ctx->grid.ncells, ctx->stream);
+        launch_cell_start(sk, n, ctx->cs, ctx->grid.ncells, ctx->gaps, ctx->sdev + 8, ctx->stream);
     }
     return SPH_OK;
+}
+
+void density_range(sph_ctx* ctx, int32_t b, int32_t e) {
+    if (ctx->nb_variant == 0)
+        launch_density(ctx->pos, ctx->cs, b, e, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
+    else
+        launch_density_tiled(ctx->pos, ctx->cs, b, e, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
+}
+
+void force_range(sph_ctx* ctx, int32_t b, int32_t e, float dt, float fext) {
+    if (ctx->nb_variant == 0)
+        launch_force_integrate(ctx->pos, ctx->vel, ctx->rp, ctx->cs, b, e, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
+                               ctx->vel2, ctx->keys, ctx->stream);
+    else
+        launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, b, e, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
+                           ctx->vel2, ctx->keys, ctx->stream);
 }
 
 int step_wcsph(sph_ctx* ctx, float dt) {
@@ -339,22 +377,14 @@ int step_wcsph(sph_ctx* ctx, float dt) {
     if (r != SPH_OK) return r;
     {
         KTimer t(ctx, "density", 24.0 * n);
-        if (ctx->nb_variant == 0)
-            launch_density(ctx->pos, ctx->cs, 0, n, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
-        else
-            launch_density_tiled(ctx->pos, ctx->cs, 0, n, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
+        density_range(ctx, 0, n);
     }
     const sph_params& p = ctx->prm;
     const float tt = (float)ctx->sim_time;
     const float fext = p.forcing_amp != 0.0f ? p.forcing_amp * sinf(6.28318530718f * p.forcing_freq * tt) : 0.0f;
     {
         KTimer t(ctx, "force_integrate", 76.0 * n);
-        if (ctx->nb_variant == 0)
-            launch_force_integrate(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, n, ctx->grid, ctx->sc, dt, fext,
-                                   ctx->pos2, ctx->vel2, ctx->keys, ctx->stream);
-        else
-            launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, n, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
-                               ctx->vel2, ctx->keys, ctx->stream);
+        force_range(ctx, 0, n, dt, fext);
     }
     swap_sv(ctx);
     ctx->keys_valid = true;
@@ -971,7 +1001,7 @@ int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void
     }
     {
         KTimer t(ctx, "cell_start", 4.0 * (ctx->grid.ncells + 1));
-        launch_cell_start(sk, (int32_t)n, ctx->cs, ctx->grid.ncells, s);
+        launch_cell_start(sk, (int32_t)n, ctx->cs, ctx->grid.ncells, ctx->gaps, ctx->sdev + 8, s);
     }
     // ranges from the cell table at column starts
     const int32_t lc_lo = ctx->sl.cx_lo - ctx->grid.cx0, lc_hi = ctx->sl.cx_hi - ctx->grid.cx0;
@@ -1007,10 +1037,7 @@ int sph_slab_density(sph_ctx* ctx) {
     if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
     HIPCHK(hipSetDevice(ctx->device));
     KTimer t(ctx, "density", 24.0 * (ctx->o1 - ctx->o0));
-    if (ctx->nb_variant == 0)
-        launch_density(ctx->pos, ctx->cs, ctx->o0, ctx->o1, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
-    else
-        launch_density_tiled(ctx->pos, ctx->cs, ctx->o0, ctx->o1, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
+    density_range(ctx, ctx->o0, ctx->o1);
     HIPCHK(hipGetLastError());
     return SPH_OK;
 }
@@ -1042,12 +1069,7 @@ static void slab_force_range(sph_ctx* ctx, float dt, int32_t b, int32_t e) {
     const float tt = (float)ctx->sim_time;
     const float fext = p.forcing_amp != 0.0f ? p.forcing_amp * sinf(6.28318530718f * p.forcing_freq * tt) : 0.0f;
     KTimer t(ctx, "force_integrate", 76.0 * (e - b));
-    if (ctx->nb_variant == 0)
-        launch_force_integrate(ctx->pos, ctx->vel, ctx->rp, ctx->cs, b, e, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
-                               ctx->vel2, ctx->keys, ctx->stream);
-    else
-        launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, b, e, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
-                           ctx->vel2, ctx->keys, ctx->stream);
+    force_range(ctx, b, e, dt, fext);
 }
 
 int sph_slab_force(sph_ctx* ctx, float dt, int32_t part) {

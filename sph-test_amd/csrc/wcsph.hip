@@ -16,29 +16,31 @@ namespace sph {
 
 constexpr int NB_BLK = 256;
 
-// The 9 contiguous neighbour rows (SPEC_SPH.md §0) of a particle at (x,y,z).
+// The 9 neighbour rows (SPEC_SPH.md §0) of a particle at (x,y,z), each trimmed to its z window.
 struct RowIter {
-    int32_t cx, cy, z0, z1;
+    int32_t cx, cy;
+    float fx, fy, gzf;
 };
 
 __device__ __forceinline__ RowIter row_iter(const GridDesc& g, float x, float y, float z) {
     RowIter it;
     it.cx = cell_cx(g, x);
     it.cy = cell_coord(y, g.oy, g.inv_cell, g.gy);
-    const int32_t cz = cell_coord(z, g.oz, g.inv_cell, g.gz);
-    it.z0 = cz > 0 ? cz - 1 : 0;
-    it.z1 = cz < g.gz - 1 ? cz + 1 : g.gz - 1;
+    cell_fracs(g, x, y, z, it.cx, it.cy, it.fx, it.fy, it.gzf);
     return it;
 }
 
-// Row k (0..8, dx-major) as a sorted-index range; false if the row is outside the grid.
+// Row k (0..8, dx-major) as a sorted-index range; false if the row is outside the grid or ≥ 2h away.
 __device__ __forceinline__ bool row_range(const GridDesc& g, const uint32_t* __restrict__ cs,
                                           const RowIter& it, int k, uint32_t& j0, uint32_t& j1) {
-    const int32_t xx = it.cx + k / 3 - 1, yy = it.cy + k % 3 - 1;
+    const int dx = k / 3 - 1, dy = k % 3 - 1;
+    const int32_t xx = it.cx + dx, yy = it.cy + dy;
     if (xx < 0 || xx >= g.gx || yy < 0 || yy >= g.gy) return false;
+    int32_t zlo, zhi;
+    if (!row_window(g, it.fx, it.fy, it.gzf, dx, dy, zlo, zhi)) return false;
     const uint32_t rowk = ((uint32_t)xx * (uint32_t)g.gy + (uint32_t)yy) * (uint32_t)g.gz;
-    j0 = cs[rowk + (uint32_t)it.z0];
-    j1 = cs[rowk + (uint32_t)it.z1 + 1u];
+    j0 = cs[rowk + (uint32_t)zlo];
+    j1 = cs[rowk + (uint32_t)zhi + 1u];
     return true;
 }
 

@@ -2,31 +2,33 @@
 //
 // A workgroup owns 256 consecutive cell-sorted targets. Their keys span [kf, kl]. For each of
 // the 9 (dx,dy) row offsets `off`, the block's candidates are the ONE contiguous sorted
-// interval of keys [kf+off-1, kl+off+1], and every target's own row range lies inside it
-// (SPEC_SPH.md §0). The interval is staged into LDS with coalesced loads (chunks of TT_CH),
-// and every target walks its own sub-range out of LDS. Lanes of one cell read the same LDS
-// address (broadcast). The visit order is the §0 order.
+// interval of keys [kf+off-zwin, kl+off+zwin], and every target's own trimmed row window
+// lies inside it (SPEC_SPH.md §0). The three intervals of one dx plane are staged into LDS
+// together: one barrier pair per plane, three coalesced streams in flight. Every target then
+// walks its own three windows out of LDS, and lanes of one cell read the same address
+// (broadcast). The visit order is the §0 order.
 //
 // Scan: 4 candidates per iteration, branchless (clamped LDS reads, predicated
-// accumulation), so four ds_reads are in flight per lane instead of one.
-// Force pass: only ~16% of candidates are within 2h. Running the ~50-op pair body under a
-// divergent mask would cost every candidate the full body. So the scan appends hits (u16
-// LDS index) to a per-lane LDS list (unconditional store, predicated increment), and a
-// wave-uniform flush runs the body over the lists with nearly full lanes.
-// A block whose targets span many sparse rows gets huge intervals. If an interval exceeds
-// TT_FALLBACK candidates, that offset is gathered directly from global memory instead.
+// accumulation). Force pass: only ~25% of the trimmed candidates are within 2h. So the scan
+// appends hits (u16 LDS index) to a per-lane LDS list with an unconditional store and a
+// predicated increment. A wave-uniform flush then runs the ~50-op pair body with nearly full
+// lanes, once per plane (or when a list fills).
+// A plane whose intervals exceed TT_GCAP candidates (sparse blocks spanning many rows) is
+// processed offset by offset in chunks, and an offset beyond TT_FALLBACK is gathered directly
+// from global memory.
 #include "common.h"
 
 namespace sph {
 
 constexpr int TT_BLK = 256;        // targets per workgroup
-constexpr int TT_CH = 512;         // candidates per LDS chunk
+constexpr int TT_GCAP = 1024;      // candidates staged per plane (LDS)
 constexpr int TT_CAP = 32;         // per-lane hit list (force)
-constexpr int TT_FALLBACK = 4 * TT_CH;
+constexpr int TT_FALLBACK = 4 * TT_GCAP;
 
 struct BlockRows {
     int64_t kf, kl;           // key range of the block's targets
-    int32_t cx, cy, z0, z1;   // this lane's cell (x, y) and z window
+    int32_t cx, cy;           // this lane's cell (x, y)
+    float fx, fy, gzf;        // in-cell fractions and z sub-cell coordinate (row_window)
 };
 
 __device__ __forceinline__ BlockRows block_rows(const GridDesc& g, const float4* __restrict__ pos, int32_t i0,
@@ -37,34 +39,39 @@ __device__ __forceinline__ BlockRows block_rows(const GridDesc& g, const float4*
     b.kl = cell_key(g, pl.x, pl.y, pl.z);
     b.cx = cell_cx(g, pi.x);
     b.cy = cell_coord(pi.y, g.oy, g.inv_cell, g.gy);
-    const int32_t cz = cell_coord(pi.z, g.oz, g.inv_cell, g.gz);
-    b.z0 = cz > 0 ? cz - 1 : 0;
-    b.z1 = cz < g.gz - 1 ? cz + 1 : g.gz - 1;
+    cell_fracs(g, pi.x, pi.y, pi.z, b.cx, b.cy, b.fx, b.fy, b.gzf);
     return b;
 }
 
-// Interval of row offset k for the block ([c0,c1) sorted indices) and this lane's row [r0,r1).
-__device__ __forceinline__ void offset_ranges(const GridDesc& g, const uint32_t* __restrict__ cs,
-                                              const BlockRows& b, bool valid, int k, int32_t& c0, int32_t& c1,
-                                              int32_t& r0, int32_t& r1) {
+// Block interval of row offset k ([c0,c1) sorted slots; uniform over the block).
+__device__ __forceinline__ void block_interval(const GridDesc& g, const uint32_t* __restrict__ cs, const BlockRows& b,
+                                               int k, int32_t& c0, int32_t& c1) {
     const int32_t dxk = k / 3 - 1, dyk = k % 3 - 1;
     const int64_t off = ((int64_t)dxk * g.gy + dyk) * g.gz;
-    int64_t ka = b.kf + off - 1, kb = b.kl + off + 1;
+    int64_t ka = b.kf + off - g.zwin, kb = b.kl + off + g.zwin;
     const int64_t last = (int64_t)g.ncells - 1;
     if (kb < 0 || ka > last) {
         c0 = c1 = 0;
-    } else {
-        ka = ka < 0 ? 0 : ka;
-        kb = kb > last ? last : kb;
-        c0 = (int32_t)cs[ka];
-        c1 = (int32_t)cs[kb + 1];
+        return;
     }
+    ka = ka < 0 ? 0 : ka;
+    kb = kb > last ? last : kb;
+    c0 = (int32_t)cs[ka];
+    c1 = (int32_t)cs[kb + 1];
+}
+
+// This lane's trimmed window of row offset k ([r0,r1) sorted slots, empty if out of range).
+__device__ __forceinline__ void lane_window(const GridDesc& g, const uint32_t* __restrict__ cs, const BlockRows& b,
+                                            bool valid, int k, int32_t& r0, int32_t& r1) {
+    const int32_t dxk = k / 3 - 1, dyk = k % 3 - 1;
     const int32_t xx = b.cx + dxk, yy = b.cy + dyk;
     r0 = r1 = 0;
-    if (valid && xx >= 0 && xx < g.gx && yy >= 0 && yy < g.gy) {
+    int32_t zlo, zhi;
+    if (valid && xx >= 0 && xx < g.gx && yy >= 0 && yy < g.gy &&
+        row_window(g, b.fx, b.fy, b.gzf, dxk, dyk, zlo, zhi)) {
         const uint32_t rowk = ((uint32_t)xx * (uint32_t)g.gy + (uint32_t)yy) * (uint32_t)g.gz;
-        r0 = (int32_t)cs[rowk + (uint32_t)b.z0];
-        r1 = (int32_t)cs[rowk + (uint32_t)b.z1 + 1u];
+        r0 = (int32_t)cs[rowk + (uint32_t)zlo];
+        r1 = (int32_t)cs[rowk + (uint32_t)zhi + 1u];
     }
 }
 
@@ -81,43 +88,76 @@ __device__ __forceinline__ float spline_w(const SphConst& c, float r2) {
     return r2 < c.four_h2 ? w : 0.0f;
 }
 
+// Stage the plane's three intervals back to back: slot t of interval r sits at off[r] + t.
+template <typename F>
+__device__ __forceinline__ void stage_plane(const int32_t (&c0)[3], const int32_t (&len)[3], int32_t total, F&& put) {
+    for (int32_t t = threadIdx.x; t < total; t += TT_BLK) {
+        const int r = t < len[0] ? 0 : (t < len[0] + len[1] ? 1 : 2);
+        const int32_t o = r == 0 ? 0 : (r == 1 ? len[0] : len[0] + len[1]);
+        put(t, (r == 0 ? c0[0] : (r == 1 ? c0[1] : c0[2])) + (t - o));
+    }
+}
+
 __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restrict__ pos,
                                                           const uint32_t* __restrict__ cs, int32_t ib, int32_t n,
                                                           GridDesc g, SphConst c, float2* __restrict__ rp) {
-    __shared__ float4 sp[TT_CH + 4];
-    const int tid = threadIdx.x;
+    __shared__ float4 sp[TT_GCAP + 4];
     const int32_t i0 = ib + blockIdx.x * TT_BLK;
-    const int32_t i = i0 + tid;
+    const int32_t i = i0 + threadIdx.x;
     const bool valid = i < n;
     const int32_t ilast = min(i0 + TT_BLK, n) - 1;
     const float4 pi = pos[valid ? i : ilast];
     const BlockRows b = block_rows(g, pos, i0, ilast, pi);
     float s = 0.0f;
+    auto scan = [&](int32_t lo, int32_t ln) {
+        int32_t t = 0;
+        for (; t + 4 <= ln; t += 4) {
+            const float4 a = sp[lo + t], bb = sp[lo + t + 1], cc = sp[lo + t + 2], d = sp[lo + t + 3];
+            s += spline_w(c, dist2(pi, a));
+            s += spline_w(c, dist2(pi, bb));
+            s += spline_w(c, dist2(pi, cc));
+            s += spline_w(c, dist2(pi, d));
+        }
+        for (; t < ln; ++t) s += spline_w(c, dist2(pi, sp[lo + t]));
+    };
 #pragma unroll 1
-    for (int k = 0; k < 9; ++k) {
-        int32_t c0, c1, r0, r1;
-        offset_ranges(g, cs, b, valid, k, c0, c1, r0, r1);
-        if (c1 - c0 > TT_FALLBACK) {           // sparse block: gather this row directly
-            for (int32_t j = r0; j < r1; ++j) s += spline_w(c, dist2(pi, pos[j]));
+    for (int p = 0; p < 3; ++p) {
+        int32_t c0[3], c1[3], len[3], r0[3], r1[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            block_interval(g, cs, b, 3 * p + r, c0[r], c1[r]);
+            len[r] = c1[r] - c0[r];
+            lane_window(g, cs, b, valid, 3 * p + r, r0[r], r1[r]);
+        }
+        const int32_t total = len[0] + len[1] + len[2];
+        if (total <= TT_GCAP) {
+            __syncthreads();
+            stage_plane(c0, len, total, [&](int32_t t, int32_t src) { sp[t] = pos[src]; });
+            __syncthreads();
+            int32_t o = 0;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                scan(o + (r0[r] - c0[r]), r1[r] - r0[r]);
+                o += len[r];
+            }
             continue;
         }
+        // sparse block: offset by offset, in chunks, or straight from global memory
 #pragma unroll 1
-        for (int32_t base = c0; base < c1; base += TT_CH) {
-            const int32_t len = min(TT_CH, c1 - base);
-            __syncthreads();
-            for (int t = tid; t < len; t += TT_BLK) sp[t] = pos[base + t];
-            __syncthreads();
-            const int32_t lo = max(r0, base) - base;
-            const int32_t ln = max(min(r1, base + len) - base - lo, 0);
-            int32_t t = 0;
-            for (; t + 4 <= ln; t += 4) {
-                const float4 a = sp[lo + t], bb = sp[lo + t + 1], cc = sp[lo + t + 2], d = sp[lo + t + 3];
-                s += spline_w(c, dist2(pi, a));
-                s += spline_w(c, dist2(pi, bb));
-                s += spline_w(c, dist2(pi, cc));
-                s += spline_w(c, dist2(pi, d));
+        for (int r = 0; r < 3; ++r) {
+            if (len[r] > TT_FALLBACK) {
+                for (int32_t j = r0[r]; j < r1[r]; ++j) s += spline_w(c, dist2(pi, pos[j]));
+                continue;
             }
-            for (; t < ln; ++t) s += spline_w(c, dist2(pi, sp[lo + t]));
+#pragma unroll 1
+            for (int32_t base = c0[r]; base < c1[r]; base += TT_GCAP) {
+                const int32_t ln = min(TT_GCAP, c1[r] - base);
+                __syncthreads();
+                for (int32_t t = threadIdx.x; t < ln; t += TT_BLK) sp[t] = pos[base + t];
+                __syncthreads();
+                const int32_t lo = max(r0[r], base) - base;
+                scan(lo, max(min(r1[r], base + ln) - base - lo, 0));
+            }
         }
     }
     if (!valid) return;
@@ -158,8 +198,8 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
     const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, float dt, float fext_x,
     float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o) {
-    __shared__ float4 sp[TT_CH + 4];     // (x, y, z, ρ)
-    __shared__ float4 sv[TT_CH + 4];     // (u, v, w, P/ρ²)
+    __shared__ float4 sp[TT_GCAP + 4];     // (x, y, z, ρ)
+    __shared__ float4 sv[TT_GCAP + 4];     // (u, v, w, P/ρ²)
     __shared__ uint16_t lst[TT_CAP][TT_BLK];
     const int tid = threadIdx.x;
     const int32_t i0 = ib + blockIdx.x * TT_BLK;
@@ -181,51 +221,76 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         }
         cnt = 0;
     };
-#pragma unroll 1
-    for (int k = 0; k < 9; ++k) {
-        int32_t c0, c1, r0, r1;
-        offset_ranges(g, cs, b, valid, k, c0, c1, r0, r1);
-        if (c1 - c0 > TT_FALLBACK) {           // sparse block: gather this row directly
-            for (int32_t j = r0; j < r1; ++j) {
-                const float4 pj = pos[j];
-                if (j != i && dist2(pi, pj) < c.four_h2) {
-                    const float4 vj = vel[j];
-                    const float2 rj = rp[j];
-                    pair_force(c, pi, vi, ri.x, ri.y, make_float4(pj.x, pj.y, pj.z, rj.x),
-                               make_float4(vj.x, vj.y, vj.z, rj.y), acc);
-                }
-            }
-            continue;
+    // scan LDS slots [lo, lo+ln) (self at LDS slot `self`), appending hits
+    auto scan = [&](int32_t lo, int32_t ln, int32_t self) {
+        for (int t = 0; __any(t < ln); t += 4) {
+            const int32_t j = min(lo + t, TT_GCAP);   // lanes past their range stay in the array
+            const float4 a = sp[j], bb = sp[j + 1], cc = sp[j + 2], d = sp[j + 3];
+            const bool h0 = t < ln && j != self && dist2(pi, a) < c.four_h2;
+            const bool h1 = t + 1 < ln && j + 1 != self && dist2(pi, bb) < c.four_h2;
+            const bool h2 = t + 2 < ln && j + 2 != self && dist2(pi, cc) < c.four_h2;
+            const bool h3 = t + 3 < ln && j + 3 != self && dist2(pi, d) < c.four_h2;
+            lst[cnt][tid] = (uint16_t)j;       cnt += h0;
+            lst[cnt][tid] = (uint16_t)(j + 1); cnt += h1;
+            lst[cnt][tid] = (uint16_t)(j + 2); cnt += h2;
+            lst[cnt][tid] = (uint16_t)(j + 3); cnt += h3;
+            if (__any(cnt > TT_CAP - 4)) flush();
         }
+    };
+    auto put = [&](int32_t t, int32_t src) {
+        const float4 p = pos[src], v = vel[src];
+        const float2 r = rp[src];
+        sp[t] = make_float4(p.x, p.y, p.z, r.x);
+        sv[t] = make_float4(v.x, v.y, v.z, r.y);
+    };
 #pragma unroll 1
-        for (int32_t base = c0; base < c1; base += TT_CH) {
-            const int32_t len = min(TT_CH, c1 - base);
+    for (int p = 0; p < 3; ++p) {
+        int32_t c0[3], c1[3], len[3], r0[3], r1[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            block_interval(g, cs, b, 3 * p + r, c0[r], c1[r]);
+            len[r] = c1[r] - c0[r];
+            lane_window(g, cs, b, valid, 3 * p + r, r0[r], r1[r]);
+        }
+        const int32_t total = len[0] + len[1] + len[2];
+        if (total <= TT_GCAP) {
             __syncthreads();
-            for (int t = tid; t < len; t += TT_BLK) {
-                const float4 p = pos[base + t], v = vel[base + t];
-                const float2 r = rp[base + t];
-                sp[t] = make_float4(p.x, p.y, p.z, r.x);
-                sv[t] = make_float4(v.x, v.y, v.z, r.y);
-            }
+            stage_plane(c0, len, total, put);
             __syncthreads();
-            const int32_t lo = max(r0, base) - base;
-            const int32_t ln = max(min(r1, base + len) - base - lo, 0);
-            const int32_t self = i - base - lo;     // self's position in my sub-range
-            for (int t = 0; __any(t < ln); t += 4) {
-                // four candidates per iteration; reads past ln hit the padded tail (masked)
-                const int32_t j = min(lo + t, TT_CH);   // lanes past their range stay in the array
-                const float4 a = sp[j], bb = sp[j + 1], cc = sp[j + 2], d = sp[j + 3];
-                const bool h0 = t < ln && t != self && dist2(pi, a) < c.four_h2;
-                const bool h1 = t + 1 < ln && t + 1 != self && dist2(pi, bb) < c.four_h2;
-                const bool h2 = t + 2 < ln && t + 2 != self && dist2(pi, cc) < c.four_h2;
-                const bool h3 = t + 3 < ln && t + 3 != self && dist2(pi, d) < c.four_h2;
-                lst[cnt][tid] = (uint16_t)j;       cnt += h0;
-                lst[cnt][tid] = (uint16_t)(j + 1); cnt += h1;
-                lst[cnt][tid] = (uint16_t)(j + 2); cnt += h2;
-                lst[cnt][tid] = (uint16_t)(j + 3); cnt += h3;
-                if (__any(cnt > TT_CAP - 4)) flush();
+            int32_t o = 0;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                scan(o + (r0[r] - c0[r]), r1[r] - r0[r], o + (i - c0[r]));
+                o += len[r];
             }
             flush();
+            continue;
+        }
+        // sparse block: offset by offset, in chunks, or straight from global memory
+#pragma unroll 1
+        for (int r = 0; r < 3; ++r) {
+            if (len[r] > TT_FALLBACK) {
+                for (int32_t j = r0[r]; j < r1[r]; ++j) {
+                    const float4 pj = pos[j];
+                    if (j != i && dist2(pi, pj) < c.four_h2) {
+                        const float4 vj = vel[j];
+                        const float2 rj = rp[j];
+                        pair_force(c, pi, vi, ri.x, ri.y, make_float4(pj.x, pj.y, pj.z, rj.x),
+                                   make_float4(vj.x, vj.y, vj.z, rj.y), acc);
+                    }
+                }
+                continue;
+            }
+#pragma unroll 1
+            for (int32_t base = c0[r]; base < c1[r]; base += TT_GCAP) {
+                const int32_t ln = min(TT_GCAP, c1[r] - base);
+                __syncthreads();
+                for (int32_t t = tid; t < ln; t += TT_BLK) put(t, base + t);
+                __syncthreads();
+                const int32_t lo = max(r0[r], base) - base;
+                scan(lo, max(min(r1[r], base + ln) - base - lo, 0), i - base);
+                flush();
+            }
         }
     }
     if (!valid) return;

@@ -211,12 +211,13 @@ def test_grid_sort_and_cell_start(oracle):
 
 def test_grid_keys_clamp(oracle):
     O = oracle
-    p = _sph(O, L=(0.24, 0.24, 0.24))            # cell 0.024 -> G = 11
+    p = _sph(O, L=(0.24, 0.24, 0.24))            # cell 0.024 -> 11 cells in x, y; z sub-cells 0.006 -> 41
     G = list(p.grid.G)
-    assert G == [11, 11, 11]
-    pos = np.array([[-1, -1, -1], [0.0, 0.0, 0.0], [0.0241, 0.0, 0.0], [5, 5, 5], [np.nan, 0, 0]], np.float32)
+    assert G == [11, 11, 41]
+    pos = np.array([[-1, -1, -1], [0.0, 0.0, 0.0], [0.0241, 0.0, 0.0], [5, 5, 5], [np.nan, 0, 0],
+                    [0.0, 0.0, 0.0061]], np.float32)
     k = O.grid_keys(p, pos)
-    assert k.tolist() == [0, 0, 1 * 121, 10 * 121 + 10 * 11 + 10, 0]
+    assert k.tolist() == [0, 0, 1 * 11 * 41, 10 * 11 * 41 + 10 * 41 + 40, 0, 1]
 
 
 def test_lattice_deterministic_and_bounded(oracle):
