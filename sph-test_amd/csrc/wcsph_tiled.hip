@@ -20,6 +20,10 @@
 
 namespace sph {
 
+#ifndef SPH_FORCE_ABL
+#define SPH_FORCE_ABL 0   // ablation builds for profiling only (scripts/gpu_ablate.sh)
+#endif
+
 constexpr int TT_BLK = 256;        // targets per workgroup
 constexpr int TT_GCAP = 1024;      // candidates staged per plane (LDS)
 constexpr int TT_CAP = 32;         // per-lane hit list (force)
@@ -80,12 +84,22 @@ __device__ __forceinline__ float dist2(float4 a, float4 b) {
     return dx * dx + dy * dy + dz * dz;
 }
 
-// Unnormalised cubic spline w(q) (W = σ·w) for r² < 4h², else 0; branchless.
-__device__ __forceinline__ float spline_w(const SphConst& c, float r2) {
+// 4·w(q) of the unnormalised cubic spline (W = σ·w) for r² < 4h², else 0. Branchless: both arms
+// are computed and selected (a ?: over expressions compiles to an exec branch per candidate).
+// Scaling by 4 (and the final 0.25) is exact in binary floating point: no rounding is added.
+__device__ __forceinline__ float spline_w4(const SphConst& c, float r2) {
     const float q = __builtin_amdgcn_sqrtf(r2) * c.inv_h;
     const float t = 2.0f - q;
-    const float w = q < 1.0f ? 1.0f + q * q * (-1.5f + 0.75f * q) : 0.25f * t * t * t;
+    const float w_in = fmaf(q * q, fmaf(3.0f, q, -6.0f), 4.0f), w_out = t * t * t;
+    const float w = q < 1.0f ? w_in : w_out;
     return r2 < c.four_h2 ? w : 0.0f;
+}
+
+// The scans use x, y, z only, and the compiler then narrows the float4 LDS read to
+// ds_read_b96: 8 LDS cycles per wave with 32-bank grouping, against 4 for ds_read_b128
+// (MI355X_MICROARCH.md §LDS). The empty asm consumes .w at no instruction cost so the 16-B read stays.
+__device__ __forceinline__ void keep_b128(float4 a, float4 b, float4 c, float4 d) {
+    asm volatile("" ::"v"(a.w), "v"(b.w), "v"(c.w), "v"(d.w));
 }
 
 // Stage the plane's three intervals back to back: slot t of interval r sits at off[r] + t.
@@ -113,12 +127,13 @@ __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restri
         int32_t t = 0;
         for (; t + 4 <= ln; t += 4) {
             const float4 a = sp[lo + t], bb = sp[lo + t + 1], cc = sp[lo + t + 2], d = sp[lo + t + 3];
-            s += spline_w(c, dist2(pi, a));
-            s += spline_w(c, dist2(pi, bb));
-            s += spline_w(c, dist2(pi, cc));
-            s += spline_w(c, dist2(pi, d));
+            s += spline_w4(c, dist2(pi, a));
+            s += spline_w4(c, dist2(pi, bb));
+            s += spline_w4(c, dist2(pi, cc));
+            s += spline_w4(c, dist2(pi, d));
+            keep_b128(a, bb, cc, d);
         }
-        for (; t < ln; ++t) s += spline_w(c, dist2(pi, sp[lo + t]));
+        for (; t < ln; ++t) s += spline_w4(c, dist2(pi, sp[lo + t]));
     };
 #pragma unroll 1
     for (int p = 0; p < 3; ++p) {
@@ -146,7 +161,7 @@ __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restri
 #pragma unroll 1
         for (int r = 0; r < 3; ++r) {
             if (len[r] > TT_FALLBACK) {
-                for (int32_t j = r0[r]; j < r1[r]; ++j) s += spline_w(c, dist2(pi, pos[j]));
+                for (int32_t j = r0[r]; j < r1[r]; ++j) s += spline_w4(c, dist2(pi, pos[j]));
                 continue;
             }
 #pragma unroll 1
@@ -161,7 +176,7 @@ __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restri
         }
     }
     if (!valid) return;
-    const float d = c.mass * (c.sigma * s);
+    const float d = c.mass * (c.sigma * (0.25f * s));
     const float tr = d * c.inv_rho0;
     const float t2 = tr * tr, t4 = t2 * t2;
     const float P = c.B * (t4 * t2 * tr - 1.0f);
@@ -172,32 +187,55 @@ struct ForceAcc {
     float ax, ay, az, sx, sy, sz;
 };
 
-// Pair body (SPEC_SPH.md §2). pj = (x, y, z, ρ_j), vj = (u, v, w, P_j/ρ_j²). Branchless.
-__device__ __forceinline__ void pair_force(const SphConst& c, float4 pi, float4 vi, float rhoi, float prhoi,
-                                           float4 pj, float4 vj, ForceAcc& a) {
+// Per-launch constants of the pair body, folded on the host from SphConst (SPEC_SPH.md §2):
+//   W = σ·w4/4 with w4 = 4 + q²(3q − 6) (q < 1) or (2 − q)³;  G = −m·F (the kernel-gradient factor)
+//   G = kin_a·q + kin_b (q < 1) or kout·(2 − q)²/r;  Π_ij·ρ̄ = 2·α·c0·h·min(v·r, 0)/(r² + η²)
+struct PairK {
+    float inv_h, kin_a, kin_b, kout, kvisc, eta2, kx;
+};
+
+static PairK pair_constants(const SphConst& c) {
+    PairK k;
+    k.inv_h = c.inv_h;
+    k.kin_a = -2.25f * c.mass * c.sigma_h2;
+    k.kin_b = 3.0f * c.mass * c.sigma_h2;
+    k.kout = 0.75f * c.mass * c.sigma_h;
+    k.kvisc = -2.0f * c.ac0 * c.h;            // inv_rbar = 2/(ρi + ρj)
+    k.eta2 = c.eta2;
+    k.kx = 0.5f * c.eps * c.mass * c.sigma;   // ε·m·W/ρ̄ = kx·w4/(ρi + ρj)
+    return k;
+}
+
+// Pair body (SPEC_SPH.md §2). pj = (x, y, z, ρ_j), vj = (u, v, w, P_j/ρ_j²). Branchless, for
+// pairs with r < 2h: one rsq gives r and 1/r; r = 0 (coincident, distinct particles) gives q = 0.
+__device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi, float rhoi, float prhoi, float4 pj,
+                                           float4 vj, ForceAcc& a) {
     const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
     const float r2 = dx * dx + dy * dy + dz * dz;
-    const float r = __builtin_amdgcn_sqrtf(r2);
-    const float q = r * c.inv_h;
+    const float rs = __builtin_amdgcn_rsqf(fmaxf(r2, 1e-30f));
+    const float q = r2 * rs * k.inv_h;
     const float t = 2.0f - q;
+    const float t2 = t * t;
     const bool inner = q < 1.0f;
-    const float W = c.sigma * (inner ? 1.0f + q * q * (-1.5f + 0.75f * q) : 0.25f * t * t * t);
-    const float F = inner ? c.sigma_h2 * (-3.0f + 2.25f * q) : -c.sigma_h * 0.75f * t * t * __builtin_amdgcn_rcpf(r);
+    // both arms first, then a plain select (a ?: over expressions compiles to an exec branch)
+    const float w_in = fmaf(q * q, fmaf(3.0f, q, -6.0f), 4.0f), w_out = t2 * t;
+    const float g_in = fmaf(k.kin_a, q, k.kin_b), g_out = k.kout * t2 * rs;
+    const float w4 = inner ? w_in : w_out;
+    const float G = inner ? g_in : g_out;
     const float du = vi.x - vj.x, dv = vi.y - vj.y, dw = vi.z - vj.z;
     const float vr = du * dx + dv * dy + dw * dz;
-    const float inv_rbar = __builtin_amdgcn_rcpf(0.5f * (rhoi + pj.w));
-    const float mu = c.h * vr * __builtin_amdgcn_rcpf(r2 + c.eta2);
-    const float pij = vr < 0.0f ? -c.ac0 * mu * inv_rbar : 0.0f;
-    const float cf = -c.mass * (prhoi + vj.w + pij) * F;
+    const float inv_s = __builtin_amdgcn_rcpf(rhoi + pj.w);
+    const float pij = fminf(vr, 0.0f) * k.kvisc * __builtin_amdgcn_rcpf(r2 + k.eta2) * inv_s;
+    const float cf = (prhoi + vj.w + pij) * G;
     a.ax += cf * dx; a.ay += cf * dy; a.az += cf * dz;
-    const float cx = c.eps * c.mass * inv_rbar * W;
+    const float cx = k.kx * inv_s * w4;
     a.sx -= cx * du; a.sy -= cx * dv; a.sz -= cx * dw;
 }
 
 __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
-    const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, float dt, float fext_x,
-    float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o) {
+    const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, PairK pk, float dt,
+    float fext_x, float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o) {
     __shared__ float4 sp[TT_GCAP + 4];     // (x, y, z, ρ)
     __shared__ float4 sv[TT_GCAP + 4];     // (u, v, w, P/ρ²)
     __shared__ uint16_t lst[TT_CAP][TT_BLK];
@@ -212,28 +250,47 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     const BlockRows b = block_rows(g, pos, i0, ilast, pi);
     ForceAcc acc{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int cnt = 0;
+    // hit lists hold LDS byte offsets (slot·16) of the candidate in sp / sv
+    auto at = [](const float4* base, uint32_t off) {
+        return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + off);
+    };
     auto flush = [&]() {
+#if SPH_FORCE_ABL == 2   // measurement build: scan only, hits dropped
+        acc.ax += 1e-30f * (float)cnt;
+        cnt = 0;
+        return;
+#endif
         for (int q = 0; __any(q < cnt); ++q) {
             if (q < cnt) {
-                const int lj = lst[q][tid];
-                pair_force(c, pi, vi, ri.x, ri.y, sp[lj], sv[lj], acc);
+                const uint32_t off = lst[q][tid];
+#if SPH_FORCE_ABL == 1   // measurement build: trivial pair body
+                acc.ax += 1e-30f * at(sp, off).x; acc.sx += 1e-30f * at(sv, off).w;
+#else
+                pair_force(pk, pi, vi, ri.x, ri.y, at(sp, off), at(sv, off), acc);
+#endif
             }
         }
         cnt = 0;
     };
     // scan LDS slots [lo, lo+ln) (self at LDS slot `self`), appending hits
     auto scan = [&](int32_t lo, int32_t ln, int32_t self) {
+#if SPH_FORCE_ABL == 3   // measurement build: staging only
+        return;
+#endif
         for (int t = 0; __any(t < ln); t += 4) {
             const int32_t j = min(lo + t, TT_GCAP);   // lanes past their range stay in the array
             const float4 a = sp[j], bb = sp[j + 1], cc = sp[j + 2], d = sp[j + 3];
-            const bool h0 = t < ln && j != self && dist2(pi, a) < c.four_h2;
-            const bool h1 = t + 1 < ln && j + 1 != self && dist2(pi, bb) < c.four_h2;
-            const bool h2 = t + 2 < ln && j + 2 != self && dist2(pi, cc) < c.four_h2;
-            const bool h3 = t + 3 < ln && j + 3 != self && dist2(pi, d) < c.four_h2;
-            lst[cnt][tid] = (uint16_t)j;       cnt += h0;
-            lst[cnt][tid] = (uint16_t)(j + 1); cnt += h1;
-            lst[cnt][tid] = (uint16_t)(j + 2); cnt += h2;
-            lst[cnt][tid] = (uint16_t)(j + 3); cnt += h3;
+            // bitwise &, not &&: every read is unconditional (no exec branches around LDS loads)
+            const bool h0 = (t < ln) & (j != self) & (dist2(pi, a) < c.four_h2);
+            const bool h1 = (t + 1 < ln) & (j + 1 != self) & (dist2(pi, bb) < c.four_h2);
+            const bool h2 = (t + 2 < ln) & (j + 2 != self) & (dist2(pi, cc) < c.four_h2);
+            const bool h3 = (t + 3 < ln) & (j + 3 != self) & (dist2(pi, d) < c.four_h2);
+            const uint32_t jb = (uint32_t)j * 16u;
+            lst[cnt][tid] = (uint16_t)jb;         cnt += h0;
+            lst[cnt][tid] = (uint16_t)(jb + 16u); cnt += h1;
+            lst[cnt][tid] = (uint16_t)(jb + 32u); cnt += h2;
+            lst[cnt][tid] = (uint16_t)(jb + 48u); cnt += h3;
+            keep_b128(a, bb, cc, d);
             if (__any(cnt > TT_CAP - 4)) flush();
         }
     };
@@ -275,7 +332,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
                     if (j != i && dist2(pi, pj) < c.four_h2) {
                         const float4 vj = vel[j];
                         const float2 rj = rp[j];
-                        pair_force(c, pi, vi, ri.x, ri.y, make_float4(pj.x, pj.y, pj.z, rj.x),
+                        pair_force(pk, pi, vi, ri.x, ri.y, make_float4(pj.x, pj.y, pj.z, rj.x),
                                    make_float4(vj.x, vj.y, vj.z, rj.y), acc);
                     }
                 }
@@ -316,7 +373,7 @@ void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, 
                         int32_t ie, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o,
                         uint32_t* keys_o, hipStream_t s) {
     if (ie > ib)
-        k_force_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, vel, rp, cs, ib, ie, g, c, dt, fext_x,
+        k_force_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt, fext_x,
                                                                          pos_o, vel_o, keys_o);
 }
 
