@@ -89,8 +89,53 @@ __device__ __forceinline__ void cell_fracs(const GridDesc& g, float x, float y, 
     gzf = (z - g.oz) * g.inv_cz;
 }
 
+// Workgroups are dispatched round-robin over the 8 XCDs, each with its own L2
+// (MI355X_MICROARCH.md). Remapped so that XCD x runs one contiguous range of logical blocks, in
+// order: blocks that stage the same neighbour rows then share one L2 instead of fetching them 8 times.
+__device__ __forceinline__ int32_t xcd_block(int32_t b, int32_t nb) {
+    constexpr int32_t NX = 8;
+    const int32_t x = b % NX, k = b / NX, per = nb / NX, rem = nb % NX;
+    return x * per + (x < rem ? x : rem) + k;
+}
+
 __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+#endif
+
+// Movers of a Model S step (resort.hip): particles whose new cell key differs from the sorted key
+// of their slot. The force pass appends them (any order) for the incremental re-sort.
+struct MoverSink {
+    const uint32_t* sk;   // sorted keys of the slot order; nullptr: no append
+    uint32_t* count;      // this step's mover counter (zero on entry)
+    uint32_t* mi;         // slot index
+    uint32_t* mk;         // new key
+    uint32_t* mo;         // old key
+    uint32_t* rank;       // 3 x cap rank accumulators, zeroed here
+    uint32_t cap;
+};
+
+#if defined(__HIPCC__)
+// Called by every lane that holds a particle (lanes past n have returned): one atomic per wave.
+__device__ __forceinline__ void append_mover(const MoverSink& s, int32_t i, uint32_t key) {
+    if (!s.sk) return;
+    const uint32_t ko = s.sk[i];
+    const bool mv = key != ko;
+    const uint64_t b = __ballot(mv);
+    if (b == 0) return;
+    const int leader = __builtin_ctzll(b);
+    uint32_t base = 0;
+    if ((int)lane_id() == leader) base = atomicAdd(s.count, (uint32_t)__popcll(b));
+    base = __shfl(base, leader, 64);
+    if (mv) {
+        const uint32_t r = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        s.mi[r] = (uint32_t)i;
+        s.mk[r] = key;
+        s.mo[r] = ko;
+        s.rank[r] = 0u;
+        s.rank[s.cap + r] = 0u;
+        s.rank[2 * s.cap + r] = 0u;
+    }
 }
 #endif
 
@@ -103,6 +148,20 @@ size_t radix_hist_elems(int32_t capacity);
 int radix_sort(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, int32_t n,
                int32_t key_bits, bool identity_vals, uint32_t* hist, uint32_t* bin_total,
                hipStream_t s);
+
+// incremental re-sort of a Model S step (resort.hip), from the movers the force pass appended.
+// sk: sorted keys of the slot order; cs: its cell starts, updated in place; count: the movers'
+// counter, count_other: the next step's counter (zeroed here). Writes the re-sorted state to *_o.
+struct ResortScratch {
+    uint32_t *mi, *mk, *mo, *rank;   // appended movers (MoverSink), rank: 3 x cap
+    uint64_t* ms;                    // movers by (new key, slot)
+    uint32_t *mx, *mos;              // movers by slot: slot, old key
+    uint32_t cap;
+};
+void launch_resort(const uint32_t* sk, uint32_t* cs, uint32_t ncells, int32_t n, const float4* pos,
+                   const float4* vel, const int32_t* id, const uint32_t* keys, const uint32_t* count,
+                   uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,
+                   uint32_t* sk_o, hipStream_t s);
 
 // grid / data movement (grid.hip)
 void launch_keys(const float4* pos, int32_t n, const int32_t* id, int32_t n_active_id,
@@ -138,14 +197,14 @@ void launch_density(const float4* pos, const uint32_t* cs, int32_t ib, int32_t i
 void launch_force_integrate(const float4* pos, const float4* vel, const float2* rp,
                             const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
                             float dt, float fext_x, float4* pos_o, float4* vel_o, uint32_t* keys_o,
-                            hipStream_t s);
+                            MoverSink mv, hipStream_t s);
 
 // Model S, LDS-tiled (wcsph_tiled.hip)
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g,
                           SphConst c, float2* rp, hipStream_t s);
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs,
                         int32_t ib, int32_t ie, GridDesc g, SphConst c, float dt, float fext_x,
-                        float4* pos_o, float4* vel_o, uint32_t* keys_o, hipStream_t s);
+                        float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv, hipStream_t s);
 
 // slab decomposition (slab.hip)
 // Order-preserving compaction of the sorted slots [b, e) whose key column satisfies

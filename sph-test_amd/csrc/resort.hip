@@ -1,0 +1,222 @@
+// resort.hip — incremental stable re-sort of a Model S step (SPEC_SPH.md §0 "Sort"), gfx950.
+//
+// After a step the particles are still in the previous step's sorted order, and the force pass
+// has written each particle's new cell key. A key changes only when the particle crosses a
+// sub-cell boundary (~0.5% of the particles per step on C3). The "stayers" (unchanged key) form
+// a subsequence that is already sorted by (key, index), because their keys are the previous
+// sorted keys. The force pass appends the "movers" (append_mover, common.h; any order). Their
+// destinations, and the stayers', follow from counting alone:
+//
+//   stayer i : dst = (i − A(i)) + #{movers x : (k_x, x) < (k_i, i)}
+//   mover  x : dst = (q − A(q)) + #{movers y : (k_y, y) < (k_x, x)},
+//              q = clamp(x, cs_old[k_x], cs_old[k_x + 1])
+//
+// A(q) = #movers with index < q, and cs_old is the previous cell-start table. Stayers with a key
+// below k_x sit exactly below cs_old[k_x]. Stayers with key k_x and a smaller index sit in
+// [cs_old[k_x], q). (key, index) is the total order the stable LSD radix sort realises, so the
+// permutation is bit-identical to the full sort's. All counts are order-independent (the append
+// order does not matter), so every output is deterministic; the only atomics are integer adds.
+// tests/test_resort_logic.py restates the formulas; tests/test_gpu_resort.py compares runs bit
+// for bit with the full sort.
+//
+// Kernels:
+//   k_mv_rank        all-pairs counts per mover: (key, index) rank, index rank, A(q)
+//   k_mv_place       movers: scatter of (pos, vel, id, key); tables by (key, index) and by index
+//   k_mv_merge       stayers: scatter of (pos, vel, id, key)
+//   k_mv_cell_start  cs[k] += #{movers: new key < k} − #{movers: old key < k}, in place
+// The scatters replace the permutation gather, and the update the cell-start rebuild, of the full path.
+#include "common.h"
+
+namespace sph {
+
+constexpr int MV_BLK = 256;
+constexpr int MV_TILE = 256;
+constexpr int MV_RANK_GRID = 2048;
+
+static __device__ __forceinline__ uint64_t comp(uint32_t key, uint32_t idx) { return (uint64_t)key << 32 | idx; }
+
+// first position in sorted a[0, n) with a[pos] >= v
+template <typename T>
+static __device__ __forceinline__ uint32_t lower_bound(const T* __restrict__ a, uint32_t n, T v) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// lower_bound by one wave: 64 probes per level, so a few dependent loads for any n (wave-uniform).
+template <typename T>
+static __device__ uint32_t wave_lower_bound(const T* __restrict__ a, uint32_t n, T v) {
+    const uint32_t lane = lane_id();
+    uint32_t base = 0, len = n;
+    while (len > 64) {
+        const uint32_t step = (len + 63) / 64;
+        const uint32_t idx = base + lane * step;
+        const bool lt = idx < base + len && a[idx] < v;
+        const uint32_t k = (uint32_t)__popcll(__ballot(lt));   // probes below v form a prefix
+        if (k == 0) return base;
+        const uint32_t nb = base + (k - 1) * step + 1;
+        const uint32_t end = k * step < len ? base + k * step : base + len;   // a[end] >= v (or end of range)
+        base = nb;
+        len = end - nb;
+    }
+    const bool lt = lane < len && a[base + lane] < v;
+    return base + (uint32_t)__popcll(__ballot(lt));
+}
+
+// A(i) for the calling lane: movers with index < i (block offset + earlier waves + earlier lanes)
+static __device__ __forceinline__ uint32_t movers_before(bool mv, uint32_t block_off, uint32_t* wc) {
+    const uint64_t b = __ballot(mv);
+    const int w = threadIdx.x >> 6;
+    if (lane_id() == 0) wc[w] = (uint32_t)__popcll(b);
+    __syncthreads();
+    uint32_t off = block_off;
+    for (int k = 0; k < w; ++k) off += wc[k];
+    return off + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+
+// Per mover x (append order): rank[x] = #{y : (k_y, i_y) < (k_x, i_x)}, rank[cap + x] =
+// #{y : i_y < i_x}, rank[2cap + x] = A(q_x) = #{y : i_y < q_x}. Work items = (256 movers) x
+// (256-mover tile); partial counts are added atomically (integers: order-independent).
+// Also zeroes the next step's mover counter.
+__global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__ mtotal,
+                                                    uint32_t* __restrict__ next_count,
+                                                    const uint32_t* __restrict__ cs_old, ResortScratch w) {
+    __shared__ uint64_t tile[MV_TILE];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *next_count = 0u;
+    const uint32_t m = *mtotal;
+    const uint64_t nr = (m + MV_BLK - 1) / MV_BLK, nt = (m + MV_TILE - 1) / MV_TILE;
+    for (uint64_t item = blockIdx.x; item < nr * nt; item += gridDim.x) {
+        const uint32_t ir = (uint32_t)(item % nr), it = (uint32_t)(item / nr);
+        __syncthreads();
+        for (int t = threadIdx.x; t < MV_TILE; t += MV_BLK) {
+            const uint32_t y = it * MV_TILE + t;
+            tile[t] = y < m ? comp(w.mk[y], w.mi[y]) : ~0ull;
+        }
+        __syncthreads();
+        const uint32_t x = ir * MV_BLK + threadIdx.x;
+        if (x < m) {
+            const uint32_t ix = w.mi[x], k = w.mk[x];
+            const uint64_t cx = comp(k, ix);
+            const uint32_t c0 = cs_old[k], c1 = cs_old[k + 1];
+            const uint32_t q = ix < c0 ? c0 : (ix > c1 ? c1 : ix);
+            uint32_t nk = 0, ni = 0, nq = 0;
+#pragma unroll 4
+            for (int t = 0; t < MV_TILE; ++t) {
+                const uint64_t c = tile[t];
+                const uint32_t iy = (uint32_t)c;   // padding: 0xffffffff, never below
+                nk += c < cx;
+                ni += iy < ix;
+                nq += iy < q;
+            }
+            if (nk) atomicAdd(&w.rank[x], nk);
+            if (ni) atomicAdd(&w.rank[w.cap + x], ni);
+            if (nq) atomicAdd(&w.rank[2 * w.cap + x], nq);
+        }
+    }
+}
+
+__global__ __launch_bounds__(MV_BLK) void k_mv_place(const uint32_t* __restrict__ mtotal,
+                                                     const uint32_t* __restrict__ cs_old, ResortScratch w,
+                                                     const float4* __restrict__ pos, const float4* __restrict__ vel,
+                                                     const int32_t* __restrict__ id, float4* __restrict__ pos_o,
+                                                     float4* __restrict__ vel_o, int32_t* __restrict__ id_o,
+                                                     uint32_t* __restrict__ sk_o) {
+    const uint32_t m = *mtotal;
+    for (uint32_t r = blockIdx.x * MV_BLK + threadIdx.x; r < m; r += gridDim.x * MV_BLK) {
+        const uint32_t x = w.mi[r], k = w.mk[r];
+        const uint32_t c0 = cs_old[k], c1 = cs_old[k + 1];
+        const uint32_t q = x < c0 ? c0 : (x > c1 ? c1 : x);
+        const uint32_t rk = w.rank[r], ri = w.rank[w.cap + r], aq = w.rank[2 * w.cap + r];
+        const uint32_t dst = (q - aq) + rk;
+        pos_o[dst] = pos[x];
+        vel_o[dst] = vel[x];
+        id_o[dst] = id[x];
+        sk_o[dst] = k;
+        w.ms[rk] = comp(k, x);
+        w.mx[ri] = x;
+        w.mos[ri] = w.mo[r];   // old keys by slot: ascending
+    }
+}
+
+__global__ __launch_bounds__(MV_BLK) void k_mv_merge(const uint32_t* __restrict__ keys,
+                                                     const uint32_t* __restrict__ sk, int32_t n,
+                                                     const uint32_t* __restrict__ mtotal, ResortScratch w,
+                                                     const float4* __restrict__ pos, const float4* __restrict__ vel,
+                                                     const int32_t* __restrict__ id, float4* __restrict__ pos_o,
+                                                     float4* __restrict__ vel_o, int32_t* __restrict__ id_o,
+                                                     uint32_t* __restrict__ sk_o) {
+    __shared__ uint32_t wc[MV_BLK / 64];
+    __shared__ uint32_t b[3];
+    const int32_t i0 = xcd_block(blockIdx.x, gridDim.x) * MV_BLK;
+    const int32_t i = i0 + threadIdx.x;
+    const int32_t ilast = min(i0 + MV_BLK, n) - 1;
+    const uint32_t m = *mtotal;
+    const int wv = threadIdx.x >> 6;
+    // movers below this block's first slot, and the movers whose (key, index) falls inside its
+    // stayers' range: ms[b1, b2)
+    if (wv == 0) {
+        const uint32_t p = wave_lower_bound(w.mx, m, (uint32_t)i0);
+        if (lane_id() == 0) b[0] = p;
+    } else if (wv < 3) {
+        const uint64_t v = wv == 1 ? comp(sk[i0], (uint32_t)i0) : comp(sk[ilast], (uint32_t)ilast) + 1;
+        const uint32_t p = wave_lower_bound(w.ms, m, v);
+        if (lane_id() == 0) b[wv] = p;
+    }
+    const uint32_t ko = i < n ? sk[i] : 0u;
+    const bool stay = i < n && keys[i] == ko;
+    __syncthreads();
+    const uint32_t a = movers_before(i < n && !stay, b[0], wc);
+    if (!stay) return;
+    const uint32_t lo = b[1], hi = b[2];
+    const uint32_t below = lo + lower_bound(w.ms + lo, hi - lo, comp(ko, (uint32_t)i));
+    const uint32_t dst = ((uint32_t)i - a) + below;
+    pos_o[dst] = pos[i];
+    vel_o[dst] = vel[i];
+    id_o[dst] = id[i];
+    sk_o[dst] = ko;
+}
+
+// cs[k] += #{movers: new key < k} − #{movers: old key < k}, for k in [0, ncells]; 1024 cells per
+// block. A block whose counts agree at its start and that holds no mover key leaves its cells.
+constexpr int MV_CS_CELLS = 4 * MV_BLK;
+
+__global__ __launch_bounds__(MV_BLK) void k_mv_cell_start(uint32_t* __restrict__ cs, uint32_t ncells,
+                                                          const uint32_t* __restrict__ mtotal, ResortScratch w) {
+    __shared__ uint32_t b[4];
+    const uint32_t m = *mtotal;
+    const uint32_t k0 = blockIdx.x * MV_CS_CELLS, k1 = k0 + MV_CS_CELLS;
+    const int wv = threadIdx.x >> 6;
+    const uint32_t p = wv < 2 ? wave_lower_bound(w.ms, m, comp(wv == 0 ? k0 : k1, 0u))
+                              : wave_lower_bound(w.mos, m, wv == 2 ? k0 : k1);
+    if (lane_id() == 0) b[wv] = p;
+    __syncthreads();
+    const uint32_t nlo = b[0], nhi = b[1], olo = b[2], ohi = b[3];
+    if (nlo == olo && nhi == nlo && ohi == olo) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t k = k0 + j * MV_BLK + threadIdx.x;
+        if (k > ncells) break;
+        const uint32_t cn = nlo + lower_bound(w.ms + nlo, nhi - nlo, comp(k, 0u));
+        const uint32_t co = olo + lower_bound(w.mos + olo, ohi - olo, k);
+        cs[k] += cn - co;
+    }
+}
+
+void launch_resort(const uint32_t* sk, uint32_t* cs, uint32_t ncells, int32_t n, const float4* pos,
+                   const float4* vel, const int32_t* id, const uint32_t* keys, const uint32_t* count,
+                   uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,
+                   uint32_t* sk_o, hipStream_t s) {
+    if (n <= 0) return;
+    const int32_t nb = (n + MV_BLK - 1) / MV_BLK;
+    k_mv_rank<<<MV_RANK_GRID, MV_BLK, 0, s>>>(count, count_other, cs, w);
+    k_mv_place<<<std::min(nb, 1024), MV_BLK, 0, s>>>(count, cs, w, pos, vel, id, pos_o, vel_o, id_o, sk_o);
+    k_mv_merge<<<nb, MV_BLK, 0, s>>>(keys, sk, n, count, w, pos, vel, id, pos_o, vel_o, id_o, sk_o);
+    // after every reader of cs_old (k_mv_rank, k_mv_place)
+    k_mv_cell_start<<<(ncells + MV_CS_CELLS) / MV_CS_CELLS, MV_BLK, 0, s>>>(cs, ncells, count, w);
+}
+
+}  // namespace sph

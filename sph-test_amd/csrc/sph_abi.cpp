@@ -68,6 +68,14 @@ struct sph_ctx {
     size_t staging_bytes = 0;
     bool keys_valid = false;
     int32_t keys_active = -1;
+    // incremental re-sort (resort.hip): sorted keys of the current slot order, and scratch
+    uint32_t *sk_cur = nullptr, *sk_next = nullptr;
+    uint32_t *mv_mi = nullptr, *mv_mk = nullptr, *mv_mo = nullptr, *mv_rank = nullptr, *mv_mx = nullptr, *mv_mos = nullptr;
+    uint64_t* mv_ms = nullptr;
+    uint32_t* mv_count = nullptr;   // [2] mover counters, ping-pong by step
+    int mv_par = 0;                 // counter the next force pass appends into
+    bool sk_valid = false;       // sk_cur matches the slot order and cs (set by a Model S sort)
+    bool resort_on = true;       // env SPH_RESORT=0 forces the full radix sort every step
     int64_t steps = 0;
     double sim_time = 0.0;
     sph_drag_input drag{-1, {0.f, 0.f, 0.f}, 0.f};
@@ -137,6 +145,10 @@ void free_all(sph_ctx* c) {
     dfree(c->cs); dfree(c->gaps);
     c->gaps_cap = 0;
     dfree(c->sblk); dfree(c->sdev);
+    dfree(c->sk_cur); dfree(c->sk_next);
+    dfree(c->mv_mi); dfree(c->mv_mk); dfree(c->mv_mo); dfree(c->mv_rank); dfree(c->mv_mx); dfree(c->mv_mos);
+    dfree(c->mv_ms); dfree(c->mv_count);
+    c->sk_valid = false;
     if (c->staging) (void)hipFree(c->staging);
     c->staging = nullptr;
     c->staging_bytes = 0;
@@ -166,6 +178,9 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
         AL(mode, n); AL(mode2, n); AL(torque, 3 * n);
     } else {
         AL(rp, n);
+        AL(sk_cur, n); AL(sk_next, n);
+        AL(mv_mi, n); AL(mv_mk, n); AL(mv_mo, n); AL(mv_rank, 3 * n); AL(mv_mx, n); AL(mv_mos, n); AL(mv_ms, n);
+        AL(mv_count, 2);
     }
 #undef AL
     ctx->staging_bytes = n * 84;
@@ -248,6 +263,7 @@ int derive(sph_ctx* ctx) {
     ctx->grid = g;
     ctx->key_bits = bit_width(g.ncells);   // the sentinel key == ncells must sort last
     ctx->keys_valid = false;
+    ctx->sk_valid = false;
     return ensure_cells(ctx);
 }
 
@@ -311,7 +327,7 @@ void swap_sv(sph_ctx* c) {
     std::swap(c->vel, c->vel2);
 }
 
-int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id) {
+int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id, const uint32_t** sorted_keys = nullptr) {
     const int32_t n = ctx->n;
     if (!ctx->keys_valid || ctx->keys_active != n_active_id) {
         KTimer t(ctx, "keys", 20.0 * n);
@@ -352,6 +368,7 @@ int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id) {
         KTimer t(ctx, "cell_start", 4.0 * (ctx->grid.ncells + 1));
         launch_cell_start(sk, n, ctx->cs, ctx->grid.ncells, ctx->gaps, ctx->sdev + 8, ctx->stream);
     }
+    if (sorted_keys) *sorted_keys = sk;
     return SPH_OK;
 }
 
@@ -362,18 +379,57 @@ void density_range(sph_ctx* ctx, int32_t b, int32_t e) {
         launch_density_tiled(ctx->pos, ctx->cs, b, e, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
 }
 
-void force_range(sph_ctx* ctx, int32_t b, int32_t e, float dt, float fext) {
+void force_range(sph_ctx* ctx, int32_t b, int32_t e, float dt, float fext, MoverSink mv = MoverSink{}) {
     if (ctx->nb_variant == 0)
         launch_force_integrate(ctx->pos, ctx->vel, ctx->rp, ctx->cs, b, e, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
-                               ctx->vel2, ctx->keys, ctx->stream);
+                               ctx->vel2, ctx->keys, mv, ctx->stream);
     else
         launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, b, e, ctx->grid, ctx->sc, dt, fext, ctx->pos2,
-                           ctx->vel2, ctx->keys, ctx->stream);
+                           ctx->vel2, ctx->keys, mv, ctx->stream);
+}
+
+ResortScratch resort_scratch(sph_ctx* ctx) {
+    return ResortScratch{ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_rank, ctx->mv_ms, ctx->mv_mx, ctx->mv_mos,
+                         (uint32_t)std::max(ctx->capacity, 1)};
+}
+
+// The force pass appends movers for the next step's incremental re-sort.
+MoverSink mover_sink(sph_ctx* ctx) {
+    if (!ctx->resort_on || !ctx->sk_valid) return MoverSink{};
+    return MoverSink{ctx->sk_cur, ctx->mv_count + ctx->mv_par, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_rank,
+                     (uint32_t)std::max(ctx->capacity, 1)};
+}
+
+// Bring the slots into stable (key, index) order: the incremental re-sort when the previous
+// step's sorted keys and cell starts describe the current slot order, else the full radix sort.
+int sort_wcsph(sph_ctx* ctx) {
+    const int32_t n = ctx->n;
+    if (ctx->resort_on && ctx->keys_valid && ctx->keys_active == 0 && ctx->sk_valid) {
+        {
+            KTimer t(ctx, "resort", (double)n * (2 * 4 + 2 * 36));
+            const int used = ctx->mv_par;
+            launch_resort(ctx->sk_cur, ctx->cs, ctx->grid.ncells, n, ctx->pos, ctx->vel, ctx->id, ctx->keys,
+                          ctx->mv_count + used, ctx->mv_count + (1 - used), resort_scratch(ctx), ctx->pos2,
+                          ctx->vel2, ctx->id2, ctx->sk_next, ctx->stream);
+            ctx->mv_par = 1 - used;
+        }
+        swap_sv(ctx);
+        std::swap(ctx->id, ctx->id2);
+        std::swap(ctx->sk_cur, ctx->sk_next);
+        return SPH_OK;
+    }
+    const uint32_t* sk = nullptr;
+    int r = sort_and_reorder(ctx, 0, &sk);
+    if (r != SPH_OK) return r;
+    if (n > 0) HIPCHK(hipMemcpyAsync(ctx->sk_cur, sk, (size_t)n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->mv_count, 0, 2 * sizeof(uint32_t), ctx->stream));
+    ctx->sk_valid = true;
+    return SPH_OK;
 }
 
 int step_wcsph(sph_ctx* ctx, float dt) {
     const int32_t n = ctx->n;
-    int r = sort_and_reorder(ctx, 0);
+    int r = sort_wcsph(ctx);
     if (r != SPH_OK) return r;
     {
         KTimer t(ctx, "density", 24.0 * n);
@@ -384,7 +440,7 @@ int step_wcsph(sph_ctx* ctx, float dt) {
     const float fext = p.forcing_amp != 0.0f ? p.forcing_amp * sinf(6.28318530718f * p.forcing_freq * tt) : 0.0f;
     {
         KTimer t(ctx, "force_integrate", 76.0 * n);
-        force_range(ctx, 0, n, dt, fext);
+        force_range(ctx, 0, n, dt, fext, mover_sink(ctx));
     }
     swap_sv(ctx);
     ctx->keys_valid = true;
@@ -458,6 +514,7 @@ int sph_create(const sph_config* cfg, int32_t device, sph_ctx** out) {
     ctx->device = device;
     ctx->profiling = (cfg->flags & SPH_FLAG_PROFILE) != 0;
     if (const char* v = std::getenv("SPH_NB_VARIANT")) ctx->nb_variant = std::atoi(v);
+    if (const char* v = std::getenv("SPH_RESORT")) ctx->resort_on = std::atoi(v) != 0;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return SPH_ERR_HIP;
@@ -586,6 +643,7 @@ int sph_upload_particles_aos84(sph_ctx* ctx, const void* src, int32_t count) {
     HIPCHK(hipStreamSynchronize(ctx->stream));
     ctx->n = count;
     ctx->keys_valid = false;
+    ctx->sk_valid = false;
     ctx->steps = 0;
     ctx->sim_time = 0.0;
     return SPH_OK;
@@ -621,6 +679,7 @@ int sph_upload_state(sph_ctx* ctx, const float* pos3, const float* vel3, int32_t
     HIPCHK(hipStreamSynchronize(ctx->stream));
     ctx->n = count;
     ctx->keys_valid = false;
+    ctx->sk_valid = false;
     ctx->steps = 0;
     ctx->sim_time = 0.0;
     return SPH_OK;
@@ -640,6 +699,7 @@ int sph_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
     HIPCHK(hipStreamSynchronize(ctx->stream));
     ctx->n = (int32_t)n;
     ctx->keys_valid = false;
+    ctx->sk_valid = false;
     ctx->steps = 0;
     ctx->sim_time = 0.0;
     return SPH_OK;
@@ -858,6 +918,7 @@ static int slab_local_grid(sph_ctx* ctx) {
     ctx->grid = g;
     ctx->key_bits = bit_width(g.ncells);
     ctx->keys_valid = false;
+    ctx->sk_valid = false;
     return ensure_cells(ctx);
 }
 
@@ -918,6 +979,7 @@ int sph_slab_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
     ctx->n = ctx->o1 = (int32_t)total;
     ctx->o0 = 0;
     ctx->keys_valid = false;
+    ctx->sk_valid = false;
     ctx->steps = 0;
     ctx->sim_time = 0.0;
     return SPH_OK;
@@ -1023,6 +1085,7 @@ int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void
     ctx->o0 = r[2];
     ctx->o1 = r[3];
     ctx->keys_valid = false;
+    ctx->sk_valid = false;
     return SPH_OK;
 }
 

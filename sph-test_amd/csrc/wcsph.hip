@@ -94,7 +94,7 @@ __global__ __launch_bounds__(NB_BLK) void k_density(const float4* __restrict__ p
 __global__ __launch_bounds__(NB_BLK) void k_force_integrate(
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
     const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, float dt, float fext_x,
-    float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o) {
+    float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o, MoverSink mv) {
     const int32_t i = ib + blockIdx.x * NB_BLK + threadIdx.x;
     if (i >= n) return;
     const float4 pi = pos[i];
@@ -140,7 +140,9 @@ __global__ __launch_bounds__(NB_BLK) void k_force_integrate(
     }
     pos_o[i] = make_float4(np[0], np[1], np[2], 0.f);
     vel_o[i] = make_float4(nv[0], nv[1], nv[2], 0.f);
-    keys_o[i] = cell_key(g, np[0], np[1], np[2]);
+    const uint32_t key = cell_key(g, np[0], np[1], np[2]);
+    keys_o[i] = key;
+    append_mover(mv, i, key);
 }
 
 void launch_density(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
@@ -150,10 +152,10 @@ void launch_density(const float4* pos, const uint32_t* cs, int32_t ib, int32_t i
 
 void launch_force_integrate(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,
                             int32_t ie, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o,
-                            float4* vel_o, uint32_t* keys_o, hipStream_t s) {
+                            float4* vel_o, uint32_t* keys_o, MoverSink mv, hipStream_t s) {
     if (ie > ib)
         k_force_integrate<<<(ie - ib + NB_BLK - 1) / NB_BLK, NB_BLK, 0, s>>>(pos, vel, rp, cs, ib, ie, g, c, dt,
-                                                                             fext_x, pos_o, vel_o, keys_o);
+                                                                             fext_x, pos_o, vel_o, keys_o, mv);
 }
 
 }  // namespace sph

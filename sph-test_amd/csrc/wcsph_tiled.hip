@@ -116,7 +116,7 @@ __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restri
                                                           const uint32_t* __restrict__ cs, int32_t ib, int32_t n,
                                                           GridDesc g, SphConst c, float2* __restrict__ rp) {
     __shared__ float4 sp[TT_GCAP + 4];
-    const int32_t i0 = ib + blockIdx.x * TT_BLK;
+    const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
     const int32_t i = i0 + threadIdx.x;
     const bool valid = i < n;
     const int32_t ilast = min(i0 + TT_BLK, n) - 1;
@@ -235,12 +235,12 @@ __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi,
 __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
     const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, PairK pk, float dt,
-    float fext_x, float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o) {
+    float fext_x, float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o, MoverSink mv) {
     __shared__ float4 sp[TT_GCAP + 4];     // (x, y, z, ρ)
     __shared__ float4 sv[TT_GCAP + 4];     // (u, v, w, P/ρ²)
     __shared__ uint16_t lst[TT_CAP][TT_BLK];
     const int tid = threadIdx.x;
-    const int32_t i0 = ib + blockIdx.x * TT_BLK;
+    const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
     const int32_t i = i0 + tid;
     const bool valid = i < n;
     const int32_t ilast = min(i0 + TT_BLK, n) - 1;
@@ -361,7 +361,9 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     }
     pos_o[i] = make_float4(np[0], np[1], np[2], 0.f);
     vel_o[i] = make_float4(nv[0], nv[1], nv[2], 0.f);
-    keys_o[i] = cell_key(g, np[0], np[1], np[2]);
+    const uint32_t key = cell_key(g, np[0], np[1], np[2]);
+    keys_o[i] = key;
+    append_mover(mv, i, key);
 }
 
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
@@ -371,10 +373,10 @@ void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int
 
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,
                         int32_t ie, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o,
-                        uint32_t* keys_o, hipStream_t s) {
+                        uint32_t* keys_o, MoverSink mv, hipStream_t s) {
     if (ie > ib)
         k_force_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt, fext_x,
-                                                                         pos_o, vel_o, keys_o);
+                                                                         pos_o, vel_o, keys_o, mv);
 }
 
 }  // namespace sph

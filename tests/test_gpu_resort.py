@@ -1,0 +1,90 @@
+"""Incremental re-sort (sph-test_amd/csrc/resort.hip) against the full radix sort.
+
+Both realise the stable (cell key, slot index) order of SPEC_SPH.md §0, so the slot
+permutation is identical. Every later float operation then runs on the same data in the same
+order, and whole runs must agree BIT FOR BIT: positions, velocities, density, sorted ids, cell
+starts. SPH_RESORT=0 (read at context creation) forces the full sort every step.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(monkeypatch, make):
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("SPH_RESORT", flag)
+        out.append(make())
+    monkeypatch.delenv("SPH_RESORT")
+    return out
+
+
+def _assert_same(a, b, what):
+    for f in ("positions", "velocities", "density", "sorted_ids", "cell_start"):
+        x, y = getattr(a, f)(), getattr(b, f)()
+        assert np.array_equal(x, y, equal_nan=True), f"{what}: {f} differs"
+
+
+def test_resort_bitwise_dambreak(pkg, monkeypatch):
+    full, inc = _pair(monkeypatch, lambda: pkg.SPHSim.from_config("C2", profile=True))
+    try:
+        for k in (1, 9, 40):
+            full.step(k)
+            inc.step(k)
+            _assert_same(full.ctx, inc.ctx, f"after {k} more steps")
+        ks_inc, ks_full = inc.ctx.kernel_stats(), full.ctx.kernel_stats()
+        # the incremental path ran on every step after the first; the full path never did
+        assert ks_inc["resort"]["launches"] == 49 and ks_inc["radix_sort"]["launches"] == 1
+        assert "resort" not in ks_full and ks_full["radix_sort"]["launches"] == 50
+    finally:
+        full.close()
+        inc.close()
+
+
+def test_resort_bitwise_many_movers(pkg, monkeypatch):
+    """A violent state: random velocities that move ~half the particles across a sub-cell per
+    step, in every direction, including wall clamps (keys far from their old ones)."""
+    sc = pkg.make_scenario(pkg.SPH_SCENARIO_DAMBREAK, 3, 24, 20, 16, 40, 40, 40, dx=0.01, seed=5)
+
+    def make():
+        s = pkg.SPHSim(sc, profile=True)
+        rng = np.random.default_rng(11)
+        x = s.positions()
+        sub = 2 * s.params.h / 4                  # z sub-cell (SPEC_SPH.md §0)
+        v = rng.uniform(-1.0, 1.0, x.shape).astype(np.float32) * (sub / s.dt)
+        s.ctx.upload_state(x, v)
+        return s
+
+    full, inc = _pair(monkeypatch, make)
+    try:
+        for k in (1, 1, 3, 5):
+            full.step(k)
+            inc.step(k)
+            _assert_same(full.ctx, inc.ctx, "violent state")
+        assert inc.ctx.kernel_stats()["resort"]["launches"] == 9
+    finally:
+        full.close()
+        inc.close()
+
+
+def test_resort_after_state_changes(pkg, monkeypatch):
+    """Uploads, parameter changes and resizes invalidate the sorted keys: the next step falls
+    back to the full sort, and both paths still agree."""
+    full, inc = _pair(monkeypatch, lambda: pkg.SPHSim.from_config("C1", profile=True))
+    try:
+        for s in (full, inc):
+            s.step(5)
+            x, v = s.positions(), s.velocities()
+            s.ctx.upload_state(x[::-1].copy(), v[::-1].copy())   # new slot order
+            s.step(3)
+            s.ctx.resize(s.n + 100)
+            s.step(3)
+            s.ctx.set_params(s.params)
+            s.step(3)
+        _assert_same(full.ctx, inc.ctx, "after state changes")
+        ks = inc.ctx.kernel_stats()
+        assert ks["radix_sort"]["launches"] == 4 and ks["resort"]["launches"] == 10
+    finally:
+        full.close()
+        inc.close()
