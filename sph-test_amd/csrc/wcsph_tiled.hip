@@ -224,8 +224,11 @@ __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi,
     const float G = inner ? g_in : g_out;
     const float du = vi.x - vj.x, dv = vi.y - vj.y, dw = vi.z - vj.z;
     const float vr = du * dx + dv * dy + dw * dz;
-    const float inv_s = __builtin_amdgcn_rcpf(rhoi + pj.w);
-    const float pij = fminf(vr, 0.0f) * k.kvisc * __builtin_amdgcn_rcpf(r2 + k.eta2) * inv_s;
+    // one reciprocal for both 1/(ρi + ρj) and 1/((r² + η²)(ρi + ρj))
+    const float e = r2 + k.eta2;
+    const float inv_es = __builtin_amdgcn_rcpf(e * (rhoi + pj.w));
+    const float inv_s = e * inv_es;
+    const float pij = fminf(vr, 0.0f) * k.kvisc * inv_es;
     const float cf = (prhoi + vj.w + pij) * G;
     a.ax += cf * dx; a.ay += cf * dy; a.az += cf * dz;
     const float cx = k.kx * inv_s * w4;
@@ -272,19 +275,21 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         }
         cnt = 0;
     };
-    // scan LDS slots [lo, lo+ln) (self at LDS slot `self`), appending hits
-    auto scan = [&](int32_t lo, int32_t ln, int32_t self) {
+    // scan LDS slots [lo, lo+ln), appending hits
+    auto scan = [&](int32_t lo, int32_t ln) {
 #if SPH_FORCE_ABL == 3   // measurement build: staging only
         return;
 #endif
         for (int t = 0; __any(t < ln); t += 4) {
             const int32_t j = min(lo + t, TT_GCAP);   // lanes past their range stay in the array
             const float4 a = sp[j], bb = sp[j + 1], cc = sp[j + 2], d = sp[j + 3];
-            // bitwise &, not &&: every read is unconditional (no exec branches around LDS loads)
-            const bool h0 = (t < ln) & (j != self) & (dist2(pi, a) < c.four_h2);
-            const bool h1 = (t + 1 < ln) & (j + 1 != self) & (dist2(pi, bb) < c.four_h2);
-            const bool h2 = (t + 2 < ln) & (j + 2 != self) & (dist2(pi, cc) < c.four_h2);
-            const bool h3 = (t + 3 < ln) & (j + 3 != self) & (dist2(pi, d) < c.four_h2);
+            // bitwise &, not &&: every read is unconditional (no exec branches around LDS loads).
+            // The target itself is a hit: its pair adds exactly ±0 (dx = du = 0, q = 0 finite), so
+            // no per-candidate self test is needed.
+            const bool h0 = (t < ln) & (dist2(pi, a) < c.four_h2);
+            const bool h1 = (t + 1 < ln) & (dist2(pi, bb) < c.four_h2);
+            const bool h2 = (t + 2 < ln) & (dist2(pi, cc) < c.four_h2);
+            const bool h3 = (t + 3 < ln) & (dist2(pi, d) < c.four_h2);
             const uint32_t jb = (uint32_t)j * 16u;
             lst[cnt][tid] = (uint16_t)jb;         cnt += h0;
             lst[cnt][tid] = (uint16_t)(jb + 16u); cnt += h1;
@@ -317,7 +322,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
             int32_t o = 0;
 #pragma unroll
             for (int r = 0; r < 3; ++r) {
-                scan(o + (r0[r] - c0[r]), r1[r] - r0[r], o + (i - c0[r]));
+                scan(o + (r0[r] - c0[r]), r1[r] - r0[r]);
                 o += len[r];
             }
             flush();
@@ -345,7 +350,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
                 for (int32_t t = tid; t < ln; t += TT_BLK) put(t, base + t);
                 __syncthreads();
                 const int32_t lo = max(r0[r], base) - base;
-                scan(lo, max(min(r1[r], base + ln) - base - lo, 0), i - base);
+                scan(lo, max(min(r1[r], base + ln) - base - lo, 0));
                 flush();
             }
         }
