@@ -45,18 +45,34 @@ def parse():
     return ap.parse_args()
 
 
-def load_traffic(config: str):
-    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 PMC passes
-    (profiles/pmc_*.json, FETCH_SIZE×2 + WRITE_SIZE per MI355X_MICROARCH.md §HBM)."""
-    best = None
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD
+# (MI355X_MICROARCH.md: a wave issues each VALU instruction over 2 cycles), at 2.4 GHz.
+PEAK_VALU_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 2
+
+
+def force_kernel_name() -> str:
+    return "k_force_integrate" if os.environ.get("SPH_NB_VARIANT", "1") == "0" else "k_force_tiled"
+
+
+def load_pmc(config: str):
+    """Per-launch counters of the dominant kernel from the committed rocprofv3 PMC passes
+    (profiles/pmc_*.json): HBM bytes = FETCH_SIZE×2 + WRITE_SIZE (MI355X_MICROARCH.md §HBM) and
+    SQ_INSTS_VALU (wave-level VALU instructions)."""
+    out = {}
     for f in sorted((ROOT / "profiles").glob("pmc_*.json")):
         try:
             d = json.loads(f.read_text())
         except Exception:
             continue
-        if d.get("config") == config and d.get("kernel_bytes", {}).get("force_integrate"):
-            best = d["kernel_bytes"]["force_integrate"]
-    return best
+        if d.get("config") != config:
+            continue
+        if d.get("kernel_bytes", {}).get("force_integrate"):
+            out["traffic"] = d["kernel_bytes"]["force_integrate"]
+        for ks in d.get("kernels", {}).values():
+            k = ks.get(force_kernel_name(), {})
+            if "SQ_INSTS_VALU" in k:
+                out["valu_instr"] = k["SQ_INSTS_VALU"]
+    return out
 
 
 def cpu_baseline(config: str, budget_s: float):
@@ -156,11 +172,18 @@ def main():
         avg_s = fi["total_ms"] / fi["launches"] / 1e3
         bytes_per_launch = FORCE_BYTES_PER_PARTICLE * runner.local_particles()
         achieved = bytes_per_launch / avg_s / 1e9
-        traffic = load_traffic(args.config) if world == 1 else None
+        pmc = load_pmc(args.config) if world == 1 else {}
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
-                    "kernel": "k_force_integrate", "kernel_avg_us": round(avg_s * 1e6, 2),
+                    "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": pmc.get("traffic"),
+                    "kernel": force_kernel_name(), "kernel_avg_us": round(avg_s * 1e6, 2),
                     "bytes_per_launch": bytes_per_launch}
+        if "valu_instr" in pmc:
+            # what bounds the neighbour pass in practice: VALU issue, from the same
+            # kernel's committed PMC pass and this run's kernel time
+            va = pmc["valu_instr"] / avg_s
+            roofline["valu"] = {"achieved": round(va / 1e9, 2), "peak": round(PEAK_VALU_WAVE_INSTR_PER_S / 1e9, 1),
+                                "unit": "G wave-instr/s", "frac": round(va / PEAK_VALU_WAVE_INSTR_PER_S, 4),
+                                "source": "rocprofv3 SQ_INSTS_VALU per launch (profiles/pmc_C3.json)"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
