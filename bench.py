@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event pass")
+    ap.add_argument("--slab", action="store_true", help="run the multi-GPU slab step even at N=1 (rehearsal)")
     return ap.parse_args()
 
 
@@ -129,7 +130,7 @@ def main():
         torch.cuda.set_device(0)
     pkg = GE.load_package()
 
-    if world > 1:
+    if world > 1 or args.slab:
         from sph_test_amd import slab
         runner = slab.SlabRunner(args.config, rank, world, device=local, profile=not args.no_profile)
     else:

@@ -22,8 +22,8 @@
 // Kernels:
 //   k_mv_rank        all-pairs counts per mover: (key, index) rank, index rank, A(q)
 //   k_mv_place       movers: scatter of (pos, vel, id, key); tables by (key, index) and by index
-//   k_mv_merge       stayers: scatter of (pos, vel, id, key)
-//   k_mv_cell_start  cs[k] += #{movers: new key < k} − #{movers: old key < k}, in place
+//   k_mv_merge       stayers: scatter of (pos, vel, id, key); extra workgroups update the cell
+//                    starts in place: cs[k] += #{movers: new key < k} − #{movers: old key < k}
 // The scatters replace the permutation gather, and the update the cell-start rebuild, of the full path.
 #include "common.h"
 
@@ -142,16 +142,46 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_place(const uint32_t* __restrict_
     }
 }
 
+// cs[k] += #{movers: new key < k} − #{movers: old key < k}, for k in [0, ncells]; 1024 cells per
+// workgroup. A workgroup whose counts agree at its start and that holds no mover key leaves its cells.
+// Runs as extra workgroups of k_mv_merge (it needs only k_mv_place's tables), beside the scatter.
+constexpr int MV_CS_CELLS = 4 * MV_BLK;
+
+static __device__ void mv_cell_start(uint32_t* __restrict__ cs, uint32_t ncells, uint32_t m, const ResortScratch& w,
+                                     uint32_t blk, uint32_t* b) {
+    const uint32_t k0 = blk * MV_CS_CELLS, k1 = k0 + MV_CS_CELLS;
+    const int wv = threadIdx.x >> 6;
+    const uint32_t p = wv < 2 ? wave_lower_bound(w.ms, m, comp(wv == 0 ? k0 : k1, 0u))
+                              : wave_lower_bound(w.mos, m, wv == 2 ? k0 : k1);
+    if (lane_id() == 0) b[wv] = p;
+    __syncthreads();
+    const uint32_t nlo = b[0], nhi = b[1], olo = b[2], ohi = b[3];
+    if (nlo == olo && nhi == nlo && ohi == olo) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t k = k0 + j * MV_BLK + threadIdx.x;
+        if (k > ncells) break;
+        const uint32_t cn = nlo + lower_bound(w.ms + nlo, nhi - nlo, comp(k, 0u));
+        const uint32_t co = olo + lower_bound(w.mos + olo, ohi - olo, k);
+        cs[k] += cn - co;
+    }
+}
+
 __global__ __launch_bounds__(MV_BLK) void k_mv_merge(const uint32_t* __restrict__ keys,
                                                      const uint32_t* __restrict__ sk, int32_t n,
                                                      const uint32_t* __restrict__ mtotal, ResortScratch w,
                                                      const float4* __restrict__ pos, const float4* __restrict__ vel,
                                                      const int32_t* __restrict__ id, float4* __restrict__ pos_o,
                                                      float4* __restrict__ vel_o, int32_t* __restrict__ id_o,
-                                                     uint32_t* __restrict__ sk_o) {
+                                                     uint32_t* __restrict__ sk_o, int32_t nb, uint32_t* __restrict__ cs,
+                                                     uint32_t ncells) {
     __shared__ uint32_t wc[MV_BLK / 64];
-    __shared__ uint32_t b[3];
-    const int32_t i0 = xcd_block(blockIdx.x, gridDim.x) * MV_BLK;
+    __shared__ uint32_t b[4];
+    if ((int32_t)blockIdx.x >= nb) {   // the cell-start workgroups
+        mv_cell_start(cs, ncells, *mtotal, w, blockIdx.x - nb, b);
+        return;
+    }
+    const int32_t i0 = xcd_block(blockIdx.x, nb) * MV_BLK;
     const int32_t i = i0 + threadIdx.x;
     const int32_t ilast = min(i0 + MV_BLK, n) - 1;
     const uint32_t m = *mtotal;
@@ -180,32 +210,6 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(const uint32_t* __restrict_
     sk_o[dst] = ko;
 }
 
-// cs[k] += #{movers: new key < k} − #{movers: old key < k}, for k in [0, ncells]; 1024 cells per
-// block. A block whose counts agree at its start and that holds no mover key leaves its cells.
-constexpr int MV_CS_CELLS = 4 * MV_BLK;
-
-__global__ __launch_bounds__(MV_BLK) void k_mv_cell_start(uint32_t* __restrict__ cs, uint32_t ncells,
-                                                          const uint32_t* __restrict__ mtotal, ResortScratch w) {
-    __shared__ uint32_t b[4];
-    const uint32_t m = *mtotal;
-    const uint32_t k0 = blockIdx.x * MV_CS_CELLS, k1 = k0 + MV_CS_CELLS;
-    const int wv = threadIdx.x >> 6;
-    const uint32_t p = wv < 2 ? wave_lower_bound(w.ms, m, comp(wv == 0 ? k0 : k1, 0u))
-                              : wave_lower_bound(w.mos, m, wv == 2 ? k0 : k1);
-    if (lane_id() == 0) b[wv] = p;
-    __syncthreads();
-    const uint32_t nlo = b[0], nhi = b[1], olo = b[2], ohi = b[3];
-    if (nlo == olo && nhi == nlo && ohi == olo) return;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t k = k0 + j * MV_BLK + threadIdx.x;
-        if (k > ncells) break;
-        const uint32_t cn = nlo + lower_bound(w.ms + nlo, nhi - nlo, comp(k, 0u));
-        const uint32_t co = olo + lower_bound(w.mos + olo, ohi - olo, k);
-        cs[k] += cn - co;
-    }
-}
-
 void launch_resort(const uint32_t* sk, uint32_t* cs, uint32_t ncells, int32_t n, const float4* pos,
                    const float4* vel, const int32_t* id, const uint32_t* keys, const uint32_t* count,
                    uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,
@@ -214,9 +218,10 @@ void launch_resort(const uint32_t* sk, uint32_t* cs, uint32_t ncells, int32_t n,
     const int32_t nb = (n + MV_BLK - 1) / MV_BLK;
     k_mv_rank<<<MV_RANK_GRID, MV_BLK, 0, s>>>(count, count_other, cs, w);
     k_mv_place<<<std::min(nb, 1024), MV_BLK, 0, s>>>(count, cs, w, pos, vel, id, pos_o, vel_o, id_o, sk_o);
-    k_mv_merge<<<nb, MV_BLK, 0, s>>>(keys, sk, n, count, w, pos, vel, id, pos_o, vel_o, id_o, sk_o);
-    // after every reader of cs_old (k_mv_rank, k_mv_place)
-    k_mv_cell_start<<<(ncells + MV_CS_CELLS) / MV_CS_CELLS, MV_BLK, 0, s>>>(cs, ncells, count, w);
+    // + the cell-start update, after every reader of cs_old (k_mv_rank, k_mv_place)
+    const int32_t ncs = (int32_t)((ncells + MV_CS_CELLS) / MV_CS_CELLS);
+    k_mv_merge<<<nb + ncs, MV_BLK, 0, s>>>(keys, sk, n, count, w, pos, vel, id, pos_o, vel_o, id_o, sk_o, nb, cs,
+                                           ncells);
 }
 
 }  // namespace sph

@@ -20,12 +20,24 @@
 
 namespace sph {
 
+#ifndef SPH_FLUSH_BATCH
+#define SPH_FLUSH_BATCH 0   // 4-hit batched flush: measured 3% slower (kept for A/B)
+#endif
+#ifndef SPH_FORCE_QUAD
+#define SPH_FORCE_QUAD 0   // quadrant lanes: measured neutral on the force pass (kept for density)
+#endif
 #ifndef SPH_FORCE_ABL
 #define SPH_FORCE_ABL 0   // ablation builds for profiling only (scripts/gpu_ablate.sh)
 #endif
 
-constexpr int TT_BLK = 256;        // targets per workgroup
-constexpr int TT_GCAP = 1024;      // candidates staged per plane (LDS)
+#ifndef SPH_TT_BLK
+#define SPH_TT_BLK 256
+#endif
+#ifndef SPH_TT_GCAP
+#define SPH_TT_GCAP 1024
+#endif
+constexpr int TT_BLK = SPH_TT_BLK;    // targets per workgroup
+constexpr int TT_GCAP = SPH_TT_GCAP;  // candidates staged per plane (LDS)
 constexpr int TT_CAP = 32;         // per-lane hit list (force)
 constexpr int TT_FALLBACK = 4 * TT_GCAP;
 
@@ -112,12 +124,51 @@ __device__ __forceinline__ void stage_plane(const int32_t (&c0)[3], const int32_
     }
 }
 
+// Lanes of one wave take targets of one in-cell quadrant (fx < ½, fy < ½). A side row's trimmed z
+// window and a plane's hit count grow with the target's distance to the neighbour column, so lanes
+// with alike windows idle less in the wave-wide scan and flush loops. Stable within a quadrant;
+// every target keeps its own visit order, so results are bit-identical. Returns the lane's slot
+// (>= n for the padding lanes of the last block, which sort last).
+__device__ __forceinline__ int32_t quadrant_target(const GridDesc& g, const float4* __restrict__ pos, int32_t i0,
+                                                   int32_t n, int32_t* perm, uint32_t (*cnt)[5]) {
+    static_assert(TT_BLK % 64 == 0, "whole waves");
+    const int32_t i = i0 + threadIdx.x;
+    int bin = 4;
+    if (i < n) {
+        const float4 p = pos[i];
+        const int32_t cx = cell_cx(g, p.x), cy = cell_coord(p.y, g.oy, g.inv_cell, g.gy);
+        float fx, fy, gzf;
+        cell_fracs(g, p.x, p.y, p.z, cx, cy, fx, fy, gzf);
+        bin = (fx >= 0.5f ? 1 : 0) + (fy >= 0.5f ? 2 : 0);
+    }
+    const int w = threadIdx.x >> 6;
+    uint64_t mine = 0;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+        const uint64_t m = __ballot(bin == b);
+        if (bin == b) mine = m;
+        if (lane_id() == 0) cnt[w][b] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    uint32_t off = 0;
+    for (int b = 0; b < bin; ++b)
+#pragma unroll
+        for (int v = 0; v < TT_BLK / 64; ++v) off += cnt[v][b];
+    for (int v = 0; v < w; ++v) off += cnt[v][bin];
+    off += __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+    perm[off] = i;
+    __syncthreads();
+    return perm[threadIdx.x];
+}
+
 __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restrict__ pos,
                                                           const uint32_t* __restrict__ cs, int32_t ib, int32_t n,
                                                           GridDesc g, SphConst c, float2* __restrict__ rp) {
     __shared__ float4 sp[TT_GCAP + 4];
+    __shared__ int32_t perm[TT_BLK];
+    __shared__ uint32_t qcnt[TT_BLK / 64][5];
     const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
-    const int32_t i = i0 + threadIdx.x;
+    const int32_t i = quadrant_target(g, pos, i0, n, perm, qcnt);
     const bool valid = i < n;
     const int32_t ilast = min(i0 + TT_BLK, n) - 1;
     const float4 pi = pos[valid ? i : ilast];
@@ -208,8 +259,10 @@ static PairK pair_constants(const SphConst& c) {
 
 // Pair body (SPEC_SPH.md §2). pj = (x, y, z, ρ_j), vj = (u, v, w, P_j/ρ_j²). Branchless, for
 // pairs with r < 2h: one rsq gives r and 1/r; r = 0 (coincident, distinct particles) gives q = 0.
+// live = false adds exact zeros (selected contributions, so a garbage slot cannot leak NaN): the two-hit flush
+// computes both bodies unconditionally and the compiler interleaves their chains.
 __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi, float rhoi, float prhoi, float4 pj,
-                                           float4 vj, ForceAcc& a) {
+                                           float4 vj, ForceAcc& a, bool live = true) {
     const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
     const float r2 = dx * dx + dy * dy + dz * dz;
     const float rs = __builtin_amdgcn_rsqf(fmaxf(r2, 1e-30f));
@@ -230,9 +283,9 @@ __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi,
     const float inv_s = e * inv_es;
     const float pij = fminf(vr, 0.0f) * k.kvisc * inv_es;
     const float cf = (prhoi + vj.w + pij) * G;
-    a.ax += cf * dx; a.ay += cf * dy; a.az += cf * dz;
+    a.ax += live ? cf * dx : 0.0f; a.ay += live ? cf * dy : 0.0f; a.az += live ? cf * dz : 0.0f;
     const float cx = k.kx * inv_s * w4;
-    a.sx -= cx * du; a.sy -= cx * dv; a.sz -= cx * dw;
+    a.sx -= live ? cx * du : 0.0f; a.sy -= live ? cx * dv : 0.0f; a.sz -= live ? cx * dw : 0.0f;
 }
 
 __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
@@ -244,7 +297,13 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     __shared__ uint16_t lst[TT_CAP][TT_BLK];
     const int tid = threadIdx.x;
     const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
+#if SPH_FORCE_QUAD
+    __shared__ int32_t perm[TT_BLK];
+    __shared__ uint32_t qcnt[TT_BLK / 64][5];
+    const int32_t i = quadrant_target(g, pos, i0, n, perm, qcnt);
+#else
     const int32_t i = i0 + tid;
+#endif
     const bool valid = i < n;
     const int32_t ilast = min(i0 + TT_BLK, n) - 1;
     const int32_t ii = valid ? i : ilast;
@@ -263,6 +322,19 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         cnt = 0;
         return;
 #endif
+#if SPH_FLUSH_BATCH
+        // two hits per iteration, both bodies unconditional (the second masked by a select when
+        // q + 1 >= cnt), so their dependency chains interleave. Slots past cnt hold stale in-range
+        // offsets or are clamped into the padded array.
+        constexpr uint32_t OMAX = 16u * TT_GCAP;
+        for (int q = 0; __any(q < cnt); q += 2) {
+            const uint32_t o0 = min((uint32_t)lst[q][tid], OMAX);
+            const uint32_t o1 = min((uint32_t)lst[min(q + 1, TT_CAP - 1)][tid], OMAX);
+            const float4 p0 = at(sp, o0), v0 = at(sv, o0), p1 = at(sp, o1), v1 = at(sv, o1);
+            pair_force(pk, pi, vi, ri.x, ri.y, p0, v0, acc, q < cnt);
+            pair_force(pk, pi, vi, ri.x, ri.y, p1, v1, acc, q + 1 < cnt);
+        }
+#else
         for (int q = 0; __any(q < cnt); ++q) {
             if (q < cnt) {
                 const uint32_t off = lst[q][tid];
@@ -273,6 +345,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
 #endif
             }
         }
+#endif
         cnt = 0;
     };
     // scan LDS slots [lo, lo+ln), appending hits
