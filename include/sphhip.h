@@ -172,7 +172,7 @@ int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int3
  *      GPU. One context per rank owns global cell columns [cx_lo, cx_hi)
  *      plus one halo column per side. The HOST moves the packed device buffers between ranks
  *      (RCCL over xGMI: sph_test_amd.slab / bench.py). Per step:
- *        count_sends → pack_send(0/1) → [exchange] → assemble → ranges → density →
+ *        count_sends(_async) → pack_send(0/1) → [exchange] → assemble → density → ranges →
  *        pack_rho(0/1) → [exchange] → force(interior) ∥ [rho in flight] → unpack_rho → force(boundary)
  *        → finish_step.
  *      Particle records are 32 bytes: (x, y, z, id-bits, u, v, w, 0). ---- */
@@ -186,9 +186,17 @@ typedef struct sph_slab {
 int sph_slab_set(sph_ctx* ctx, const sph_slab* slab);
 int sph_slab_init_scenario(sph_ctx* ctx, const sph_scenario* sc);
 int sph_slab_count_sends(sph_ctx* ctx, int32_t counts[2]);
+/* the same counts written to DEVICE memory (int64[2]: left, right) without a host sync; the
+ * host sends them to the neighbours as they are. pack_send then needs capacity >= the owned
+ * count (sph_slab_send_capacity) instead of the exact count. */
+int sph_slab_count_sends_async(sph_ctx* ctx, int64_t* dev_counts);
+int sph_slab_send_capacity(sph_ctx* ctx, int32_t* capacity);
 int sph_slab_pack_send(sph_ctx* ctx, int32_t side, void* dev_records, int32_t capacity);
 int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t n_left, const void* dev_right,
                       int32_t n_right);
+/* assemble reads the ranges back asynchronously; sph_slab_ranges waits for that copy (and so
+ * does every call below that needs them, except density, which reads them on the device).
+ * Calling density before ranges keeps the GPU busy while the host waits. */
 int sph_slab_ranges(sph_ctx* ctx, int32_t ranges[10]);
 int sph_slab_density(sph_ctx* ctx);
 int sph_slab_pack_rho(sph_ctx* ctx, int32_t side, void* dev_rho_prho, int32_t capacity);

@@ -103,6 +103,13 @@ __device__ __forceinline__ uint32_t lane_id() {
 }
 #endif
 
+// Slot bounds held in device memory (slab mode: known on the device before the host reads
+// them back). lo == nullptr: use the launch's host bounds.
+struct DevRange {
+    const uint32_t* lo = nullptr;
+    const uint32_t* hi = nullptr;
+};
+
 // Movers of a Model S step (resort.hip): particles whose new cell key differs from the sorted key
 // of their slot. The force pass appends them (any order) for the incremental re-sort.
 struct MoverSink {
@@ -193,7 +200,7 @@ void launch_iota(uint32_t* v, int32_t n, hipStream_t s);
 
 // Model S (wcsph.hip): targets are the sorted slots [ib, ie)
 void launch_density(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g,
-                    SphConst c, float2* rp, hipStream_t s);
+                    SphConst c, float2* rp, hipStream_t s, DevRange dr = DevRange{});
 void launch_force_integrate(const float4* pos, const float4* vel, const float2* rp,
                             const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
                             float dt, float fext_x, float4* pos_o, float4* vel_o, uint32_t* keys_o,
@@ -201,7 +208,7 @@ void launch_force_integrate(const float4* pos, const float4* vel, const float2* 
 
 // Model S, LDS-tiled (wcsph_tiled.hip)
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g,
-                          SphConst c, float2* rp, hipStream_t s);
+                          SphConst c, float2* rp, hipStream_t s, DevRange dr = DevRange{});
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs,
                         int32_t ib, int32_t ie, GridDesc g, SphConst c, float dt, float fext_x,
                         float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv, hipStream_t s);
@@ -212,7 +219,8 @@ void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, 
 int32_t slab_compact_blocks(int32_t b, int32_t e);
 void launch_slab_count(const uint32_t* keys, int32_t b, int32_t e, uint32_t gyz, int32_t col_le,
                        int32_t col_ge, uint32_t* blk /*[2][nblk]*/, uint32_t* totals /*[2]*/,
-                       hipStream_t s);
+                       hipStream_t s,
+                       int64_t* totals64 = nullptr);
 void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
                       int32_t b, int32_t e, uint32_t gyz, int32_t side, int32_t col_le, int32_t col_ge,
                       const uint32_t* blk, float4* out, hipStream_t s);

@@ -52,18 +52,21 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_count(const uint32_t* __restric
     }
 }
 
-// one workgroup: exclusive scan of both count rows in place, totals[2]
-__global__ __launch_bounds__(SL_BLK) void k_slab_scan(uint32_t* __restrict__ blk, int32_t nblk,
-                                                      uint32_t* __restrict__ totals) {
-    __shared__ uint32_t ws[SL_WAVES];
+// one workgroup of 1024: exclusive scan of both count rows in place, totals[2] (u32), and the
+// same totals as int64 into totals64 when given (the async send counts)
+constexpr int SL_SCAN = 1024;
+
+__global__ __launch_bounds__(SL_SCAN) void k_slab_scan(uint32_t* __restrict__ blk, int32_t nblk,
+                                                       uint32_t* __restrict__ totals, int64_t* __restrict__ totals64) {
+    __shared__ uint32_t ws[SL_SCAN / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int side = 0; side < 2; ++side) {
         uint32_t* row = blk + side * nblk;
         uint32_t carry = 0;
-        for (int32_t base = 0; base < nblk; base += SL_BLK) {
+        for (int32_t base = 0; base < nblk; base += SL_SCAN) {
             const int32_t i = base + threadIdx.x;
             const uint32_t v = i < nblk ? row[i] : 0u;
             uint32_t inc = v;
-            const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
                 const uint32_t t = __shfl_up(inc, o, 64);
@@ -73,7 +76,7 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_scan(uint32_t* __restrict__ blk
             __syncthreads();
             uint32_t pre = 0, tot = 0;
 #pragma unroll
-            for (int k = 0; k < SL_WAVES; ++k) {
+            for (int k = 0; k < SL_SCAN / 64; ++k) {
                 pre += k < w ? ws[k] : 0u;
                 tot += ws[k];
             }
@@ -81,8 +84,10 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_scan(uint32_t* __restrict__ blk
             if (i < nblk) row[i] = carry + pre + inc - v;
             carry += tot;
         }
-        if (threadIdx.x == 0) totals[side] = carry;
-        __syncthreads();
+        if (threadIdx.x == 0) {
+            totals[side] = carry;
+            if (totals64) totals64[side] = (int64_t)carry;
+        }
     }
 }
 
@@ -189,10 +194,10 @@ void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, 
 }
 
 void launch_slab_count(const uint32_t* keys, int32_t b, int32_t e, uint32_t gyz, int32_t col_le, int32_t col_ge,
-                       uint32_t* blk, uint32_t* totals, hipStream_t s) {
+                       uint32_t* blk, uint32_t* totals, hipStream_t s, int64_t* totals64) {
     const int32_t nb = slab_compact_blocks(b, e);
     k_slab_count<<<nb, SL_BLK, 0, s>>>(keys, b, e, gyz, col_le, col_ge, blk, nb);
-    k_slab_scan<<<1, SL_BLK, 0, s>>>(blk, nb, totals);
+    k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb, totals, totals64);
 }
 
 void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id, int32_t b,
@@ -213,7 +218,7 @@ void launch_slab_select_columns(const float4* pos, const float4* vel, const int3
     k_sel_count<<<nb, SL_BLK, 0, s>>>(pos, n, g, lo, hi, blk);
     // reuse the two-row scan: row 1 is a dummy of zeros
     (void)hipMemsetAsync(blk + nb, 0, sizeof(uint32_t) * nb, s);
-    k_slab_scan<<<1, SL_BLK, 0, s>>>(blk, nb, total);
+    k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb, total, nullptr);
     if (n > 0 && pos_o != nullptr) k_sel_scatter<<<nb, SL_BLK, 0, s>>>(pos, vel, id, n, g, lo, hi, blk, pos_o, vel_o, id_o);
 }
 

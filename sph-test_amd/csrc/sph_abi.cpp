@@ -96,6 +96,9 @@ struct sph_ctx {
     int32_t send_counts[2] = {0, 0};
     uint32_t* sblk = nullptr;    // compaction block counts [2][nblk]
     uint32_t* sdev = nullptr;    // small device scratch (totals, picks)
+    uint32_t* rng_host = nullptr;   // pinned: column-start picks of the last assemble
+    hipEvent_t rng_ev = nullptr;    // recorded after their device->host copy
+    bool rng_pending = false;       // rng[] / o0 / o1 not yet updated from rng_host
 };
 
 namespace {
@@ -549,6 +552,8 @@ void sph_destroy(sph_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     resolve_pending(ctx);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
+    if (ctx->rng_ev) (void)hipEventDestroy(ctx->rng_ev);
+    if (ctx->rng_host) (void)hipHostFree(ctx->rng_host);
     free_all(ctx);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -906,6 +911,25 @@ int sph_resize(sph_ctx* ctx, int32_t capacity) {
 }
 
 // ---------------------------------------------------------------- slab decomposition
+// Wait for the last assemble's range copy and publish rng / o0 / o1 (no-op when up to date).
+static int slab_sync_ranges(sph_ctx* ctx) {
+    if (!ctx->rng_pending) return SPH_OK;
+    HIPCHK(hipEventSynchronize(ctx->rng_ev));
+    ctx->rng_pending = false;
+    const uint32_t* v = ctx->rng_host;
+    int32_t* r = ctx->rng;
+    r[0] = (int32_t)v[0]; r[1] = (int32_t)v[1];                          // ghost left
+    r[2] = (int32_t)v[1]; r[3] = (int32_t)v[4];                          // owned
+    r[4] = (int32_t)v[4]; r[5] = (int32_t)v[5];                          // ghost right
+    r[6] = (int32_t)v[1]; r[7] = (int32_t)v[2];                          // boundary column cx_lo
+    r[8] = (int32_t)v[3]; r[9] = (int32_t)v[4];                          // boundary column cx_hi-1
+    ctx->o0 = r[2];
+    ctx->o1 = r[3];
+    if (r[5] != ctx->n)
+        return fail(ctx, SPH_ERR_STATE, "slab assemble: %d particles fall outside the held columns", ctx->n - r[5]);
+    return SPH_OK;
+}
+
 static int slab_local_grid(sph_ctx* ctx) {
     const GridDesc& G = ctx->gglobal;
     GridDesc g = G;
@@ -935,9 +959,12 @@ int sph_slab_set(sph_ctx* ctx, const sph_slab* slab) {
     const int32_t GX = ctx->gglobal.gx;
     if (slab->cx_lo < 0 || slab->cx_hi > GX || slab->cx_lo >= slab->cx_hi)
         return fail(ctx, SPH_ERR_INVALID, "slab [%d,%d) outside 0..%d", slab->cx_lo, slab->cx_hi, GX);
+    if (!ctx->rng_host) HIPCHK(hipHostMalloc((void**)&ctx->rng_host, 16 * sizeof(uint32_t), hipHostMallocDefault));
+    if (!ctx->rng_ev) HIPCHK(hipEventCreateWithFlags(&ctx->rng_ev, hipEventDisableTiming));
     ctx->slab = true;
     ctx->sl = *slab;
     ctx->n = ctx->o0 = ctx->o1 = 0;
+    ctx->rng_pending = false;
     return slab_local_grid(ctx);
 }
 
@@ -985,10 +1012,8 @@ int sph_slab_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
     return SPH_OK;
 }
 
-int sph_slab_count_sends(sph_ctx* ctx, int32_t counts[2]) {
-    if (!ctx || !counts) return SPH_ERR_INVALID;
-    if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
-    HIPCHK(hipSetDevice(ctx->device));
+static int slab_count(sph_ctx* ctx, int64_t* dev_counts) {
+    if (int rc = slab_sync_ranges(ctx)) return rc;
     const int32_t no = ctx->o1 - ctx->o0;
     if (!ctx->keys_valid && no > 0) {
         KTimer t(ctx, "keys", 20.0 * no);
@@ -998,11 +1023,34 @@ int sph_slab_count_sends(sph_ctx* ctx, int32_t counts[2]) {
     const uint32_t gyz = (uint32_t)ctx->grid.gy * (uint32_t)ctx->grid.gz;
     const int32_t col_le = ctx->has_left ? ctx->sl.cx_lo - ctx->grid.cx0 : -1;
     const int32_t col_ge = ctx->has_right ? ctx->sl.cx_hi - 1 - ctx->grid.cx0 : 0x7fffffff;
+    KTimer t(ctx, "slab_count", 4.0 * no);
+    launch_slab_count(ctx->keys, ctx->o0, ctx->o1, gyz, col_le, col_ge, ctx->sblk, ctx->sdev, ctx->stream, dev_counts);
+    return SPH_OK;
+}
+
+int sph_slab_count_sends_async(sph_ctx* ctx, int64_t* dev_counts) {
+    if (!ctx || !dev_counts) return SPH_ERR_INVALID;
+    if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
+    HIPCHK(hipSetDevice(ctx->device));
+    if (int rc = slab_count(ctx, dev_counts)) return rc;
+    HIPCHK(hipGetLastError());
+    ctx->send_counts[0] = ctx->send_counts[1] = -1;   // known on the device only
+    return SPH_OK;
+}
+
+int sph_slab_send_capacity(sph_ctx* ctx, int32_t* capacity) {
+    if (!ctx || !capacity) return SPH_ERR_INVALID;
+    if (int rc = slab_sync_ranges(ctx)) return rc;
+    *capacity = std::max(ctx->o1 - ctx->o0, 1);
+    return SPH_OK;
+}
+
+int sph_slab_count_sends(sph_ctx* ctx, int32_t counts[2]) {
+    if (!ctx || !counts) return SPH_ERR_INVALID;
+    if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
+    HIPCHK(hipSetDevice(ctx->device));
+    if (int rc = slab_count(ctx, nullptr)) return rc;
     uint32_t tot[2] = {0, 0};
-    {
-        KTimer t(ctx, "slab_count", 4.0 * no);
-        launch_slab_count(ctx->keys, ctx->o0, ctx->o1, gyz, col_le, col_ge, ctx->sblk, ctx->sdev, ctx->stream);
-    }
     HIPCHK(hipMemcpyAsync(tot, ctx->sdev, 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     counts[0] = ctx->send_counts[0] = (int32_t)tot[0];
@@ -1014,8 +1062,11 @@ int sph_slab_pack_send(sph_ctx* ctx, int32_t side, void* dev_records, int32_t ca
     if (!ctx || side < 0 || side > 1) return SPH_ERR_INVALID;
     if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
     if (ctx->send_counts[side] == 0) return SPH_OK;
-    if (!dev_records || capacity < ctx->send_counts[side])
-        return fail(ctx, SPH_ERR_CAPACITY, "send buffer %d < %d records", capacity, ctx->send_counts[side]);
+    // exact count known on the host (count_sends), or only on the device (count_sends_async):
+    // then the buffer must hold every owned particle
+    const int32_t need = ctx->send_counts[side] > 0 ? ctx->send_counts[side] : ctx->o1 - ctx->o0;
+    if (!dev_records || capacity < need)
+        return fail(ctx, SPH_ERR_CAPACITY, "send buffer %d < %d records", capacity, need);
     HIPCHK(hipSetDevice(ctx->device));
     const uint32_t gyz = (uint32_t)ctx->grid.gy * (uint32_t)ctx->grid.gz;
     const int32_t col_le = ctx->has_left ? ctx->sl.cx_lo - ctx->grid.cx0 : -1;
@@ -1065,25 +1116,16 @@ int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void
         KTimer t(ctx, "cell_start", 4.0 * (ctx->grid.ncells + 1));
         launch_cell_start(sk, (int32_t)n, ctx->cs, ctx->grid.ncells, ctx->gaps, ctx->sdev + 8, s);
     }
-    // ranges from the cell table at column starts
+    // ranges from the cell table at column starts: picked on the device (density reads them
+    // there) and copied back asynchronously; slab_sync_ranges waits for the copy
     const int32_t lc_lo = ctx->sl.cx_lo - ctx->grid.cx0, lc_hi = ctx->sl.cx_hi - ctx->grid.cx0;
     const int32_t idx[6] = {col_start(ctx, 0), col_start(ctx, lc_lo), col_start(ctx, lc_lo + 1),
                             col_start(ctx, lc_hi - 1), col_start(ctx, lc_hi), col_start(ctx, ctx->grid.gx)};
-    uint32_t v[6];
     launch_pick(ctx->cs, idx, 6, ctx->sdev, s);
-    HIPCHK(hipMemcpyAsync(v, ctx->sdev, sizeof v, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    int32_t* r = ctx->rng;
-    r[0] = (int32_t)v[0]; r[1] = (int32_t)v[1];                          // ghost left
-    r[2] = (int32_t)v[1]; r[3] = (int32_t)v[4];                          // owned
-    r[4] = (int32_t)v[4]; r[5] = (int32_t)v[5];                          // ghost right
-    r[6] = (int32_t)v[1]; r[7] = (int32_t)v[2];                          // boundary column cx_lo
-    r[8] = (int32_t)v[3]; r[9] = (int32_t)v[4];                          // boundary column cx_hi-1
-    if (r[5] != (int32_t)n)
-        return fail(ctx, SPH_ERR_STATE, "slab assemble: %d particles fall outside the held columns", (int32_t)n - r[5]);
+    HIPCHK(hipMemcpyAsync(ctx->rng_host, ctx->sdev, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(ctx->rng_ev, s));
+    ctx->rng_pending = true;
     ctx->n = (int32_t)n;
-    ctx->o0 = r[2];
-    ctx->o1 = r[3];
     ctx->keys_valid = false;
     ctx->sk_valid = false;
     return SPH_OK;
@@ -1091,6 +1133,8 @@ int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void
 
 int sph_slab_ranges(sph_ctx* ctx, int32_t ranges[10]) {
     if (!ctx || !ranges) return SPH_ERR_INVALID;
+    int rc = slab_sync_ranges(ctx);
+    if (rc != SPH_OK) return rc;
     std::memcpy(ranges, ctx->rng, sizeof ctx->rng);
     return SPH_OK;
 }
@@ -1099,6 +1143,16 @@ int sph_slab_density(sph_ctx* ctx) {
     if (!ctx) return SPH_ERR_INVALID;
     if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
     HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->rng_pending) {   // owned range [sdev[1], sdev[4]) on the device; grid sized for all slots
+        KTimer t(ctx, "density", 24.0 * ctx->n);
+        const DevRange dr{ctx->sdev + 1, ctx->sdev + 4};
+        if (ctx->nb_variant == 0)
+            launch_density(ctx->pos, ctx->cs, 0, ctx->n, ctx->grid, ctx->sc, ctx->rp, ctx->stream, dr);
+        else
+            launch_density_tiled(ctx->pos, ctx->cs, 0, ctx->n, ctx->grid, ctx->sc, ctx->rp, ctx->stream, dr);
+        HIPCHK(hipGetLastError());
+        return SPH_OK;
+    }
     KTimer t(ctx, "density", 24.0 * (ctx->o1 - ctx->o0));
     density_range(ctx, ctx->o0, ctx->o1);
     HIPCHK(hipGetLastError());
@@ -1107,6 +1161,7 @@ int sph_slab_density(sph_ctx* ctx) {
 
 int sph_slab_pack_rho(sph_ctx* ctx, int32_t side, void* dev, int32_t capacity) {
     if (!ctx || side < 0 || side > 1) return SPH_ERR_INVALID;
+    if (int rc = slab_sync_ranges(ctx)) return rc;
     const int32_t b = ctx->rng[6 + 2 * side], e = ctx->rng[7 + 2 * side];
     if (e == b) return SPH_OK;
     if (!dev || capacity < e - b) return fail(ctx, SPH_ERR_CAPACITY, "rho buffer %d < %d", capacity, e - b);
@@ -1117,6 +1172,7 @@ int sph_slab_pack_rho(sph_ctx* ctx, int32_t side, void* dev, int32_t capacity) {
 
 int sph_slab_unpack_rho(sph_ctx* ctx, int32_t side, const void* dev, int32_t count) {
     if (!ctx || side < 0 || side > 1) return SPH_ERR_INVALID;
+    if (int rc = slab_sync_ranges(ctx)) return rc;
     const int32_t b = ctx->rng[4 * side], e = ctx->rng[4 * side + 1];
     if (count != e - b)
         return fail(ctx, SPH_ERR_STATE, "ghost column %d holds %d particles but %d densities arrived", side, e - b, count);
@@ -1138,6 +1194,7 @@ static void slab_force_range(sph_ctx* ctx, float dt, int32_t b, int32_t e) {
 int sph_slab_force(sph_ctx* ctx, float dt, int32_t part) {
     if (!ctx || part < 0 || part > 2) return SPH_ERR_INVALID;
     if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
+    if (int rc = slab_sync_ranges(ctx)) return rc;
     HIPCHK(hipSetDevice(ctx->device));
     const int32_t* r = ctx->rng;
     // interior = owned slots whose neighbourhood holds no ghost
@@ -1170,6 +1227,7 @@ int sph_slab_finish_step(sph_ctx* ctx, float dt) {
 
 int sph_slab_read_owned(sph_ctx* ctx, float* rec, int32_t count, int32_t* n_owned) {
     if (!ctx || !n_owned) return SPH_ERR_INVALID;
+    if (int rc = slab_sync_ranges(ctx)) return rc;
     const int32_t no = ctx->o1 - ctx->o0;
     *n_owned = no;
     if (count < no || (no > 0 && !rec)) return fail(ctx, SPH_ERR_INVALID, "count %d < owned %d", count, no);

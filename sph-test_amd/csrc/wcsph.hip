@@ -60,7 +60,11 @@ __device__ __forceinline__ void spline(const SphConst& c, float r2, float& W, fl
 
 __global__ __launch_bounds__(NB_BLK) void k_density(const float4* __restrict__ pos,
                                                     const uint32_t* __restrict__ cs, int32_t ib, int32_t n,
-                                                    GridDesc g, SphConst c, float2* __restrict__ rp) {
+                                                    GridDesc g, SphConst c, float2* __restrict__ rp, DevRange dr) {
+    if (dr.lo) {
+        ib = (int32_t)*dr.lo;
+        n = (int32_t)*dr.hi;
+    }
     const int32_t i = ib + blockIdx.x * NB_BLK + threadIdx.x;
     if (i >= n) return;
     const float4 pi = pos[i];
@@ -145,9 +149,10 @@ __global__ __launch_bounds__(NB_BLK) void k_force_integrate(
     append_mover(mv, i, key);
 }
 
+// dr set: [ib, ie) only sizes the grid (an upper bound); the kernel reads its bounds from dr
 void launch_density(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
-                    float2* rp, hipStream_t s) {
-    if (ie > ib) k_density<<<(ie - ib + NB_BLK - 1) / NB_BLK, NB_BLK, 0, s>>>(pos, cs, ib, ie, g, c, rp);
+                    float2* rp, hipStream_t s, DevRange dr) {
+    if (ie > ib) k_density<<<(ie - ib + NB_BLK - 1) / NB_BLK, NB_BLK, 0, s>>>(pos, cs, ib, ie, g, c, rp, dr);
 }
 
 void launch_force_integrate(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,

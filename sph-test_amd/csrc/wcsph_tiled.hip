@@ -163,11 +163,17 @@ __device__ __forceinline__ int32_t quadrant_target(const GridDesc& g, const floa
 
 __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restrict__ pos,
                                                           const uint32_t* __restrict__ cs, int32_t ib, int32_t n,
-                                                          GridDesc g, SphConst c, float2* __restrict__ rp) {
+                                                          GridDesc g, SphConst c, float2* __restrict__ rp,
+                                                          DevRange dr) {
     __shared__ float4 sp[TT_GCAP + 4];
     __shared__ int32_t perm[TT_BLK];
     __shared__ uint32_t qcnt[TT_BLK / 64][5];
+    if (dr.lo) {   // device-resident bounds (slab mode); the grid is an upper bound
+        ib = (int32_t)*dr.lo;
+        n = (int32_t)*dr.hi;
+    }
     const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
+    if (i0 >= n) return;   // whole workgroup: before any barrier
     const int32_t i = quadrant_target(g, pos, i0, n, perm, qcnt);
     const bool valid = i < n;
     const int32_t ilast = min(i0 + TT_BLK, n) - 1;
@@ -444,9 +450,10 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     append_mover(mv, i, key);
 }
 
+// dr set: [ib, ie) only sizes the grid (an upper bound); the kernel reads its bounds from dr
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
-                          float2* rp, hipStream_t s) {
-    if (ie > ib) k_density_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, cs, ib, ie, g, c, rp);
+                          float2* rp, hipStream_t s, DevRange dr) {
+    if (ie > ib) k_density_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, cs, ib, ie, g, c, rp, dr);
 }
 
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,

@@ -7,9 +7,11 @@ that is RCCL over xGMI, ordered on the same HIP stream as libsphhip's kernels. P
 
   1. count_sends / pack_send: owned particles now in column <= cx_lo go left, those in
      column >= cx_hi-1 go right (ballot/scan compaction, order preserved) — one exchange
-     carries both the migrants and the position/velocity halo;
-  2. assemble: [from left | own | from right] -> keys -> radix sort -> cell start;
-  3. density on the owned slots;
+     carries both the migrants and the position/velocity halo. The counts stay on the device
+     until one host read of all four (sent and received);
+  2. assemble: [from left | own | from right] -> keys -> radix sort -> cell start; the slot
+     ranges are copied back asynchronously;
+  3. density on the owned slots (range read on the device), then the ranges on the host;
   4. ρ, P/ρ² of the two boundary columns -> neighbours' ghost columns, in flight while the
      interior columns' force pass runs; then the boundary columns' force pass;
   5. finish_step.
@@ -89,8 +91,18 @@ class GpuSlabBackend:
         self._chk("sph_slab_count_sends", self._L.sph_slab_count_sends(self._h, c))
         return int(c[0]), int(c[1])
 
-    def pack_send(self, side: int, buf, n: int) -> None:
-        self._chk("sph_slab_pack_send", self._L.sph_slab_pack_send(self._h, side, A.ptr(buf.data_ptr()), n))
+    def count_sends_into(self, counts) -> None:
+        """(left, right) send counts into a device int64[2] tensor, without a host sync."""
+        self._chk("sph_slab_count_sends_async",
+                  self._L.sph_slab_count_sends_async(self._h, A.ptr(counts.data_ptr())))
+
+    def send_capacity(self) -> int:
+        c = C.c_int32()
+        self._chk("sph_slab_send_capacity", self._L.sph_slab_send_capacity(self._h, C.byref(c)))
+        return int(c.value)
+
+    def pack_send(self, side: int, buf, capacity: int) -> None:
+        self._chk("sph_slab_pack_send", self._L.sph_slab_pack_send(self._h, side, A.ptr(buf.data_ptr()), capacity))
 
     def assemble(self, left, nl: int, right, nr: int) -> None:
         self._chk("sph_slab_assemble", self._L.sph_slab_assemble(self._h, A.ptr(left.data_ptr() if nl else 0), nl,
@@ -178,6 +190,10 @@ class SlabRunner:
         self.right = rank + 1 if rank + 1 < world else None
         self.ranges = None
         self._owned = None
+        dev = probe.device
+        self._cnt_out = torch.zeros(2, dtype=torch.int64, device=dev)
+        self._cnt_in = torch.zeros(2, dtype=torch.int64, device=dev)
+        self._bufs = {}
 
     # ----------------------------------------------------------------- plumbing
     def bind_stream(self, handle: int) -> None:
@@ -211,45 +227,67 @@ class SlabRunner:
         for _ in range(k):
             self._one_step()
 
+    def _buf(self, name: str, n: int, width: int):
+        """Persistent device buffer of at least n rows (grown by 1/8 when too small)."""
+        b = self._bufs.get(name)
+        if b is None or b.shape[0] < n:
+            b = self.be.empty(max(n + n // 8, 1), width)
+            self._bufs[name] = b
+        return b
+
     def _one_step(self) -> None:
         be, dt = self.be, self.dt
-        # 1. migrants + x,v halo in one exchange
-        nl, nr = be.count_sends()
+        # 1. migrants + x,v halo in one exchange. The send counts stay on the device: the packs go
+        #    to capacity-sized buffers, the counts go to the neighbours as device tensors, and the
+        #    host reads all four counts once.
+        be.count_sends_into(self._cnt_out)
+        cap = be.send_capacity()
+        bl, br = self._buf("send_l", cap, REC_FLOATS), self._buf("send_r", cap, REC_FLOATS)
+        if self.left is not None:
+            be.pack_send(0, bl, bl.shape[0])
+        if self.right is not None:
+            be.pack_send(1, br, br.shape[0])
+        self._cnt_in.zero_()
+        sends, recvs = [], []
+        if self.left is not None:
+            sends.append((self._cnt_out[0:1], self.left))
+            recvs.append((self._cnt_in[0:1], self.left))
+        if self.right is not None:
+            sends.append((self._cnt_out[1:2], self.right))
+            recvs.append((self._cnt_in[1:2], self.right))
+        for w in self._p2p(sends, recvs):
+            w.wait()
+        nl, nr, il, ir = (int(v) for v in self.torch.cat([self._cnt_out, self._cnt_in]).cpu().tolist())
         if self.left is None:
-            nl = 0
+            nl = il = 0
         if self.right is None:
-            nr = 0
-        bl, br = be.empty(nl, REC_FLOATS), be.empty(nr, REC_FLOATS)
-        if nl:
-            be.pack_send(0, bl, nl)
-        if nr:
-            be.pack_send(1, br, nr)
-        il, ir = self._exchange_counts(nl, nr)
-        rl, rr = be.empty(il, REC_FLOATS), be.empty(ir, REC_FLOATS)
+            nr = ir = 0
+        rl, rr = self._buf("recv_l", il, REC_FLOATS), self._buf("recv_r", ir, REC_FLOATS)
         sends = [(bl[:nl], self.left)] if nl else []
         sends += [(br[:nr], self.right)] if nr else []
         recvs = [(rl[:il], self.left)] if il else []
         recvs += [(rr[:ir], self.right)] if ir else []
         for w in self._p2p(sends, recvs):
             w.wait()
-        # 2. rebuild + sort; 3. density
+        # 2. rebuild + sort; 3. density (reads its slot range on the device), then the ranges
+        #    (their copy-back completes while density runs)
         be.assemble(rl, il, rr, ir)
+        be.density()
         r = be.ranges()
         self.ranges = r
-        be.density()
         # 4. ρ halo: boundary columns out, ghost columns in; interior force meanwhile
         nbl, nbr = r[7] - r[6], r[9] - r[8]
         ngl, ngr = r[1] - r[0], r[5] - r[4]
         sends, recvs = [], []
         if self.left is not None and nbl:
-            sl = be.empty(nbl, 2)
+            sl = self._buf("rho_sl", nbl, 2)
             be.pack_rho(0, sl, nbl)
             sends.append((sl[:nbl], self.left))
         if self.right is not None and nbr:
-            sr = be.empty(nbr, 2)
+            sr = self._buf("rho_sr", nbr, 2)
             be.pack_rho(1, sr, nbr)
             sends.append((sr[:nbr], self.right))
-        gl, gr = be.empty(ngl, 2), be.empty(ngr, 2)
+        gl, gr = self._buf("rho_gl", ngl, 2), self._buf("rho_gr", ngr, 2)
         if ngl:
             recvs.append((gl[:ngl], self.left))
         if ngr:

@@ -51,6 +51,13 @@ class CpuSlabBackend:
         nr = int((col >= self.cx_hi - 1).sum()) if self.has_right else 0
         return nl, nr
 
+    def count_sends_into(self, counts):
+        nl, nr = self.count_sends()
+        counts[0], counts[1] = nl, nr
+
+    def send_capacity(self):
+        return max(self.o1 - self.o0, 1)
+
     def pack_send(self, side, buf, n):
         col = self._cols()
         sel = (col <= self.cx_lo) if side == 0 else (col >= self.cx_hi - 1)
@@ -59,7 +66,8 @@ class CpuSlabBackend:
         rec[:, 0:3] = self.pos[idx]
         rec[:, 3] = self.id[idx].view(np.float32)
         rec[:, 4:7] = self.vel[idx]
-        buf[:n] = torch.from_numpy(rec)
+        assert len(rec) <= n, "send buffer smaller than the records"
+        buf[:len(rec)] = torch.from_numpy(rec)
 
     def assemble(self, left, nl, right, nr):
         L = left[:nl].numpy() if nl else np.zeros((0, 8), np.float32)
