@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event pass")
     ap.add_argument("--slab", action="store_true", help="run the multi-GPU slab step even at N=1 (rehearsal)")
+    ap.add_argument("--rebalance", type=int, default=50, help="slab cut re-balancing interval in steps (0: off)")
     return ap.parse_args()
 
 
@@ -132,7 +133,8 @@ def main():
 
     if world > 1 or args.slab:
         from sph_test_amd import slab
-        runner = slab.SlabRunner(args.config, rank, world, device=local, profile=not args.no_profile)
+        runner = slab.SlabRunner(args.config, rank, world, device=local, profile=not args.no_profile,
+                                 rebalance_every=args.rebalance)
     else:
         runner = SingleRunner(pkg, args.config, local, profile=not args.no_profile)
 

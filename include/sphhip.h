@@ -184,6 +184,11 @@ typedef struct sph_slab {
 /* ranges[]: ghost-left [0,1), owned [2,3), ghost-right [4,5), boundary column cx_lo [6,7),
  * boundary column cx_hi-1 [8,9), all as sorted-slot index ranges [begin, end). */
 int sph_slab_set(sph_ctx* ctx, const sph_slab* slab);
+/* re-balancing (between steps): the owned particles per GLOBAL column (zero outside the owned
+ * columns; ncols >= the grid's columns), and a new owned range that keeps the particles: the next
+ * step's exchange sends the columns that changed owner (move each cut by at most one column). */
+int sph_slab_column_counts(sph_ctx* ctx, int64_t* counts, int32_t ncols);
+int sph_slab_recut(sph_ctx* ctx, const sph_slab* slab);
 int sph_slab_init_scenario(sph_ctx* ctx, const sph_scenario* sc);
 int sph_slab_count_sends(sph_ctx* ctx, int32_t counts[2]);
 /* the same counts written to DEVICE memory (int64[2]: left, right) without a host sync; the

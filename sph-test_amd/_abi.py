@@ -130,6 +130,8 @@ SIGNATURES = {
     "sph_slab_init_scenario": ([_P, C.POINTER(SphScenario)], C.c_int),
     "sph_slab_count_sends": ([_P, C.POINTER(C.c_int32)], C.c_int),
     "sph_slab_count_sends_async": ([_P, _P], C.c_int),
+    "sph_slab_column_counts": ([_P, _P, _I], C.c_int),
+    "sph_slab_recut": ([_P, C.POINTER(SphSlab)], C.c_int),
     "sph_slab_send_capacity": ([_P, C.POINTER(C.c_int32)], C.c_int),
     "sph_slab_pack_send": ([_P, _I, _P, _I], C.c_int),
     "sph_slab_assemble": ([_P, _P, _I, _P, _I], C.c_int),

@@ -171,8 +171,9 @@ void launch_resort(const uint32_t* sk, uint32_t* cs, uint32_t ncells, int32_t n,
                    uint32_t* sk_o, hipStream_t s);
 
 // grid / data movement (grid.hip)
+// window_sentinel (slab): a particle outside the held columns gets key ncells (sorts last)
 void launch_keys(const float4* pos, int32_t n, const int32_t* id, int32_t n_active_id,
-                 GridDesc g, uint32_t* keys, hipStream_t s);
+                 GridDesc g, uint32_t* keys, hipStream_t s, bool window_sentinel = false);
 // cell_start[k] = lower_bound(sorted keys, k) for k = 0..ncells, every cell written once:
 // each particle boundary fills the cells up to its key; gaps longer than CS_SHORT cells are
 // queued (gap list + counter, zeroed by the call) and filled by whole workgroups.
@@ -226,6 +227,7 @@ void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel
                       const uint32_t* blk, float4* out, hipStream_t s);
 void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, int32_t* id,
                         hipStream_t s);
+void launch_column_starts(const uint32_t* cs, uint32_t gyz, int32_t c0, int32_t m, uint32_t* out, hipStream_t s);
 void launch_pick(const uint32_t* cs, const int32_t* idx, int32_t m, uint32_t* out, hipStream_t s);
 // owned slots [o0, o0+n) -> records of 8 floats (x,y,z,u,v,w,id-bits,ρ)
 void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, const float2* rp,

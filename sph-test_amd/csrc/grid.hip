@@ -19,12 +19,16 @@ static inline int nblk(int64_t n) { return (int)((n + BLK - 1) / BLK); }
 
 __global__ __launch_bounds__(BLK) void k_keys(const float4* __restrict__ pos, int32_t n,
                                               const int32_t* __restrict__ id, int32_t n_active_id,
-                                              GridDesc g, uint32_t* __restrict__ keys) {
+                                              GridDesc g, uint32_t* __restrict__ keys, bool window_sentinel) {
     const int32_t i = blockIdx.x * BLK + threadIdx.x;
     if (i >= n) return;
     const float4 p = pos[i];
     uint32_t k = cell_key(g, p.x, p.y, p.z);
     if (id != nullptr && id[i] >= n_active_id) k = g.ncells;   // inactive: sorts last
+    if (window_sentinel) {   // slab: outside the held columns (already sent away): sorts last
+        const int32_t c = cell_coord(p.x, g.ox, g.inv_cell, g.gx_all) - g.cx0;
+        if (c < 0 || c >= g.gx) k = g.ncells;
+    }
     keys[i] = k;
 }
 
@@ -216,8 +220,8 @@ __global__ __launch_bounds__(BLK) void k_iota(uint32_t* __restrict__ v, int32_t 
 
 // ---------------------------------------------------------------- launchers
 void launch_keys(const float4* pos, int32_t n, const int32_t* id, int32_t n_active_id, GridDesc g,
-                 uint32_t* keys, hipStream_t s) {
-    if (n > 0) k_keys<<<nblk(n), BLK, 0, s>>>(pos, n, id, n_active_id, g, keys);
+                 uint32_t* keys, hipStream_t s, bool window_sentinel) {
+    if (n > 0) k_keys<<<nblk(n), BLK, 0, s>>>(pos, n, id, n_active_id, g, keys, window_sentinel);
 }
 void launch_cell_start(const uint32_t* sk, int32_t n, uint32_t* cs, uint32_t ncells, uint4* gaps,
                        uint32_t* gap_count, hipStream_t s) {

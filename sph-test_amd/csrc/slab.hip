@@ -182,6 +182,17 @@ __global__ __launch_bounds__(SL_BLK) void k_pack_owned(const float4* __restrict_
     q[7] = rp ? rp[o0 + i].x : 0.f;
 }
 
+// out[t] = cs at the start of local column c0 + t, t in [0, m)
+__global__ __launch_bounds__(SL_BLK) void k_column_starts(const uint32_t* __restrict__ cs, uint32_t gyz, int32_t c0,
+                                                          int32_t m, uint32_t* __restrict__ out) {
+    const int32_t t = blockIdx.x * SL_BLK + threadIdx.x;
+    if (t < m) out[t] = cs[(size_t)(c0 + t) * gyz];
+}
+
+void launch_column_starts(const uint32_t* cs, uint32_t gyz, int32_t c0, int32_t m, uint32_t* out, hipStream_t s) {
+    if (m > 0) k_column_starts<<<(m + SL_BLK - 1) / SL_BLK, SL_BLK, 0, s>>>(cs, gyz, c0, m, out);
+}
+
 void launch_pick(const uint32_t* cs, const int32_t* idx, int32_t m, uint32_t* out, hipStream_t s) {
     Pick10 p{};
     for (int k = 0; k < m && k < 10; ++k) p.idx[k] = idx[k];

@@ -99,6 +99,7 @@ struct sph_ctx {
     uint32_t* rng_host = nullptr;   // pinned: column-start picks of the last assemble
     hipEvent_t rng_ev = nullptr;    // recorded after their device->host copy
     bool rng_pending = false;       // rng[] / o0 / o1 not yet updated from rng_host
+    int32_t dropped = 0;            // own particles the last assemble dropped (outside the window)
 };
 
 namespace {
@@ -925,8 +926,9 @@ static int slab_sync_ranges(sph_ctx* ctx) {
     r[8] = (int32_t)v[3]; r[9] = (int32_t)v[4];                          // boundary column cx_hi-1
     ctx->o0 = r[2];
     ctx->o1 = r[3];
-    if (r[5] != ctx->n)
-        return fail(ctx, SPH_ERR_STATE, "slab assemble: %d particles fall outside the held columns", ctx->n - r[5]);
+    if (r[5] > ctx->n) return fail(ctx, SPH_ERR_STATE, "slab assemble: %d slots > %d particles", r[5], ctx->n);
+    ctx->dropped = ctx->n - r[5];   // own particles outside the held columns, already sent away
+    ctx->n = r[5];
     return SPH_OK;
 }
 
@@ -966,6 +968,38 @@ int sph_slab_set(sph_ctx* ctx, const sph_slab* slab) {
     ctx->n = ctx->o0 = ctx->o1 = 0;
     ctx->rng_pending = false;
     return slab_local_grid(ctx);
+}
+
+int sph_slab_recut(sph_ctx* ctx, const sph_slab* slab) {
+    if (!ctx || !slab) return SPH_ERR_INVALID;
+    if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "sph_slab_set first");
+    const int32_t GX = ctx->gglobal.gx;
+    if (slab->cx_lo < 0 || slab->cx_hi > GX || slab->cx_lo >= slab->cx_hi)
+        return fail(ctx, SPH_ERR_INVALID, "slab [%d,%d) outside 0..%d", slab->cx_lo, slab->cx_hi, GX);
+    if (int rc = slab_sync_ranges(ctx)) return rc;
+    HIPCHK(hipSetDevice(ctx->device));
+    // the owned slots [o0, o1) keep their particles; only the held window moves. Their keys are
+    // recomputed in the new window by the next count_sends.
+    ctx->sl = *slab;
+    return slab_local_grid(ctx);
+}
+
+int sph_slab_column_counts(sph_ctx* ctx, int64_t* counts, int32_t ncols) {
+    if (!ctx || !counts) return SPH_ERR_INVALID;
+    if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
+    if (ncols < ctx->gglobal.gx) return fail(ctx, SPH_ERR_INVALID, "ncols %d < columns %d", ncols, ctx->gglobal.gx);
+    if (int rc = slab_sync_ranges(ctx)) return rc;
+    HIPCHK(hipSetDevice(ctx->device));
+    for (int32_t c = 0; c < ncols; ++c) counts[c] = 0;
+    const int32_t m = ctx->sl.cx_hi - ctx->sl.cx_lo + 1;
+    std::vector<uint32_t> st(m);
+    const uint32_t gyz = (uint32_t)ctx->grid.gy * (uint32_t)ctx->grid.gz;
+    launch_column_starts(ctx->cs, gyz, ctx->sl.cx_lo - ctx->grid.cx0, m, (uint32_t*)ctx->staging, ctx->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(st.data(), ctx->staging, (size_t)m * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (int32_t k = 0; k + 1 < m; ++k) counts[ctx->sl.cx_lo + k] = (int64_t)st[k + 1] - (int64_t)st[k];
+    return SPH_OK;
 }
 
 int sph_slab_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
@@ -1097,7 +1131,8 @@ int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void
             HIPCHK(hipMemcpyAsync(ctx->id2 + nl, ctx->id + ctx->o0, (size_t)no * 4, hipMemcpyDeviceToDevice, s));
         }
         launch_slab_unpack((const float4*)dev_right, nr, ctx->pos2 + nl + no, ctx->vel2 + nl + no, ctx->id2 + nl + no, s);
-        launch_keys(ctx->pos2, (int32_t)n, nullptr, 0, ctx->grid, ctx->keys, s);
+        // own particles outside the held columns were sent away this step: they sort last and drop
+        launch_keys(ctx->pos2, (int32_t)n, nullptr, 0, ctx->grid, ctx->keys, s, true);
     }
     int side;
     {

@@ -40,13 +40,19 @@ def weak_scenario(config: str, world: int, dx: float = 0.01, seed: int = 1234) -
     return make_scenario(kind, dim, nx * world, ny, nz, tx * world, ty, tz, dx=dx, seed=seed)
 
 
+def global_columns(params: A.SphParams) -> int:
+    """Cell columns of the global grid along x (cells 2h, SPEC_SPH.md §0)."""
+    cell = np.float32(2.0) * np.float32(params.h)
+    return int(np.floor(np.float32(params.box[0]) / cell)) + 1
+
+
 def balanced_cuts(sc: A.SphScenario, params: A.SphParams, world: int) -> List[Tuple[int, int]]:
     """Column cuts with equal initial particle counts (the lattice is uniform in y and z, so
     counts per column come from the x lattice index alone; jitter is ignored, cuts only need
     to be identical on every rank)."""
     cell = np.float32(2.0) * np.float32(params.h)
     inv = np.float32(1.0) / cell
-    G = int(np.floor(np.float32(params.box[0]) / cell)) + 1
+    G = global_columns(params)
     x = (np.arange(sc.nx, dtype=np.float32) + np.float32(0.5)) * np.float32(sc.dx)
     col = np.clip(np.floor(x * inv).astype(np.int64), 0, G - 1)
     per_col = np.bincount(col, minlength=G).astype(np.float64)
@@ -60,6 +66,43 @@ def balanced_cuts(sc: A.SphScenario, params: A.SphParams, world: int) -> List[Tu
         cuts.append(c)
     cuts.append(G)
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def column_counts(sc: A.SphScenario, params: A.SphParams) -> np.ndarray:
+    """Initial particles per global column (lattice, jitter ignored)."""
+    cell = np.float32(2.0) * np.float32(params.h)
+    inv = np.float32(1.0) / cell
+    G = global_columns(params)
+    x = (np.arange(sc.nx, dtype=np.float32) + np.float32(0.5)) * np.float32(sc.dx)
+    col = np.clip(np.floor(x * inv).astype(np.int64), 0, G - 1)
+    per_x = sc.ny * (sc.nz if sc.dim == 3 else 1)
+    return np.bincount(col, minlength=G).astype(np.int64) * per_x
+
+
+def rebalance_cuts(cuts: List[Tuple[int, int]], hist: np.ndarray, max_move: int = 1,
+                   min_width: int = 2) -> List[Tuple[int, int]]:
+    """New cuts from the global per-column particle histogram: every inner
+    cut moves toward the equal-count position by at most max_move columns, and a move is dropped
+    when it would leave a slab narrower than min_width. With max_move = 1 every particle changes
+    owner only between neighbouring ranks, which the step's exchange already handles. A pure
+    function of its inputs, so every rank computes the same cuts."""
+    world = len(cuts)
+    b = [c[0] for c in cuts] + [cuts[-1][1]]
+    cum = np.cumsum(np.asarray(hist, dtype=np.float64))
+    total = cum[-1] if len(cum) else 0.0
+    nb = list(b)
+    if total > 0:
+        for r in range(1, world):
+            ideal = int(np.searchsorted(cum, total * r / world, side="left")) + 1
+            nb[r] = b[r] + max(-max_move, min(max_move, ideal - b[r]))
+    changed = True
+    while changed:                       # drop moves that squeeze a slab (terminates: moves only revert)
+        changed = False
+        for r in range(1, world):
+            if nb[r] != b[r] and (nb[r] - nb[r - 1] < min_width or nb[r + 1] - nb[r] < min_width):
+                nb[r] = b[r]
+                changed = True
+    return [(nb[r], nb[r + 1]) for r in range(world)]
 
 
 class GpuSlabBackend:
@@ -128,6 +171,15 @@ class GpuSlabBackend:
     def finish(self, dt: float) -> None:
         self._chk("sph_slab_finish_step", self._L.sph_slab_finish_step(self._h, dt))
 
+    def column_counts(self, ncols: int) -> np.ndarray:
+        """Owned particles per global column (zero outside the owned columns)."""
+        out = np.zeros(ncols, np.int64)
+        self._chk("sph_slab_column_counts", self._L.sph_slab_column_counts(self._h, A.ptr(out), ncols))
+        return out
+
+    def recut(self, cut: Tuple[int, int]) -> None:
+        self._chk("sph_slab_recut", self._L.sph_slab_recut(self._h, C.byref(A.SphSlab(cut[0], cut[1]))))
+
     def read_owned(self) -> np.ndarray:
         """(n, 8) records: x, y, z, u, v, w, id (as int32 bits), ρ."""
         cap = self.ctx.capacity
@@ -167,18 +219,27 @@ class SlabRunner:
     """Drives one rank's backend through the decomposed step (see module doc)."""
 
     def __init__(self, config: str, rank: int, world: int, device: int = 0, profile: bool = False,
-                 backend=None, scenario: Optional[A.SphScenario] = None, capacity_factor: float = 1.5):
+                 backend=None, scenario: Optional[A.SphScenario] = None, capacity_factor: float = 1.5,
+                 cuts: Optional[List[Tuple[int, int]]] = None, rebalance_every: int = 0):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
         self.config, self.rank, self.world = config, rank, world
         self.scenario = scenario if scenario is not None else weak_scenario(config, world)
         self.params, self.dt = scenario_params(self.scenario)
-        self.cuts = balanced_cuts(self.scenario, self.params, world)
+        self.cuts = [tuple(c) for c in cuts] if cuts is not None else balanced_cuts(self.scenario, self.params, world)
+        self.rebalance_every = rebalance_every
+        self.steps_done = 0
+        self.rebalances = 0
         sc = self.scenario
         self.n_global = sc.nx * sc.ny * (sc.nz if sc.dim == 3 else 1)
         if backend is None:
-            cap = int(self.n_global / world * capacity_factor) + 4096
+            # room for the larger of an even share and this rank's initial share, plus a halo
+            # column on each side, times capacity_factor (re-balancing only moves toward even)
+            per_col = column_counts(sc, self.params)
+            lo, hi = self.cuts[rank]
+            share = max(self.n_global / world, float(per_col[lo:hi].sum()))
+            cap = int((share + 2 * float(per_col.max())) * capacity_factor) + 4096
             backend = GpuSlabBackend(sc, self.params, self.cuts[rank], cap, device=device, profile=profile)
         elif callable(backend) and not hasattr(backend, "count_sends"):
             backend = backend(self.cuts[rank])          # factory: cut -> backend
@@ -225,7 +286,27 @@ class SlabRunner:
     # ----------------------------------------------------------------- step
     def step(self, k: int = 1) -> None:
         for _ in range(k):
+            if self.rebalance_every and self.steps_done and self.steps_done % self.rebalance_every == 0:
+                self._rebalance()
             self._one_step()
+            self.steps_done += 1
+
+    def _rebalance(self) -> None:
+        """All-reduce the per-column owned counts, move the cuts (identically on every rank), and
+        re-window this rank's context; the next exchange moves the particles that changed owner."""
+        hist = self.be.column_counts(global_columns(self.params))
+        if self.world > 1 and self.dist.is_initialized():
+            on_cpu = self.dist.get_backend() == "gloo"
+            t = self.torch.from_numpy(hist)
+            if not on_cpu:
+                t = t.to(self.be.empty(1, 1).device)
+            self.dist.all_reduce(t)
+            hist = t.cpu().numpy()
+        new = rebalance_cuts(self.cuts, hist)
+        if new != self.cuts:
+            self.cuts = new
+            self.be.recut(new[self.rank])
+            self.rebalances += 1
 
     def _buf(self, name: str, n: int, width: int):
         """Persistent device buffer of at least n rows (grown by 1/8 when too small)."""

@@ -136,6 +136,18 @@ class CpuSlabBackend:
         del self.pos_out, self.vel_out
         self.t += dt
 
+    def column_counts(self, ncols):
+        out = np.zeros(ncols, np.int64)
+        cs, g = self.cs, self.gyz
+        for c in range(self.cx_lo, self.cx_hi):
+            out[c] = int(cs[(c + 1) * g]) - int(cs[c * g])
+        return out
+
+    def recut(self, cut):
+        self.cx_lo, self.cx_hi = cut
+        self.has_left = self.cx_lo > 0
+        self.has_right = self.cx_hi < self.G[0]
+
     def read_owned(self):
         s = slice(self.o0, self.o1)
         rec = np.zeros((self.o1 - self.o0, 8), np.float32)

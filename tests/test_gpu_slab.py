@@ -2,7 +2,8 @@
 
 * world 1: the slab path (no neighbours) must reproduce the single-context step bit for bit;
 * world 2: two ranks share the one GPU of the test box (gloo transport staged through the
-  host; bench.py uses RCCL between GPUs), compared with the single-context step.
+  host; bench.py uses RCCL between GPUs), compared with the single-context step;
+* world 3 from lopsided cuts with re-balancing every step, compared with the single-context step.
 """
 import os
 import socket
@@ -37,7 +38,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, cuts=None, rebalance_every=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, str(ROOT))
     import torch
@@ -49,11 +50,13 @@ def _worker(rank, world, port, outdir):
     from sph_test_amd import slab
     s = torch.cuda.Stream()
     torch.cuda.set_stream(s)
-    runner = slab.SlabRunner("C3", rank, world, device=0, scenario=_scenario(pkg))
+    runner = slab.SlabRunner("C3", rank, world, device=0, scenario=_scenario(pkg), cuts=cuts,
+                             rebalance_every=rebalance_every)
     runner.bind_stream(s.cuda_stream)
     runner.step(STEPS)
     torch.cuda.synchronize()
     np.save(os.path.join(outdir, f"rank{rank}.npy"), runner.owned())
+    np.save(os.path.join(outdir, f"cuts{rank}.npy"), np.array(runner.cuts))
     runner.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -77,21 +80,45 @@ def test_slab_world1_bitwise(pkg):
     assert np.array_equal(rec[order, 3:6], vs)
 
 
-def test_slab_world2_matches_single(pkg, tmp_path):
+def _run_ranks(world, tmp_path, cuts=None, rebalance_every=0):
     import multiprocessing as mp
-    sc = _scenario(pkg)
-    xs, vs = _single(pkg, sc)
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), cuts, rebalance_every))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=400)
         assert p.exitcode == 0, f"rank exited with {p.exitcode}"
-    rec = np.concatenate([np.load(tmp_path / f"rank{r}.npy") for r in range(2)])
+    return np.concatenate([np.load(tmp_path / f"rank{r}.npy") for r in range(world)])
+
+
+def _check(rec, xs, vs):
     ids = rec[:, 6].view(np.int32)
     assert np.array_equal(np.sort(ids), np.arange(len(xs)))
     order = np.argsort(ids)
     np.testing.assert_allclose(rec[order, 0:3], xs, rtol=0, atol=2e-6)
     np.testing.assert_allclose(rec[order, 3:6], vs, rtol=1e-3, atol=2e-3)
+
+
+def test_slab_world2_matches_single(pkg, tmp_path):
+    sc = _scenario(pkg)
+    xs, vs = _single(pkg, sc)
+    _check(_run_ranks(2, tmp_path), xs, vs)
+
+
+def test_slab_world3_rebalancing_matches_single(pkg, tmp_path):
+    """Lopsided initial cuts, re-balanced every step (cuts walk one column per step; whole
+    columns change owner through the exchange; own particles left outside the moved window drop
+    out of the assemble): still the single-context step."""
+    sc = _scenario(pkg)
+    xs, vs = _single(pkg, sc)
+    from sph_test_amd import slab
+    p, _ = pkg.scenario_params(sc)
+    G = slab.global_columns(p)
+    lopsided = [(0, 3), (3, 6), (6, G)]
+    rec = _run_ranks(3, tmp_path, cuts=lopsided, rebalance_every=1)
+    final = [tuple(c) for c in np.load(tmp_path / "cuts0.npy")]
+    assert final != lopsided
+    _check(rec, xs, vs)

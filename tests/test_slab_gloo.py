@@ -24,7 +24,7 @@ def _scenario(pkg):
     return pkg.make_scenario(0, 3, 24, 16, 8, 60, 24, 8, dx=0.01, seed=4321)
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, cuts=None, rebalance_every=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1")
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "tests"))
@@ -39,29 +39,31 @@ def _worker(rank, world, port, outdir):
     p, _ = pkg.scenario_params(sc)
     op = O.sph_params(3, p.dx, p.h, p.rho0, p.c0, p.alpha, p.xsph_eps, tuple(p.gravity), tuple(p.box),
                       p.wall_restitution, p.forcing_amp, p.forcing_freq)
-    runner = slab.SlabRunner("C3", rank, world, scenario=sc,
+    runner = slab.SlabRunner("C3", rank, world, scenario=sc, cuts=cuts, rebalance_every=rebalance_every,
                              backend=lambda cut: CpuSlabBackend(O, op, sc, cut, jitter_frac=sc.jitter))
     runner.step(STEPS)
     np.save(os.path.join(outdir, f"rank{rank}.npy"), runner.owned())
     np.save(os.path.join(outdir, f"cuts{rank}.npy"), np.array(runner.cuts))
+    np.save(os.path.join(outdir, f"rebal{rank}.npy"), np.array([runner.rebalances]))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_slab_decomposition_matches_single_domain(pkg, oracle, tmp_path, world):
+def _run(world, tmp_path, cuts=None, rebalance_every=0):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), cuts, rebalance_every))
+             for r in range(world)]
     for pr in procs:
         pr.start()
     for pr in procs:
         pr.join(timeout=300)
         assert pr.exitcode == 0, f"rank exited with {pr.exitcode}"
-    parts = [np.load(tmp_path / f"rank{r}.npy") for r in range(world)]
-    cuts = np.load(tmp_path / "cuts0.npy")
-    assert len(cuts) == world and all(c[0] < c[1] for c in cuts)
+    return [np.load(tmp_path / f"rank{r}.npy") for r in range(world)]
+
+
+def _check_against_single_domain(pkg, oracle, parts):
     rec = np.concatenate(parts)
     ids = rec[:, 6].view(np.int32)
     sc = _scenario(pkg)
@@ -87,3 +89,51 @@ def test_slab_decomposition_matches_single_domain(pkg, oracle, tmp_path, world):
     # identical physics; only the summation order of key ties differs
     np.testing.assert_allclose(got_x, ref_x, rtol=0, atol=2e-6)
     np.testing.assert_allclose(got_v, ref_v, rtol=1e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_slab_decomposition_matches_single_domain(pkg, oracle, tmp_path, world):
+    parts = _run(world, tmp_path)
+    cuts = np.load(tmp_path / "cuts0.npy")
+    assert len(cuts) == world and all(c[0] < c[1] for c in cuts)
+    _check_against_single_domain(pkg, oracle, parts)
+
+
+def test_slab_rebalancing_matches_single_domain(pkg, oracle, tmp_path):
+    """Start 3 ranks from lopsided cuts and re-balance every step: the cuts walk
+    toward equal counts one column at a time, whole columns change owner through the normal
+    exchange, and the result still equals the single-domain step."""
+    from sph_test_amd import slab
+    sc = _scenario(pkg)
+    p, _ = pkg.scenario_params(sc)
+    bal = slab.balanced_cuts(sc, p, 3)
+    G = slab.global_columns(p)
+    lopsided = [(0, 2), (2, 4), (4, G)]
+    assert lopsided != bal
+    parts = _run(3, tmp_path, cuts=lopsided, rebalance_every=1)
+    final = [tuple(c) for c in np.load(tmp_path / "cuts0.npy")]
+    assert final != lopsided and np.load(tmp_path / "rebal0.npy")[0] > 0
+    for r in range(3):   # identical on every rank
+        assert [tuple(c) for c in np.load(tmp_path / f"cuts{r}.npy")] == final
+    _check_against_single_domain(pkg, oracle, parts)
+
+
+def test_rebalance_cuts_rules(pkg):
+    from sph_test_amd import slab
+    hist = np.zeros(20, np.int64)
+    hist[:8] = 100                     # all particles in columns 0..7
+    cuts = [(0, 6), (6, 12), (12, 20)]
+    new = slab.rebalance_cuts(cuts, hist)
+    assert new == [(0, 5), (5, 11), (11, 20)]          # each inner cut moves one column
+    # fixed point: a balanced cut set is kept
+    bal = [(0, 3), (3, 6), (6, 20)]
+    assert slab.rebalance_cuts(bal, hist) == bal
+    # moves right, one column each
+    assert slab.rebalance_cuts([(0, 2), (2, 4), (4, 20)], np.r_[np.zeros(15), np.full(5, 10)].astype(np.int64)) \
+        == [(0, 3), (3, 5), (5, 20)]
+    # min width: both moves would leave a 1-column slab, so both are dropped
+    h2 = np.zeros(20, np.int64)
+    h2[:2] = 100
+    assert slab.rebalance_cuts([(0, 2), (2, 4), (4, 20)], h2) == [(0, 2), (2, 4), (4, 20)]
+    # empty histogram: unchanged
+    assert slab.rebalance_cuts(cuts, np.zeros(20, np.int64)) == cuts
