@@ -143,8 +143,17 @@ int sph_init_scenario(sph_ctx* ctx, const sph_scenario* sc);
 int sph_step(sph_ctx* ctx, float dt, int32_t nsteps);
 /* replaces HandleMouseDrag → dragInputBuffer.SetData (controller:975-1034) */
 int sph_set_drag(sph_ctx* ctx, const sph_drag_input* drag);
-/* next (§8f-1): adhesion bonds, 84-byte AdhesionConnection (compute:43-55) */
+/* replaces: adhesionConnectionBuffer.SetData + the ApplyAdhesionConstraints /
+ * ApplyAdhesionDeltas dispatches (controller:285-310; compute:424-607). `conn84` holds `count`
+ * 84-byte AdhesionConnection records (compute:43-55, CellAdhesionManager.cs:511-524) whose
+ * particleA/B are particle indices. The bonds persist: every later sph_step applies them
+ * (Model R only) until the next call; count 0 removes them. The caller applies its own cap
+ * (the reference's maxAdhesionConnections, controller:129,287). */
 int sph_set_adhesion(sph_ctx* ctx, const void* conn84, int32_t count);
+/* the last step's per-bond fixed-point terms (×1e6), 16 int32 per bond:
+ * Δv_A(x,y,z,0), Δv_B(x,y,z,0), Δq_A(x,y,z,w), Δq_B(x,y,z,w) — what each bond's thread adds
+ * with InterlockedAdd in the reference (compute:451-456, 509-512, 536-539, 568-581). */
+int sph_read_adhesion_terms(sph_ctx* ctx, int32_t* terms16, int32_t count);
 
 /* ---- readback: replaces Copy*ToReadbackBuffer + GetData (compute:410-422,
  *      controller:327-333) and AsyncGPUReadback (controller:1115-1159) ---- */

@@ -20,6 +20,7 @@
 
 #define GRID_DIM 32
 #define TORQUE_SCALE 10000
+#define ADHESION_DELTA_SCALE 1000000
 
 typedef struct { float x, y, z; } f3;
 static inline f3 mk(float x, float y, float z) { f3 r = {x, y, z}; return r; }
@@ -89,6 +90,100 @@ static inline pair_out contact_pair(const or_contact_params* P, const or_particl
     return o;
 }
 
+/* ---- adhesion (compute:424-584) ---- */
+typedef struct { float x, y, z, w; } f4;
+static inline f4 q4(const float* q) { f4 r = {q[0], q[1], q[2], q[3]}; return r; }
+static inline f3 qv(f4 q) { return mk(q.x, q.y, q.z); }
+static inline f4 qmul(f4 q1, f4 q2) {            /* quat_mul :359-365 */
+    f3 v = add(add(mul(qv(q2), q1.w), mul(qv(q1), q2.w)), cross(qv(q1), qv(q2)));
+    f4 r = {v.x, v.y, v.z, q1.w * q2.w - dot(qv(q1), qv(q2))};
+    return r;
+}
+static inline f4 qconj(f4 q) { f4 r = {-q.x, -q.y, -q.z, q.w}; return r; }   /* :368-371 */
+static inline f3 qrot(f4 q, f3 v) {                                          /* :374-377 */
+    return add(v, mul(cross(qv(q), add(cross(qv(q), v), mul(v, q.w))), 2.0f));
+}
+/* (int)round(x * ADHESION_DELTA_SCALE): HLSL round = round half to even (rintf in the default
+ * rounding mode), the cast = D3D ftoi */
+static inline int32_t fixp(float x) { return ftoi(rintf(x * (float)ADHESION_DELTA_SCALE)); }
+static inline void add_q(int32_t* acc, f4 d) {
+    acc[0] = (int32_t)((uint32_t)acc[0] + (uint32_t)fixp(d.x));
+    acc[1] = (int32_t)((uint32_t)acc[1] + (uint32_t)fixp(d.y));
+    acc[2] = (int32_t)((uint32_t)acc[2] + (uint32_t)fixp(d.z));
+    acc[3] = (int32_t)((uint32_t)acc[3] + (uint32_t)fixp(d.w));
+}
+static inline f4 qdiff(f4 a, f4 b) { f4 r = {a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w}; return r; }
+
+/* :474-514 (side A) / :516-540 (side B) */
+static void anchor_push(float strength, f4 q, f3 anchorLocal, f3 desiredMove, int32_t* acc) {
+    f3 rWorld = qrot(q, anchorLocal);
+    f3 rotAxis = cross(rWorld, desiredMove);
+    float rotAxisLength = len(rotAxis);
+    if (!(rotAxisLength > 1e-6f)) return;
+    rotAxis = nrm(rotAxis);
+    float effectiveness = fabsf(dot(cross(rotAxis, rWorld), desiredMove));
+    if (!(effectiveness > 1e-6f)) return;
+    float rotAngle = strength * effectiveness * 5.0f;
+    f4 rotQuat = {rotAxis.x * sinf(rotAngle * 0.5f), rotAxis.y * sinf(rotAngle * 0.5f),
+                  rotAxis.z * sinf(rotAngle * 0.5f), cosf(rotAngle * 0.5f)};
+    add_q(acc, qdiff(qmul(rotQuat, q), q));
+}
+
+/* One bond's thread of ApplyAdhesionConstraints: the 16 ints it would InterlockedAdd
+ * (Δv_A xyz 0, Δv_B xyz 0, Δq_A xyzw, Δq_B xyzw). `v1` = velocities after ApplySPHForces. */
+static void bond_terms(const or_adhesion84* c, int n, const or_particle84* in, const f3* v1, float dt,
+                       int32_t t[16]) {
+    memset(t, 0, 16 * sizeof(int32_t));
+    int idxA = c->particleA, idxB = c->particleB;
+    if (idxA < 0 || idxB < 0 || idxA >= n || idxB >= n) return;              /* :432 */
+    const or_particle84* pA = &in[idxA];
+    const or_particle84* pB = &in[idxB];
+    f3 posA = ld3(pA->position), posB = ld3(pB->position);
+    f4 rotA = q4(pA->rotation), rotB = q4(pB->rotation);
+    /* spring :437-456 */
+    f3 delta = sub(posB, posA);
+    float dist = len(delta);
+    if (dist > 1e-6f) {
+        f3 dir = divs(delta, dist);
+        float displacement = dist - c->restLength;
+        float springMultiplier = 1.0f;
+        f3 force = mul(dir, displacement * c->springStiffness * springMultiplier);
+        f3 relVel = sub(v1[idxB], v1[idxA]);
+        float dampingForce = dot(relVel, dir) * c->springDamping;
+        force = add(force, mul(dir, dampingForce));
+        f3 deltaVA = mul(divs(force, pA->mass), dt);
+        f3 deltaVB = mul(divs(neg(force), pB->mass), dt);
+        t[0] = fixp(deltaVA.x); t[1] = fixp(deltaVA.y); t[2] = fixp(deltaVA.z);
+        t[4] = fixp(deltaVB.x); t[5] = fixp(deltaVB.y); t[6] = fixp(deltaVB.z);
+    }
+    if (c->enableAnchorConstraint != 1) return;                               /* :457 */
+    float constraintStrength = c->anchorConstraintStiffness * dt;
+    f3 ancA = ld3(c->anchorLocalPosA), ancB = ld3(c->anchorLocalPosB);
+    f3 currentAnchorA = add(posA, qrot(rotA, ancA));
+    f3 currentAnchorB = add(posB, qrot(rotB, ancB));
+    f3 anchorDelta = sub(currentAnchorB, currentAnchorA);
+    float anchorDist = len(anchorDelta);
+    if (anchorDist > 1e-6f) {
+        f3 anchorDir = divs(anchorDelta, anchorDist);
+        anchor_push(constraintStrength, rotA, ancA, anchorDir, t + 8);
+        anchor_push(constraintStrength, rotB, ancB, neg(anchorDir), t + 12);
+    }
+    /* relative orientation :541-582 */
+    f4 currentRel = qmul(qconj(rotA), rotB);
+    f4 correction = qmul(q4(c->initialRelOrientation), qconj(currentRel));
+    float correctionAngle = 2.0f * atan2f(len(qv(correction)), fabsf(correction.w));
+    if (correctionAngle > 1e-6f) {
+        f3 axis = nrm(qv(correction));
+        float ocs = constraintStrength * 2.0f;
+        float angA = -ocs * correctionAngle * 0.5f;
+        float angB = ocs * correctionAngle * 0.5f;
+        f4 rqA = {axis.x * sinf(angA * 0.5f), axis.y * sinf(angA * 0.5f), axis.z * sinf(angA * 0.5f), cosf(angA * 0.5f)};
+        f4 rqB = {axis.x * sinf(angB * 0.5f), axis.y * sinf(angB * 0.5f), axis.z * sinf(angB * 0.5f), cosf(angB * 0.5f)};
+        add_q(t + 8, qdiff(qmul(rqA, rotA), rotA));
+        add_q(t + 12, qdiff(qmul(rqB, rotB), rotB));
+    }
+}
+
 static inline int32_t or_coord_r(float x, float R) {   /* compute:102-105 */
     float g = (x + R) / 4.0f;
     if (!(g > 0.0f)) return 0;
@@ -96,8 +191,10 @@ static inline int32_t or_coord_r(float x, float R) {   /* compute:102-105 */
     return (int32_t)g;
 }
 
-int or_contact_step(const or_contact_params* P, int n, or_particle84* parts, int32_t* torque_out,
-                    int nthreads) {
+/* One frame (controller:265-331): ApplySPHForces for every particle, then (nconn > 0) the
+ * adhesion pass :424-607, then drag / UpdateMotion / UpdateRotation. */
+int or_contact_step_bonds(const or_contact_params* P, int n, or_particle84* parts, int32_t* torque_out,
+                          const or_adhesion84* conns, int nconn, int32_t* terms_out, int nthreads) {
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #else
@@ -110,6 +207,9 @@ int or_contact_step(const or_contact_params* P, int n, or_particle84* parts, int
     uint32_t* sk = (uint32_t*)malloc(sizeof(uint32_t) * nn);
     uint32_t* cs = (uint32_t*)malloc(sizeof(uint32_t) * (NK + 1));
     or_particle84* in = (or_particle84*)malloc(sizeof(or_particle84) * nn);
+    f3* v1 = (f3*)malloc(sizeof(f3) * nn);
+    f3* w1 = (f3*)malloc(sizeof(f3) * nn);
+    uint32_t* tqa = (uint32_t*)malloc(sizeof(uint32_t) * 3 * nn);
     memcpy(in, parts, sizeof(or_particle84) * (size_t)n);
     /* grid: same neighbour set as the reference's linked lists, visited in stable-sorted order */
     for (int i = 0; i < n; ++i) {
@@ -158,13 +258,53 @@ int or_contact_step(const or_contact_params* P, int n, or_particle84* parts, int
                 }
             }
         }
-        or_particle84 p = *self;
         /* :302-306 */
-        f3 linearAccel = divs(totalForce, p.mass);
-        f3 angularAccel = divs(totalTorque, p.momentOfInertia);
-        f3 vel = add(ld3(p.velocity), mul(linearAccel, dt));
-        f3 omg = add(ld3(p.angularVelocity), mul(angularAccel, dt));
+        f3 linearAccel = divs(totalForce, self->mass);
+        f3 angularAccel = divs(totalTorque, self->momentOfInertia);
+        v1[a] = add(ld3(self->velocity), mul(linearAccel, dt));
+        w1[a] = add(ld3(self->angularVelocity), mul(angularAccel, dt));
+        tqa[3 * a] = tq[0]; tqa[3 * a + 1] = tq[1]; tqa[3 * a + 2] = tq[2];
+    }
+
+    /* adhesion: ApplyAdhesionConstraints :424-584 on the post-ApplySPHForces state */
+    uint32_t* dv = NULL;
+    uint32_t* dq = NULL;
+    if (nconn > 0) {
+        dv = (uint32_t*)calloc(3 * nn, sizeof(uint32_t));
+        dq = (uint32_t*)calloc(4 * nn, sizeof(uint32_t));
+        for (int b = 0; b < nconn; ++b) {
+            int32_t t[16];
+            bond_terms(&conns[b], n, in, v1, dt, t);
+            if (terms_out) memcpy(terms_out + 16 * (size_t)b, t, sizeof t);
+            int32_t ia = conns[b].particleA, ib = conns[b].particleB;
+            if (ia < 0 || ib < 0 || ia >= n || ib >= n) continue;
+            for (int k = 0; k < 3; ++k) {
+                dv[3 * (size_t)ia + k] += (uint32_t)t[k];
+                dv[3 * (size_t)ib + k] += (uint32_t)t[4 + k];
+            }
+            for (int k = 0; k < 4; ++k) {
+                dq[4 * (size_t)ia + k] += (uint32_t)t[8 + k];
+                dq[4 * (size_t)ib + k] += (uint32_t)t[12 + k];
+            }
+        }
+    }
+
+#pragma omp parallel for schedule(static)
+    for (int a = 0; a < n; ++a) {
+        or_particle84 p = in[a];
+        f3 vel = v1[a], omg = w1[a];
         f3 pos = ld3(p.position);
+        const uint32_t* tq = tqa + 3 * (size_t)a;
+        if (nconn > 0) {   /* ApplyAdhesionDeltas :593-601 */
+            const uint32_t* d = dv + 3 * (size_t)a;
+            const uint32_t* e = dq + 4 * (size_t)a;
+            vel = add(vel, divs(mk((float)(int32_t)d[0], (float)(int32_t)d[1], (float)(int32_t)d[2]),
+                                (float)ADHESION_DELTA_SCALE));
+            float r[4];
+            for (int k = 0; k < 4; ++k) r[k] = p.rotation[k] + (float)(int32_t)e[k] / (float)ADHESION_DELTA_SCALE;
+            float l = sqrtf(r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3]);
+            for (int k = 0; k < 4; ++k) p.rotation[k] = r[k] / l;
+        }
         /* ApplyDragForce :316-323 */
         if (P->drag_id >= 0 && P->drag_id == a) {
             f3 toTarget = sub(ld3(P->drag_target), pos);
@@ -216,6 +356,12 @@ int or_contact_step(const or_contact_params* P, int n, or_particle84* parts, int
             torque_out[3 * a + 2] = (int32_t)tq[2];
         }
     }
-    free(keys); free(perm); free(sk); free(cs); free(in);
+    free(keys); free(perm); free(sk); free(cs); free(in); free(v1); free(w1); free(tqa);
+    free(dv); free(dq);
     return 0;
+}
+
+int or_contact_step(const or_contact_params* P, int n, or_particle84* parts, int32_t* torque_out,
+                    int nthreads) {
+    return or_contact_step_bonds(P, n, parts, torque_out, NULL, 0, NULL, nthreads);
 }

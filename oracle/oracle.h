@@ -89,6 +89,24 @@ typedef struct {
 int or_contact_step(const or_contact_params* p, int n, or_particle84* parts, int32_t* torque_int,
                     int nthreads);
 
+/* AdhesionConnection (compute:43-55; CellAdhesionManager.cs:511-524), 84 bytes */
+typedef struct {
+    int32_t particleA, particleB;
+    float restLength, springStiffness, springDamping;
+    float connectionColor[4];
+    float initialRelOrientation[4];
+    float anchorLocalPosA[3];
+    float anchorLocalPosB[3];
+    float anchorConstraintStiffness;
+    int32_t enableAnchorConstraint;
+} or_adhesion84;
+
+/* The same step with nconn adhesion bonds applied between ApplySPHForces and the drag
+ * (controller:284-310; compute:424-607). terms (optional, 16*nconn int32) receives what each
+ * bond's thread adds: Δv_A(x,y,z,0), Δv_B(x,y,z,0), Δq_A(xyzw), Δq_B(xyzw), fixed point ×1e6. */
+int or_contact_step_bonds(const or_contact_params* p, int n, or_particle84* parts, int32_t* torque_int,
+                          const or_adhesion84* conns, int nconn, int32_t* terms, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -29,6 +29,15 @@ PARTICLE84 = np.dtype([
 ])
 assert PARTICLE84.itemsize == 84
 
+# SimulateParticles.compute:43-55 (84 bytes, field order kept)
+ADHESION84 = np.dtype([
+    ("particleA", "<i4"), ("particleB", "<i4"), ("restLength", "<f4"), ("springStiffness", "<f4"),
+    ("springDamping", "<f4"), ("connectionColor", "<f4", (4,)), ("initialRelOrientation", "<f4", (4,)),
+    ("anchorLocalPosA", "<f4", (3,)), ("anchorLocalPosB", "<f4", (3,)),
+    ("anchorConstraintStiffness", "<f4"), ("enableAnchorConstraint", "<i4"),
+])
+assert ADHESION84.itemsize == 84
+
 
 class OrGrid(C.Structure):
     _fields_ = [("origin", C.c_float * 3), ("inv_cell", C.c_float), ("inv_cell_z", C.c_float),
@@ -78,6 +87,8 @@ def lib():
         L.or_sph_lattice.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
                                      C.c_float, C.c_float, C.c_uint32, C.c_float, C.c_void_p]
         L.or_contact_step.argtypes = [P(OrContactParams), C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+        L.or_contact_step_bonds.argtypes = [P(OrContactParams), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                            C.c_int, C.c_void_p, C.c_int]
         L.or_stable_sort.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p]
         L.or_cell_start.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p]
         L.or_keys.argtypes = [P(OrGrid), C.c_int, C.c_void_p, C.c_void_p]
@@ -185,6 +196,18 @@ def contact_step(p: OrContactParams, parts, nthreads=0):
     tq = np.empty((n, 3), np.int32)
     lib().or_contact_step(C.byref(p), n, _ptr(parts), _ptr(tq), nthreads)
     return parts, tq
+
+
+def contact_step_bonds(p: OrContactParams, parts, conns, nthreads=0):
+    """One Model R step with adhesion bonds (AoS-84 particles, AoS-84 connections).
+    Returns (parts, torque_int[n,3], terms[nconn,16])."""
+    parts = np.ascontiguousarray(parts, dtype=PARTICLE84).copy()
+    conns = np.ascontiguousarray(conns, dtype=ADHESION84)
+    n, m = parts.shape[0], conns.shape[0]
+    tq = np.empty((n, 3), np.int32)
+    terms = np.zeros((max(m, 1), 16), np.int32)
+    lib().or_contact_step_bonds(C.byref(p), n, _ptr(parts), _ptr(tq), _ptr(conns), m, _ptr(terms), nthreads)
+    return parts, tq, terms[:m]
 
 
 def default_threads() -> int:

@@ -43,6 +43,15 @@ PARTICLE84 = np.dtype([
 ])
 assert PARTICLE84.itemsize == 84
 
+# AdhesionConnection (SimulateParticles.compute:43-55; CellAdhesionManager.cs:511-524), 84 bytes
+ADHESION84 = np.dtype([
+    ("particleA", "<i4"), ("particleB", "<i4"), ("restLength", "<f4"), ("springStiffness", "<f4"),
+    ("springDamping", "<f4"), ("connectionColor", "<f4", (4,)), ("initialRelOrientation", "<f4", (4,)),
+    ("anchorLocalPosA", "<f4", (3,)), ("anchorLocalPosB", "<f4", (3,)),
+    ("anchorConstraintStiffness", "<f4"), ("enableAnchorConstraint", "<i4"),
+])
+assert ADHESION84.itemsize == 84
+
 
 class SphConfig(C.Structure):
     _fields_ = [("model", C.c_int32), ("dim", C.c_int32), ("capacity", C.c_int32), ("flags", C.c_int32)]
@@ -113,6 +122,7 @@ SIGNATURES = {
     "sph_step": ([_P, C.c_float, _I], C.c_int),
     "sph_set_drag": ([_P, C.POINTER(SphDragInput)], C.c_int),
     "sph_set_adhesion": ([_P, _P, _I], C.c_int),
+    "sph_read_adhesion_terms": ([_P, _P, _I], C.c_int),
     "sph_read_positions": ([_P, _P, _I], C.c_int),
     "sph_read_rotations": ([_P, _P, _I], C.c_int),
     "sph_read_velocities": ([_P, _P, _I], C.c_int),

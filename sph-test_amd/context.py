@@ -22,6 +22,7 @@ class Context:
         self._h = h
         self.model, self.dim, self.capacity, self.device = model, dim, capacity, device
         self.n = 0
+        self.nbonds = 0
 
     # -------------------------------------------------------------- lifetime
     def close(self) -> None:
@@ -96,6 +97,22 @@ class Context:
     def set_drag(self, selected_id: int, target, strength: float) -> None:
         d = A.SphDragInput(selected_id, (C.c_float * 3)(*target), strength)
         self._chk("sph_set_drag", self._L.sph_set_drag(self._h, C.byref(d)))
+
+    def set_adhesion(self, conns: Optional[np.ndarray]) -> None:
+        """Adhesion bonds (AoS-84 AdhesionConnection records); None or empty removes them."""
+        if conns is None or len(conns) == 0:
+            self._chk("sph_set_adhesion", self._L.sph_set_adhesion(self._h, None, 0))
+            self.nbonds = 0
+            return
+        conns = np.ascontiguousarray(conns, dtype=A.ADHESION84)
+        self._chk("sph_set_adhesion", self._L.sph_set_adhesion(self._h, A.ptr(conns), len(conns)))
+        self.nbonds = len(conns)
+
+    def adhesion_terms(self) -> np.ndarray:
+        """The last step's per-bond fixed-point terms, [nbonds, 16] int32 (include/sphhip.h)."""
+        out = np.zeros((max(self.nbonds, 1), 16), np.int32)
+        self._chk("sph_read_adhesion_terms", self._L.sph_read_adhesion_terms(self._h, A.ptr(out), self.nbonds))
+        return out[: self.nbonds]
 
     def synchronize(self) -> None:
         self._chk("sph_synchronize", self._L.sph_synchronize(self._h))

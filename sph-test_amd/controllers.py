@@ -104,6 +104,11 @@ class ParticleSystemController:
         self.CpuParticleRotations: Optional[np.ndarray] = None   # :91-92
         self.LastSelectedParticleID = -1        # :125-126
         self.drag = DragInput()
+        # [Header("Adhesion Visualization")] :55-56 — any object with GetAdhesionConnectionsForGPU()
+        # returning an ADHESION84 array (CellAdhesionManager.cs:524-564)
+        self.adhesionManager = None
+        self.maxAdhesionConnections = 4096      # :128-129
+        self._bonds_uploaded: Optional[bytes] = None
         self._ctx: Optional[Context] = None
 
     # ------------------------------------------------------------------ lifecycle
@@ -131,9 +136,22 @@ class ParticleSystemController:
         p.active_particle_count = self.activeParticleCount
         self._ctx.set_params(p)
 
+    def _push_adhesion(self) -> None:
+        """:285-303 — the manager's bonds, capped at maxAdhesionConnections, applied this frame
+        when there is at least one. Re-uploaded only when they changed."""
+        conns = None
+        if self.adhesionManager is not None:
+            conns = np.ascontiguousarray(self.adhesionManager.GetAdhesionConnectionsForGPU(), dtype=A.ADHESION84)
+            conns = conns[: min(len(conns), self.maxAdhesionConnections)]
+        blob = conns.tobytes() if conns is not None and len(conns) > 0 else b""
+        if blob != self._bonds_uploaded:
+            self._ctx.set_adhesion(conns if blob else None)
+            self._bonds_uploaded = blob
+
     def Update(self, dt: float) -> None:
-        """One frame: uniforms (:255-263), the step (:265-331), readback (:332-333)."""
+        """One frame: uniforms (:255-263), the step with adhesion (:265-331), readback (:332-333)."""
         self._push_uniforms()
+        self._push_adhesion()
         d = self.drag
         self._ctx.set_drag(d.selectedID, d.targetPosition, d.strength)
         self._ctx.step(dt, 1)

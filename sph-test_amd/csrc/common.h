@@ -238,11 +238,39 @@ void launch_slab_select_columns(const float4* pos, const float4* vel, const int3
                                 uint32_t* total, float4* pos_o, float4* vel_o, int32_t* id_o,
                                 hipStream_t s);
 
+// Adhesion bonds (§8f-1), SoA of the reference's 84-byte AdhesionConnection (compute:43-55).
+struct BondSet {
+    const int2* ends;       // (particleA, particleB): particle indices
+    const float4* spring;   // (restLength, springStiffness, springDamping, anchorConstraintStiffness)
+    const float4* relq;     // initialRelOrientation
+    const float4* anc_a;    // anchorLocalPosA, w = enableAnchorConstraint (int bits)
+    const float4* anc_b;    // anchorLocalPosB
+    int32_t count;
+};
+// Per-bond int terms and the per-particle incidence lists the finishing pass gathers them by.
+struct BondView {
+    int32_t count;          // bonds this step; 0: ApplyAdhesionDeltas is not dispatched
+    int32_t n_index;        // particle indices covered by off[]
+    const uint32_t* off;    // [n_index + 1] CSR offsets by particle index
+    const uint32_t* ent;    // bond << 1 | side (0: particleA, 1: particleB)
+    const int4* terms;      // [4 * count]: Δv_A, Δv_B, Δq_A, Δq_B (fixed point ×1e6)
+};
+
 // Model R (contact.hip)
 void launch_contact_step(const float4* pos, const float4* vel, const float4* omg, const float4* rot,
                          const float4* aux, const int32_t* id, const uint32_t* cs, int32_t n_active,
                          int32_t n, GridDesc g, ContactConst c, float4* pos_o, float4* vel_o,
-                         float4* omg_o, float4* rot_o, int32_t* torque_o, uint32_t* keys_o,
-                         int32_t n_active_id, hipStream_t s);
+                         float4* omg_o, float4* rot_o, int32_t* torque_o, uint32_t* keys_o, hipStream_t s);
+void launch_contact_forces(const float4* pos, const float4* vel, const float4* omg, const int32_t* id,
+                           const uint32_t* cs, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
+                           float4* vel_o, float4* omg_o, int32_t* torque_o, int32_t* slot_of, hipStream_t s);
+void launch_contact_finish(const float4* pos, const float4* rot, const float4* aux, const int32_t* id,
+                           const int32_t* torque, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
+                           BondView b, float4* vel_io, float4* omg_io, float4* pos_o, float4* rot_o,
+                           uint32_t* keys_o, hipStream_t s);
+// ApplyAdhesionConstraints (compute:424-584), one lane per bond: reads the start-of-step
+// position and rotation and the post-contact velocity, writes the bond's four int terms.
+void launch_bond_terms(BondSet bs, const int32_t* slot_of, int32_t n, const float4* pos, const float4* vel1,
+                       const float4* rot, float dt, int4* terms, hipStream_t s);
 
 }  // namespace sph

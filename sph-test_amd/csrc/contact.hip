@@ -4,41 +4,23 @@
 //   ApplySPHForces (SimulateParticles.compute:211-309), ApplyDragForce (:311-324),
 //   UpdateMotion (:326-357), UpdateRotation (:379-408) and the torqueAccumBuffer clear
 //   (ParticleSystemController.cs:265).
+// With adhesion bonds the reference runs its two bond kernels between ApplySPHForces and the
+// drag (controller:284-310), so the frame splits in three: k_contact_forces, the bond pass
+// (adhesion.hip), k_contact_finish.
 // Jacobi semantics: all reads come from the start-of-step arrays, all writes go to the
 // *_o arrays. The reaction torque the reference scatters with three InterlockedAdds per
 // contact (compute:291-294) is gathered instead: particle a evaluates each contact pair a
 // second time from b's side and sums the same truncated int3 terms. int32 addition is
 // associative, so the sum is bit-identical to the atomic one, with no atomics and no
 // ordering dependence.
+#include "bonds.h"
 #include "common.h"
+#include "vec3.h"
 
 namespace sph {
 
 constexpr int CT_BLK = 256;
 constexpr float TORQUE_SCALE = 10000.0f;   // compute:19
-
-struct f3 { float x, y, z; };
-__device__ __forceinline__ f3 mk(float x, float y, float z) { return {x, y, z}; }
-__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
-__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
-__device__ __forceinline__ f3 operator*(f3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
-__device__ __forceinline__ f3 operator/(f3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
-__device__ __forceinline__ f3 operator-(f3 a) { return {-a.x, -a.y, -a.z}; }
-__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ float len(f3 a) { return sqrtf(dot(a, a)); }
-__device__ __forceinline__ f3 cross(f3 a, f3 b) {
-    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
-}
-__device__ __forceinline__ float saturate(float x) { return x > 0.0f ? (x < 1.0f ? x : 1.0f) : 0.0f; }
-__device__ __forceinline__ f3 normalize(f3 a) { return a / len(a); }
-__device__ __forceinline__ f3 xyz(float4 v) { return {v.x, v.y, v.z}; }
-
-__device__ __forceinline__ int32_t ftoi(float x) {   // D3D ftoi: truncate, saturate, NaN -> 0
-    if (x != x) return 0;
-    if (x >= 2147483648.0f) return 2147483647;
-    if (x <= -2147483648.0f) return (int32_t)0x80000000;
-    return (int32_t)x;
-}
 
 struct Body { f3 pos, vel, omg; float r; };
 
@@ -76,27 +58,16 @@ __device__ __forceinline__ int contact_pair(const ContactConst& c, const Body& A
     return 2;
 }
 
-__global__ __launch_bounds__(CT_BLK) void k_contact_step(
-    const float4* __restrict__ pos, const float4* __restrict__ vel, const float4* __restrict__ omg,
-    const float4* __restrict__ rot, const float4* __restrict__ aux, const int32_t* __restrict__ id,
-    const uint32_t* __restrict__ cs, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
-    float4* __restrict__ pos_o, float4* __restrict__ vel_o, float4* __restrict__ omg_o,
-    float4* __restrict__ rot_o, int32_t* __restrict__ torque_o, uint32_t* __restrict__ keys_o) {
-    const int32_t a = blockIdx.x * CT_BLK + threadIdx.x;
-    if (a >= n) return;
-    const float4 pa = pos[a], va = vel[a], wa = omg[a], qa = rot[a];
-    if (a >= n_active) {   // inactive slots (id >= activeParticleCount) pass through
-        pos_o[a] = pa; vel_o[a] = va; omg_o[a] = wa; rot_o[a] = qa;
-        if (torque_o) { torque_o[3 * a] = 0; torque_o[3 * a + 1] = 0; torque_o[3 * a + 2] = 0; }
-        keys_o[a] = g.ncells;
-        return;
-    }
+// ApplySPHForces' neighbour loop (compute:228-300) for slot a, then its integration
+// (:302-306): v1 = v + F/m·dt, w1 = ω + T/I·dt, and the int reaction torque sums.
+__device__ __forceinline__ void contact_accumulate(const float4* __restrict__ pos, const float4* __restrict__ vel,
+                                                   const float4* __restrict__ omg, const uint32_t* __restrict__ cs,
+                                                   const GridDesc& g, const ContactConst& c, int32_t a, float4 pa,
+                                                   float4 va, float4 wa, f3& v, f3& w, uint32_t tq[3]) {
     const Body A{xyz(pa), xyz(va), xyz(wa), pa.w};
-    const float mass = va.w, inertia = wa.w, drag = aux[a].x;
     const float dt = c.dt;
     f3 totalForce = mk(0, 0, 0), totalTorque = mk(0, 0, 0);
-    uint32_t tq0 = 0, tq1 = 0, tq2 = 0;   // wrapping int32 sums (InterlockedAdd)
-
+    tq[0] = tq[1] = tq[2] = 0u;   // wrapping int32 sums (InterlockedAdd)
     const int32_t cx = cell_cx(g, pa.x);
     const int32_t cy = cell_coord(pa.y, g.oy, g.inv_cell, g.gy);
     const int32_t cz = cell_coord(pa.z, g.oz, g.inv_cz, g.gz);
@@ -124,23 +95,35 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step(
             f3 F2, TA2, TB2;
             if (contact_pair(c, B, A, F2, TA2, TB2) == 2) {                  // b's scatter into a
                 const f3 sc = TB2 * dt * TORQUE_SCALE;                       // :291
-                tq0 += (uint32_t)ftoi(sc.x);
-                tq1 += (uint32_t)ftoi(sc.y);
-                tq2 += (uint32_t)ftoi(sc.z);
+                tq[0] += (uint32_t)ftoi(sc.x);
+                tq[1] += (uint32_t)ftoi(sc.y);
+                tq[2] += (uint32_t)ftoi(sc.z);
             }
         }
     }
-    // :302-306
-    f3 v = A.vel + (totalForce / mass) * dt;
-    f3 w = A.omg + (totalTorque / inertia) * dt;
-    f3 p = A.pos;
-    // ApplyDragForce :316-323 (selectedID is a particle index)
-    if (c.drag_id >= 0 && id[a] == c.drag_id) {
+    v = A.vel + (totalForce / va.w) * dt;                                    // :302-306
+    w = A.omg + (totalTorque / wa.w) * dt;
+}
+
+// ApplyDragForce (compute:316-323; selectedID is a particle index). The reference applies it
+// to any particle below particleBuffer.Length, active or not.
+__device__ __forceinline__ f3 apply_drag(const ContactConst& c, int32_t pid, f3 p, f3 v, float mass) {
+    if (c.drag_id >= 0 && pid == c.drag_id) {
         const f3 toTarget = mk(c.drag_tx, c.drag_ty, c.drag_tz) - p;
-        const f3 force = toTarget * c.drag_strength * dt;
+        const f3 force = toTarget * c.drag_strength * c.dt;
         v = v + force / mass;
     }
-    // UpdateMotion :332-354
+    return v;
+}
+
+// Drag, UpdateMotion (compute:332-354) and UpdateRotation (:385-406) of an active particle.
+__device__ __forceinline__ void contact_finish(const ContactConst& c, int32_t pid, float4 pa, f3 v, f3 w,
+                                               float mass, float inertia, float drag, float4 qa,
+                                               const uint32_t tq[3], f3& p_out, f3& v_out, f3& w_out,
+                                               float4& q_out) {
+    const float dt = c.dt;
+    f3 p = xyz(pa);
+    v = apply_drag(c, pid, p, v, mass);
     const float linearDamping = expf(-drag * c.global_drag * dt);
     const float angularDamping = expf(-c.torque_damping * dt);
     v = v * linearDamping;
@@ -153,12 +136,11 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step(
         const f3 tangentialVel = v - norm * dot(v, norm);
         const f3 frictionDir = normalize(tangentialVel + mk(1e-6f, 1e-6f, 1e-6f));
         const float frictionMag = len(tangentialVel) * c.boundary_friction;
-        const float effectiveRadius = A.r * c.roll_mult;
+        const float effectiveRadius = pa.w * c.roll_mult;
         const f3 torque = cross(-norm * effectiveRadius, -frictionDir * frictionMag);
         w = w + (torque / inertia) * dt;
     }
-    // UpdateRotation :385-406
-    const f3 torque = mk((float)(int32_t)tq0, (float)(int32_t)tq1, (float)(int32_t)tq2) / TORQUE_SCALE;
+    const f3 torque = mk((float)(int32_t)tq[0], (float)(int32_t)tq[1], (float)(int32_t)tq[2]) / TORQUE_SCALE;
     w = w + torque / inertia;
     w = w * expf(-c.torque_damping * dt);
     float4 q = qa;
@@ -166,33 +148,123 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step(
     if (angle > 0.00001f) {
         const f3 axis = normalize(w);
         const float s = sinf(angle * 0.5f), co = cosf(angle * 0.5f);
-        const f3 dqv = axis * s;
-        const f3 qv = xyz(qa);
-        const f3 r = qv * co + dqv * qa.w + cross(dqv, qv);                // quat_mul(dq, q) :359-365
-        const float rw = co * qa.w - dot(dqv, qv);
-        const float l = sqrtf(r.x * r.x + r.y * r.y + r.z * r.z + rw * rw);
-        q = make_float4(r.x / l, r.y / l, r.z / l, rw / l);
+        const float4 r = quat_mul(make_float4(axis.x * s, axis.y * s, axis.z * s, co), qa);
+        const float l = sqrtf(r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w);
+        q = make_float4(r.x / l, r.y / l, r.z / l, r.w / l);
     }
+    p_out = p; v_out = v; w_out = w; q_out = q;
+}
+
+// The whole frame without adhesion: ApplySPHForces + drag + motion + rotation in one pass.
+__global__ __launch_bounds__(CT_BLK) void k_contact_step(
+    const float4* __restrict__ pos, const float4* __restrict__ vel, const float4* __restrict__ omg,
+    const float4* __restrict__ rot, const float4* __restrict__ aux, const int32_t* __restrict__ id,
+    const uint32_t* __restrict__ cs, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
+    float4* __restrict__ pos_o, float4* __restrict__ vel_o, float4* __restrict__ omg_o,
+    float4* __restrict__ rot_o, int32_t* __restrict__ torque_o, uint32_t* __restrict__ keys_o) {
+    const int32_t a = blockIdx.x * CT_BLK + threadIdx.x;
+    if (a >= n) return;
+    const float4 pa = pos[a], va = vel[a], wa = omg[a], qa = rot[a];
+    if (a >= n_active) {   // inactive slots (id >= activeParticleCount): drag only
+        const f3 v = apply_drag(c, id[a], xyz(pa), xyz(va), va.w);
+        pos_o[a] = pa; vel_o[a] = make_float4(v.x, v.y, v.z, va.w); omg_o[a] = wa; rot_o[a] = qa;
+        if (torque_o) { torque_o[3 * a] = 0; torque_o[3 * a + 1] = 0; torque_o[3 * a + 2] = 0; }
+        keys_o[a] = g.ncells;
+        return;
+    }
+    f3 v, w;
+    uint32_t tq[3];
+    contact_accumulate(pos, vel, omg, cs, g, c, a, pa, va, wa, v, w, tq);
+    f3 p;
+    float4 q;
+    contact_finish(c, id[a], pa, v, w, va.w, wa.w, aux[a].x, qa, tq, p, v, w, q);
     pos_o[a] = make_float4(p.x, p.y, p.z, pa.w);
-    vel_o[a] = make_float4(v.x, v.y, v.z, mass);
-    omg_o[a] = make_float4(w.x, w.y, w.z, inertia);
+    vel_o[a] = make_float4(v.x, v.y, v.z, va.w);
+    omg_o[a] = make_float4(w.x, w.y, w.z, wa.w);
     rot_o[a] = q;
     if (torque_o) {
-        torque_o[3 * a] = (int32_t)tq0; torque_o[3 * a + 1] = (int32_t)tq1; torque_o[3 * a + 2] = (int32_t)tq2;
+        torque_o[3 * a] = (int32_t)tq[0]; torque_o[3 * a + 1] = (int32_t)tq[1]; torque_o[3 * a + 2] = (int32_t)tq[2];
     }
+    keys_o[a] = cell_key(g, p.x, p.y, p.z);
+}
+
+// With adhesion, phase 1: ApplySPHForces only (v1, ω1 and the int torque into *_o), plus the
+// particle-index → slot map the bond pass reads particles through.
+__global__ __launch_bounds__(CT_BLK) void k_contact_forces(
+    const float4* __restrict__ pos, const float4* __restrict__ vel, const float4* __restrict__ omg,
+    const int32_t* __restrict__ id, const uint32_t* __restrict__ cs, int32_t n_active, int32_t n, GridDesc g,
+    ContactConst c, float4* __restrict__ vel_o, float4* __restrict__ omg_o, int32_t* __restrict__ torque_o,
+    int32_t* __restrict__ slot_of) {
+    const int32_t a = blockIdx.x * CT_BLK + threadIdx.x;
+    if (a >= n) return;
+    const float4 pa = pos[a], va = vel[a], wa = omg[a];
+    const int32_t pid = id[a];
+    if ((uint32_t)pid < (uint32_t)n) slot_of[pid] = a;
+    f3 v = xyz(va), w = xyz(wa);
+    uint32_t tq[3] = {0u, 0u, 0u};
+    if (a < n_active) contact_accumulate(pos, vel, omg, cs, g, c, a, pa, va, wa, v, w, tq);
+    vel_o[a] = make_float4(v.x, v.y, v.z, va.w);
+    omg_o[a] = make_float4(w.x, w.y, w.z, wa.w);
+    torque_o[3 * a] = (int32_t)tq[0]; torque_o[3 * a + 1] = (int32_t)tq[1]; torque_o[3 * a + 2] = (int32_t)tq[2];
+}
+
+// With adhesion, phase 3: ApplyAdhesionDeltas (compute:587-607) as a gather of this particle's
+// bond terms (adhesion.hip), then drag, motion and rotation. vel_io / omg_io hold phase 1's
+// v1, ω1 and are updated in place (each slot touches only its own element).
+__global__ __launch_bounds__(CT_BLK) void k_contact_finish(
+    const float4* __restrict__ pos, const float4* __restrict__ rot, const float4* __restrict__ aux,
+    const int32_t* __restrict__ id, const int32_t* __restrict__ torque, int32_t n_active, int32_t n,
+    GridDesc g, ContactConst c, BondView b, float4* __restrict__ vel_io, float4* __restrict__ omg_io,
+    float4* __restrict__ pos_o, float4* __restrict__ rot_o, uint32_t* __restrict__ keys_o) {
+    const int32_t a = blockIdx.x * CT_BLK + threadIdx.x;
+    if (a >= n) return;
+    const float4 pa = pos[a], va = vel_io[a], wa = omg_io[a], qa = rot[a];
+    const int32_t pid = id[a];
+    if (a >= n_active) {   // inactive: ApplyAdhesionDeltas and UpdateMotion skip it, drag does not
+        const f3 v = apply_drag(c, pid, xyz(pa), xyz(va), va.w);
+        vel_io[a] = make_float4(v.x, v.y, v.z, va.w);
+        pos_o[a] = pa; rot_o[a] = qa;
+        keys_o[a] = g.ncells;
+        return;
+    }
+    f3 v = xyz(va);
+    float4 q = qa;
+    bond_gather(b, pid, v, q);
+    const uint32_t tq[3] = {(uint32_t)torque[3 * a], (uint32_t)torque[3 * a + 1], (uint32_t)torque[3 * a + 2]};
+    f3 p, w;
+    contact_finish(c, pid, pa, v, xyz(wa), va.w, wa.w, aux[a].x, q, tq, p, v, w, q);
+    pos_o[a] = make_float4(p.x, p.y, p.z, pa.w);
+    vel_io[a] = make_float4(v.x, v.y, v.z, va.w);
+    omg_io[a] = make_float4(w.x, w.y, w.z, wa.w);
+    rot_o[a] = q;
     keys_o[a] = cell_key(g, p.x, p.y, p.z);
 }
 
 void launch_contact_step(const float4* pos, const float4* vel, const float4* omg, const float4* rot,
                          const float4* aux, const int32_t* id, const uint32_t* cs, int32_t n_active,
                          int32_t n, GridDesc g, ContactConst c, float4* pos_o, float4* vel_o,
-                         float4* omg_o, float4* rot_o, int32_t* torque_o, uint32_t* keys_o,
-                         int32_t n_active_id, hipStream_t s) {
-    (void)n_active_id;
+                         float4* omg_o, float4* rot_o, int32_t* torque_o, uint32_t* keys_o, hipStream_t s) {
     if (n > 0)
         k_contact_step<<<(n + CT_BLK - 1) / CT_BLK, CT_BLK, 0, s>>>(pos, vel, omg, rot, aux, id, cs,
                                                                     n_active, n, g, c, pos_o, vel_o,
                                                                     omg_o, rot_o, torque_o, keys_o);
+}
+
+void launch_contact_forces(const float4* pos, const float4* vel, const float4* omg, const int32_t* id,
+                           const uint32_t* cs, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
+                           float4* vel_o, float4* omg_o, int32_t* torque_o, int32_t* slot_of, hipStream_t s) {
+    if (n > 0)
+        k_contact_forces<<<(n + CT_BLK - 1) / CT_BLK, CT_BLK, 0, s>>>(pos, vel, omg, id, cs, n_active, n, g, c,
+                                                                      vel_o, omg_o, torque_o, slot_of);
+}
+
+void launch_contact_finish(const float4* pos, const float4* rot, const float4* aux, const int32_t* id,
+                           const int32_t* torque, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
+                           BondView b, float4* vel_io, float4* omg_io, float4* pos_o, float4* rot_o,
+                           uint32_t* keys_o, hipStream_t s) {
+    if (n > 0)
+        k_contact_finish<<<(n + CT_BLK - 1) / CT_BLK, CT_BLK, 0, s>>>(pos, rot, aux, id, torque, n_active, n, g, c,
+                                                                      b, vel_io, omg_io, pos_o, rot_o, keys_o);
 }
 
 }  // namespace sph

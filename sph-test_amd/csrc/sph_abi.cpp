@@ -57,6 +57,17 @@ struct sph_ctx {
     int32_t *id = nullptr, *id2 = nullptr, *mode = nullptr, *mode2 = nullptr;
     float2* rp = nullptr;        // Model S (ρ, P/ρ²)
     int32_t* torque = nullptr;   // Model R int torque of the last step (slot order)
+    int32_t* slot_of = nullptr;  // Model R particle index -> slot (bond pass)
+    // adhesion bonds (Model R, §8f-1): device SoA, host copy of the ends for the incidence lists
+    int32_t nbonds = 0, bond_cap = 0;
+    int2* b_ends = nullptr;
+    float4 *b_spring = nullptr, *b_relq = nullptr, *b_anc_a = nullptr, *b_anc_b = nullptr;
+    int4* b_terms = nullptr;
+    uint32_t *b_off = nullptr, *b_ent = nullptr;
+    int32_t b_off_cap = 0;
+    std::vector<int2> bonds_host;
+    std::vector<uint32_t> b_off_host, b_ent_host;
+    int32_t b_index_n = -1;      // particle count the incidence lists were built for (-1: stale)
     // sort / grid
     uint32_t *keys = nullptr, *keys2 = nullptr, *vals = nullptr, *vals2 = nullptr;
     uint32_t *hist = nullptr, *bin_total = nullptr;
@@ -144,7 +155,7 @@ void free_all(sph_ctx* c) {
     dfree(c->pos); dfree(c->vel); dfree(c->pos2); dfree(c->vel2);
     dfree(c->omg); dfree(c->rot); dfree(c->aux); dfree(c->omg2); dfree(c->rot2); dfree(c->aux2);
     dfree(c->id); dfree(c->id2); dfree(c->mode); dfree(c->mode2);
-    dfree(c->rp); dfree(c->torque);
+    dfree(c->rp); dfree(c->torque); dfree(c->slot_of);
     dfree(c->keys); dfree(c->keys2); dfree(c->vals); dfree(c->vals2); dfree(c->hist); dfree(c->bin_total);
     dfree(c->cs); dfree(c->gaps);
     c->gaps_cap = 0;
@@ -179,7 +190,7 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
     AL(sblk, 2 * (size_t)slab_compact_blocks(0, (int32_t)n) + 2); AL(sdev, 16);
     if (is_contact(ctx)) {
         AL(omg, n); AL(rot, n); AL(aux, n); AL(omg2, n); AL(rot2, n); AL(aux2, n);
-        AL(mode, n); AL(mode2, n); AL(torque, 3 * n);
+        AL(mode, n); AL(mode2, n); AL(torque, 3 * n); AL(slot_of, n);
     } else {
         AL(rp, n);
         AL(sk_cur, n); AL(sk_next, n);
@@ -452,6 +463,52 @@ int step_wcsph(sph_ctx* ctx, float dt) {
     return SPH_OK;
 }
 
+// ---------------------------------------------------------------- adhesion bonds (§8f-1)
+void free_bonds(sph_ctx* c) {
+    dfree(c->b_ends); dfree(c->b_spring); dfree(c->b_relq); dfree(c->b_anc_a); dfree(c->b_anc_b);
+    dfree(c->b_terms); dfree(c->b_off); dfree(c->b_ent);
+    c->bond_cap = 0;
+    c->b_off_cap = 0;
+    c->b_index_n = -1;
+}
+
+BondSet bond_set(const sph_ctx* c) {
+    return BondSet{c->b_ends, c->b_spring, c->b_relq, c->b_anc_a, c->b_anc_b, c->nbonds};
+}
+
+// The per-particle incidence lists (CSR by particle index) of the current bonds, rebuilt on the
+// host when the bonds or the particle count changed. Bonds naming an index outside [0, n) are
+// skipped by the reference (compute:432), so they have no entries (their terms stay zero).
+int bond_index(sph_ctx* ctx) {
+    const int32_t n = ctx->n;
+    if (ctx->b_index_n == n) return SPH_OK;
+    HIPCHK(hipStreamSynchronize(ctx->stream));   // the previous lists may still be in flight
+    std::vector<uint32_t>& off = ctx->b_off_host;
+    std::vector<uint32_t>& ent = ctx->b_ent_host;
+    off.assign((size_t)n + 1, 0u);
+    for (const int2& e : ctx->bonds_host)
+        if (e.x >= 0 && e.y >= 0 && e.x < n && e.y < n) { off[(size_t)e.x + 1]++; off[(size_t)e.y + 1]++; }
+    for (int32_t i = 0; i < n; ++i) off[(size_t)i + 1] += off[(size_t)i];
+    ent.assign(off[(size_t)n] > 0 ? off[(size_t)n] : 1u, 0u);
+    std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+    for (int32_t b = 0; b < ctx->nbonds; ++b) {
+        const int2 e = ctx->bonds_host[(size_t)b];
+        if (!(e.x >= 0 && e.y >= 0 && e.x < n && e.y < n)) continue;
+        ent[fill[(size_t)e.x]++] = (uint32_t)b << 1;
+        ent[fill[(size_t)e.y]++] = ((uint32_t)b << 1) | 1u;
+    }
+    int r;
+    if ((int64_t)n + 1 > ctx->b_off_cap) {
+        if ((r = dalloc(ctx, &ctx->b_off, (size_t)n + 1)) != SPH_OK) return r;
+        ctx->b_off_cap = n + 1;
+    }
+    if ((r = dalloc(ctx, &ctx->b_ent, ent.size())) != SPH_OK) return r;
+    HIPCHK(hipMemcpyAsync(ctx->b_off, off.data(), off.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->b_ent, ent.data(), ent.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    ctx->b_index_n = n;
+    return SPH_OK;
+}
+
 int32_t contact_active(const sph_ctx* c) {
     int32_t a = c->prm.active_particle_count;
     if (a <= 0 || a > c->n) a = c->n;
@@ -478,11 +535,30 @@ int step_contact(sph_ctx* ctx, float dt) {
     c.drag_ty = ctx->drag.target[1];
     c.drag_tz = ctx->drag.target[2];
     c.drag_strength = ctx->drag.strength;
-    {
+    if (ctx->nbonds == 0) {
         KTimer t(ctx, "contact_step", (double)n * (2 * 64 + 4 + 12 + 4));
         launch_contact_step(ctx->pos, ctx->vel, ctx->omg, ctx->rot, ctx->aux, ctx->id, ctx->cs, act, n, ctx->grid,
-                            c, ctx->pos2, ctx->vel2, ctx->omg2, ctx->rot2, ctx->torque, ctx->keys, act,
-                            ctx->stream);
+                            c, ctx->pos2, ctx->vel2, ctx->omg2, ctx->rot2, ctx->torque, ctx->keys, ctx->stream);
+    } else {
+        // adhesion (controller:284-310): forces, bond terms, then deltas + drag + motion + rotation
+        r = bond_index(ctx);
+        if (r != SPH_OK) return r;
+        {
+            KTimer t(ctx, "contact_forces", (double)n * (3 * 16 + 4 + 2 * 16 + 12 + 4));
+            launch_contact_forces(ctx->pos, ctx->vel, ctx->omg, ctx->id, ctx->cs, act, n, ctx->grid, c, ctx->vel2,
+                                  ctx->omg2, ctx->torque, ctx->slot_of, ctx->stream);
+        }
+        {
+            KTimer t(ctx, "bond_terms", (double)ctx->nbonds * (8 + 4 * 16 + 2 * (4 + 3 * 16) + 64));
+            launch_bond_terms(bond_set(ctx), ctx->slot_of, n, ctx->pos, ctx->vel2, ctx->rot, dt, ctx->b_terms,
+                              ctx->stream);
+        }
+        {
+            KTimer t(ctx, "contact_finish", (double)n * (5 * 16 + 4 + 12 + 8 + 4 * 16 + 4) + 4.0 * ctx->nbonds * 36);
+            BondView bv{ctx->nbonds, ctx->b_index_n, ctx->b_off, ctx->b_ent, ctx->b_terms};
+            launch_contact_finish(ctx->pos, ctx->rot, ctx->aux, ctx->id, ctx->torque, act, n, ctx->grid, c, bv,
+                                  ctx->vel2, ctx->omg2, ctx->pos2, ctx->rot2, ctx->keys, ctx->stream);
+        }
     }
     swap_sv(ctx);
     std::swap(ctx->omg, ctx->omg2);
@@ -556,6 +632,7 @@ void sph_destroy(sph_ctx* ctx) {
     if (ctx->rng_ev) (void)hipEventDestroy(ctx->rng_ev);
     if (ctx->rng_host) (void)hipHostFree(ctx->rng_host);
     free_all(ctx);
+    free_bonds(ctx);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -735,10 +812,71 @@ int sph_set_drag(sph_ctx* ctx, const sph_drag_input* drag) {
 }
 
 int sph_set_adhesion(sph_ctx* ctx, const void* conn84, int32_t count) {
-    (void)conn84;
-    if (!ctx) return SPH_ERR_INVALID;
-    if (count == 0) return SPH_OK;
-    return fail(ctx, SPH_ERR_STATE, "adhesion constraints are not implemented yet (SURVEY §8f-1)");
+    if (!ctx || count < 0 || (count > 0 && !conn84)) return SPH_ERR_INVALID;
+    if (!is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "adhesion bonds are Model R only");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamSynchronize(ctx->stream));   // earlier steps may still read the old bonds
+    if (count > ctx->bond_cap) {
+        int r;
+        const size_t cap = (size_t)count;
+        if ((r = dalloc(ctx, &ctx->b_ends, cap)) != SPH_OK || (r = dalloc(ctx, &ctx->b_spring, cap)) != SPH_OK ||
+            (r = dalloc(ctx, &ctx->b_relq, cap)) != SPH_OK || (r = dalloc(ctx, &ctx->b_anc_a, cap)) != SPH_OK ||
+            (r = dalloc(ctx, &ctx->b_anc_b, cap)) != SPH_OK || (r = dalloc(ctx, &ctx->b_terms, 4 * cap)) != SPH_OK) {
+            free_bonds(ctx);
+            ctx->nbonds = 0;
+            ctx->bonds_host.clear();
+            return r;
+        }
+        ctx->bond_cap = count;
+    }
+    // AdhesionConnection (compute:43-55; CellAdhesionManager.cs:511-524), 84 bytes:
+    //  0 particleA, 4 particleB, 8 restLength, 12 springStiffness, 16 springDamping,
+    //  20 connectionColor[4], 36 initialRelOrientation[4], 52 anchorLocalPosA[3],
+    //  64 anchorLocalPosB[3], 76 anchorConstraintStiffness, 80 enableAnchorConstraint
+    const unsigned char* src = (const unsigned char*)conn84;
+    std::vector<int2> ends((size_t)count);
+    std::vector<float4> spring((size_t)count), relq((size_t)count), anc_a((size_t)count), anc_b((size_t)count);
+    for (int32_t b = 0; b < count; ++b) {
+        const unsigned char* r = src + (size_t)b * 84;
+        int32_t i[2], en;
+        float f[3], q[4], a[3], bb[3], ks;
+        std::memcpy(i, r, 8);
+        std::memcpy(f, r + 8, 12);
+        std::memcpy(q, r + 36, 16);
+        std::memcpy(a, r + 52, 12);
+        std::memcpy(bb, r + 64, 12);
+        std::memcpy(&ks, r + 76, 4);
+        std::memcpy(&en, r + 80, 4);
+        float enf;
+        std::memcpy(&enf, &en, 4);
+        ends[(size_t)b] = make_int2(i[0], i[1]);
+        spring[(size_t)b] = make_float4(f[0], f[1], f[2], ks);
+        relq[(size_t)b] = make_float4(q[0], q[1], q[2], q[3]);
+        anc_a[(size_t)b] = make_float4(a[0], a[1], a[2], enf);
+        anc_b[(size_t)b] = make_float4(bb[0], bb[1], bb[2], 0.f);
+    }
+    if (count > 0) {
+        HIPCHK(hipMemcpy(ctx->b_ends, ends.data(), (size_t)count * sizeof(int2), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(ctx->b_spring, spring.data(), (size_t)count * sizeof(float4), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(ctx->b_relq, relq.data(), (size_t)count * sizeof(float4), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(ctx->b_anc_a, anc_a.data(), (size_t)count * sizeof(float4), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(ctx->b_anc_b, anc_b.data(), (size_t)count * sizeof(float4), hipMemcpyHostToDevice));
+    }
+    ctx->bonds_host.swap(ends);
+    ctx->nbonds = count;
+    ctx->b_index_n = -1;
+    return SPH_OK;
+}
+
+int sph_read_adhesion_terms(sph_ctx* ctx, int32_t* terms16, int32_t count) {
+    if (!ctx || count < 0 || (count > 0 && !terms16)) return SPH_ERR_INVALID;
+    if (!is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "adhesion bonds are Model R only");
+    if (count < ctx->nbonds) return fail(ctx, SPH_ERR_INVALID, "count %d < bonds %d", count, ctx->nbonds);
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->nbonds > 0)
+        HIPCHK(hipMemcpyAsync(terms16, ctx->b_terms, (size_t)ctx->nbonds * 64, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SPH_OK;
 }
 
 static int read_f4(sph_ctx* ctx, const float4* src, float* dst, int32_t count, int comps) {

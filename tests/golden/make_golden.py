@@ -58,11 +58,27 @@ def sph_case(steps):
     return x0, x[o], v[o], rho[o], dt, c0
 
 
+def adhesion_case(n, steps, dt=0.01):
+    """A bonded sphere (tests/adhesion_cases.py) stepped with its bonds (compute:424-607)."""
+    sys.path.insert(0, str(HERE.parent))
+    from adhesion_cases import bonded_sphere
+    parts, conns = bonded_sphere(O.PARTICLE84, O.ADHESION84, n, seed=21)
+    cp = O.contact_params(dt, global_drag=10.0)
+    cur, tq, terms = parts, None, None
+    for _ in range(steps):
+        cur, tq, terms = O.contact_step_bonds(cp, cur, conns, nthreads=1)
+    return parts, conns, cur, tq, terms
+
+
 def main():
     for n, steps in [(64, 1), (64, 10), (4096, 1)]:
         inp, out, tq = contact_case(n, steps)
         np.savez_compressed(HERE / f"contact_n{n}_s{steps}.npz", input=inp.view(np.uint8), output=out.view(np.uint8),
                             torque=tq)
+    for n, steps in [(512, 1), (512, 5)]:
+        inp, conns, out, tq, terms = adhesion_case(n, steps)
+        np.savez_compressed(HERE / f"adhesion_n{n}_s{steps}.npz", input=inp.view(np.uint8),
+                            conns=conns.view(np.uint8), output=out.view(np.uint8), torque=tq, terms=terms)
     for steps in [1, 10]:
         x0, x, v, rho, dt, c0 = sph_case(steps)
         np.savez_compressed(HERE / f"wcsph_c1_s{steps}.npz", x0=x0, x=x, v=v, rho=rho, dt=dt, c0=c0)
