@@ -137,6 +137,39 @@ int sph_download_particles_aos84(sph_ctx* ctx, void* dst, int32_t count);
 int sph_upload_state(sph_ctx* ctx, const float* pos_xyz, const float* vel_xyz, int32_t count);
 int sph_init_scenario(sph_ctx* ctx, const sph_scenario* sc);
 
+/* ---- Model R particle lifecycle ---- */
+/* replaces: InitParticles (compute:118-194) dispatched by InitializeParticles
+ * (controller:484-512). `count` particles (the buffer length, <= capacity); the first `active`
+ * are initialised by the reference's hash RNG from the current params (spawnRadius, min/maxRadius,
+ * density), the rest are zero as a fresh ComputeBuffer. genome_modes / default_mode are the
+ * reference's genomeModesCount / defaultGenomeMode (compute:64-68; 0 = no genome, modeIndex -1).
+ * Sets active_particle_count = active. */
+int sph_init_particles(sph_ctx* ctx, int32_t count, int32_t active, int32_t genome_modes,
+                       int32_t default_mode);
+
+/* CellSplitData (controller:136-147), 92 bytes */
+typedef struct sph_split {
+    int32_t parent_index;
+    float position_a[3], position_b[3];
+    float velocity_a[3], velocity_b[3];
+    float rotation_a[4], rotation_b[4];   /* x, y, z, w */
+    int32_t child_a_mode, child_b_mode;
+} sph_split;
+
+/* replaces: the buffer half of ProcessPendingSplits (controller:780-959): per split, child A
+ * overwrites the parent's position/velocity/rotation/modeIndex, child B is a copy of child A at
+ * index active+k with its own position/velocity/rotation/modeIndex; then active += count.
+ * Grows the capacity on the device when needed to max(active+count, 2·capacity) (:788-792) and the
+ * particle count to at least active+count. Parents must be distinct and < active.
+ * *active_out (optional) receives the new activeParticleCount. No host round trip of the
+ * particle buffer (the reference reads and rewrites all of it, :793-794, :959). */
+int sph_split_particles(sph_ctx* ctx, const sph_split* splits, int32_t count, int32_t* active_out);
+
+/* replaces: particleBuffer.GetData / SetData (array, 0, first, count) on a particle index range
+ * (controller:519-522, 535, 691, 736). 84-byte records, Model R only. */
+int sph_get_particles_aos84(sph_ctx* ctx, int32_t first, int32_t count, void* dst);
+int sph_set_particles_aos84(sph_ctx* ctx, int32_t first, int32_t count, const void* src);
+
 /* ---- the per-frame step: replaces the Dispatch sequence of Update()
  *      (controller:265-331: torque clear, ClearGrid, BuildHashGrid, ApplySPHForces,
  *       ApplyDragForce, UpdateMotion, UpdateRotation) ---- */

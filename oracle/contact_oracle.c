@@ -365,3 +365,74 @@ int or_contact_step(const or_contact_params* P, int n, or_particle84* parts, int
                     int nthreads) {
     return or_contact_step_bonds(P, n, parts, torque_out, NULL, 0, NULL, nthreads);
 }
+
+/* ---- InitParticles (compute:118-194) ----
+ * HLSL sin / pow are evaluated in double and rounded once to float: the correctly rounded float
+ * value (D3D leaves their precision to the hardware; the device kernel does the same, so both
+ * produce the same bits). frac(x) = x - floor(x); lerp(a, b, t) = a + t·(b − a). */
+static inline float hsin(float x) { return (float)sin((double)x); }
+static inline float hpow(float x, float y) { return (float)pow((double)x, (double)y); }
+static inline float hfrac(float x) { return x - floorf(x); }
+static inline float sgn_hash(float sf, float a, float b) { return hfrac(hsin(sf * a) * b) * 2.0f - 1.0f; }
+
+void or_init_particles(int n, int active, float spawn_radius, float min_radius, float max_radius, float density,
+                       int genome_modes, int default_mode, or_particle84* out) {
+    memset(out, 0, sizeof(or_particle84) * (size_t)(n > 0 ? n : 0));   /* a fresh ComputeBuffer is zero */
+    for (int i = 0; i < active && i < n; ++i) {
+        or_particle84 p;
+        memset(&p, 0, sizeof p);
+        uint32_t seed = (uint32_t)i * 65537u + 17u;                                       /* :123 */
+        float sf = (float)seed;
+        if (i != 0) {
+            f3 dir = nrm(mk(sgn_hash(sf, 12.9898f, 43758.5453f), sgn_hash(sf, 78.233f, 43758.5453f),
+                            sgn_hash(sf, 91.934f, 43758.5453f)));                        /* :134-138 */
+            float randVal = hfrac(hsin(sf * 1.2345f) * 10000.0f);                          /* :141 */
+            float dist = hpow(randVal, 1.0f / 3.0f) * spawn_radius;
+            f3 pos = mul(dir, dist);
+            if (i > 1) {                                                                  /* :147-155 */
+                float repelDist = hpow(0.5f * (float)i / (float)n, 1.0f / 3.0f) * spawn_radius * 0.1f;
+                f3 e = nrm(mk(sgn_hash(sf, 45.678f, 43758.5453f), sgn_hash(sf, 67.890f, 43758.5453f),
+                              sgn_hash(sf, 12.345f, 43758.5453f)));
+                pos = add(pos, mul(e, repelDist));
+            }
+            st3(p.position, pos);
+        }
+        p.radius = min_radius + hfrac(hsin(sf * 3.456f) * 999.0f) * (max_radius - min_radius);   /* :160 */
+        float volume = (4.0f / 3.0f) * 3.1415926f * hpow(p.radius, 3.0f);
+        p.mass = density * volume;
+        p.momentOfInertia = (2.0f / 5.0f) * p.mass * p.radius * p.radius;
+        p.drag = 0.5f + hfrac(hsin(sf * 5.6789f) * 888.0f) * (1.0f - 0.5f);                  /* :166 */
+        p.repulsionStrength = 1.0f;
+        int modeIndex = -1;                                                               /* :172-186 */
+        if (genome_modes > 0) {
+            if (hfrac(hsin(sf * 78.123f) * 5432.1f) < 0.5f)
+                modeIndex = default_mode;
+            else
+                modeIndex = (int)(hfrac(hsin(sf * 43.21f) * 8765.43f) * (float)genome_modes);
+            modeIndex = modeIndex < 0 ? 0 : (modeIndex > genome_modes - 1 ? genome_modes - 1 : modeIndex);
+        }
+        p.modeIndex = modeIndex;
+        p.rotation[3] = 1.0f;
+        out[i] = p;
+    }
+}
+
+/* The buffer half of ProcessPendingSplits (ParticleSystemController.cs:832-959) on an AoS
+ * array of n_cap records; returns the new active count. */
+int or_split_particles(or_particle84* parts, int active, const or_split92* sp, int count) {
+    for (int k = 0; k < count; ++k) {
+        or_particle84* a = &parts[sp[k].parent];
+        memcpy(a->position, sp[k].posA, 12);
+        memcpy(a->velocity, sp[k].velA, 12);
+        memcpy(a->rotation, sp[k].rotA, 16);
+        a->modeIndex = sp[k].modeA;
+        or_particle84* b = &parts[active];
+        *b = *a;
+        memcpy(b->position, sp[k].posB, 12);
+        memcpy(b->velocity, sp[k].velB, 12);
+        memcpy(b->rotation, sp[k].rotB, 16);
+        b->modeIndex = sp[k].modeB;
+        active += 1;
+    }
+    return active;
+}

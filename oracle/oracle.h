@@ -107,6 +107,19 @@ typedef struct {
 int or_contact_step_bonds(const or_contact_params* p, int n, or_particle84* parts, int32_t* torque_int,
                           const or_adhesion84* conns, int nconn, int32_t* terms, int nthreads);
 
+/* InitParticles (compute:118-194): n records, the first `active` initialised, the rest zero */
+void or_init_particles(int n, int active, float spawn_radius, float min_radius, float max_radius, float density,
+                       int genome_modes, int default_mode, or_particle84* out);
+
+/* CellSplitData (ParticleSystemController.cs:136-147), 92 bytes */
+typedef struct {
+    int32_t parent;
+    float posA[3], posB[3], velA[3], velB[3], rotA[4], rotB[4];
+    int32_t modeA, modeB;
+} or_split92;
+/* ProcessPendingSplits' buffer edit (:832-959): returns the new active count */
+int or_split_particles(or_particle84* parts, int active, const or_split92* splits, int count);
+
 #ifdef __cplusplus
 }
 #endif

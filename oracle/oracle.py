@@ -89,6 +89,10 @@ def lib():
         L.or_contact_step.argtypes = [P(OrContactParams), C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         L.or_contact_step_bonds.argtypes = [P(OrContactParams), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_int, C.c_void_p, C.c_int]
+        L.or_init_particles.argtypes = [C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int,
+                                        C.c_int, C.c_void_p]
+        L.or_split_particles.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int]
+        L.or_split_particles.restype = C.c_int
         L.or_stable_sort.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p]
         L.or_cell_start.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p]
         L.or_keys.argtypes = [P(OrGrid), C.c_int, C.c_void_p, C.c_void_p]
@@ -208,6 +212,34 @@ def contact_step_bonds(p: OrContactParams, parts, conns, nthreads=0):
     terms = np.zeros((max(m, 1), 16), np.int32)
     lib().or_contact_step_bonds(C.byref(p), n, _ptr(parts), _ptr(tq), _ptr(conns), m, _ptr(terms), nthreads)
     return parts, tq, terms[:m]
+
+
+def init_particles(n, active, spawn_radius=15.0, min_radius=1.5, max_radius=2.0, density=0.1, genome_modes=0,
+                   default_mode=0):
+    """InitParticles (compute:118-194) for a buffer of n particles, the first `active` initialised."""
+    out = np.zeros(max(n, 1), PARTICLE84)
+    lib().or_init_particles(n, active, spawn_radius, min_radius, max_radius, density, genome_modes, default_mode,
+                            _ptr(out))
+    return out[:n]
+
+
+# CellSplitData (ParticleSystemController.cs:136-147), 92 bytes
+SPLIT92 = np.dtype([
+    ("parentIndex", "<i4"), ("positionA", "<f4", (3,)), ("positionB", "<f4", (3,)),
+    ("velocityA", "<f4", (3,)), ("velocityB", "<f4", (3,)), ("rotationA", "<f4", (4,)),
+    ("rotationB", "<f4", (4,)), ("childAModeIndex", "<i4"), ("childBModeIndex", "<i4"),
+])
+
+
+def split_particles(parts, active, splits):
+    """ProcessPendingSplits' buffer edit on a copy of `parts` (grown with zero records when needed).
+    Returns (parts, new_active)."""
+    splits = np.ascontiguousarray(splits, dtype=SPLIT92)
+    need = active + len(splits)
+    out = np.zeros(max(len(parts), need), PARTICLE84)
+    out[: len(parts)] = parts
+    new_active = lib().or_split_particles(_ptr(out), active, _ptr(splits), len(splits))
+    return out, new_active
 
 
 def default_threads() -> int:

@@ -52,6 +52,14 @@ ADHESION84 = np.dtype([
 ])
 assert ADHESION84.itemsize == 84
 
+# CellSplitData (ParticleSystemController.cs:136-147) == sph_split, 92 bytes
+SPLIT92 = np.dtype([
+    ("parentIndex", "<i4"), ("positionA", "<f4", (3,)), ("positionB", "<f4", (3,)),
+    ("velocityA", "<f4", (3,)), ("velocityB", "<f4", (3,)), ("rotationA", "<f4", (4,)),
+    ("rotationB", "<f4", (4,)), ("childAModeIndex", "<i4"), ("childBModeIndex", "<i4"),
+])
+assert SPLIT92.itemsize == 92
+
 
 class SphConfig(C.Structure):
     _fields_ = [("model", C.c_int32), ("dim", C.c_int32), ("capacity", C.c_int32), ("flags", C.c_int32)]
@@ -119,6 +127,10 @@ SIGNATURES = {
     "sph_download_particles_aos84": ([_P, _P, _I], C.c_int),
     "sph_upload_state": ([_P, _P, _P, _I], C.c_int),
     "sph_init_scenario": ([_P, C.POINTER(SphScenario)], C.c_int),
+    "sph_init_particles": ([_P, _I, _I, _I, _I], C.c_int),
+    "sph_split_particles": ([_P, _P, _I, C.POINTER(C.c_int32)], C.c_int),
+    "sph_get_particles_aos84": ([_P, _I, _I, _P], C.c_int),
+    "sph_set_particles_aos84": ([_P, _I, _I, _P], C.c_int),
     "sph_step": ([_P, C.c_float, _I], C.c_int),
     "sph_set_drag": ([_P, C.POINTER(SphDragInput)], C.c_int),
     "sph_set_adhesion": ([_P, _P, _I], C.c_int),

@@ -91,6 +91,31 @@ class Context:
         self._chk("sph_init_scenario", self._L.sph_init_scenario(self._h, C.byref(sc)))
         self.n = sc.nx * sc.ny * (sc.nz if sc.dim == 3 else 1)
 
+    def init_particles(self, count: int, active: int, genome_modes: int = 0, default_mode: int = 0) -> None:
+        """InitParticles (compute:118-194): count particles, the first `active` initialised."""
+        self._chk("sph_init_particles", self._L.sph_init_particles(self._h, count, active, genome_modes, default_mode))
+        self.n = count
+
+    def split_particles(self, splits: np.ndarray) -> int:
+        """Cell division's buffer edit (sph_split_particles); returns the new active count."""
+        splits = np.ascontiguousarray(splits, dtype=A.SPLIT92)
+        out = C.c_int32()
+        self._chk("sph_split_particles", self._L.sph_split_particles(self._h, A.ptr(splits), len(splits), C.byref(out)))
+        self.n = max(self.n, int(out.value))
+        self.capacity = max(self.capacity, self.stats().capacity)
+        return int(out.value)
+
+    def get_particles(self, first: int, count: int) -> np.ndarray:
+        """particleBuffer.GetData(array, 0, first, count) (84-byte records)."""
+        out = np.zeros(max(count, 1), A.PARTICLE84)
+        self._chk("sph_get_particles_aos84", self._L.sph_get_particles_aos84(self._h, first, count, A.ptr(out)))
+        return out[:count]
+
+    def set_particles(self, first: int, parts: np.ndarray) -> None:
+        """particleBuffer.SetData(array, 0, first, len(array))."""
+        parts = np.ascontiguousarray(parts, dtype=A.PARTICLE84)
+        self._chk("sph_set_particles_aos84", self._L.sph_set_particles_aos84(self._h, first, len(parts), A.ptr(parts)))
+
     def step(self, dt: float, nsteps: int = 1) -> None:
         self._chk("sph_step", self._L.sph_step(self._h, dt, nsteps))
 

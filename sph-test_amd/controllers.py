@@ -12,12 +12,14 @@ and sloshing scenarios of BASELINE.json.
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Optional
+from typing import List, Optional
 
 import numpy as np
 
 from . import _abi as A
 from .context import Context, make_scenario, scenario_params
+from .genome import (CellGenome, get_direction, initial_mode_index, load_genome_asset, load_scene_controller,
+                     look_rotation, rotate)
 
 # BASELINE.json configs: (kind, dim, fluid nx,ny,nz, tank tx,ty,tz)
 CONFIGS = {
@@ -78,8 +80,26 @@ class DragInput:
     strength: float = 0.0
 
 
+@dataclass
+class ParticleIDData:
+    """ParticleIDData (ParticleSystemController.cs:178-191)."""
+    parentID: int = 0
+    uniqueID: int = 0
+    childType: str = "\0"
+
+    def GetFormattedID(self) -> str:
+        if self.childType == "\0":
+            return "Unknown"
+        return f"{self.parentID:02d}.{self.uniqueID:02d}.{self.childType}"
+
+
 class ParticleSystemController:
-    """Mirror of the reference controller's public API, driving Model R on the GPU."""
+    """Mirror of the reference controller's public API, driving Model R on the GPU.
+
+    The per-frame GPU work is one `sph_step` (contact, adhesion, drag, motion, rotation). Cell
+    division keeps the reference's host logic (timers, SplitCell's child placement) and hands the
+    buffer edit to the device (`sph_split_particles`), so the particle buffer never makes the
+    host round trip the reference's ProcessPendingSplits does (:793-794, :959)."""
 
     def __init__(self, particleCount: int = 10000, device: int = 0):
         # [Header("Particle Configuration")]  ParticleSystemController.cs:11-15
@@ -95,9 +115,11 @@ class ParticleSystemController:
         self.rollingContactRadiusMultiplier = 5.0
         self.density = 0.1
         self.repulsionStrength = 200.0
-        # [Header("Cell Division Settings")]  :26-28 (division itself is §8f-2, not yet built)
+        # [Header("Cell Division Settings")]  :26-28
         self.spawnOverlapOffset = 0.5
         self.splitVelocityMagnitude = 0.5
+        # [Header("Genome")] :30-31 (a genome.CellGenome)
+        self.genome: Optional[CellGenome] = None
         self.device = device
         self.activeParticleCount = 1            # :95
         self.CpuParticlePositions: Optional[np.ndarray] = None   # :89-90
@@ -108,19 +130,52 @@ class ParticleSystemController:
         # returning an ADHESION84 array (CellAdhesionManager.cs:524-564)
         self.adhesionManager = None
         self.maxAdhesionConnections = 4096      # :128-129
+        self.nextUniqueIDCounter = 1            # :98
+        self.cellSplitTimers: Optional[np.ndarray] = None   # :101
+        self.pendingSplits: List[np.void] = []  # :104 (CellSplitData records)
+        self.ParticleIDs: List[ParticleIDData] = []          # :118-119
         self._bonds_uploaded: Optional[bytes] = None
         self._ctx: Optional[Context] = None
 
+    @classmethod
+    def from_scene(cls, scene_path, genome_path=None, device: int = 0) -> "ParticleSystemController":
+        """The controller as a Unity scene serializes it (e.g. Particle Simulation.unity:151-178),
+        with an optional genome asset (e.g. NewCellGenome.asset)."""
+        vals = load_scene_controller(scene_path)
+        ctl = cls(particleCount=vals.pop("particleCount"), device=device)
+        for k, v in vals.items():
+            setattr(ctl, k, float(v))
+        if genome_path is not None:
+            ctl.genome = load_genome_asset(genome_path)
+        return ctl
+
     # ------------------------------------------------------------------ lifecycle
     def Start(self, particles: Optional[np.ndarray] = None) -> None:
-        """InitializeBuffers (:373) + particle upload. `particles` is an AoS-84 array (PARTICLE84)."""
+        """Start (:211-242): InitializeBuffers (:373) then InitializeParticles (:484-552), or the given
+        AoS-84 particles (PARTICLE84) uploaded as they are."""
+        if self.genome is not None:
+            self.genome.ValidateForSimulation()             # :216-226 (raises on several initial modes)
         self._ctx = Context(A.SPH_MODEL_CONTACT, 3, self.particleCount, device=self.device)
         if particles is not None:
             self._ctx.upload_aos84(particles)
             self.activeParticleCount = len(particles)
-        self._push_uniforms()
+            self._push_uniforms()
+        else:
+            self.activeParticleCount = 1                    # :506-508
+            self._push_uniforms()
+            # genomeModesCount / defaultGenomeMode are never set on the compute shader, so
+            # InitParticles sees 0 modes (modeIndex -1) and the host then sets particle 0's mode (:514-523)
+            self._ctx.init_particles(self.particleCount, self.activeParticleCount)
+            if self.genome is not None and self.genome.modes:
+                first = self._ctx.get_particles(0, 1)
+                first["modeIndex"] = initial_mode_index(self.genome)
+                self._ctx.set_particles(0, first)
+        self.ParticleIDs = [ParticleIDData() for _ in range(self.particleCount)]
+        self.ParticleIDs[0] = ParticleIDData(0, 0, "A")     # :486-494
+        self.cellSplitTimers = np.zeros(self.particleCount, np.float32)
         self.CpuParticlePositions = np.zeros((self.particleCount, 3), np.float32)
         self.CpuParticleRotations = np.zeros((self.particleCount, 4), np.float32)
+        self._readback()
 
     def _push_uniforms(self) -> None:
         p = self._ctx.get_params()
@@ -148,26 +203,118 @@ class ParticleSystemController:
             self._ctx.set_adhesion(conns if blob else None)
             self._bonds_uploaded = blob
 
+    def _readback(self) -> None:
+        """Copy*ToReadbackBuffer + GetData (:325-333)."""
+        n = self._ctx.n
+        self.CpuParticlePositions[:n] = self._ctx.positions()
+        self.CpuParticleRotations[:n] = self._ctx.rotations()
+
     def Update(self, dt: float) -> None:
-        """One frame: uniforms (:255-263), the step with adhesion (:265-331), readback (:332-333)."""
+        """One frame (:244-351): division (:253), uniforms (:255-263), the step with adhesion
+        (:265-331), readback (:332-333)."""
+        self.UpdateCellDivisionTimers(dt)
         self._push_uniforms()
         self._push_adhesion()
         d = self.drag
         self._ctx.set_drag(d.selectedID, d.targetPosition, d.strength)
         self._ctx.step(dt, 1)
-        n = self._ctx.n
-        self.CpuParticlePositions[:n] = self._ctx.positions()
-        self.CpuParticleRotations[:n] = self._ctx.rotations()
+        self._readback()
+
+    # ------------------------------------------------------------------ cell division
+    def UpdateCellDivisionTimers(self, deltaTime: float) -> None:
+        """:631-727 — process last frame's splits, advance the timers, pick the cells due."""
+        if self.pendingSplits:
+            self.ProcessPendingSplits()
+        allowed = self.particleCount - self.activeParticleCount
+        if allowed <= 0 or self.genome is None or not self.genome.modes:
+            return
+        act = self.activeParticleCount
+        self.cellSplitTimers[:act] += np.float32(deltaTime)
+        modes = self._ctx.get_particles(0, act)["modeIndex"]   # the cached readback (:662-714)
+        ready = []
+        eps = np.float32(0.001)
+        for i in range(act):
+            m = int(modes[i])
+            if 0 <= m < len(self.genome.modes):
+                if self.cellSplitTimers[i] >= np.float32(self.genome.modes[m].splitInterval) - eps:
+                    if len(ready) < allowed:
+                        ready.append(i)
+                    self.cellSplitTimers[i] = 0.0
+        for i in ready:
+            self.SplitCell(i, int(modes[i]))
+
+    def SplitCell(self, parentIndex: int, parentModeIndex: Optional[int] = None) -> None:
+        """:729-778 — the children's placement from the parent's last read-back pose."""
+        g = self.genome
+        if g is None or not g.modes or parentIndex >= self.activeParticleCount:
+            return
+        parentPos = self.CpuParticlePositions[parentIndex]
+        parentRot = self.CpuParticleRotations[parentIndex]
+        if parentModeIndex is None:
+            parentModeIndex = int(self._ctx.get_particles(parentIndex, 1)["modeIndex"][0])
+        if not 0 <= parentModeIndex < len(g.modes):
+            parentModeIndex = initial_mode_index(g)
+        mode = g.modes[parentModeIndex]
+        a = mode.childAModeIndex if 0 <= mode.childAModeIndex < len(g.modes) else parentModeIndex
+        b = mode.childBModeIndex if 0 <= mode.childBModeIndex < len(g.modes) else parentModeIndex
+        forward, up, right = (rotate(parentRot, v) for v in ((0, 0, 1), (0, 1, 0), (1, 0, 0)))
+
+        def world(d):
+            return (right * d[0] + up * d[1] + forward * d[2]).astype(np.float32)
+
+        split_dir = world(get_direction(mode.parentSplitYaw, mode.parentSplitPitch))
+        off = np.float32(self.spawnOverlapOffset)
+        vmag = np.float32(self.splitVelocityMagnitude)
+        rec = np.zeros(1, A.SPLIT92)[0]
+        rec["parentIndex"] = parentIndex
+        rec["positionA"] = parentPos + split_dir * off
+        rec["positionB"] = parentPos - split_dir * off
+        rec["velocityA"] = split_dir * vmag          # parentVelocity = zero (:761)
+        rec["velocityB"] = -split_dir * vmag
+        rec["rotationA"] = look_rotation(world(get_direction(mode.childA_OrientationYaw, mode.childA_OrientationPitch)), up)
+        rec["rotationB"] = look_rotation(world(get_direction(mode.childB_OrientationYaw, mode.childB_OrientationPitch)), up)
+        rec["childAModeIndex"], rec["childBModeIndex"] = a, b
+        self.pendingSplits.append(rec)
+
+    def ProcessPendingSplits(self) -> None:
+        """:780-964 — IDs, timers and the device-side buffer edit (sph_split_particles)."""
+        if not self.pendingSplits:
+            return
+        splits = np.array(self.pendingSplits, dtype=A.SPLIT92)
+        self.pendingSplits = []
+        act0 = self.activeParticleCount
+        new_active = self._ctx.split_particles(splits)
+        cap = self._ctx.stats().capacity
+        if cap > self.particleCount:                        # the device grew the buffers (:788-792)
+            self._grow_host(cap)
+        for k, sp in enumerate(splits):
+            pidx = int(sp["parentIndex"])
+            parent_uid = self.ParticleIDs[pidx].uniqueID
+            b_idx = act0 + k
+            self.ParticleIDs[pidx] = ParticleIDData(parent_uid, self.nextUniqueIDCounter, "A")
+            self.ParticleIDs[b_idx] = ParticleIDData(parent_uid, self.nextUniqueIDCounter + 1, "B")
+            self.nextUniqueIDCounter += 2
+            self.cellSplitTimers[pidx] = 0.0
+            self.cellSplitTimers[b_idx] = 0.0
+        self.activeParticleCount = new_active
+
+    def _grow_host(self, cap: int) -> None:
+        old = self.particleCount
+        self.particleCount = cap
+        self.ParticleIDs += [ParticleIDData() for _ in range(cap - old)]
+        for name, shape in (("cellSplitTimers", (cap,)), ("CpuParticlePositions", (cap, 3)),
+                            ("CpuParticleRotations", (cap, 4))):
+            arr = getattr(self, name)
+            new = np.zeros(shape, np.float32)
+            new[:old] = arr[:old]
+            setattr(self, name, new)
 
     def ResizeParticleBuffers(self, newCapacity: int) -> None:
-        """:1162-1222 — keep the particles, grow the buffers."""
+        """:1162-1222 — keep the particles, grow the buffers (device-to-device)."""
         self._ctx.resize(newCapacity)
+        if newCapacity > self.particleCount:
+            self._grow_host(newCapacity)
         self.particleCount = newCapacity
-        pos = np.zeros((newCapacity, 3), np.float32)
-        rot = np.zeros((newCapacity, 4), np.float32)
-        pos[: len(self.CpuParticlePositions)] = self.CpuParticlePositions[:newCapacity]
-        rot[: len(self.CpuParticleRotations)] = self.CpuParticleRotations[:newCapacity]
-        self.CpuParticlePositions, self.CpuParticleRotations = pos, rot
 
     def GetParticles(self) -> np.ndarray:
         """particleBuffer.GetData (:519, :794): the full AoS-84 state."""

@@ -256,6 +256,30 @@ struct BondView {
     const int4* terms;      // [4 * count]: Δv_A, Δv_B, Δq_A, Δq_B (fixed point ×1e6)
 };
 
+// Model R particle lifecycle (particles.hip)
+struct InitConst {   // InitParticles uniforms (compute:89-100) + genome selection (:64-68)
+    float spawn_radius, min_radius, max_radius, density;
+    int32_t length;          // particleBuffer.Length
+    int32_t genome_modes;    // genomeModesCount
+    int32_t default_mode;    // defaultGenomeMode
+};
+struct SplitRec {    // CellSplitData (ParticleSystemController.cs:136-147) == sph_split (sphhip.h)
+    int32_t parent;
+    float posA[3], posB[3], velA[3], velB[3], rotA[4], rotB[4];
+    int32_t modeA, modeB;
+};
+void launch_slot_map(const int32_t* id, int32_t n, int32_t* slot_of, hipStream_t s);
+void launch_init_sphere(int32_t n, int32_t active, InitConst c, float4* pos, float4* vel, float4* omg, float4* rot,
+                        float4* aux, int32_t* mode, int32_t* id, int32_t* torque, hipStream_t s);
+void launch_split(const SplitRec* sp, int32_t count, int32_t active, int32_t n_old, const int32_t* slot_of,
+                  float4* pos, float4* vel, float4* omg, float4* rot, float4* aux, int32_t* mode, int32_t* id,
+                  hipStream_t s);
+void launch_get_range(const float4* pos, const float4* vel, const float4* omg, const float4* rot, const float4* aux,
+                      const int32_t* mode, const int32_t* slot_of, int32_t first, int32_t count, void* aos,
+                      hipStream_t s);
+void launch_set_range(const void* aos, const int32_t* slot_of, int32_t first, int32_t count, float4* pos,
+                      float4* vel, float4* omg, float4* rot, float4* aux, int32_t* mode, hipStream_t s);
+
 // Model R (contact.hip)
 void launch_contact_step(const float4* pos, const float4* vel, const float4* omg, const float4* rot,
                          const float4* aux, const int32_t* id, const uint32_t* cs, int32_t n_active,

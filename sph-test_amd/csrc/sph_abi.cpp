@@ -788,6 +788,144 @@ int sph_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
     return SPH_OK;
 }
 
+static_assert(sizeof(sph_split) == 92 && sizeof(SplitRec) == sizeof(sph_split), "CellSplitData layout");
+
+static int ensure_staging(sph_ctx* ctx, size_t bytes) {
+    if (bytes <= ctx->staging_bytes) return SPH_OK;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (ctx->staging) (void)hipFree(ctx->staging);
+    ctx->staging = nullptr;
+    ctx->staging_bytes = 0;
+    HIPCHK(hipMalloc(&ctx->staging, bytes));
+    ctx->staging_bytes = bytes;
+    return SPH_OK;
+}
+
+int sph_init_particles(sph_ctx* ctx, int32_t count, int32_t active, int32_t genome_modes, int32_t default_mode) {
+    if (!ctx || count < 0 || active < 0 || active > count || genome_modes < 0) return SPH_ERR_INVALID;
+    if (!is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "sph_init_particles is Model R (InitParticles) only");
+    if (count > ctx->capacity) return fail(ctx, SPH_ERR_CAPACITY, "count %d > capacity %d", count, ctx->capacity);
+    HIPCHK(hipSetDevice(ctx->device));
+    const sph_params& p = ctx->prm;
+    InitConst c{p.spawn_radius, p.min_radius, p.max_radius, p.density, count, genome_modes, default_mode};
+    launch_init_sphere(count, active, c, ctx->pos, ctx->vel, ctx->omg, ctx->rot, ctx->aux, ctx->mode, ctx->id,
+                       ctx->torque, ctx->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->n = count;
+    ctx->prm.active_particle_count = active;
+    ctx->keys_valid = false;
+    ctx->steps = 0;
+    ctx->sim_time = 0.0;
+    return SPH_OK;
+}
+
+// Grow the particle arrays to `capacity` on the device, keeping the current slots (D2D copies).
+static int grow_d2d(sph_ctx* ctx, int32_t capacity) {
+    const int32_t n = ctx->n;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    float4 *pos = ctx->pos, *vel = ctx->vel, *omg = ctx->omg, *rot = ctx->rot, *aux = ctx->aux;
+    int32_t *id = ctx->id, *mode = ctx->mode;
+    ctx->pos = ctx->vel = ctx->omg = ctx->rot = ctx->aux = nullptr;
+    ctx->id = ctx->mode = nullptr;
+    free_all(ctx);
+    ctx->capacity = capacity;
+    int r = alloc_particles(ctx, capacity);
+    if (r == SPH_OK && ctx->params_set) r = derive(ctx);
+    hipError_t e = hipSuccess;
+    const size_t f4 = (size_t)n * sizeof(float4), i4 = (size_t)n * 4;
+    if (r == SPH_OK && n > 0) {
+        e = hipMemcpyAsync(ctx->pos, pos, f4, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(ctx->vel, vel, f4, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(ctx->id, id, i4, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e == hipSuccess && omg) e = hipMemcpyAsync(ctx->omg, omg, f4, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e == hipSuccess && rot) e = hipMemcpyAsync(ctx->rot, rot, f4, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e == hipSuccess && aux) e = hipMemcpyAsync(ctx->aux, aux, f4, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e == hipSuccess && mode) e = hipMemcpyAsync(ctx->mode, mode, i4, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    }
+    dfree(pos); dfree(vel); dfree(omg); dfree(rot); dfree(aux); dfree(id); dfree(mode);
+    if (r != SPH_OK) return r;
+    if (e != hipSuccess) return fail(ctx, SPH_ERR_HIP, "resize copy: %s", hipGetErrorString(e));
+    ctx->keys_valid = false;
+    ctx->sk_valid = false;
+    return SPH_OK;
+}
+
+int sph_split_particles(sph_ctx* ctx, const sph_split* splits, int32_t count, int32_t* active_out) {
+    if (!ctx || count < 0 || (count > 0 && !splits)) return SPH_ERR_INVALID;
+    if (!is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "cell division is Model R only");
+    if (ctx->slab) return fail(ctx, SPH_ERR_STATE, "slab mode");
+    HIPCHK(hipSetDevice(ctx->device));
+    const int32_t active = contact_active(ctx);
+    if (count == 0) {
+        if (active_out) *active_out = active;
+        return SPH_OK;
+    }
+    std::vector<unsigned char> seen((size_t)active, 0);
+    for (int32_t k = 0; k < count; ++k) {
+        const int32_t p = splits[k].parent_index;
+        if (p < 0 || p >= active) return fail(ctx, SPH_ERR_INVALID, "split %d: parent %d not in [0, %d)", k, p, active);
+        if (seen[(size_t)p]++) return fail(ctx, SPH_ERR_INVALID, "split %d: parent %d split twice", k, p);
+    }
+    const int64_t need = (int64_t)active + count;
+    if (need > INT32_MAX) return fail(ctx, SPH_ERR_CAPACITY, "too many particles");
+    if (need > ctx->capacity) {   // controller:788-792
+        const int64_t cap = std::max<int64_t>(need, std::min<int64_t>(2 * (int64_t)ctx->capacity, INT32_MAX));
+        int r = grow_d2d(ctx, (int32_t)cap);
+        if (r != SPH_OK) return r;
+    }
+    int r = ensure_staging(ctx, (size_t)count * sizeof(sph_split));
+    if (r != SPH_OK) return r;
+    const int32_t n_old = ctx->n;
+    HIPCHK(hipMemcpyAsync(ctx->staging, splits, (size_t)count * sizeof(sph_split), hipMemcpyHostToDevice, ctx->stream));
+    launch_slot_map(ctx->id, n_old, ctx->slot_of, ctx->stream);
+    launch_split((const SplitRec*)ctx->staging, count, active, n_old, ctx->slot_of, ctx->pos, ctx->vel, ctx->omg,
+                 ctx->rot, ctx->aux, ctx->mode, ctx->id, ctx->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));   // the split records live in the caller's memory
+    ctx->n = std::max<int32_t>(n_old, (int32_t)need);
+    ctx->prm.active_particle_count = (int32_t)need;
+    ctx->keys_valid = false;
+    if (active_out) *active_out = (int32_t)need;
+    return SPH_OK;
+}
+
+static int range_args(sph_ctx* ctx, int32_t first, int32_t count, const void* buf) {
+    if (!ctx || first < 0 || count < 0 || (count > 0 && !buf)) return SPH_ERR_INVALID;
+    if (!is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "84-byte particle ranges are Model R only");
+    if ((int64_t)first + count > ctx->n)
+        return fail(ctx, SPH_ERR_INVALID, "range [%d, %d) outside the %d particles", first, first + count, ctx->n);
+    return SPH_OK;
+}
+
+int sph_get_particles_aos84(sph_ctx* ctx, int32_t first, int32_t count, void* dst) {
+    int r = range_args(ctx, first, count, dst);
+    if (r != SPH_OK || count == 0) return r;
+    HIPCHK(hipSetDevice(ctx->device));
+    launch_slot_map(ctx->id, ctx->n, ctx->slot_of, ctx->stream);
+    launch_get_range(ctx->pos, ctx->vel, ctx->omg, ctx->rot, ctx->aux, ctx->mode, ctx->slot_of, first, count,
+                     ctx->staging, ctx->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(dst, ctx->staging, (size_t)count * 84, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SPH_OK;
+}
+
+int sph_set_particles_aos84(sph_ctx* ctx, int32_t first, int32_t count, const void* src) {
+    int r = range_args(ctx, first, count, src);
+    if (r != SPH_OK || count == 0) return r;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemcpyAsync(ctx->staging, src, (size_t)count * 84, hipMemcpyHostToDevice, ctx->stream));
+    launch_slot_map(ctx->id, ctx->n, ctx->slot_of, ctx->stream);
+    launch_set_range(ctx->staging, ctx->slot_of, first, count, ctx->pos, ctx->vel, ctx->omg, ctx->rot, ctx->aux,
+                     ctx->mode, ctx->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->keys_valid = false;
+    return SPH_OK;
+}
+
 int sph_step(sph_ctx* ctx, float dt, int32_t nsteps) {
     if (!ctx || nsteps < 0 || !(dt >= 0.f)) return SPH_ERR_INVALID;
     if (ctx->slab) return fail(ctx, SPH_ERR_STATE, "slab mode: the host drives sph_slab_* phases");
@@ -1027,26 +1165,10 @@ int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int3
 int sph_resize(sph_ctx* ctx, int32_t capacity) {
     if (!ctx || capacity < 0) return SPH_ERR_INVALID;
     if (capacity < ctx->n) return fail(ctx, SPH_ERR_CAPACITY, "capacity %d < active particles %d", capacity, ctx->n);
+    if (ctx->slab) return fail(ctx, SPH_ERR_STATE, "slab mode");
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    // keep the active particles: download in index order, reallocate, upload
-    const int32_t n = ctx->n;
-    std::vector<unsigned char> host((size_t)n * 84);
-    int r = n > 0 ? sph_download_particles_aos84(ctx, host.data(), n) : SPH_OK;
-    if (r != SPH_OK) return r;
-    free_all(ctx);
-    ctx->capacity = capacity;
-    r = alloc_particles(ctx, capacity);
-    if (r != SPH_OK) return r;
-    if (ctx->params_set) {
-        r = derive(ctx);
-        if (r != SPH_OK) return r;
-    }
-    if (n > 0) {
-        r = sph_upload_particles_aos84(ctx, host.data(), n);
-        if (r != SPH_OK) return r;
-    }
-    return SPH_OK;
+    // keep the particles: device-to-device copies of the slot arrays (no host round trip)
+    return grow_d2d(ctx, capacity);
 }
 
 // ---------------------------------------------------------------- slab decomposition
