@@ -75,7 +75,8 @@ typedef struct sph_params {
 typedef enum sph_scenario_kind {
     SPH_SCENARIO_DAMBREAK = 0,  /* fluid column at the tank's low-x corner */
     SPH_SCENARIO_SLOSHING = 1,  /* fluid layer filling the tank floor + lateral forcing */
-    SPH_SCENARIO_SPHERE = 2     /* Model R: InitParticles-style random sphere (compute:118-194) */
+    SPH_SCENARIO_SPHERE = 2     /* Model R: sph_init_scenario with nx = count initialises all nx
+                                   particles as InitParticles does (= sph_init_particles(nx, nx, 0, 0)) */
 } sph_scenario_kind;
 
 typedef struct sph_scenario {
@@ -196,6 +197,30 @@ int sph_read_velocities(sph_ctx* ctx, float* xyz, int32_t count);
 int sph_read_angular_velocities(sph_ctx* ctx, float* xyz, int32_t count);
 int sph_read_density(sph_ctx* ctx, float* rho, int32_t count);   /* Model S, pass-1 ρ */
 int sph_synchronize(sph_ctx* ctx);
+
+/* replaces: AsyncGPUReadback.Request(buffer, callback) + r.GetData<T>() (controller:1115-1159).
+ * request: the chosen fields of the CURRENT state (particle index order) are copied on the device
+ * and sent to pinned host memory on a side stream; the caller keeps stepping meanwhile. One
+ * request is outstanding per context: a new one replaces an unread one. status: SPH_OK when the
+ * data is on the host, SPH_READBACK_PENDING while in flight (the callback's "done" test).
+ * get: waits if needed, then copies `field` (one flag) into dst (count >= sph_readback_count). */
+#define SPH_READBACK_POSITIONS 1    /* float xyz  (positionReadbackBuffer, compute:410-415) */
+#define SPH_READBACK_ROTATIONS 2    /* float xyzw (rotationReadbackBuffer, compute:417-422), Model R */
+#define SPH_READBACK_PARTICLES 4    /* 84-byte Particle (particleBuffer), Model R */
+#define SPH_READBACK_PENDING 1
+int sph_request_readback(sph_ctx* ctx, int32_t fields);
+int sph_readback_status(sph_ctx* ctx);
+int sph_readback_get(sph_ctx* ctx, int32_t field, void* dst, int32_t count);
+int sph_readback_count(sph_ctx* ctx, int32_t* count);
+
+/* ---- render interop: replaces sphereMaterial.SetBuffer("particleBuffer") + the indirect-args
+ * update (controller:335-347; InstancedParticles.shader:27-47 reads the 84-byte records) ----
+ * export: the particles as 84-byte records in index order into a caller DEVICE buffer (e.g. the
+ * renderer's structured buffer), enqueued on the context stream (sph_get_stream), no host copy.
+ * draw args: args[1] (instanceCount of a 5-uint DrawMeshInstancedIndirect buffer in device memory)
+ * = activeParticleCount, enqueued on the context stream. */
+int sph_export_aos84_device(sph_ctx* ctx, void* dev_dst, int32_t count);
+int sph_write_draw_args(sph_ctx* ctx, void* dev_args);
 
 /* ---- introspection (tests / bench) ---- */
 int sph_get_stats(sph_ctx* ctx, sph_stats* out);

@@ -31,6 +31,10 @@ SPH_FLAG_PROFILE = 1
 SPH_SCENARIO_DAMBREAK = 0
 SPH_SCENARIO_SLOSHING = 1
 SPH_SCENARIO_SPHERE = 2
+SPH_READBACK_POSITIONS = 1
+SPH_READBACK_ROTATIONS = 2
+SPH_READBACK_PARTICLES = 4
+SPH_READBACK_PENDING = 1
 
 # SimulateParticles.compute:23-40 / ParticleSystemController.cs:157-175 (84 bytes)
 PARTICLE84 = np.dtype([
@@ -141,6 +145,12 @@ SIGNATURES = {
     "sph_read_angular_velocities": ([_P, _P, _I], C.c_int),
     "sph_read_density": ([_P, _P, _I], C.c_int),
     "sph_synchronize": ([_P], C.c_int),
+    "sph_request_readback": ([_P, _I], C.c_int),
+    "sph_readback_status": ([_P], C.c_int),
+    "sph_readback_get": ([_P, _I, _P, _I], C.c_int),
+    "sph_readback_count": ([_P, C.POINTER(C.c_int32)], C.c_int),
+    "sph_export_aos84_device": ([_P, _P, _I], C.c_int),
+    "sph_write_draw_args": ([_P, _P], C.c_int),
     "sph_get_stats": ([_P, C.POINTER(SphStats)], C.c_int),
     "sph_get_kernel_stat": ([_P, _I, C.POINTER(SphKernelStat)], C.c_int),
     "sph_reset_kernel_stats": ([_P], C.c_int),

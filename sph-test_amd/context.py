@@ -139,6 +139,36 @@ class Context:
         self._chk("sph_read_adhesion_terms", self._L.sph_read_adhesion_terms(self._h, A.ptr(out), self.nbonds))
         return out[: self.nbonds]
 
+    # -------------------------------------------------------------- async readback / render interop
+    def request_readback(self, fields: int) -> None:
+        """AsyncGPUReadback.Request of SPH_READBACK_* fields of the current state."""
+        self._chk("sph_request_readback", self._L.sph_request_readback(self._h, fields))
+
+    def readback_ready(self) -> bool:
+        st = self._L.sph_readback_status(self._h)
+        if st == A.SPH_READBACK_PENDING:
+            return False
+        self._chk("sph_readback_status", st)
+        return True
+
+    def readback_get(self, field: int) -> np.ndarray:
+        cnt = C.c_int32()
+        self._chk("sph_readback_count", self._L.sph_readback_count(self._h, C.byref(cnt)))
+        n = cnt.value
+        if field == A.SPH_READBACK_PARTICLES:
+            out = np.zeros(max(n, 1), A.PARTICLE84)
+        else:
+            out = np.zeros((max(n, 1), 3 if field == A.SPH_READBACK_POSITIONS else 4), np.float32)
+        self._chk("sph_readback_get", self._L.sph_readback_get(self._h, field, A.ptr(out), max(n, 1)))
+        return out[:n]
+
+    def export_aos84_device(self, dev_ptr: int, count: int) -> None:
+        """84-byte records (index order) into a device buffer, on the context stream."""
+        self._chk("sph_export_aos84_device", self._L.sph_export_aos84_device(self._h, C.c_void_p(dev_ptr), count))
+
+    def write_draw_args(self, dev_ptr: int) -> None:
+        self._chk("sph_write_draw_args", self._L.sph_write_draw_args(self._h, C.c_void_p(dev_ptr)))
+
     def synchronize(self) -> None:
         self._chk("sph_synchronize", self._L.sph_synchronize(self._h))
 

@@ -130,11 +130,16 @@ class ParticleSystemController:
         # returning an ADHESION84 array (CellAdhesionManager.cs:524-564)
         self.adhesionManager = None
         self.maxAdhesionConnections = 4096      # :128-129
+        # True: Update ends with the reference's synchronous GetData (:332-333). False: positions and
+        # rotations arrive through the asynchronous readback one frame later (:1142-1158), so the
+        # host never waits on the GPU inside Update.
+        self.immediateReadback = True
         self.nextUniqueIDCounter = 1            # :98
         self.cellSplitTimers: Optional[np.ndarray] = None   # :101
         self.pendingSplits: List[np.void] = []  # :104 (CellSplitData records)
         self.ParticleIDs: List[ParticleIDData] = []          # :118-119
         self._bonds_uploaded: Optional[bytes] = None
+        self._rb_requested = False
         self._ctx: Optional[Context] = None
 
     @classmethod
@@ -209,16 +214,31 @@ class ParticleSystemController:
         self.CpuParticlePositions[:n] = self._ctx.positions()
         self.CpuParticleRotations[:n] = self._ctx.rotations()
 
+    def RequestParticleDataAsync(self) -> None:
+        """:1115-1159 — deliver a finished asynchronous readback into the CPU arrays."""
+        if self._rb_requested and self._ctx.readback_ready():
+            pos = self._ctx.readback_get(A.SPH_READBACK_POSITIONS)
+            rot = self._ctx.readback_get(A.SPH_READBACK_ROTATIONS)
+            self.CpuParticlePositions[: len(pos)] = pos
+            self.CpuParticleRotations[: len(rot)] = rot
+            self._rb_requested = False
+
     def Update(self, dt: float) -> None:
-        """One frame (:244-351): division (:253), uniforms (:255-263), the step with adhesion
-        (:265-331), readback (:332-333)."""
+        """One frame (:244-351): readback delivery (:250), division (:253), uniforms (:255-263), the
+        step with adhesion (:265-331), readback (:332-333)."""
+        if not self.immediateReadback:
+            self.RequestParticleDataAsync()
         self.UpdateCellDivisionTimers(dt)
         self._push_uniforms()
         self._push_adhesion()
         d = self.drag
         self._ctx.set_drag(d.selectedID, d.targetPosition, d.strength)
         self._ctx.step(dt, 1)
-        self._readback()
+        if self.immediateReadback:
+            self._readback()
+        elif not self._rb_requested:
+            self._ctx.request_readback(A.SPH_READBACK_POSITIONS | A.SPH_READBACK_ROTATIONS)
+            self._rb_requested = True
 
     # ------------------------------------------------------------------ cell division
     def UpdateCellDivisionTimers(self, deltaTime: float) -> None:

@@ -111,6 +111,15 @@ struct sph_ctx {
     hipEvent_t rng_ev = nullptr;    // recorded after their device->host copy
     bool rng_pending = false;       // rng[] / o0 / o1 not yet updated from rng_host
     int32_t dropped = 0;            // own particles the last assemble dropped (outside the window)
+    // asynchronous readback (AsyncGPUReadback, controller:1115-1159): index-order copies on the
+    // device, D2H on a side stream into pinned host buffers
+    hipStream_t rb_stream = nullptr;
+    hipEvent_t rb_src = nullptr, rb_ready = nullptr;
+    void* rb_dev[3] = {nullptr, nullptr, nullptr};
+    void* rb_host[3] = {nullptr, nullptr, nullptr};
+    size_t rb_cap[3] = {0, 0, 0};
+    int32_t rb_fields = 0;          // fields of the outstanding request (0: none)
+    int32_t rb_count = 0;           // particles it holds
 };
 
 namespace {
@@ -633,6 +642,13 @@ void sph_destroy(sph_ctx* ctx) {
     if (ctx->rng_host) (void)hipHostFree(ctx->rng_host);
     free_all(ctx);
     free_bonds(ctx);
+    for (int f = 0; f < 3; ++f) {
+        if (ctx->rb_dev[f]) (void)hipFree(ctx->rb_dev[f]);
+        if (ctx->rb_host[f]) (void)hipHostFree(ctx->rb_host[f]);
+    }
+    if (ctx->rb_src) (void)hipEventDestroy(ctx->rb_src);
+    if (ctx->rb_ready) (void)hipEventDestroy(ctx->rb_ready);
+    if (ctx->rb_stream) (void)hipStreamDestroy(ctx->rb_stream);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -770,7 +786,10 @@ int sph_upload_state(sph_ctx* ctx, const float* pos3, const float* vel3, int32_t
 
 int sph_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
     if (!ctx || !sc) return SPH_ERR_INVALID;
-    if (is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "scenario init for Model R is not implemented");
+    if (is_contact(ctx)) {
+        if (sc->kind != SPH_SCENARIO_SPHERE) return fail(ctx, SPH_ERR_INVALID, "Model R scenarios: SPH_SCENARIO_SPHERE");
+        return sph_init_particles(ctx, sc->nx, sc->nx, 0, 0);
+    }
     if (sc->dim != ctx->cfg.dim) return fail(ctx, SPH_ERR_INVALID, "scenario dim %d != context dim %d", sc->dim, ctx->cfg.dim);
     const int64_t n = (int64_t)sc->nx * sc->ny * (sc->dim == 3 ? sc->nz : 1);
     if (n <= 0) return fail(ctx, SPH_ERR_INVALID, "empty scenario");
@@ -1072,6 +1091,105 @@ int sph_read_torque_int(sph_ctx* ctx, int32_t* xyz, int32_t count) {
         HIPCHK(hipMemcpyAsync(xyz, ctx->staging, (size_t)ctx->n * 12, hipMemcpyDeviceToHost, ctx->stream));
     }
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SPH_OK;
+}
+
+// ---------------------------------------------------------------- async readback / render interop
+static const size_t RB_BYTES[3] = {12, 16, 84};   // positions, rotations, 84-byte particles
+
+int sph_request_readback(sph_ctx* ctx, int32_t fields) {
+    if (!ctx || fields <= 0 || (fields & ~(SPH_READBACK_POSITIONS | SPH_READBACK_ROTATIONS | SPH_READBACK_PARTICLES)))
+        return SPH_ERR_INVALID;
+    if (ctx->slab) return fail(ctx, SPH_ERR_STATE, "slab mode: use sph_slab_read_owned");
+    if ((fields & (SPH_READBACK_ROTATIONS | SPH_READBACK_PARTICLES)) && !is_contact(ctx))
+        return fail(ctx, SPH_ERR_STATE, "rotations / 84-byte particles are Model R fields");
+    HIPCHK(hipSetDevice(ctx->device));
+    if (!ctx->rb_stream) {
+        HIPCHK(hipStreamCreateWithFlags(&ctx->rb_stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&ctx->rb_src, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ctx->rb_ready, hipEventDisableTiming));
+    }
+    const int32_t n = ctx->n;
+    // the previous request's copy must finish before its buffers are overwritten (device-side wait)
+    if (ctx->rb_fields) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->rb_ready, 0));
+    for (int f = 0; f < 3; ++f) {
+        if (!(fields & (1 << f))) continue;
+        const size_t need = (size_t)std::max(n, 1) * RB_BYTES[f];
+        if (need > ctx->rb_cap[f]) {
+            HIPCHK(hipStreamSynchronize(ctx->rb_stream));
+            if (ctx->rb_dev[f]) (void)hipFree(ctx->rb_dev[f]);
+            if (ctx->rb_host[f]) (void)hipHostFree(ctx->rb_host[f]);
+            ctx->rb_dev[f] = ctx->rb_host[f] = nullptr;
+            ctx->rb_cap[f] = 0;
+            HIPCHK(hipMalloc(&ctx->rb_dev[f], need));
+            HIPCHK(hipHostMalloc(&ctx->rb_host[f], need, hipHostMallocDefault));
+            ctx->rb_cap[f] = need;
+        }
+        if (n == 0) continue;
+        if (f == 0) launch_scatter_f4_by_id(ctx->pos, ctx->id, n, (float*)ctx->rb_dev[0], 3, ctx->stream);
+        if (f == 1) launch_scatter_f4_by_id(ctx->rot, ctx->id, n, (float*)ctx->rb_dev[1], 4, ctx->stream);
+        if (f == 2)
+            launch_soa_to_aos84(ctx->pos, ctx->vel, ctx->omg, ctx->rot, ctx->aux, ctx->mode, ctx->id, n, ctx->rb_dev[2],
+                                ctx->stream);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ctx->rb_src, ctx->stream));
+    HIPCHK(hipStreamWaitEvent(ctx->rb_stream, ctx->rb_src, 0));
+    for (int f = 0; f < 3; ++f)
+        if ((fields & (1 << f)) && n > 0)
+            HIPCHK(hipMemcpyAsync(ctx->rb_host[f], ctx->rb_dev[f], (size_t)n * RB_BYTES[f], hipMemcpyDeviceToHost,
+                                  ctx->rb_stream));
+    HIPCHK(hipEventRecord(ctx->rb_ready, ctx->rb_stream));
+    ctx->rb_fields = fields;
+    ctx->rb_count = n;
+    return SPH_OK;
+}
+
+int sph_readback_status(sph_ctx* ctx) {
+    if (!ctx) return SPH_ERR_INVALID;
+    if (!ctx->rb_fields) return fail(ctx, SPH_ERR_STATE, "no readback requested");
+    HIPCHK(hipSetDevice(ctx->device));
+    const hipError_t e = hipEventQuery(ctx->rb_ready);
+    if (e == hipSuccess) return SPH_OK;
+    if (e == hipErrorNotReady) return SPH_READBACK_PENDING;
+    return fail(ctx, SPH_ERR_HIP, "readback: %s", hipGetErrorString(e));
+}
+
+int sph_readback_get(sph_ctx* ctx, int32_t field, void* dst, int32_t count) {
+    if (!ctx || (!dst && count > 0)) return SPH_ERR_INVALID;
+    int f = field == SPH_READBACK_POSITIONS ? 0 : field == SPH_READBACK_ROTATIONS ? 1 : field == SPH_READBACK_PARTICLES ? 2 : -1;
+    if (f < 0) return SPH_ERR_INVALID;
+    if (!(ctx->rb_fields & field)) return fail(ctx, SPH_ERR_STATE, "field %d was not requested", field);
+    if (count < ctx->rb_count) return fail(ctx, SPH_ERR_INVALID, "count %d < %d particles read back", count, ctx->rb_count);
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipEventSynchronize(ctx->rb_ready));
+    if (ctx->rb_count > 0) std::memcpy(dst, ctx->rb_host[f], (size_t)ctx->rb_count * RB_BYTES[f]);
+    return SPH_OK;
+}
+
+int sph_readback_count(sph_ctx* ctx, int32_t* count) {
+    if (!ctx || !count) return SPH_ERR_INVALID;
+    *count = ctx->rb_fields ? ctx->rb_count : 0;
+    return SPH_OK;
+}
+
+int sph_export_aos84_device(sph_ctx* ctx, void* dev_dst, int32_t count) {
+    if (!ctx || (!dev_dst && count > 0)) return SPH_ERR_INVALID;
+    if (ctx->slab) return fail(ctx, SPH_ERR_STATE, "slab mode");
+    if (count < ctx->n) return fail(ctx, SPH_ERR_INVALID, "count %d < particles %d", count, ctx->n);
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->n > 0)
+        launch_soa_to_aos84(ctx->pos, ctx->vel, ctx->omg, ctx->rot, ctx->aux, ctx->mode, ctx->id, ctx->n, dev_dst,
+                            ctx->stream);
+    HIPCHK(hipGetLastError());
+    return SPH_OK;
+}
+
+int sph_write_draw_args(sph_ctx* ctx, void* dev_args) {
+    if (!ctx || !dev_args) return SPH_ERR_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    const int32_t inst = is_contact(ctx) ? contact_active(ctx) : ctx->n;
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)((uint32_t*)dev_args + 1), inst, 1, ctx->stream));
     return SPH_OK;
 }
 
