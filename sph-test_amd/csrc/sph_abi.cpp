@@ -86,7 +86,10 @@ struct sph_ctx {
     uint32_t* mv_count = nullptr;   // [2] mover counters, ping-pong by step
     int mv_par = 0;                 // counter the next force pass appends into
     bool sk_valid = false;       // sk_cur matches the slot order and cs (set by a Model S sort)
-    bool resort_on = true;       // env SPH_RESORT=0 forces the full radix sort every step
+    // env SPH_RESORT: 0 full radix sort every step, 1 (default) incremental re-sort unless the last
+    // seen mover count exceeds resort_limit(n), 2 incremental whenever possible (tests)
+    int resort_mode = 1;
+    uint32_t* mv_host = nullptr;    // pinned: the mover count of the latest step copied back
     int64_t steps = 0;
     double sim_time = 0.0;
     sph_drag_input drag{-1, {0.f, 0.f, 0.f}, 0.f};
@@ -419,16 +422,25 @@ ResortScratch resort_scratch(sph_ctx* ctx) {
 
 // The force pass appends movers for the next step's incremental re-sort.
 MoverSink mover_sink(sph_ctx* ctx) {
-    if (!ctx->resort_on || !ctx->sk_valid) return MoverSink{};
+    if (ctx->resort_mode == 0 || !ctx->sk_valid) return MoverSink{};
     return MoverSink{ctx->sk_cur, ctx->mv_count + ctx->mv_par, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_rank,
                      (uint32_t)std::max(ctx->capacity, 1)};
 }
 
 // Bring the slots into stable (key, index) order: the incremental re-sort when the previous
 // step's sorted keys and cell starts describe the current slot order, else the full radix sort.
+// Movers above which the full radix sort is cheaper than the incremental re-sort: k_mv_rank's
+// all-pairs counts grow as m², the full sort as n (C3: ~12k movers, where the two cross).
+uint32_t resort_limit(int32_t n) {
+    return std::max<uint32_t>(4096u, (uint32_t)(12.0 * std::sqrt((double)std::max(n, 0))));
+}
+
 int sort_wcsph(sph_ctx* ctx) {
     const int32_t n = ctx->n;
-    if (ctx->resort_on && ctx->keys_valid && ctx->keys_active == 0 && ctx->sk_valid) {
+    // adaptive mode: the latest mover count the host has seen (a step or more behind the device;
+    // both paths give the same permutation, so the choice only affects time)
+    const bool many = ctx->resort_mode == 1 && *(volatile uint32_t*)ctx->mv_host > resort_limit(n);
+    if (ctx->resort_mode != 0 && !many && ctx->keys_valid && ctx->keys_active == 0 && ctx->sk_valid) {
         {
             KTimer t(ctx, "resort", (double)n * (2 * 4 + 2 * 36));
             const int used = ctx->mv_par;
@@ -462,10 +474,13 @@ int step_wcsph(sph_ctx* ctx, float dt) {
     const sph_params& p = ctx->prm;
     const float tt = (float)ctx->sim_time;
     const float fext = p.forcing_amp != 0.0f ? p.forcing_amp * sinf(6.28318530718f * p.forcing_freq * tt) : 0.0f;
+    const MoverSink mv = mover_sink(ctx);
     {
         KTimer t(ctx, "force_integrate", 76.0 * n);
-        force_range(ctx, 0, n, dt, fext, mover_sink(ctx));
+        force_range(ctx, 0, n, dt, fext, mv);
     }
+    if (mv.sk)   // this step's mover count, for the next steps' sort choice (no host wait)
+        HIPCHK(hipMemcpyAsync(ctx->mv_host, mv.count, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
     swap_sv(ctx);
     ctx->keys_valid = true;
     ctx->keys_active = 0;
@@ -603,11 +618,14 @@ int sph_create(const sph_config* cfg, int32_t device, sph_ctx** out) {
     ctx->device = device;
     ctx->profiling = (cfg->flags & SPH_FLAG_PROFILE) != 0;
     if (const char* v = std::getenv("SPH_NB_VARIANT")) ctx->nb_variant = std::atoi(v);
-    if (const char* v = std::getenv("SPH_RESORT")) ctx->resort_on = std::atoi(v) != 0;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (const char* v = std::getenv("SPH_RESORT")) ctx->resort_mode = std::atoi(v);
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void**)&ctx->mv_host, sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+        if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
         delete ctx;
         return SPH_ERR_HIP;
     }
+    *ctx->mv_host = 0u;
     ctx->own_stream = true;
     ctx->capacity = cfg->capacity;
     int r = alloc_particles(ctx, cfg->capacity);
@@ -649,6 +667,7 @@ void sph_destroy(sph_ctx* ctx) {
     if (ctx->rb_src) (void)hipEventDestroy(ctx->rb_src);
     if (ctx->rb_ready) (void)hipEventDestroy(ctx->rb_ready);
     if (ctx->rb_stream) (void)hipStreamDestroy(ctx->rb_stream);
+    if (ctx->mv_host) (void)hipHostFree(ctx->mv_host);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -346,6 +346,10 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
                 const uint32_t off = lst[q][tid];
 #if SPH_FORCE_ABL == 1   // measurement build: trivial pair body
                 acc.ax += 1e-30f * at(sp, off).x; acc.sx += 1e-30f * at(sv, off).w;
+#elif SPH_FORCE_ABL == 4   // measurement build: list read only
+                acc.ax += 1e-30f * (float)off;
+#elif SPH_FORCE_ABL == 5   // measurement build: one 16-B hit read
+                acc.ax += 1e-30f * at(sp, off).x;
 #else
                 pair_force(pk, pi, vi, ri.x, ri.y, at(sp, off), at(sv, off), acc);
 #endif

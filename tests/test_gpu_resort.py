@@ -3,7 +3,9 @@
 Both realise the stable (cell key, slot index) order of SPEC_SPH.md §0, so the slot
 permutation is identical. Every later float operation then runs on the same data in the same
 order, and whole runs must agree BIT FOR BIT: positions, velocities, density, sorted ids, cell
-starts. SPH_RESORT=0 (read at context creation) forces the full sort every step.
+starts. SPH_RESORT (read at context creation): 0 forces the full sort every step, 2 the
+incremental re-sort whenever possible, 1 (default) switches to the full sort while the last
+mover count the host has seen exceeds the crossover (sph_abi.cpp resort_limit).
 """
 import numpy as np
 import pytest
@@ -11,9 +13,9 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _pair(monkeypatch, make):
+def _pair(monkeypatch, make, flags=("0", "2")):
     out = []
-    for flag in ("0", "1"):
+    for flag in flags:
         monkeypatch.setenv("SPH_RESORT", flag)
         out.append(make())
     monkeypatch.delenv("SPH_RESORT")
@@ -88,3 +90,40 @@ def test_resort_after_state_changes(pkg, monkeypatch):
     finally:
         full.close()
         inc.close()
+
+
+def test_resort_adaptive_falls_back_when_many_move(pkg, monkeypatch):
+    """Default mode: a violent state (about half the particles change sub-cell per step, far above
+    the crossover) goes back to the full sort once the host has seen the mover count; the quiet
+    dam-break keeps the incremental path. Results stay bit-identical to the full sort."""
+    sc = pkg.make_scenario(pkg.SPH_SCENARIO_DAMBREAK, 3, 32, 32, 32, 48, 48, 48, dx=0.01, seed=5)
+
+    def make():
+        s = pkg.SPHSim(sc, profile=True)
+        rng = np.random.default_rng(12)
+        x = s.positions()
+        sub = 2 * s.params.h / 4
+        v = rng.uniform(-1.0, 1.0, x.shape).astype(np.float32) * (sub / s.dt)
+        s.ctx.upload_state(x, v)
+        return s
+
+    full, ada = _pair(monkeypatch, make, flags=("0", "1"))
+    try:
+        for k in (1, 1, 1, 3):
+            full.step(k)
+            ada.step(k)
+            _assert_same(full.ctx, ada.ctx, "adaptive, violent state")   # also syncs: the count is seen
+        ks = ada.ctx.kernel_stats()
+        assert ks["radix_sort"]["launches"] >= 4, ks      # fell back after the first incremental step
+    finally:
+        full.close()
+        ada.close()
+    quiet = pkg.SPHSim.from_config("C2", profile=True)
+    try:
+        quiet.step(1)
+        quiet.ctx.synchronize()
+        quiet.step(20)
+        ks = quiet.ctx.kernel_stats()
+        assert ks["resort"]["launches"] == 20 and ks["radix_sort"]["launches"] == 1
+    finally:
+        quiet.close()
