@@ -38,8 +38,20 @@ namespace sph {
 #endif
 constexpr int TT_BLK = SPH_TT_BLK;    // targets per workgroup
 constexpr int TT_GCAP = SPH_TT_GCAP;  // candidates staged per plane (LDS)
-constexpr int TT_CAP = 32;         // per-lane hit list (force)
+#ifndef SPH_TT_CAP
+#define SPH_TT_CAP 16
+#endif
+constexpr int TT_CAP = SPH_TT_CAP;  // per-lane hit list (force)
 constexpr int TT_FALLBACK = 4 * TT_GCAP;
+// The force pass stages 32 B per candidate and keeps per-lane hit lists in LDS. Its flush loop is
+// latency-bound (LDS list read -> candidate reads -> body), so occupancy pays: 704 candidates and
+// 16-entry lists keep a workgroup under 32 KiB, 5 workgroups per CU instead of 3 (C3, MI355X:
+// force pass 305 -> 258 us; 1024/32 and 768/16 measured 305 and 282).
+#ifndef SPH_TF_GCAP
+#define SPH_TF_GCAP 704
+#endif
+constexpr int TF_GCAP = SPH_TF_GCAP;
+constexpr int TF_FALLBACK = 4 * TF_GCAP;
 
 struct BlockRows {
     int64_t kf, kl;           // key range of the block's targets
@@ -298,8 +310,8 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
     const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, PairK pk, float dt,
     float fext_x, float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o, MoverSink mv) {
-    __shared__ float4 sp[TT_GCAP + 4];     // (x, y, z, ρ)
-    __shared__ float4 sv[TT_GCAP + 4];     // (u, v, w, P/ρ²)
+    __shared__ float4 sp[TF_GCAP + 4];     // (x, y, z, ρ)
+    __shared__ float4 sv[TF_GCAP + 4];     // (u, v, w, P/ρ²)
     __shared__ uint16_t lst[TT_CAP][TT_BLK];
     const int tid = threadIdx.x;
     const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
@@ -332,7 +344,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         // two hits per iteration, both bodies unconditional (the second masked by a select when
         // q + 1 >= cnt), so their dependency chains interleave. Slots past cnt hold stale in-range
         // offsets or are clamped into the padded array.
-        constexpr uint32_t OMAX = 16u * TT_GCAP;
+        constexpr uint32_t OMAX = 16u * TF_GCAP;
         for (int q = 0; __any(q < cnt); q += 2) {
             const uint32_t o0 = min((uint32_t)lst[q][tid], OMAX);
             const uint32_t o1 = min((uint32_t)lst[min(q + 1, TT_CAP - 1)][tid], OMAX);
@@ -364,7 +376,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         return;
 #endif
         for (int t = 0; __any(t < ln); t += 4) {
-            const int32_t j = min(lo + t, TT_GCAP);   // lanes past their range stay in the array
+            const int32_t j = min(lo + t, TF_GCAP);   // lanes past their range stay in the array
             const float4 a = sp[j], bb = sp[j + 1], cc = sp[j + 2], d = sp[j + 3];
             // bitwise &, not &&: every read is unconditional (no exec branches around LDS loads).
             // The target itself is a hit: its pair adds exactly ±0 (dx = du = 0, q = 0 finite), so
@@ -398,7 +410,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
             lane_window(g, cs, b, valid, 3 * p + r, r0[r], r1[r]);
         }
         const int32_t total = len[0] + len[1] + len[2];
-        if (total <= TT_GCAP) {
+        if (total <= TF_GCAP) {
             __syncthreads();
             stage_plane(c0, len, total, put);
             __syncthreads();
@@ -414,7 +426,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         // sparse block: offset by offset, in chunks, or straight from global memory
 #pragma unroll 1
         for (int r = 0; r < 3; ++r) {
-            if (len[r] > TT_FALLBACK) {
+            if (len[r] > TF_FALLBACK) {
                 for (int32_t j = r0[r]; j < r1[r]; ++j) {
                     const float4 pj = pos[j];
                     if (j != i && dist2(pi, pj) < c.four_h2) {
@@ -427,8 +439,8 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
                 continue;
             }
 #pragma unroll 1
-            for (int32_t base = c0[r]; base < c1[r]; base += TT_GCAP) {
-                const int32_t ln = min(TT_GCAP, c1[r] - base);
+            for (int32_t base = c0[r]; base < c1[r]; base += TF_GCAP) {
+                const int32_t ln = min(TF_GCAP, c1[r] - base);
                 __syncthreads();
                 for (int32_t t = tid; t < ln; t += TT_BLK) put(t, base + t);
                 __syncthreads();
