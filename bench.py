@@ -47,9 +47,10 @@ def parse():
     return ap.parse_args()
 
 
-# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD
-# (MI355X_MICROARCH.md: a wave issues each VALU instruction over 2 cycles), at 2.4 GHz.
-PEAK_VALU_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 2
+# VALU issue peak, MEASURED on MI355X (scripts/valu_peak.hip, profiles/r01_valu_peak.log): independent
+# f32 FMA chains at 8 waves per SIMD issue 891.9 G wave64-instructions/s chip-wide (114 TFLOP/s);
+# 2 waves/SIMD 778, 4 waves 861. Packed f32 (v_pk_fma_f32) issues 473 G/s, 121 TFLOP/s: no faster per flop.
+PEAK_VALU_WAVE_INSTR_PER_S = 891.9e9
 
 
 def force_kernel_name() -> str:
@@ -186,7 +187,8 @@ def main():
             va = pmc["valu_instr"] / avg_s
             roofline["valu"] = {"achieved": round(va / 1e9, 2), "peak": round(PEAK_VALU_WAVE_INSTR_PER_S / 1e9, 1),
                                 "unit": "G wave-instr/s", "frac": round(va / PEAK_VALU_WAVE_INSTR_PER_S, 4),
-                                "source": "rocprofv3 SQ_INSTS_VALU per launch (profiles/pmc_C3.json)"}
+                                "source": "rocprofv3 SQ_INSTS_VALU per launch (profiles/pmc_C3.json); peak measured by "
+                                          "scripts/valu_peak.hip (profiles/r01_valu_peak.log)"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -479,7 +479,9 @@ int step_wcsph(sph_ctx* ctx, float dt) {
         KTimer t(ctx, "force_integrate", 76.0 * n);
         force_range(ctx, 0, n, dt, fext, mv);
     }
-    if (mv.sk)   // this step's mover count, for the next steps' sort choice (no host wait)
+    // this step's mover count, for the next steps' sort choice (no host wait); every 8th step, as the
+    // copy is a ~4 us blit and the count drifts slowly
+    if (mv.sk && (ctx->steps & 7) == 0)
         HIPCHK(hipMemcpyAsync(ctx->mv_host, mv.count, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
     swap_sv(ctx);
     ctx->keys_valid = true;
