@@ -111,12 +111,14 @@ __device__ __forceinline__ float dist2(float4 a, float4 b) {
 // 4·w(q) of the unnormalised cubic spline (W = σ·w) for r² < 4h², else 0. Branchless: both arms
 // are computed and selected (a ?: over expressions compiles to an exec branch per candidate).
 // Scaling by 4 (and the final 0.25) is exact in binary floating point: no rounding is added.
+// 4w = (2−q)₊³ − 4(1−q)₊³: the outer arm (2−q)₊³ lies below the inner polynomial exactly where
+// q ≥ 1 (their difference is 4(1−q)³), and (2−q)₊ is 0 past the support, where the polynomial is ≥ 4.
+// So one min replaces both selects (18 VALU slots per candidate instead of 20; C3 pass 1 −5%).
+// A candidate at r² ≥ 4h² whose q rounds just below 2 adds (2−q)³ < 1e-20 instead of 0.
 __device__ __forceinline__ float spline_w4(const SphConst& c, float r2) {
     const float q = __builtin_amdgcn_sqrtf(r2) * c.inv_h;
-    const float t = 2.0f - q;
-    const float w_in = fmaf(q * q, fmaf(3.0f, q, -6.0f), 4.0f), w_out = t * t * t;
-    const float w = q < 1.0f ? w_in : w_out;
-    return r2 < c.four_h2 ? w : 0.0f;
+    const float t = fmaxf(2.0f - q, 0.0f);
+    return fminf(fmaf(q * q, fmaf(3.0f, q, -6.0f), 4.0f), t * t * t);
 }
 
 // The scans use x, y, z only, and the compiler then narrows the float4 LDS read to
