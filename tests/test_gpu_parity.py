@@ -131,6 +131,28 @@ def test_wcsph_c3_invariants(pkg):
     sim.close()
 
 
+@pytest.mark.parametrize("cfg,steps", [("C4", 10), ("C5", 4)])
+def test_wcsph_full_size_configs(pkg, cfg, steps):
+    """BASELINE.json's multi-GPU configs at full size on one GPU (4,194,304 sloshing, 16,777,216
+    dam-break): finite, in the box, no particle lost, sorted cell table, sane density."""
+    sim = pkg.SPHSim.from_config(cfg)
+    n = sim.n
+    assert n == {"C4": 4_194_304, "C5": 16_777_216}[cfg]
+    if cfg == "C4":
+        assert sim.params.forcing_amp > 0
+    sim.step(steps)
+    x, v, rho = sim.positions(), sim.velocities(), sim.density()
+    box = np.array(sim.params.box)
+    assert np.isfinite(x).all() and np.isfinite(v).all() and np.isfinite(rho).all()
+    assert (x >= 0).all() and (x <= box).all()
+    ids = sim.ctx.sorted_ids()
+    assert np.array_equal(np.sort(ids), np.arange(n))
+    cs = sim.ctx.cell_start()
+    assert cs[0] == 0 and cs[-1] == n and np.all(np.diff(cs.astype(np.int64)) >= 0)
+    assert 500 < np.median(rho) < 1100
+    sim.close()
+
+
 def test_wcsph_upload_state_and_empty(pkg, oracle):
     sc = pkg.config_scenario("C1")
     p, dt = pkg.scenario_params(sc)

@@ -20,11 +20,13 @@ def _free_port():
     return p
 
 
-def _scenario(pkg):
+def _scenario(pkg, kind=0):
+    if kind == 1:   # C4-shaped sloshing (fluid layer on the tank floor, lateral forcing), scaled down
+        return pkg.make_scenario(1, 3, 48, 8, 8, 48, 16, 8, dx=0.01, seed=99)
     return pkg.make_scenario(0, 3, 24, 16, 8, 60, 24, 8, dx=0.01, seed=4321)
 
 
-def _worker(rank, world, port, outdir, cuts=None, rebalance_every=0):
+def _worker(rank, world, port, outdir, cuts=None, rebalance_every=0, kind=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1")
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "tests"))
@@ -35,7 +37,7 @@ def _worker(rank, world, port, outdir, cuts=None, rebalance_every=0):
     pkg = GE.load_package()
     O = GE.load_oracle()
     from sph_test_amd import slab
-    sc = _scenario(pkg)
+    sc = _scenario(pkg, kind)
     p, _ = pkg.scenario_params(sc)
     op = O.sph_params(3, p.dx, p.h, p.rho0, p.c0, p.alpha, p.xsph_eps, tuple(p.gravity), tuple(p.box),
                       p.wall_restitution, p.forcing_amp, p.forcing_freq)
@@ -49,11 +51,11 @@ def _worker(rank, world, port, outdir, cuts=None, rebalance_every=0):
     dist.destroy_process_group()
 
 
-def _run(world, tmp_path, cuts=None, rebalance_every=0):
+def _run(world, tmp_path, cuts=None, rebalance_every=0, kind=0):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), cuts, rebalance_every))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), cuts, rebalance_every, kind))
              for r in range(world)]
     for pr in procs:
         pr.start()
@@ -63,10 +65,10 @@ def _run(world, tmp_path, cuts=None, rebalance_every=0):
     return [np.load(tmp_path / f"rank{r}.npy") for r in range(world)]
 
 
-def _check_against_single_domain(pkg, oracle, parts):
+def _check_against_single_domain(pkg, oracle, parts, kind=0):
     rec = np.concatenate(parts)
     ids = rec[:, 6].view(np.int32)
-    sc = _scenario(pkg)
+    sc = _scenario(pkg, kind)
     n = sc.nx * sc.ny * sc.nz
     # every particle owned by exactly one rank
     assert np.array_equal(np.sort(ids), np.arange(n))
@@ -97,6 +99,14 @@ def test_slab_decomposition_matches_single_domain(pkg, oracle, tmp_path, world):
     cuts = np.load(tmp_path / "cuts0.npy")
     assert len(cuts) == world and all(c[0] < c[1] for c in cuts)
     _check_against_single_domain(pkg, oracle, parts)
+
+
+def test_slab_sloshing_four_ranks(pkg, oracle, tmp_path):
+    """C4's shape (sloshing with lateral forcing, 4 ranks), scaled down: the decomposed run equals
+    the single-domain oracle run."""
+    parts = _run(4, tmp_path, kind=1)
+    assert len(np.load(tmp_path / "cuts0.npy")) == 4
+    _check_against_single_domain(pkg, oracle, parts, kind=1)
 
 
 def test_slab_rebalancing_matches_single_domain(pkg, oracle, tmp_path):
