@@ -59,9 +59,9 @@ void or_sph_derive(or_sph_params* p) {
     p->sigma = p->dim == 3 ? 1.0f / (PI * p->h * p->h * p->h) : 10.0f / (7.0f * PI * p->h * p->h);
     p->inv_h = 1.0f / p->h;
     p->four_h2 = 4.0f * p->h * p->h;
-    /* SPEC_SPH.md §0: cells 2h in x, y; z split into zsub = 4 sub-cells (3D) */
+    /* SPEC_SPH.md §0: cells 2h in x, y; z split into zsub = 6 sub-cells (3D) */
     float cell = 2.0f * p->h;
-    int32_t zsub = p->dim == 3 ? 4 : 1;
+    int32_t zsub = p->dim == 3 ? 6 : 1;
     float cz = cell / (float)zsub;
     p->grid.inv_cell = 1.0f / cell;
     p->grid.inv_cell_z = 1.0f / cz;

@@ -21,7 +21,10 @@
 
 using namespace sph;
 
-static const int32_t SPH_ZSUB = 4;   // z sub-cells per 2h cell (SPEC_SPH.md §0)
+// z sub-cells per 2h cell (SPEC_SPH.md §0). 6 trims the neighbour windows closer than 4 (C3: both passes
+// −8 us each) while the sub-cell crossings it adds cost the re-sort 2 us; 8 costs it 14 us
+// (profiles/r01_zsub_ab.log).
+static const int32_t SPH_ZSUB = 6;
 
 namespace {
 

@@ -53,7 +53,7 @@ def test_resort_bitwise_many_movers(pkg, monkeypatch):
         s = pkg.SPHSim(sc, profile=True)
         rng = np.random.default_rng(11)
         x = s.positions()
-        sub = 2 * s.params.h / 4                  # z sub-cell (SPEC_SPH.md §0)
+        sub = 2 * s.params.h / 6                  # z sub-cell (SPEC_SPH.md §0)
         v = rng.uniform(-1.0, 1.0, x.shape).astype(np.float32) * (sub / s.dt)
         s.ctx.upload_state(x, v)
         return s
@@ -102,7 +102,7 @@ def test_resort_adaptive_falls_back_when_many_move(pkg, monkeypatch):
         s = pkg.SPHSim(sc, profile=True)
         rng = np.random.default_rng(12)
         x = s.positions()
-        sub = 2 * s.params.h / 4
+        sub = 2 * s.params.h / 6
         v = rng.uniform(-1.0, 1.0, x.shape).astype(np.float32) * (sub / s.dt)
         s.ctx.upload_state(x, v)
         return s

@@ -211,13 +211,13 @@ def test_grid_sort_and_cell_start(oracle):
 
 def test_grid_keys_clamp(oracle):
     O = oracle
-    p = _sph(O, L=(0.24, 0.24, 0.24))            # cell 0.024 -> 11 cells in x, y; z sub-cells 0.006 -> 41
-    G = list(p.grid.G)
-    assert G == [11, 11, 41]
+    p = _sph(O, L=(0.24, 0.24, 0.24))            # cell 0.024 -> 11 cells in x, y; z sub-cells 0.004 -> 60
+    G = list(p.grid.G)                           # (0.24f / 0.004f rounds just below 60: floor 59, + 1)
+    assert G == [11, 11, 60]
     pos = np.array([[-1, -1, -1], [0.0, 0.0, 0.0], [0.0241, 0.0, 0.0], [5, 5, 5], [np.nan, 0, 0],
                     [0.0, 0.0, 0.0061]], np.float32)
     k = O.grid_keys(p, pos)
-    assert k.tolist() == [0, 0, 1 * 11 * 41, 10 * 11 * 41 + 10 * 41 + 40, 0, 1]
+    assert k.tolist() == [0, 0, 1 * 11 * 60, 10 * 11 * 60 + 10 * 60 + 59, 0, 1]
 
 
 def test_lattice_deterministic_and_bounded(oracle):
