@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event pass")
     ap.add_argument("--slab", action="store_true", help="run the multi-GPU slab step even at N=1 (rehearsal)")
     ap.add_argument("--rebalance", type=int, default=50, help="slab cut re-balancing interval in steps (0: off)")
+    ap.add_argument("--table", action="store_true",
+                    help="print the GPU / 1-thread / all-thread CPU rate table (SURVEY §8d) instead of the bench line")
     return ap.parse_args()
 
 
@@ -110,9 +112,107 @@ def cpu_baseline(config: str, budget_s: float):
                       f"step, {el:.1f} s, OpenMP {threads} threads"}
 
 
+def _timed_cpu(step, budget_s):
+    """Whole steps of `step()` for about budget_s seconds after one warm-up step: (steps, seconds)."""
+    t0 = time.perf_counter()
+    step()
+    one = time.perf_counter() - t0
+    steps = max(1, min(1000, int(budget_s / max(one, 1e-6))))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    return steps, time.perf_counter() - t0
+
+
+def rate_table(budget_s: float, gpu_steps: int = 50):
+    """SURVEY.md §8d CPU-baseline table: GPU, 1-thread and all-thread oracle rates (particle-steps/s) at
+    C1, C2, C3 (Model S) and Model R at N = 4,096 / 32,768 (positions in the R = 15 sphere, the
+    test_gpu_parity recipe). Rank 0, N = 1; the oracle runs only here, as the timed CPU reference."""
+    import numpy as np
+    import torch
+    O = GE.load_oracle()
+    pkg = GE.load_package()
+    try:
+        allc = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allc = os.cpu_count() or 1
+    allc = max(1, min(allc, int(os.environ.get("OMP_NUM_THREADS", allc) or allc)))
+    rows = []
+
+    def gpu_rate(step, n):
+        step(5)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        step(gpu_steps)
+        torch.cuda.synchronize()
+        return n * gpu_steps / (time.perf_counter() - t0)
+
+    for cfg in ("C1", "C2", "C3"):
+        sim = pkg.SPHSim.from_config(cfg, device=0)
+        n = sim.n
+        g = gpu_rate(sim.step, n)
+        sim.close()
+        sc = pkg.config_scenario(cfg)
+        p, dt = pkg.scenario_params(sc)
+        op = O.sph_params(sc.dim, p.dx, p.h, p.rho0, p.c0, p.alpha, p.xsph_eps, tuple(p.gravity), tuple(p.box),
+                          p.wall_restitution, p.forcing_amp, p.forcing_freq)
+        row = {"model": "S", "config": cfg, "particles": n, "gpu": g}
+        for th in (1, allc):
+            st = {"x": O.lattice(sc.dim, sc.nx, sc.ny, sc.nz, sc.dx, seed=sc.seed, jitter_frac=sc.jitter)}
+            st["v"] = np.zeros_like(st["x"])
+            st["i"] = np.arange(n, dtype=np.int32)
+
+            def one(st=st, th=th):
+                st["x"], st["v"], st["i"], _, _, _ = O.sph_step(op, st["x"], st["v"], st["i"], dt, 0.0, nthreads=th)
+            k, el = _timed_cpu(one, budget_s)
+            row[f"cpu_{th}t"] = n * k / el
+            row[f"cpu_{th}t_steps"] = k
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+
+    for n in (4096, 32768):
+        rng = np.random.default_rng(1234)
+        parts = np.zeros(n, pkg.PARTICLE84)
+        d = rng.normal(size=(n, 3))
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        parts["position"] = d * (15.0 * rng.random((n, 1)) ** (1 / 3))
+        parts["radius"] = rng.uniform(1.5, 2.0, n)
+        parts["velocity"] = rng.normal(size=(n, 3))
+        parts["mass"] = 0.1 * 4.0 / 3.0 * 3.1415926 * parts["radius"] ** 3
+        parts["angularVelocity"] = rng.normal(size=(n, 3))
+        parts["momentOfInertia"] = 0.4 * parts["mass"] * parts["radius"] ** 2
+        parts["drag"] = rng.uniform(0.5, 1.0, n)
+        parts["repulsionStrength"] = 1.0
+        parts["rotation"] = (0, 0, 0, 1)
+        parts["modeIndex"] = -1
+        dt = 0.01
+        ctl = pkg.ParticleSystemController(particleCount=n)
+        ctl.Start(parts.copy())
+        g = gpu_rate(lambda k: ctl.context.step(dt, k), n)
+        ctl.OnDestroy()
+        row = {"model": "R", "config": f"sphere R=15, N={n}", "particles": n, "gpu": g}
+        cp = O.contact_params(dt)
+        for th in (1, allc):
+            st = {"p": parts.view(O.PARTICLE84).copy()}
+
+            def one(st=st, th=th):
+                st["p"], _ = O.contact_step(cp, st["p"], nthreads=th)
+            k, el = _timed_cpu(one, budget_s)
+            row[f"cpu_{th}t"] = n * k / el
+            row[f"cpu_{th}t_steps"] = k
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    return {"unit": "particle-steps/s", "threads_all": allc, "budget_s_per_cpu_cell": budget_s,
+            "gpu_steps": gpu_steps, "rows": rows}
+
+
 def main():
     args = parse()
     import torch
+    if args.table:
+        torch.cuda.set_device(0)
+        print(json.dumps({"rate_table": rate_table(args.cpu_seconds)}), flush=True)
+        return
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

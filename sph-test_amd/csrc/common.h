@@ -280,14 +280,17 @@ void launch_get_range(const float4* pos, const float4* vel, const float4* omg, c
 void launch_set_range(const void* aos, const int32_t* slot_of, int32_t first, int32_t count, float4* pos,
                       float4* vel, float4* omg, float4* rot, float4* aux, int32_t* mode, hipStream_t s);
 
-// Model R (contact.hip)
+// Model R (contact.hip). team: lanes per target (0 = by size, else 1, 16 or 64; any choice gives
+// bit-identical results).
 void launch_contact_step(const float4* pos, const float4* vel, const float4* omg, const float4* rot,
                          const float4* aux, const int32_t* id, const uint32_t* cs, int32_t n_active,
                          int32_t n, GridDesc g, ContactConst c, float4* pos_o, float4* vel_o,
-                         float4* omg_o, float4* rot_o, int32_t* torque_o, uint32_t* keys_o, hipStream_t s);
+                         float4* omg_o, float4* rot_o, int32_t* torque_o, uint32_t* keys_o, int team,
+                         hipStream_t s);
 void launch_contact_forces(const float4* pos, const float4* vel, const float4* omg, const int32_t* id,
                            const uint32_t* cs, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
-                           float4* vel_o, float4* omg_o, int32_t* torque_o, int32_t* slot_of, hipStream_t s);
+                           float4* vel_o, float4* omg_o, int32_t* torque_o, int32_t* slot_of, int team,
+                           hipStream_t s);
 void launch_contact_finish(const float4* pos, const float4* rot, const float4* aux, const int32_t* id,
                            const int32_t* torque, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
                            BondView b, float4* vel_io, float4* omg_io, float4* pos_o, float4* rot_o,

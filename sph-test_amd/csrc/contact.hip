@@ -90,8 +90,8 @@ __device__ __forceinline__ void contact_accumulate(const float4* __restrict__ po
             f3 F, TA, TB;
             const int hit = contact_pair(c, A, B, F, TA, TB);
             if (hit == 0) continue;
-            totalForce = totalForce + F;                                     // :261
-            if (hit == 2) totalTorque = totalTorque + TA;                    // :289
+            totalForce = add_exact(totalForce, F);                           // :261
+            if (hit == 2) totalTorque = add_exact(totalTorque, TA);          // :289
             f3 F2, TA2, TB2;
             if (contact_pair(c, B, A, F2, TA2, TB2) == 2) {                  // b's scatter into a
                 const f3 sc = TB2 * dt * TORQUE_SCALE;                       // :291
@@ -101,6 +101,98 @@ __device__ __forceinline__ void contact_accumulate(const float4* __restrict__ po
             }
         }
     }
+    v = A.vel + (totalForce / va.w) * dt;                                    // :302-306
+    w = A.omg + (totalTorque / wa.w) * dt;
+}
+
+// Team form of contact_accumulate: T lanes (T | 64) share target a and take the candidates of a
+// row T at a time, lane t taking j = base + t. That gives T times more lanes in flight at the
+// reference's scale (a few thousand dense particles, hundreds of candidates each), where one lane
+// per target leaves the chip idle and serialises every candidate load.
+// The float totals keep the serial order bit for bit: the team walks its hit mask lowest lane first
+// and every lane adds the hit lane's F and TA, which is exactly contact_accumulate's order
+// (rows k in order, j increasing; adding TA = +0 for a repulsion-only hit changes nothing since
+// the total starts at +0 and can never become −0). The int torque is a wrapping sum, so the
+// team reduces it in any order. Every team lane returns the same v, w, tq.
+template <int T>
+__device__ __forceinline__ void contact_accumulate_team(const float4* __restrict__ pos,
+                                                        const float4* __restrict__ vel,
+                                                        const float4* __restrict__ omg,
+                                                        const uint32_t* __restrict__ cs, const GridDesc& g,
+                                                        const ContactConst& c, int32_t a, float4 pa, float4 va,
+                                                        float4 wa, f3& v, f3& w, uint32_t tq[3]) {
+    static_assert(T == 16 || T == 64, "team size (lanes 0..8 fetch the rows)");
+    const int lane = (int)(threadIdx.x & 63u);
+    const int t = lane & (T - 1);
+    const int team0 = lane & ~(T - 1);
+    const Body A{xyz(pa), xyz(va), xyz(wa), pa.w};
+    const float dt = c.dt;
+    f3 totalForce = mk(0, 0, 0), totalTorque = mk(0, 0, 0);
+    uint32_t q0 = 0u, q1 = 0u, q2 = 0u;
+    const int32_t cx = cell_cx(g, pa.x);
+    const int32_t cy = cell_coord(pa.y, g.oy, g.inv_cell, g.gy);
+    const int32_t cz = cell_coord(pa.z, g.oz, g.inv_cz, g.gz);
+    const int32_t z0 = cz > 0 ? cz - 1 : 0, z1 = cz < g.gz - 1 ? cz + 1 : g.gz - 1;
+    // lanes 0..8 of the team fetch the nine row ranges at once; rows are read back by shuffle
+    uint32_t rj0 = 0u, rj1 = 0u;
+    if (t < 9) {
+        const int32_t xx = cx + t / 3 - 1, yy = cy + t % 3 - 1;
+        if (xx >= 0 && xx < g.gx && yy >= 0 && yy < g.gy) {
+            const uint32_t rowk = ((uint32_t)xx * (uint32_t)g.gy + (uint32_t)yy) * (uint32_t)g.gz;
+            rj0 = cs[rowk + (uint32_t)z0];
+            rj1 = cs[rowk + (uint32_t)z1 + 1u];
+        }
+    }
+#pragma unroll 1
+    for (int k = 0; k < 9; ++k) {
+        const uint32_t j0 = (uint32_t)__shfl((int)rj0, k, T), j1 = (uint32_t)__shfl((int)rj1, k, T);
+#pragma unroll 1
+        for (uint32_t base = j0; base < j1; base += T) {
+            const uint32_t j = base + (uint32_t)t;
+            f3 F = mk(0, 0, 0), TA = mk(0, 0, 0);
+            bool hit = false;
+            if (j < j1 && (int32_t)j != a) {                                   // :240
+                const float4 pb = pos[j];
+                const f3 d = A.pos - xyz(pb);
+                const float reff = A.r * 0.5f + pb.w * 0.5f;
+                if (reff - len(d) > 0.001f) {                                   // :253 (cheap reject)
+                    const float4 vb = vel[j], wb = omg[j];
+                    const Body B{xyz(pb), xyz(vb), xyz(wb), pb.w};
+                    f3 TB;
+                    const int h = contact_pair(c, A, B, F, TA, TB);
+                    hit = h != 0;
+                    if (h != 2) TA = mk(0, 0, 0);
+                    if (h == 0) F = mk(0, 0, 0);
+                    if (hit) {
+                        f3 F2, TA2, TB2;
+                        if (contact_pair(c, B, A, F2, TA2, TB2) == 2) {         // b's scatter into a
+                            const f3 sc = TB2 * dt * TORQUE_SCALE;              // :291
+                            q0 += (uint32_t)ftoi(sc.x);
+                            q1 += (uint32_t)ftoi(sc.y);
+                            q2 += (uint32_t)ftoi(sc.z);
+                        }
+                    }
+                }
+            }
+            // this team's hits, lowest lane (= lowest j) first
+            uint64_t m = (__ballot(hit) >> team0);
+            if (T < 64) m &= (1ull << T) - 1ull;
+            while (m) {
+                const int src = __builtin_ctzll(m);
+                m &= m - 1ull;
+                totalForce = add_exact(totalForce, mk(__shfl(F.x, src, T), __shfl(F.y, src, T), __shfl(F.z, src, T)));
+                totalTorque =
+                    add_exact(totalTorque, mk(__shfl(TA.x, src, T), __shfl(TA.y, src, T), __shfl(TA.z, src, T)));
+            }
+        }
+    }
+#pragma unroll
+    for (int o = T / 2; o > 0; o >>= 1) {
+        q0 += (uint32_t)__shfl_xor((int)q0, o, T);
+        q1 += (uint32_t)__shfl_xor((int)q1, o, T);
+        q2 += (uint32_t)__shfl_xor((int)q2, o, T);
+    }
+    tq[0] = q0; tq[1] = q1; tq[2] = q2;
     v = A.vel + (totalForce / va.w) * dt;                                    // :302-306
     w = A.omg + (totalTorque / wa.w) * dt;
 }
@@ -188,6 +280,66 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step(
     keys_o[a] = cell_key(g, p.x, p.y, p.z);
 }
 
+// k_contact_step with T lanes per target (contact_accumulate_team); team lane 0 finishes and writes.
+template <int T>
+__global__ __launch_bounds__(CT_BLK) void k_contact_step_team(
+    const float4* __restrict__ pos, const float4* __restrict__ vel, const float4* __restrict__ omg,
+    const float4* __restrict__ rot, const float4* __restrict__ aux, const int32_t* __restrict__ id,
+    const uint32_t* __restrict__ cs, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
+    float4* __restrict__ pos_o, float4* __restrict__ vel_o, float4* __restrict__ omg_o,
+    float4* __restrict__ rot_o, int32_t* __restrict__ torque_o, uint32_t* __restrict__ keys_o) {
+    const int32_t a = blockIdx.x * (CT_BLK / T) + (int32_t)(threadIdx.x / T);
+    const bool lead = (threadIdx.x & (T - 1)) == 0;
+    if (a >= n) return;                                                      // team-uniform
+    const float4 pa = pos[a], va = vel[a], wa = omg[a];
+    if (a >= n_active) {
+        if (!lead) return;
+        const float4 qa = rot[a];
+        const f3 v = apply_drag(c, id[a], xyz(pa), xyz(va), va.w);
+        pos_o[a] = pa; vel_o[a] = make_float4(v.x, v.y, v.z, va.w); omg_o[a] = wa; rot_o[a] = qa;
+        if (torque_o) { torque_o[3 * a] = 0; torque_o[3 * a + 1] = 0; torque_o[3 * a + 2] = 0; }
+        keys_o[a] = g.ncells;
+        return;
+    }
+    f3 v, w;
+    uint32_t tq[3];
+    contact_accumulate_team<T>(pos, vel, omg, cs, g, c, a, pa, va, wa, v, w, tq);
+    if (!lead) return;
+    f3 p;
+    float4 q;
+    contact_finish(c, id[a], pa, v, w, va.w, wa.w, aux[a].x, rot[a], tq, p, v, w, q);
+    pos_o[a] = make_float4(p.x, p.y, p.z, pa.w);
+    vel_o[a] = make_float4(v.x, v.y, v.z, va.w);
+    omg_o[a] = make_float4(w.x, w.y, w.z, wa.w);
+    rot_o[a] = q;
+    if (torque_o) {
+        torque_o[3 * a] = (int32_t)tq[0]; torque_o[3 * a + 1] = (int32_t)tq[1]; torque_o[3 * a + 2] = (int32_t)tq[2];
+    }
+    keys_o[a] = cell_key(g, p.x, p.y, p.z);
+}
+
+// k_contact_forces with T lanes per target.
+template <int T>
+__global__ __launch_bounds__(CT_BLK) void k_contact_forces_team(
+    const float4* __restrict__ pos, const float4* __restrict__ vel, const float4* __restrict__ omg,
+    const int32_t* __restrict__ id, const uint32_t* __restrict__ cs, int32_t n_active, int32_t n, GridDesc g,
+    ContactConst c, float4* __restrict__ vel_o, float4* __restrict__ omg_o, int32_t* __restrict__ torque_o,
+    int32_t* __restrict__ slot_of) {
+    const int32_t a = blockIdx.x * (CT_BLK / T) + (int32_t)(threadIdx.x / T);
+    const bool lead = (threadIdx.x & (T - 1)) == 0;
+    if (a >= n) return;                                                      // team-uniform
+    const float4 pa = pos[a], va = vel[a], wa = omg[a];
+    f3 v = xyz(va), w = xyz(wa);
+    uint32_t tq[3] = {0u, 0u, 0u};
+    if (a < n_active) contact_accumulate_team<T>(pos, vel, omg, cs, g, c, a, pa, va, wa, v, w, tq);
+    if (!lead) return;
+    const int32_t pid = id[a];
+    if ((uint32_t)pid < (uint32_t)n) slot_of[pid] = a;
+    vel_o[a] = make_float4(v.x, v.y, v.z, va.w);
+    omg_o[a] = make_float4(w.x, w.y, w.z, wa.w);
+    torque_o[3 * a] = (int32_t)tq[0]; torque_o[3 * a + 1] = (int32_t)tq[1]; torque_o[3 * a + 2] = (int32_t)tq[2];
+}
+
 // With adhesion, phase 1: ApplySPHForces only (v1, ω1 and the int torque into *_o), plus the
 // particle-index → slot map the bond pass reads particles through.
 __global__ __launch_bounds__(CT_BLK) void k_contact_forces(
@@ -240,22 +392,55 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_finish(
     keys_o[a] = cell_key(g, p.x, p.y, p.z);
 }
 
+// Lanes per target: enough teams to fill the chip (256 CUs × 8 waves × 64 lanes ≈ 131k lanes) without
+// splitting thin candidate lists. A forced choice (1, 16, 64) wins; every choice gives bit-identical
+// results (contact_accumulate_team).
+static int contact_team(int32_t n, int forced) {
+    if (forced == 1 || forced == 16 || forced == 64) return forced;
+    if (n <= 32768) return 64;
+    if (n <= 262144) return 16;
+    return 1;
+}
+
 void launch_contact_step(const float4* pos, const float4* vel, const float4* omg, const float4* rot,
                          const float4* aux, const int32_t* id, const uint32_t* cs, int32_t n_active,
                          int32_t n, GridDesc g, ContactConst c, float4* pos_o, float4* vel_o,
-                         float4* omg_o, float4* rot_o, int32_t* torque_o, uint32_t* keys_o, hipStream_t s) {
-    if (n > 0)
-        k_contact_step<<<(n + CT_BLK - 1) / CT_BLK, CT_BLK, 0, s>>>(pos, vel, omg, rot, aux, id, cs,
-                                                                    n_active, n, g, c, pos_o, vel_o,
-                                                                    omg_o, rot_o, torque_o, keys_o);
+                         float4* omg_o, float4* rot_o, int32_t* torque_o, uint32_t* keys_o, int team,
+                         hipStream_t s) {
+    if (n <= 0) return;
+    switch (contact_team(n, team)) {
+#define SPH_CT_STEP(T)                                                                                        \
+    case T:                                                                                                   \
+        k_contact_step_team<T><<<(n + CT_BLK / T - 1) / (CT_BLK / T), CT_BLK, 0, s>>>(                          \
+            pos, vel, omg, rot, aux, id, cs, n_active, n, g, c, pos_o, vel_o, omg_o, rot_o, torque_o, keys_o);  \
+        break;
+        SPH_CT_STEP(64)
+        SPH_CT_STEP(16)
+#undef SPH_CT_STEP
+    default:
+        k_contact_step<<<(n + CT_BLK - 1) / CT_BLK, CT_BLK, 0, s>>>(pos, vel, omg, rot, aux, id, cs, n_active, n, g,
+                                                                    c, pos_o, vel_o, omg_o, rot_o, torque_o, keys_o);
+    }
 }
 
 void launch_contact_forces(const float4* pos, const float4* vel, const float4* omg, const int32_t* id,
                            const uint32_t* cs, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
-                           float4* vel_o, float4* omg_o, int32_t* torque_o, int32_t* slot_of, hipStream_t s) {
-    if (n > 0)
+                           float4* vel_o, float4* omg_o, int32_t* torque_o, int32_t* slot_of, int team,
+                           hipStream_t s) {
+    if (n <= 0) return;
+    switch (contact_team(n, team)) {
+#define SPH_CT_FORCES(T)                                                                                      \
+    case T:                                                                                                   \
+        k_contact_forces_team<T><<<(n + CT_BLK / T - 1) / (CT_BLK / T), CT_BLK, 0, s>>>(                        \
+            pos, vel, omg, id, cs, n_active, n, g, c, vel_o, omg_o, torque_o, slot_of);                         \
+        break;
+        SPH_CT_FORCES(64)
+        SPH_CT_FORCES(16)
+#undef SPH_CT_FORCES
+    default:
         k_contact_forces<<<(n + CT_BLK - 1) / CT_BLK, CT_BLK, 0, s>>>(pos, vel, omg, id, cs, n_active, n, g, c,
                                                                       vel_o, omg_o, torque_o, slot_of);
+    }
 }
 
 void launch_contact_finish(const float4* pos, const float4* rot, const float4* aux, const int32_t* id,

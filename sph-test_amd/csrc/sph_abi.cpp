@@ -92,6 +92,7 @@ struct sph_ctx {
     // env SPH_RESORT: 0 full radix sort every step, 1 (default) incremental re-sort unless the last
     // seen mover count exceeds resort_limit(n), 2 incremental whenever possible (tests)
     int resort_mode = 1;
+    int ct_team = 0;                // env SPH_CT_TEAM: Model R lanes per target (0 = by size; tests)
     uint32_t* mv_host = nullptr;    // pinned: the mover count of the latest step copied back
     int64_t steps = 0;
     double sim_time = 0.0;
@@ -567,7 +568,8 @@ int step_contact(sph_ctx* ctx, float dt) {
     if (ctx->nbonds == 0) {
         KTimer t(ctx, "contact_step", (double)n * (2 * 64 + 4 + 12 + 4));
         launch_contact_step(ctx->pos, ctx->vel, ctx->omg, ctx->rot, ctx->aux, ctx->id, ctx->cs, act, n, ctx->grid,
-                            c, ctx->pos2, ctx->vel2, ctx->omg2, ctx->rot2, ctx->torque, ctx->keys, ctx->stream);
+                            c, ctx->pos2, ctx->vel2, ctx->omg2, ctx->rot2, ctx->torque, ctx->keys, ctx->ct_team,
+                            ctx->stream);
     } else {
         // adhesion (controller:284-310): forces, bond terms, then deltas + drag + motion + rotation
         r = bond_index(ctx);
@@ -575,7 +577,7 @@ int step_contact(sph_ctx* ctx, float dt) {
         {
             KTimer t(ctx, "contact_forces", (double)n * (3 * 16 + 4 + 2 * 16 + 12 + 4));
             launch_contact_forces(ctx->pos, ctx->vel, ctx->omg, ctx->id, ctx->cs, act, n, ctx->grid, c, ctx->vel2,
-                                  ctx->omg2, ctx->torque, ctx->slot_of, ctx->stream);
+                                  ctx->omg2, ctx->torque, ctx->slot_of, ctx->ct_team, ctx->stream);
         }
         {
             KTimer t(ctx, "bond_terms", (double)ctx->nbonds * (8 + 4 * 16 + 2 * (4 + 3 * 16) + 64));
@@ -624,6 +626,7 @@ int sph_create(const sph_config* cfg, int32_t device, sph_ctx** out) {
     ctx->profiling = (cfg->flags & SPH_FLAG_PROFILE) != 0;
     if (const char* v = std::getenv("SPH_NB_VARIANT")) ctx->nb_variant = std::atoi(v);
     if (const char* v = std::getenv("SPH_RESORT")) ctx->resort_mode = std::atoi(v);
+    if (const char* v = std::getenv("SPH_CT_TEAM")) ctx->ct_team = std::atoi(v);
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&ctx->mv_host, sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -12,6 +12,12 @@ namespace sph {
 struct f3 { float x, y, z; };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return {x, y, z}; }
 __device__ __forceinline__ f3 operator+(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+// a + b that the compiler may not fuse with the multiply producing b: accumulations whose summands
+// reach them by different routes (registers, cross-lane shuffles) then round identically.
+__device__ __forceinline__ f3 add_exact(f3 a, f3 b) {
+#pragma clang fp contract(off)
+    return {a.x + b.x, a.y + b.y, a.z + b.z};
+}
 __device__ __forceinline__ f3 operator-(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
 __device__ __forceinline__ f3 operator*(f3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
 __device__ __forceinline__ f3 operator/(f3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
