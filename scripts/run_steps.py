@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Plain step driver for rocprofv3 runs: `python scripts/run_steps.py --config C3 --steps 20`.
-SPH_NB_VARIANT in the environment selects the neighbour-pass kernels."""
+SPH_NB_VARIANT in the environment selects the neighbour-pass kernels. `--model-r N` steps the
+reference controller instead (Model R, N particles from its InitParticles, dt = 1/144)."""
 import argparse
 import sys
 from pathlib import Path
@@ -15,8 +16,17 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model-r", type=int, default=0)
     args = ap.parse_args()
     pkg = GE.load_package()
+    if args.model_r:
+        ctl = pkg.ParticleSystemController(particleCount=args.model_r)
+        ctl.Start()
+        ctl.context.step(1 / 144, args.warmup)
+        ctl.context.step(1 / 144, args.steps)
+        ctl.context.synchronize()
+        ctl.OnDestroy()
+        return
     sim = pkg.SPHSim.from_config(args.config)
     sim.step(args.warmup)
     sim.step(args.steps)

@@ -64,6 +64,12 @@ __device__ __forceinline__ uint32_t cell_key(const GridDesc& g, float x, float y
     return ((uint32_t)cx * (uint32_t)g.gy + (uint32_t)cy) * (uint32_t)g.gz + (uint32_t)cz;
 }
 
+// slab: a particle outside the held columns (already sent away) gets key ncells: it sorts last
+__device__ __forceinline__ uint32_t window_key(const GridDesc& g, float x, float y, float z) {
+    const int32_t c = cell_coord(x, g.ox, g.inv_cell, g.gx_all) - g.cx0;
+    return (c < 0 || c >= g.gx) ? g.ncells : cell_key(g, x, y, z);
+}
+
 // One of the 9 neighbour rows of a Model S particle (SPEC_SPH.md §0): the z sub-cell window
 // [zlo, zhi] of row (cx+dx, cy+dy) that can hold a particle within 2h, or false when the
 // row's column is ≥ 2h away in xy. fx, fy: the particle's position inside its cell, in [0,1].
@@ -165,10 +171,40 @@ struct ResortScratch {
     uint32_t *mx, *mos;              // movers by slot: slot, old key
     uint32_t cap;
 };
-void launch_resort(const uint32_t* sk, uint32_t* cs, uint32_t ncells, int32_t n, const float4* pos,
-                   const float4* vel, const int32_t* id, const uint32_t* keys, const uint32_t* count,
+// The slot array the re-sort reads, slot x in [0, n). Single domain: pos/vel/id/sk[x]. Slab step:
+// the assembled [from left | own | from right] without copying it: x < nl is left record rl[x],
+// x >= nre is right record rr[x - nre] (32-B halo records, old keys in skr[x]), and the own block
+// is pos/vel/id/sk[x + o_off] (its slots in the previous sorted array).
+struct AsmSrc {
+    const float4* pos;
+    const float4* vel;
+    const int32_t* id;
+    const uint32_t* sk;
+    int32_t o_off;
+    const float4* rl;
+    const float4* rr;
+    const uint32_t* skr;
+    int32_t nl, nre;
+};
+inline AsmSrc asm_plain(const float4* pos, const float4* vel, const int32_t* id, const uint32_t* sk, int32_t n) {
+    return AsmSrc{pos, vel, id, sk, 0, nullptr, nullptr, nullptr, 0, n};
+}
+// the slab step's assembled slots: new keys (window sentinel) into keys, the halo records' old keys
+// (moved into this window, clamped) into skr_out (= src.skr), and every slot whose key changed
+// appended to the sink (its counter must be zero)
+void launch_slab_keys(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base, uint32_t* keys, uint32_t* skr_out,
+                      MoverSink sink, hipStream_t s);
+// cell-start values to pick once the table is final: out[t] = cs[idx[t]] (device), and the same
+// into out_host (mapped pinned memory) when given; m = 0: none
+struct CsPick {
+    int32_t idx[8];
+    int32_t m;
+    uint32_t* out;
+    uint32_t* out_host;
+};
+void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* keys, const uint32_t* count,
                    uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,
-                   uint32_t* sk_o, hipStream_t s);
+                   uint32_t* sk_o, hipStream_t s, CsPick pick = CsPick{{0}, 0, nullptr, nullptr});
 
 // grid / data movement (grid.hip)
 // window_sentinel (slab): a particle outside the held columns gets key ncells (sorts last)
@@ -222,13 +258,17 @@ void launch_slab_count(const uint32_t* keys, int32_t b, int32_t e, uint32_t gyz,
                        int32_t col_ge, uint32_t* blk /*[2][nblk]*/, uint32_t* totals /*[2]*/,
                        hipStream_t s,
                        int64_t* totals64 = nullptr);
+// records carry the old sorted key as a global key (sk + key_base; sk null: none, see slab.hip)
 void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
-                      int32_t b, int32_t e, uint32_t gyz, int32_t side, int32_t col_le, int32_t col_ge,
-                      const uint32_t* blk, float4* out, hipStream_t s);
-void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, int32_t* id,
-                        hipStream_t s);
+                      const uint32_t* sk, uint32_t key_base, int32_t b, int32_t e, uint32_t gyz, int32_t side,
+                      int32_t col_le, int32_t col_ge, const uint32_t* blk, float4* out, hipStream_t s);
+void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, int32_t* id, hipStream_t s);
+// cell starts of the assembled old keys, in place from the previous table (ncells + 2 entries)
+void launch_slab_cs_old(uint32_t* cs, uint32_t ncells, uint32_t gyz, uint32_t gx, bool has_left, bool has_right,
+                        int32_t shift, const uint32_t* sk, int32_t nl, int32_t no, int32_t nr, hipStream_t s);
 void launch_column_starts(const uint32_t* cs, uint32_t gyz, int32_t c0, int32_t m, uint32_t* out, hipStream_t s);
-void launch_pick(const uint32_t* cs, const int32_t* idx, int32_t m, uint32_t* out, hipStream_t s);
+void launch_pick(const uint32_t* cs, const int32_t* idx, int32_t m, uint32_t* out, hipStream_t s,
+                 uint32_t* out_host = nullptr);
 // owned slots [o0, o0+n) -> records of 8 floats (x,y,z,u,v,w,id-bits,ρ)
 void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, const float2* rp,
                        int32_t o0, int32_t n, float* out, hipStream_t s);

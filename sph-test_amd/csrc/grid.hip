@@ -23,12 +23,8 @@ __global__ __launch_bounds__(BLK) void k_keys(const float4* __restrict__ pos, in
     const int32_t i = blockIdx.x * BLK + threadIdx.x;
     if (i >= n) return;
     const float4 p = pos[i];
-    uint32_t k = cell_key(g, p.x, p.y, p.z);
+    uint32_t k = window_sentinel ? window_key(g, p.x, p.y, p.z) : cell_key(g, p.x, p.y, p.z);
     if (id != nullptr && id[i] >= n_active_id) k = g.ncells;   // inactive: sorts last
-    if (window_sentinel) {   // slab: outside the held columns (already sent away): sorts last
-        const int32_t c = cell_coord(p.x, g.ox, g.inv_cell, g.gx_all) - g.cx0;
-        if (c < 0 || c >= g.gx) k = g.ncells;
-    }
     keys[i] = k;
 }
 

@@ -35,6 +35,27 @@ constexpr int MV_RANK_GRID = 2048;
 
 static __device__ __forceinline__ uint64_t comp(uint32_t key, uint32_t idx) { return (uint64_t)key << 32 | idx; }
 
+static __device__ __forceinline__ bool asm_rec(const AsmSrc& a, int32_t x) { return x < a.nl || x >= a.nre; }
+
+static __device__ __forceinline__ uint32_t asm_sk(const AsmSrc& a, int32_t x) {
+    return asm_rec(a, x) ? a.skr[x] : a.sk[x + a.o_off];
+}
+
+// a halo record reads as the slab assemble's unpack wrote it: (x, y, z, 0), (u, v, w, 0), id
+static __device__ __forceinline__ void asm_load(const AsmSrc& a, int32_t x, float4& p, float4& v, int32_t& id) {
+    if (asm_rec(a, x)) {
+        const float4* r = x < a.nl ? a.rl + 2 * (size_t)x : a.rr + 2 * (size_t)(x - a.nre);
+        const float4 r0 = r[0], r1 = r[1];
+        p = make_float4(r0.x, r0.y, r0.z, 0.f);
+        v = make_float4(r1.x, r1.y, r1.z, 0.f);
+        id = __float_as_int(r0.w);
+    } else {
+        p = a.pos[x + a.o_off];
+        v = a.vel[x + a.o_off];
+        id = a.id[x + a.o_off];
+    }
+}
+
 // first position in sorted a[0, n) with a[pos] >= v
 template <typename T>
 static __device__ __forceinline__ uint32_t lower_bound(const T* __restrict__ a, uint32_t n, T v) {
@@ -120,11 +141,9 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
 }
 
 __global__ __launch_bounds__(MV_BLK) void k_mv_place(const uint32_t* __restrict__ mtotal,
-                                                     const uint32_t* __restrict__ cs_old, ResortScratch w,
-                                                     const float4* __restrict__ pos, const float4* __restrict__ vel,
-                                                     const int32_t* __restrict__ id, float4* __restrict__ pos_o,
-                                                     float4* __restrict__ vel_o, int32_t* __restrict__ id_o,
-                                                     uint32_t* __restrict__ sk_o) {
+                                                     const uint32_t* __restrict__ cs_old, ResortScratch w, AsmSrc src,
+                                                     float4* __restrict__ pos_o, float4* __restrict__ vel_o,
+                                                     int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o) {
     const uint32_t m = *mtotal;
     for (uint32_t r = blockIdx.x * MV_BLK + threadIdx.x; r < m; r += gridDim.x * MV_BLK) {
         const uint32_t x = w.mi[r], k = w.mk[r];
@@ -132,9 +151,12 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_place(const uint32_t* __restrict_
         const uint32_t q = x < c0 ? c0 : (x > c1 ? c1 : x);
         const uint32_t rk = w.rank[r], ri = w.rank[w.cap + r], aq = w.rank[2 * w.cap + r];
         const uint32_t dst = (q - aq) + rk;
-        pos_o[dst] = pos[x];
-        vel_o[dst] = vel[x];
-        id_o[dst] = id[x];
+        float4 p, v;
+        int32_t pid;
+        asm_load(src, (int32_t)x, p, v, pid);
+        pos_o[dst] = p;
+        vel_o[dst] = v;
+        id_o[dst] = pid;
         sk_o[dst] = k;
         w.ms[rk] = comp(k, x);
         w.mx[ri] = x;
@@ -147,8 +169,9 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_place(const uint32_t* __restrict_
 // Runs as extra workgroups of k_mv_merge (it needs only k_mv_place's tables), beside the scatter.
 constexpr int MV_CS_CELLS = 4 * MV_BLK;
 
+// Picks falling in this workgroup's cells are read back once its cells are final.
 static __device__ void mv_cell_start(uint32_t* __restrict__ cs, uint32_t ncells, uint32_t m, const ResortScratch& w,
-                                     uint32_t blk, uint32_t* b) {
+                                     uint32_t blk, uint32_t* b, const CsPick& pick) {
     const uint32_t k0 = blk * MV_CS_CELLS, k1 = k0 + MV_CS_CELLS;
     const int wv = threadIdx.x >> 6;
     const uint32_t p = wv < 2 ? wave_lower_bound(w.ms, m, comp(wv == 0 ? k0 : k1, 0u))
@@ -156,29 +179,39 @@ static __device__ void mv_cell_start(uint32_t* __restrict__ cs, uint32_t ncells,
     if (lane_id() == 0) b[wv] = p;
     __syncthreads();
     const uint32_t nlo = b[0], nhi = b[1], olo = b[2], ohi = b[3];
-    if (nlo == olo && nhi == nlo && ohi == olo) return;
+    if (!(nlo == olo && nhi == nlo && ohi == olo)) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t k = k0 + j * MV_BLK + threadIdx.x;
-        if (k > ncells) break;
-        const uint32_t cn = nlo + lower_bound(w.ms + nlo, nhi - nlo, comp(k, 0u));
-        const uint32_t co = olo + lower_bound(w.mos + olo, ohi - olo, k);
-        cs[k] += cn - co;
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t k = k0 + j * MV_BLK + threadIdx.x;
+            if (k > ncells) break;
+            const uint32_t cn = nlo + lower_bound(w.ms + nlo, nhi - nlo, comp(k, 0u));
+            const uint32_t co = olo + lower_bound(w.mos + olo, ohi - olo, k);
+            cs[k] += cn - co;
+        }
+    }
+    if (pick.m == 0) return;
+    __syncthreads();   // this workgroup's cell updates are visible to all its lanes
+    const int t = threadIdx.x;
+    if (t < pick.m) {
+        const uint32_t k = (uint32_t)pick.idx[t];
+        if (k >= k0 && k < k1 && k <= ncells) {
+            const uint32_t v = cs[k];
+            pick.out[t] = v;
+            if (pick.out_host) pick.out_host[t] = v;
+        }
     }
 }
 
-__global__ __launch_bounds__(MV_BLK) void k_mv_merge(const uint32_t* __restrict__ keys,
-                                                     const uint32_t* __restrict__ sk, int32_t n,
+__global__ __launch_bounds__(MV_BLK) void k_mv_merge(const uint32_t* __restrict__ keys, AsmSrc src, int32_t n,
                                                      const uint32_t* __restrict__ mtotal, ResortScratch w,
-                                                     const float4* __restrict__ pos, const float4* __restrict__ vel,
-                                                     const int32_t* __restrict__ id, float4* __restrict__ pos_o,
+                                                     float4* __restrict__ pos_o,
                                                      float4* __restrict__ vel_o, int32_t* __restrict__ id_o,
                                                      uint32_t* __restrict__ sk_o, int32_t nb, uint32_t* __restrict__ cs,
-                                                     uint32_t ncells) {
+                                                     uint32_t ncells, CsPick pick) {
     __shared__ uint32_t wc[MV_BLK / 64];
     __shared__ uint32_t b[4];
     if ((int32_t)blockIdx.x >= nb) {   // the cell-start workgroups
-        mv_cell_start(cs, ncells, *mtotal, w, blockIdx.x - nb, b);
+        mv_cell_start(cs, ncells, *mtotal, w, blockIdx.x - nb, b, pick);
         return;
     }
     const int32_t i0 = xcd_block(blockIdx.x, nb) * MV_BLK;
@@ -192,11 +225,11 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(const uint32_t* __restrict_
         const uint32_t p = wave_lower_bound(w.mx, m, (uint32_t)i0);
         if (lane_id() == 0) b[0] = p;
     } else if (wv < 3) {
-        const uint64_t v = wv == 1 ? comp(sk[i0], (uint32_t)i0) : comp(sk[ilast], (uint32_t)ilast) + 1;
+        const uint64_t v = wv == 1 ? comp(asm_sk(src, i0), (uint32_t)i0) : comp(asm_sk(src, ilast), (uint32_t)ilast) + 1;
         const uint32_t p = wave_lower_bound(w.ms, m, v);
         if (lane_id() == 0) b[wv] = p;
     }
-    const uint32_t ko = i < n ? sk[i] : 0u;
+    const uint32_t ko = i < n ? asm_sk(src, i) : 0u;
     const bool stay = i < n && keys[i] == ko;
     __syncthreads();
     const uint32_t a = movers_before(i < n && !stay, b[0], wc);
@@ -204,24 +237,111 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(const uint32_t* __restrict_
     const uint32_t lo = b[1], hi = b[2];
     const uint32_t below = lo + lower_bound(w.ms + lo, hi - lo, comp(ko, (uint32_t)i));
     const uint32_t dst = ((uint32_t)i - a) + below;
-    pos_o[dst] = pos[i];
-    vel_o[dst] = vel[i];
-    id_o[dst] = id[i];
+    float4 p, v;
+    int32_t pid;
+    asm_load(src, i, p, v, pid);
+    pos_o[dst] = p;
+    vel_o[dst] = v;
+    id_o[dst] = pid;
     sk_o[dst] = ko;
 }
 
-void launch_resort(const uint32_t* sk, uint32_t* cs, uint32_t ncells, int32_t n, const float4* pos,
-                   const float4* vel, const int32_t* id, const uint32_t* keys, const uint32_t* count,
+// The slab step's keys and movers in one pass over the assembled slots [left | own | right] (the
+// force pass appends the movers in the single-domain path). New keys use the window sentinel (as
+// k_keys); a halo record's old key is its global old key moved into this window and clamped into
+// [0, ncells - 1]: the left neighbour's columns lie below this window's owned ones and the right
+// neighbour's above, so clamping keeps the assembled old keys sorted. A record without an old key
+// takes its side's bound (it then almost surely moves). The records' old keys go to skr_out, which
+// is src.skr. A workgroup takes MV_DET slots, counts its movers and reserves their entries with ONE
+// atomic: per-wave atomics on one counter serialise (~4,000 waves with a mover at C3).
+constexpr int MV_DET_PER = 4;
+constexpr int MV_DET = MV_BLK * MV_DET_PER;
+constexpr uint32_t REC_NO_KEY = 0xffffffffu;   // slab.hip SL_NO_KEY
+
+__global__ __launch_bounds__(MV_BLK) void k_slab_keys(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base,
+                                                      uint32_t* __restrict__ keys, uint32_t* __restrict__ skr_out,
+                                                      MoverSink sink) {
+    __shared__ uint32_t wsum[MV_BLK / 64];
+    __shared__ uint32_t base_s;
+    const int32_t x0 = blockIdx.x * MV_DET + threadIdx.x;
+    uint32_t kn[MV_DET_PER], ko[MV_DET_PER];
+    // loads first, stores after: the compiler cannot move a load above a store it may alias, and
+    // interleaving them would serialise the four round trips
+#pragma unroll
+    for (int j = 0; j < MV_DET_PER; ++j) {
+        const int32_t x = min(x0 + j * MV_BLK, n - 1);
+        if (asm_rec(src, x)) {
+            const bool left = x < src.nl;
+            const float4* r = left ? src.rl + 2 * (size_t)x : src.rr + 2 * (size_t)(x - src.nre);
+            const float4 r0 = r[0];
+            const uint32_t og = __float_as_uint(r[1].w);
+            kn[j] = window_key(g, r0.x, r0.y, r0.z);
+            if (og == REC_NO_KEY) ko[j] = left ? 0u : g.ncells - 1u;
+            else ko[j] = og < key_base ? 0u : min(og - key_base, g.ncells - 1u);
+        } else {
+            const float4 p = src.pos[x + src.o_off];
+            kn[j] = window_key(g, p.x, p.y, p.z);
+            ko[j] = src.sk[x + src.o_off];
+        }
+    }
+    uint32_t mine = 0;   // bit j: slot x0 + j * MV_BLK moved
+#pragma unroll
+    for (int j = 0; j < MV_DET_PER; ++j) {
+        const int32_t x = x0 + j * MV_BLK;
+        if (x >= n) continue;
+        keys[x] = kn[j];
+        if (asm_rec(src, x)) skr_out[x] = ko[j];
+        if (kn[j] != ko[j]) mine |= 1u << j;
+    }
+    const uint32_t c = (uint32_t)__popc(mine);
+    // exclusive prefix of c over the workgroup
+    uint32_t incl = c;
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
+        if (lane >= (uint32_t)o) incl += t;
+    }
+    const int wv = threadIdx.x >> 6;
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < MV_BLK / 64; ++k) {
+        off += k < wv ? wsum[k] : 0u;
+        tot += wsum[k];
+    }
+    if (threadIdx.x == 0) base_s = tot ? atomicAdd(sink.count, tot) : 0u;
+    __syncthreads();
+    uint32_t r = base_s + off + incl - c;
+#pragma unroll
+    for (int j = 0; j < MV_DET_PER; ++j) {
+        if (!(mine >> j & 1u)) continue;
+        sink.mi[r] = (uint32_t)(x0 + j * MV_BLK);
+        sink.mk[r] = kn[j];
+        sink.mo[r] = ko[j];
+        sink.rank[r] = 0u;
+        sink.rank[sink.cap + r] = 0u;
+        sink.rank[2 * sink.cap + r] = 0u;
+        ++r;
+    }
+}
+
+void launch_slab_keys(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base, uint32_t* keys, uint32_t* skr_out,
+                      MoverSink sink, hipStream_t s) {
+    if (n > 0) k_slab_keys<<<(n + MV_DET - 1) / MV_DET, MV_BLK, 0, s>>>(src, n, g, key_base, keys, skr_out, sink);
+}
+
+void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* keys, const uint32_t* count,
                    uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,
-                   uint32_t* sk_o, hipStream_t s) {
+                   uint32_t* sk_o, hipStream_t s, CsPick pick) {
     if (n <= 0) return;
     const int32_t nb = (n + MV_BLK - 1) / MV_BLK;
     k_mv_rank<<<MV_RANK_GRID, MV_BLK, 0, s>>>(count, count_other, cs, w);
-    k_mv_place<<<std::min(nb, 1024), MV_BLK, 0, s>>>(count, cs, w, pos, vel, id, pos_o, vel_o, id_o, sk_o);
+    k_mv_place<<<std::min(nb, 1024), MV_BLK, 0, s>>>(count, cs, w, src, pos_o, vel_o, id_o, sk_o);
     // + the cell-start update, after every reader of cs_old (k_mv_rank, k_mv_place)
     const int32_t ncs = (int32_t)((ncells + MV_CS_CELLS) / MV_CS_CELLS);
-    k_mv_merge<<<nb + ncs, MV_BLK, 0, s>>>(keys, sk, n, count, w, pos, vel, id, pos_o, vel_o, id_o, sk_o, nb, cs,
-                                           ncells);
+    k_mv_merge<<<nb + ncs, MV_BLK, 0, s>>>(keys, src, n, count, w, pos_o, vel_o, id_o, sk_o, nb, cs, ncells, pick);
 }
 
 }  // namespace sph

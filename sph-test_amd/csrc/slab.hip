@@ -36,17 +36,38 @@ __device__ __forceinline__ uint32_t block_ballot_count(bool pred, uint32_t* wcnt
     return tot;
 }
 
+// Send lists: each workgroup of the count / pack pair takes SL_SEND consecutive owned slots, so the
+// single-workgroup scan between them sees few entries (one pass per side at C3).
+constexpr int SL_PER = 16;
+constexpr int SL_SEND = SL_BLK * SL_PER;
+
+int32_t slab_send_blocks(int32_t b, int32_t e) { return e > b ? (e - b + SL_SEND - 1) / SL_SEND : 1; }
+
 __global__ __launch_bounds__(SL_BLK) void k_slab_count(const uint32_t* __restrict__ keys, int32_t b, int32_t e,
                                                        uint32_t gyz, int32_t col_le, int32_t col_ge,
                                                        uint32_t* __restrict__ blk, int32_t nblk) {
     __shared__ uint32_t wl[SL_WAVES], wr[SL_WAVES];
-    const int32_t i = b + blockIdx.x * SL_BLK + threadIdx.x;
-    const bool in = i < e;
-    const int32_t col = in ? (int32_t)(keys[i] / gyz) : 0;
-    uint32_t bl, br;
-    const uint32_t tl = block_ballot_count(in && col <= col_le, wl, bl);
-    const uint32_t tr = block_ballot_count(in && col >= col_ge, wr, br);
+    uint32_t cl = 0, cr = 0;
+    const int32_t i0 = b + blockIdx.x * SL_SEND + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < SL_PER && e > b; ++j) {   // clamped index: every load issues before any is used
+        const int32_t i = i0 + j * SL_BLK;
+        const int32_t col = (int32_t)(keys[min(i, e - 1)] / gyz);
+        cl += i < e && col <= col_le;
+        cr += i < e && col >= col_ge;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        cl += (uint32_t)__shfl_xor((int)cl, o, 64);
+        cr += (uint32_t)__shfl_xor((int)cr, o, 64);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { wl[w] = cl; wr[w] = cr; }
+    __syncthreads();
     if (threadIdx.x == 0) {
+        uint32_t tl = 0, tr = 0;
+#pragma unroll
+        for (int k = 0; k < SL_WAVES; ++k) { tl += wl[k]; tr += wr[k]; }
         blk[blockIdx.x] = tl;
         blk[nblk + blockIdx.x] = tr;
     }
@@ -91,25 +112,40 @@ __global__ __launch_bounds__(SL_SCAN) void k_slab_scan(uint32_t* __restrict__ bl
     }
 }
 
+// A record is (x, y, z, id) (u, v, w, old key): the old key is the particle's sorted key before this
+// step's drift, as a GLOBAL key (sender's local key + its window's first key), or SL_NO_KEY when
+// the sender holds no valid sorted keys. The receiver's incremental re-sort uses it.
+constexpr uint32_t SL_NO_KEY = 0xffffffffu;
+
 __global__ __launch_bounds__(SL_BLK) void k_slab_pack(const uint32_t* __restrict__ keys,
                                                       const float4* __restrict__ pos,
                                                       const float4* __restrict__ vel,
-                                                      const int32_t* __restrict__ id, int32_t b, int32_t e,
-                                                      uint32_t gyz, int32_t side, int32_t col_le, int32_t col_ge,
+                                                      const int32_t* __restrict__ id,
+                                                      const uint32_t* __restrict__ sk, uint32_t key_base,
+                                                      int32_t b, int32_t e, uint32_t gyz, int32_t side,
+                                                      int32_t col_le, int32_t col_ge,
                                                       const uint32_t* __restrict__ blk, int32_t nblk,
                                                       float4* __restrict__ out) {
     __shared__ uint32_t wc[SL_WAVES];
-    const int32_t i = b + blockIdx.x * SL_BLK + threadIdx.x;
-    const bool in = i < e;
-    const int32_t col = in ? (int32_t)(keys[i] / gyz) : 0;
-    const bool pred = in && (side == 0 ? col <= col_le : col >= col_ge);
-    uint32_t wave_base;
-    block_ballot_count(pred, wc, wave_base);
-    if (!pred) return;
-    const uint32_t r = blk[side * nblk + blockIdx.x] + wave_base + lane_prefix(__ballot(pred));
-    const float4 p = pos[i], v = vel[i];
-    out[2 * (size_t)r] = make_float4(p.x, p.y, p.z, __int_as_float(id[i]));
-    out[2 * (size_t)r + 1] = make_float4(v.x, v.y, v.z, 0.f);
+    uint32_t run = blk[side * nblk + blockIdx.x];
+    for (int j = 0; j < SL_PER; ++j) {   // sub-chunks in slot order: the records keep slot order
+        const int32_t i = b + (blockIdx.x * SL_PER + j) * SL_BLK + threadIdx.x;
+        const bool in = i < e;
+        const int32_t col = in ? (int32_t)(keys[i] / gyz) : 0;
+        const bool pred = in && (side == 0 ? col <= col_le : col >= col_ge);
+        uint32_t wave_base;
+        const uint32_t tot = block_ballot_count(pred, wc, wave_base);
+        const uint64_t m = __ballot(pred);
+        if (pred) {
+            const uint32_t r = run + wave_base + lane_prefix(m);
+            const float4 p = pos[i], v = vel[i];
+            const uint32_t ok = sk ? sk[i] + key_base : SL_NO_KEY;
+            out[2 * (size_t)r] = make_float4(p.x, p.y, p.z, __int_as_float(id[i]));
+            out[2 * (size_t)r + 1] = make_float4(v.x, v.y, v.z, __uint_as_float(ok));
+        }
+        run += tot;
+        __syncthreads();   // wc is rewritten by the next sub-chunk
+    }
 }
 
 __global__ __launch_bounds__(SL_BLK) void k_slab_unpack(const float4* __restrict__ rec, int32_t n,
@@ -121,6 +157,40 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_unpack(const float4* __restrict
     pos[i] = make_float4(a.x, a.y, a.z, 0.f);
     vel[i] = make_float4(v.x, v.y, v.z, 0.f);
     id[i] = __float_as_int(a.w);
+}
+
+// The cell-start table of the assembled old keys [left | own | right] (sk), for the incremental
+// re-sort, made from the previous step's table in place. Owned columns: the own block kept its
+// order, so cs[k] shifts by nl − o0 (o0: the previous owned start). Halo columns: lower bounds in
+// the left / right blocks. cs[ncells] = cs[ncells + 1] = n.
+__global__ __launch_bounds__(SL_BLK) void k_slab_cs_old(uint32_t* __restrict__ cs, uint32_t ncells, uint32_t gyz,
+                                                        uint32_t gx, int32_t has_left, int32_t has_right,
+                                                        int32_t shift, const uint32_t* __restrict__ sk,
+                                                        int32_t nl, int32_t no, int32_t nr) {
+    const uint32_t k = blockIdx.x * SL_BLK + threadIdx.x;
+    if (k > ncells + 1u) return;
+    const uint32_t n = (uint32_t)(nl + no + nr);
+    if (k >= ncells) {
+        cs[k] = n;
+        return;
+    }
+    const uint32_t col = k / gyz;
+    uint32_t lo, len, off;
+    if (has_left && col == 0u) {
+        lo = 0u; len = (uint32_t)nl; off = 0u;
+    } else if (has_right && col == gx - 1u) {
+        lo = (uint32_t)(nl + no); len = (uint32_t)nr; off = lo;
+    } else {
+        if (shift != 0) cs[k] = (uint32_t)((int32_t)cs[k] + shift);
+        return;
+    }
+    uint32_t a = 0u, b = len;   // lower bound of k in sk[lo, lo + len)
+    while (a < b) {
+        const uint32_t mid = (a + b) >> 1;
+        if (sk[lo + mid] < k) a = mid + 1u;
+        else b = mid;
+    }
+    cs[k] = off + a;
 }
 
 // ---- init-time selection of owned columns (global grid in `g`)
@@ -164,9 +234,16 @@ struct Pick10 {
     int32_t idx[10];
 };
 
-__global__ void k_pick(const uint32_t* __restrict__ cs, Pick10 p, int32_t m, uint32_t* __restrict__ out) {
+// out: device copy (kernels read it); out_host (optional): mapped pinned host memory, written
+// directly so no copy-back is queued (the host waits on an event after this kernel)
+__global__ void k_pick(const uint32_t* __restrict__ cs, Pick10 p, int32_t m, uint32_t* __restrict__ out,
+                       uint32_t* __restrict__ out_host) {
     const int t = threadIdx.x;
-    if (t < m) out[t] = cs[p.idx[t]];
+    if (t < m) {
+        const uint32_t v = cs[p.idx[t]];
+        out[t] = v;
+        if (out_host) out_host[t] = v;
+    }
 }
 
 __global__ __launch_bounds__(SL_BLK) void k_pack_owned(const float4* __restrict__ pos, const float4* __restrict__ vel,
@@ -193,10 +270,11 @@ void launch_column_starts(const uint32_t* cs, uint32_t gyz, int32_t c0, int32_t 
     if (m > 0) k_column_starts<<<(m + SL_BLK - 1) / SL_BLK, SL_BLK, 0, s>>>(cs, gyz, c0, m, out);
 }
 
-void launch_pick(const uint32_t* cs, const int32_t* idx, int32_t m, uint32_t* out, hipStream_t s) {
+void launch_pick(const uint32_t* cs, const int32_t* idx, int32_t m, uint32_t* out, hipStream_t s,
+                 uint32_t* out_host) {
     Pick10 p{};
     for (int k = 0; k < m && k < 10; ++k) p.idx[k] = idx[k];
-    k_pick<<<1, 64, 0, s>>>(cs, p, m, out);
+    k_pick<<<1, 64, 0, s>>>(cs, p, m, out, out_host);
 }
 
 void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, const float2* rp, int32_t o0,
@@ -206,20 +284,29 @@ void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, 
 
 void launch_slab_count(const uint32_t* keys, int32_t b, int32_t e, uint32_t gyz, int32_t col_le, int32_t col_ge,
                        uint32_t* blk, uint32_t* totals, hipStream_t s, int64_t* totals64) {
-    const int32_t nb = slab_compact_blocks(b, e);
+    const int32_t nb = slab_send_blocks(b, e);
     k_slab_count<<<nb, SL_BLK, 0, s>>>(keys, b, e, gyz, col_le, col_ge, blk, nb);
     k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb, totals, totals64);
 }
 
-void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id, int32_t b,
-                      int32_t e, uint32_t gyz, int32_t side, int32_t col_le, int32_t col_ge, const uint32_t* blk,
-                      float4* out, hipStream_t s) {
-    const int32_t nb = slab_compact_blocks(b, e);
-    if (e > b) k_slab_pack<<<nb, SL_BLK, 0, s>>>(keys, pos, vel, id, b, e, gyz, side, col_le, col_ge, blk, nb, out);
+void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
+                      const uint32_t* sk, uint32_t key_base, int32_t b, int32_t e, uint32_t gyz, int32_t side,
+                      int32_t col_le, int32_t col_ge, const uint32_t* blk, float4* out, hipStream_t s) {
+    const int32_t nb = slab_send_blocks(b, e);
+    if (e > b)
+        k_slab_pack<<<nb, SL_BLK, 0, s>>>(keys, pos, vel, id, sk, key_base, b, e, gyz, side, col_le, col_ge, blk, nb,
+                                          out);
 }
 
 void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, int32_t* id, hipStream_t s) {
     if (n > 0) k_slab_unpack<<<(n + SL_BLK - 1) / SL_BLK, SL_BLK, 0, s>>>(rec, n, pos, vel, id);
+}
+
+void launch_slab_cs_old(uint32_t* cs, uint32_t ncells, uint32_t gyz, uint32_t gx, bool has_left, bool has_right,
+                        int32_t shift, const uint32_t* sk, int32_t nl, int32_t no, int32_t nr, hipStream_t s) {
+    const uint32_t m = ncells + 2u;
+    k_slab_cs_old<<<(m + SL_BLK - 1) / SL_BLK, SL_BLK, 0, s>>>(cs, ncells, gyz, gx, has_left ? 1 : 0,
+                                                               has_right ? 1 : 0, shift, sk, nl, no, nr);
 }
 
 void launch_slab_select_columns(const float4* pos, const float4* vel, const int32_t* id, int32_t n, GridDesc g,

@@ -221,7 +221,7 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
 }
 
 int ensure_cells(sph_ctx* ctx) {
-    const uint32_t need = ctx->grid.ncells + 1;
+    const uint32_t need = ctx->grid.ncells + 2;   // + the slab re-sort's cs_old[ncells + 1]
     if (need > ctx->cs_cap) {
         int r = dalloc(ctx, &ctx->cs, need);
         if (r != SPH_OK) return r;
@@ -448,9 +448,9 @@ int sort_wcsph(sph_ctx* ctx) {
         {
             KTimer t(ctx, "resort", (double)n * (2 * 4 + 2 * 36));
             const int used = ctx->mv_par;
-            launch_resort(ctx->sk_cur, ctx->cs, ctx->grid.ncells, n, ctx->pos, ctx->vel, ctx->id, ctx->keys,
-                          ctx->mv_count + used, ctx->mv_count + (1 - used), resort_scratch(ctx), ctx->pos2,
-                          ctx->vel2, ctx->id2, ctx->sk_next, ctx->stream);
+            launch_resort(asm_plain(ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, n), ctx->cs, ctx->grid.ncells, n,
+                          ctx->keys, ctx->mv_count + used, ctx->mv_count + (1 - used), resort_scratch(ctx),
+                          ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, ctx->stream);
             ctx->mv_par = 1 - used;
         }
         swap_sv(ctx);
@@ -1511,12 +1511,22 @@ int sph_slab_pack_send(sph_ctx* ctx, int32_t side, void* dev_records, int32_t ca
     const int32_t col_le = ctx->has_left ? ctx->sl.cx_lo - ctx->grid.cx0 : -1;
     const int32_t col_ge = ctx->has_right ? ctx->sl.cx_hi - 1 - ctx->grid.cx0 : 0x7fffffff;
     KTimer t(ctx, "slab_pack", 36.0 * ctx->send_counts[side]);
-    launch_slab_pack(ctx->keys, ctx->pos, ctx->vel, ctx->id, ctx->o0, ctx->o1, gyz, side, col_le, col_ge, ctx->sblk,
+    // old sorted keys travel with the records (global keys) for the receiver's incremental re-sort
+    launch_slab_pack(ctx->keys, ctx->pos, ctx->vel, ctx->id, ctx->sk_valid ? ctx->sk_cur : nullptr,
+                     (uint32_t)ctx->grid.cx0 * gyz, ctx->o0, ctx->o1, gyz, side, col_le, col_ge, ctx->sblk,
                      (float4*)dev_records, ctx->stream);
     HIPCHK(hipGetLastError());
     return SPH_OK;
 }
 
+// The slab step's sort. [from left | own | from right] is the canonical pre-sort order: both ranks
+// sharing a column then break key ties identically (SPEC_SPH.md §3). Its OLD keys are sorted: the
+// own block keeps the previous sorted order, and the neighbours' records carry their old keys, all
+// below (left) or above (right) the owned columns. So the incremental re-sort applies to the whole
+// assembled array, with movers = every slot whose key changed (records included), and gives the
+// same permutation as the full radix sort (tests/test_gpu_slab.py compares the two bit for bit).
+// The full radix sort runs after any window change (no valid old keys) and while the last seen
+// mover count exceeds resort_limit.
 int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void* dev_right, int32_t nr) {
     if (!ctx || nl < 0 || nr < 0 || (nl > 0 && !dev_left) || (nr > 0 && !dev_right)) return SPH_ERR_INVALID;
     if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
@@ -1525,49 +1535,83 @@ int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void
     const int64_t n = (int64_t)nl + no + nr;
     if (n > ctx->capacity) return fail(ctx, SPH_ERR_CAPACITY, "slab needs %lld slots > capacity %d", (long long)n, ctx->capacity);
     hipStream_t s = ctx->stream;
-    // canonical pre-sort order [from left | own | from right]: both ranks sharing a column then
-    // break key ties identically (SPEC_SPH.md §3)
-    {
-        KTimer t(ctx, "slab_assemble", 64.0 * (double)n);
-        launch_slab_unpack((const float4*)dev_left, nl, ctx->pos2, ctx->vel2, ctx->id2, s);
-        if (no > 0) {
-            HIPCHK(hipMemcpyAsync(ctx->pos2 + nl, ctx->pos + ctx->o0, (size_t)no * 16, hipMemcpyDeviceToDevice, s));
-            HIPCHK(hipMemcpyAsync(ctx->vel2 + nl, ctx->vel + ctx->o0, (size_t)no * 16, hipMemcpyDeviceToDevice, s));
-            HIPCHK(hipMemcpyAsync(ctx->id2 + nl, ctx->id + ctx->o0, (size_t)no * 4, hipMemcpyDeviceToDevice, s));
-        }
-        launch_slab_unpack((const float4*)dev_right, nr, ctx->pos2 + nl + no, ctx->vel2 + nl + no, ctx->id2 + nl + no, s);
-        // own particles outside the held columns were sent away this step: they sort last and drop
-        launch_keys(ctx->pos2, (int32_t)n, nullptr, 0, ctx->grid, ctx->keys, s, true);
-    }
-    int side;
-    {
-        const int passes = (ctx->key_bits + 7) / 8;
-        KTimer t(ctx, "radix_sort", (double)n * (20.0 * passes));
-        side = radix_sort(ctx->keys, ctx->vals, ctx->keys2, ctx->vals2, (int32_t)n, ctx->key_bits, true, ctx->hist,
-                          ctx->bin_total, s);
-    }
-    const uint32_t* sk = side ? ctx->keys2 : ctx->keys;
-    const uint32_t* perm = side ? ctx->vals2 : ctx->vals;
-    {
-        KTimer t(ctx, "reorder", (double)n * (4 + 2 * 36));
-        launch_gather_s(perm, ctx->pos2, ctx->vel2, ctx->id2, ctx->pos, ctx->vel, ctx->id, (int32_t)n, s);
-    }
-    {
-        KTimer t(ctx, "cell_start", 4.0 * (ctx->grid.ncells + 1));
-        launch_cell_start(sk, (int32_t)n, ctx->cs, ctx->grid.ncells, ctx->gaps, ctx->sdev + 8, s);
-    }
-    // ranges from the cell table at column starts: picked on the device (density reads them
-    // there) and copied back asynchronously; slab_sync_ranges waits for the copy
+    const uint32_t gyz = (uint32_t)ctx->grid.gy * (uint32_t)ctx->grid.gz;
+    const uint32_t key_base = (uint32_t)ctx->grid.cx0 * gyz;
+    const bool many = ctx->resort_mode == 1 && *(volatile uint32_t*)ctx->mv_host > resort_limit((int32_t)n);
+    // ranges from the cell table at column starts: picked on the device (density reads them there)
+    // and written to mapped pinned memory; slab_sync_ranges waits for the event after the sort
     const int32_t lc_lo = ctx->sl.cx_lo - ctx->grid.cx0, lc_hi = ctx->sl.cx_hi - ctx->grid.cx0;
     const int32_t idx[6] = {col_start(ctx, 0), col_start(ctx, lc_lo), col_start(ctx, lc_lo + 1),
                             col_start(ctx, lc_hi - 1), col_start(ctx, lc_hi), col_start(ctx, ctx->grid.gx)};
-    launch_pick(ctx->cs, idx, 6, ctx->sdev, s);
-    HIPCHK(hipMemcpyAsync(ctx->rng_host, ctx->sdev, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (ctx->resort_mode != 0 && !many && ctx->sk_valid && n > 0) {
+        // incremental: the re-sort reads [left records | own slots | right records] in place
+        const AsmSrc src{ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->o0 - nl, (const float4*)dev_left,
+                         (const float4*)dev_right, ctx->keys2, nl, nl + no};
+        const int used = ctx->mv_par;   // zeroed by the last re-sort's k_mv_rank, or by the full path
+        const MoverSink mv{ctx->keys2, ctx->mv_count + used, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_rank,
+                           (uint32_t)std::max(ctx->capacity, 1)};
+        {
+            // new keys (own particles outside the held columns were sent away: they sort last and
+            // drop), the records' old keys, and the movers
+            KTimer t(ctx, "slab_assemble", 28.0 * (double)n);
+            launch_slab_keys(src, (int32_t)n, ctx->grid, key_base, ctx->keys, ctx->keys2, mv, s);
+        }
+        KTimer t(ctx, "resort", (double)n * (2 * 4 + 2 * 36));
+        launch_slab_cs_old(ctx->cs, ctx->grid.ncells, gyz, (uint32_t)ctx->grid.gx, ctx->has_left, ctx->has_right,
+                           nl - ctx->o0, ctx->keys2, nl, no, nr, s);
+        CsPick pick{{0}, 6, ctx->sdev, ctx->rng_host};   // the ranges, read as the cell table completes
+        for (int k = 0; k < 6; ++k) pick.idx[k] = idx[k];
+        launch_resort(src, ctx->cs, ctx->grid.ncells, (int32_t)n, ctx->keys, ctx->mv_count + used,
+                      ctx->mv_count + (1 - used), resort_scratch(ctx), ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, s,
+                      pick);
+        if ((ctx->steps & 7) == 0)
+            HIPCHK(hipMemcpyAsync(ctx->mv_host, ctx->mv_count + used, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        ctx->mv_par = 1 - used;
+        swap_sv(ctx);
+        std::swap(ctx->id, ctx->id2);
+        std::swap(ctx->sk_cur, ctx->sk_next);
+    } else {
+        {
+            KTimer t(ctx, "slab_assemble", 64.0 * (double)n);
+            launch_slab_unpack((const float4*)dev_left, nl, ctx->pos2, ctx->vel2, ctx->id2, s);
+            if (no > 0) {
+                HIPCHK(hipMemcpyAsync(ctx->pos2 + nl, ctx->pos + ctx->o0, (size_t)no * 16, hipMemcpyDeviceToDevice, s));
+                HIPCHK(hipMemcpyAsync(ctx->vel2 + nl, ctx->vel + ctx->o0, (size_t)no * 16, hipMemcpyDeviceToDevice, s));
+                HIPCHK(hipMemcpyAsync(ctx->id2 + nl, ctx->id + ctx->o0, (size_t)no * 4, hipMemcpyDeviceToDevice, s));
+            }
+            launch_slab_unpack((const float4*)dev_right, nr, ctx->pos2 + nl + no, ctx->vel2 + nl + no,
+                               ctx->id2 + nl + no, s);
+            // own particles outside the held columns were sent away this step: they sort last and drop
+            launch_keys(ctx->pos2, (int32_t)n, nullptr, 0, ctx->grid, ctx->keys, s, true);
+        }
+        int side;
+        {
+            const int passes = (ctx->key_bits + 7) / 8;
+            KTimer t(ctx, "radix_sort", (double)n * (20.0 * passes));
+            side = radix_sort(ctx->keys, ctx->vals, ctx->keys2, ctx->vals2, (int32_t)n, ctx->key_bits, true, ctx->hist,
+                              ctx->bin_total, s);
+        }
+        const uint32_t* sk = side ? ctx->keys2 : ctx->keys;
+        const uint32_t* perm = side ? ctx->vals2 : ctx->vals;
+        {
+            KTimer t(ctx, "reorder", (double)n * (4 + 2 * 36));
+            launch_gather_s(perm, ctx->pos2, ctx->vel2, ctx->id2, ctx->pos, ctx->vel, ctx->id, (int32_t)n, s);
+        }
+        {
+            KTimer t(ctx, "cell_start", 4.0 * (ctx->grid.ncells + 1));
+            launch_cell_start(sk, (int32_t)n, ctx->cs, ctx->grid.ncells, ctx->gaps, ctx->sdev + 8, s);
+        }
+        // the sorted keys of the new slot order: the next step's old keys
+        if (ctx->resort_mode != 0 && n > 0)
+            HIPCHK(hipMemcpyAsync(ctx->sk_cur, sk, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemsetAsync(ctx->mv_count, 0, 2 * sizeof(uint32_t), s));
+        launch_pick(ctx->cs, idx, 6, ctx->sdev, s, ctx->rng_host);
+    }
     HIPCHK(hipEventRecord(ctx->rng_ev, s));
     ctx->rng_pending = true;
     ctx->n = (int32_t)n;
     ctx->keys_valid = false;
-    ctx->sk_valid = false;
+    ctx->sk_valid = ctx->resort_mode != 0;
     return SPH_OK;
 }
 

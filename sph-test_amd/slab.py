@@ -252,8 +252,9 @@ class SlabRunner:
         self.ranges = None
         self._owned = None
         dev = probe.device
-        self._cnt_out = torch.zeros(2, dtype=torch.int64, device=dev)
-        self._cnt_in = torch.zeros(2, dtype=torch.int64, device=dev)
+        # [sent left, sent right, received from left, received from right]
+        self._cnt_all = torch.zeros(4, dtype=torch.int64, device=dev)
+        self._cnt_out, self._cnt_in = self._cnt_all[0:2], self._cnt_all[2:4]
         self._bufs = {}
 
     # ----------------------------------------------------------------- plumbing
@@ -328,7 +329,6 @@ class SlabRunner:
             be.pack_send(0, bl, bl.shape[0])
         if self.right is not None:
             be.pack_send(1, br, br.shape[0])
-        self._cnt_in.zero_()
         sends, recvs = [], []
         if self.left is not None:
             sends.append((self._cnt_out[0:1], self.left))
@@ -338,7 +338,7 @@ class SlabRunner:
             recvs.append((self._cnt_in[1:2], self.right))
         for w in self._p2p(sends, recvs):
             w.wait()
-        nl, nr, il, ir = (int(v) for v in self.torch.cat([self._cnt_out, self._cnt_in]).cpu().tolist())
+        nl, nr, il, ir = (int(v) for v in self._cnt_all.cpu().tolist())   # one copy-back, one sync
         if self.left is None:
             nl = il = 0
         if self.right is None:

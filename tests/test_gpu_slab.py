@@ -3,7 +3,9 @@
 * world 1: the slab path (no neighbours) must reproduce the single-context step bit for bit;
 * world 2: two ranks share the one GPU of the test box (gloo transport staged through the
   host; bench.py uses RCCL between GPUs), compared with the single-context step;
-* world 3 from lopsided cuts with re-balancing every step, compared with the single-context step.
+* world 3 from lopsided cuts with re-balancing every step, compared with the single-context step;
+* the slab step's incremental re-sort against its full radix sort (SPH_RESORT=2 vs 0): bit-identical
+  owned particles on every rank, with migration and re-balancing in between.
 """
 import os
 import socket
@@ -38,8 +40,10 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, outdir, cuts=None, rebalance_every=0):
+def _worker(rank, world, port, outdir, cuts=None, rebalance_every=0, steps=STEPS, resort=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if resort is not None:
+        os.environ["SPH_RESORT"] = resort
     sys.path.insert(0, str(ROOT))
     import torch
     import torch.distributed as dist
@@ -53,7 +57,7 @@ def _worker(rank, world, port, outdir, cuts=None, rebalance_every=0):
     runner = slab.SlabRunner("C3", rank, world, device=0, scenario=_scenario(pkg), cuts=cuts,
                              rebalance_every=rebalance_every)
     runner.bind_stream(s.cuda_stream)
-    runner.step(STEPS)
+    runner.step(steps)
     torch.cuda.synchronize()
     np.save(os.path.join(outdir, f"rank{rank}.npy"), runner.owned())
     np.save(os.path.join(outdir, f"cuts{rank}.npy"), np.array(runner.cuts))
@@ -80,11 +84,11 @@ def test_slab_world1_bitwise(pkg):
     assert np.array_equal(rec[order, 3:6], vs)
 
 
-def _run_ranks(world, tmp_path, cuts=None, rebalance_every=0):
+def _run_ranks(world, tmp_path, cuts=None, rebalance_every=0, steps=STEPS, resort=None):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), cuts, rebalance_every))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), cuts, rebalance_every, steps, resort))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -122,3 +126,25 @@ def test_slab_world3_rebalancing_matches_single(pkg, tmp_path):
     final = [tuple(c) for c in np.load(tmp_path / "cuts0.npy")]
     assert final != lopsided
     _check(rec, xs, vs)
+
+
+@pytest.mark.parametrize("world,rebalance_every", [(2, 0), (3, 5)])
+def test_slab_incremental_resort_bitwise(pkg, tmp_path, world, rebalance_every):
+    """The slab step's incremental re-sort (old keys carried in the halo records, movers = every
+    changed key of [left | own | right]) gives the full radix sort's permutation: every rank's owned
+    particles are bit-identical after 30 steps, through migration and (world 3) lopsided cuts
+    re-balanced every 5 steps (each re-cut forces one full sort)."""
+    from sph_test_amd import slab
+    sc = _scenario(pkg)
+    p, _ = pkg.scenario_params(sc)
+    G = slab.global_columns(p)
+    cuts = [(0, 3), (3, 6), (6, G)] if world == 3 else None
+    out = {}
+    for mode in ("0", "2"):
+        d = tmp_path / mode
+        d.mkdir()
+        _run_ranks(world, d, cuts=cuts, rebalance_every=rebalance_every, steps=30, resort=mode)
+        out[mode] = [np.load(d / f"rank{r}.npy") for r in range(world)]
+    for r in range(world):
+        assert out["0"][r].shape == out["2"][r].shape, f"rank {r}"
+        assert out["0"][r].tobytes() == out["2"][r].tobytes(), f"rank {r}"
