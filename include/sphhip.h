@@ -242,7 +242,10 @@ int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int3
  *        count_sends(_async) → pack_send(0/1) → [exchange] → assemble → density → ranges →
  *        pack_rho(0/1) → [exchange] → force(interior) ∥ [rho in flight] → unpack_rho → force(boundary)
  *        → finish_step.
- *      Particle records are 32 bytes: (x, y, z, id-bits, u, v, w, 0). ---- */
+ *      Particle records are 32 bytes: (x, y, z, id-bits, u, v, w, old-key-bits): the particle's
+ *      sorted key before this step as a global cell key (0xffffffff: none), which lets the
+ *      receiver re-sort incrementally. assemble reads the received records in place on the
+ *      context stream: keep dev_left / dev_right intact until that stream has passed it. ---- */
 typedef struct sph_slab {
     int32_t cx_lo, cx_hi;       /* owned columns of the global grid; neighbours exist iff
                                    cx_lo > 0 / cx_hi < columns */
