@@ -161,6 +161,11 @@ size_t radix_hist_elems(int32_t capacity);
 int radix_sort(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, int32_t n,
                int32_t key_bits, bool identity_vals, uint32_t* hist, uint32_t* bin_total,
                hipStream_t s);
+// one-workgroup LDS sort (sort_small.hip), used by radix_sort for n <= SORT_SMALL_N, key_bits <= 16
+// and identity values; the result goes to keys_out / vals_out
+constexpr int32_t SORT_SMALL_N = 16384;
+void launch_sort_small(const uint32_t* keys_in, int32_t n, int32_t key_bits, uint32_t* keys_out, uint32_t* vals_out,
+                       hipStream_t s);
 
 // incremental re-sort of a Model S step (resort.hip), from the movers the force pass appended.
 // sk: sorted keys of the slot order; cs: its cell starts, updated in place; count: the movers'
@@ -215,8 +220,14 @@ void launch_keys(const float4* pos, int32_t n, const int32_t* id, int32_t n_acti
 // queued (gap list + counter, zeroed by the call) and filled by whole workgroups.
 void launch_cell_start(const uint32_t* sorted_keys, int32_t n, uint32_t* cs, uint32_t ncells,
                        uint4* gaps, uint32_t* gap_count, hipStream_t s);
-void launch_gather_f4(const uint32_t* perm, const float4* src, float4* dst, int32_t n, hipStream_t s);
-void launch_gather_i32(const uint32_t* perm, const int32_t* src, int32_t* dst, int32_t n, hipStream_t s);
+// Model R's slot arrays (pos, vel, omg, rot, aux; id, mode) gathered by one launch
+struct GatherR {
+    const float4* f4[5];
+    float4* f4o[5];
+    const int32_t* i32[2];
+    int32_t* i32o[2];
+};
+void launch_gather_r(const uint32_t* perm, const GatherR& g, int32_t n, hipStream_t s);
 void launch_gather_s(const uint32_t* perm, const float4* pos, const float4* vel, const int32_t* id,
                      float4* pos_o, float4* vel_o, int32_t* id_o, int32_t n, hipStream_t s);
 void launch_scatter_f4_by_id(const float4* src, const int32_t* id, int32_t n, float* dst,

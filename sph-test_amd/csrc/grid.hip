@@ -63,18 +63,16 @@ __global__ __launch_bounds__(BLK) void k_cell_start_gaps(const uint4* __restrict
     }
 }
 
-__global__ __launch_bounds__(BLK) void k_gather_f4(const uint32_t* __restrict__ perm,
-                                                   const float4* __restrict__ src,
-                                                   float4* __restrict__ dst, int32_t n) {
+// Model R's seven slot arrays in one launch (at the reference's few thousand particles each
+// launch is a few µs of fixed cost and moves almost nothing)
+__global__ __launch_bounds__(BLK) void k_gather_r(const uint32_t* __restrict__ perm, GatherR g, int32_t n) {
     const int32_t i = blockIdx.x * BLK + threadIdx.x;
-    if (i < n) dst[i] = src[perm[i]];
-}
-
-__global__ __launch_bounds__(BLK) void k_gather_i32(const uint32_t* __restrict__ perm,
-                                                    const int32_t* __restrict__ src,
-                                                    int32_t* __restrict__ dst, int32_t n) {
-    const int32_t i = blockIdx.x * BLK + threadIdx.x;
-    if (i < n) dst[i] = src[perm[i]];
+    if (i >= n) return;
+    const uint32_t s = perm[i];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) g.f4o[k][i] = g.f4[k][s];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) g.i32o[k][i] = g.i32[k][s];
 }
 
 __global__ __launch_bounds__(BLK) void k_gather_s(const uint32_t* __restrict__ perm,
@@ -225,11 +223,8 @@ void launch_cell_start(const uint32_t* sk, int32_t n, uint32_t* cs, uint32_t nce
     k_cell_start<<<nblk((int64_t)n + 1), BLK, 0, s>>>(sk, n, cs, ncells, gaps, gap_count);
     k_cell_start_gaps<<<1024, BLK, 0, s>>>(gaps, gap_count, cs);
 }
-void launch_gather_f4(const uint32_t* perm, const float4* src, float4* dst, int32_t n, hipStream_t s) {
-    if (n > 0) k_gather_f4<<<nblk(n), BLK, 0, s>>>(perm, src, dst, n);
-}
-void launch_gather_i32(const uint32_t* perm, const int32_t* src, int32_t* dst, int32_t n, hipStream_t s) {
-    if (n > 0) k_gather_i32<<<nblk(n), BLK, 0, s>>>(perm, src, dst, n);
+void launch_gather_r(const uint32_t* perm, const GatherR& g, int32_t n, hipStream_t s) {
+    if (n > 0) k_gather_r<<<nblk(n), BLK, 0, s>>>(perm, g, n);
 }
 void launch_gather_s(const uint32_t* perm, const float4* pos, const float4* vel, const int32_t* id,
                      float4* pos_o, float4* vel_o, int32_t* id_o, int32_t n, hipStream_t s) {

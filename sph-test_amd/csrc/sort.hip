@@ -172,6 +172,10 @@ int radix_sort(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* v
                int32_t key_bits, bool identity_vals, uint32_t* hist, uint32_t* bin_total,
                hipStream_t s) {
     if (n <= 0) return 0;
+    if (identity_vals && n <= SORT_SMALL_N && key_bits <= 16) {   // one launch instead of 3 per pass
+        launch_sort_small(keys_a, n, key_bits, keys_b, vals_b, s);
+        return 1;
+    }
     const int32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
     const int passes = key_bits <= 0 ? 1 : (key_bits + 7) / 8;
     uint32_t* K[2] = {keys_a, keys_b};

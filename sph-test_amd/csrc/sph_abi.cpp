@@ -376,13 +376,11 @@ int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id, const uint32_t** sorted_
     const uint32_t* perm = side ? ctx->vals2 : ctx->vals;
     if (is_contact(ctx)) {
         KTimer t(ctx, "reorder", (double)n * (4 + 2 * (5 * 16 + 8)));
-        launch_gather_f4(perm, ctx->pos, ctx->pos2, n, ctx->stream);
-        launch_gather_f4(perm, ctx->vel, ctx->vel2, n, ctx->stream);
-        launch_gather_f4(perm, ctx->omg, ctx->omg2, n, ctx->stream);
-        launch_gather_f4(perm, ctx->rot, ctx->rot2, n, ctx->stream);
-        launch_gather_f4(perm, ctx->aux, ctx->aux2, n, ctx->stream);
-        launch_gather_i32(perm, ctx->id, ctx->id2, n, ctx->stream);
-        launch_gather_i32(perm, ctx->mode, ctx->mode2, n, ctx->stream);
+        const GatherR gr{{ctx->pos, ctx->vel, ctx->omg, ctx->rot, ctx->aux},
+                         {ctx->pos2, ctx->vel2, ctx->omg2, ctx->rot2, ctx->aux2},
+                         {ctx->id, ctx->mode},
+                         {ctx->id2, ctx->mode2}};
+        launch_gather_r(perm, gr, n, ctx->stream);
         swap_sv(ctx);
         std::swap(ctx->omg, ctx->omg2);
         std::swap(ctx->rot, ctx->rot2);

@@ -17,13 +17,26 @@ pytestmark = pytest.mark.gpu
 
 
 # ------------------------------------------------------------------ sort / grid
-@pytest.mark.parametrize("n,bits", [(1, 8), (2047, 8), (2048, 15), (2049, 16), (100_000, 20),
-                                    (1_048_576, 20), (333_333, 24), (65_536, 32)])
+@pytest.mark.parametrize("n,bits", [(1, 8), (2047, 8), (2048, 15), (2049, 16), (5000, 12), (16_384, 16),
+                                    (16_385, 16), (100_000, 20), (1_048_576, 20), (333_333, 24), (65_536, 32)])
 def test_radix_sort_bit_exact(pkg, n, bits):
     rng = np.random.default_rng(n + bits)
     keys = rng.integers(0, 2 ** bits, n, dtype=np.uint64).astype(np.uint32)
     with pkg.Context(pkg.SPH_MODEL_WCSPH, 3, 16) as ctx:
         perm, sk = ctx.radix_sort(keys, bits)
+    ref = np.argsort(keys, kind="stable")
+    assert np.array_equal(perm, ref)
+    assert np.array_equal(sk, keys[ref])
+
+
+@pytest.mark.parametrize("n,hi", [(16_384, 7), (4096, 32_769), (1000, 1)])
+def test_radix_sort_small_ties(pkg, n, hi):
+    """The one-workgroup sort (n <= 16,384, keys <= 16 bits): long runs of equal keys keep their
+    index order, and Model R's sentinel key 32,768 sorts last."""
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, hi, n).astype(np.uint32)
+    with pkg.Context(pkg.SPH_MODEL_WCSPH, 3, 16) as ctx:
+        perm, sk = ctx.radix_sort(keys, 16)
     ref = np.argsort(keys, kind="stable")
     assert np.array_equal(perm, ref)
     assert np.array_equal(sk, keys[ref])
