@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event pass")
     ap.add_argument("--slab", action="store_true", help="run the multi-GPU slab step even at N=1 (rehearsal)")
     ap.add_argument("--rebalance", type=int, default=50, help="slab cut re-balancing interval in steps (0: off)")
+    ap.add_argument("--strong", action="store_true",
+                    help="decompose --config itself over the N ranks (strong scaling: C4 on 4 GPUs, C5 on 8) "
+                         "instead of stretching it xN")
     ap.add_argument("--table", action="store_true",
                     help="print the GPU / 1-thread / all-thread CPU rate table (SURVEY §8d) instead of the bench line")
     return ap.parse_args()
@@ -232,10 +235,11 @@ def main():
         torch.cuda.set_device(0)
     pkg = GE.load_package()
 
-    if world > 1 or args.slab:
+    if world > 1 or args.slab or args.strong:
         from sph_test_amd import slab
         runner = slab.SlabRunner(args.config, rank, world, device=local, profile=not args.no_profile,
-                                 rebalance_every=args.rebalance)
+                                 rebalance_every=args.rebalance,
+                                 scenario=pkg.config_scenario(args.config) if args.strong else None)
     else:
         runner = SingleRunner(pkg, args.config, local, profile=not args.no_profile)
 
@@ -304,11 +308,11 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(wall * 1e3 / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (dam-break lattice, seed 1234)",
-            "config": {"workload": runner.workload(), "particles": n_total,
+            "config": {"workload": runner.workload("strong" if args.strong else "weak"), "particles": n_total,
                        "particles_per_gpu": runner.local_particles(), "h_over_dx": 1.2,
                        "parallelism": f"slab{world}" if world > 1 else "single"},
             "roofline": roofline,
@@ -325,6 +329,7 @@ def main():
 
 class SingleRunner:
     def __init__(self, pkg, config, device, profile):
+        self.pkg = pkg
         self.config = config
         self.sim = pkg.SPHSim.from_config(config, device=device, profile=profile)
 
@@ -346,9 +351,10 @@ class SingleRunner:
     def local_particles(self):
         return self.sim.n
 
-    def workload(self):
+    def workload(self, scaling: str = "weak"):
         sc = self.sim.scenario
-        return (f"{self.config}: {self.sim.n} particles, {sc.dim}D dam-break, column {sc.nx}x{sc.ny}x{sc.nz}, "
+        kind = "sloshing" if sc.kind == self.pkg.SPH_SCENARIO_SLOSHING else "dam-break"
+        return (f"{self.config}: {self.sim.n} particles, {sc.dim}D {kind}, column {sc.nx}x{sc.ny}x{sc.nz}, "
                 f"tank {sc.tx}x{sc.ty}x{sc.tz} dx")
 
     def close(self):

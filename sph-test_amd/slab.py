@@ -400,9 +400,11 @@ class SlabRunner:
     def kernel_stats(self) -> dict:
         return self.be.kernel_stats()
 
-    def workload(self) -> str:
+    def workload(self, scaling: str = "weak") -> str:
         sc = self.scenario
-        return (f"{self.config}x{self.world} weak: {self.n_global} particles, {sc.dim}D dam-break, column "
+        kind = "sloshing" if sc.kind == A.SPH_SCENARIO_SLOSHING else "dam-break"
+        name = f"{self.config}x{self.world} weak" if scaling == "weak" else f"{self.config} on {self.world} GPUs"
+        return (f"{name}: {self.n_global} particles, {sc.dim}D {kind}, column "
                 f"{sc.nx}x{sc.ny}x{sc.nz}, tank {sc.tx}x{sc.ty}x{sc.tz} dx, x-slabs {self.cuts}")
 
     def close(self) -> None:
