@@ -265,24 +265,30 @@ __global__ __launch_bounds__(MV_BLK) void k_slab_keys(AsmSrc src, int32_t n, Gri
     __shared__ uint32_t base_s;
     const int32_t x0 = blockIdx.x * MV_DET + threadIdx.x;
     uint32_t kn[MV_DET_PER], ko[MV_DET_PER];
-    // loads first, stores after: the compiler cannot move a load above a store it may alias, and
-    // interleaving them would serialise the four round trips
+    // All loads first and unconditional (the source is picked by address, not by branch), stores
+    // after: a branch per slot, or a load below a store it may alias, serialises the round trips.
+    // A record's (x, y, z) sits where pos has it; its old key is the second float4's w.
+    float4 pv[MV_DET_PER];
+    uint32_t kv[MV_DET_PER];
 #pragma unroll
     for (int j = 0; j < MV_DET_PER; ++j) {
         const int32_t x = min(x0 + j * MV_BLK, n - 1);
-        if (asm_rec(src, x)) {
-            const bool left = x < src.nl;
-            const float4* r = left ? src.rl + 2 * (size_t)x : src.rr + 2 * (size_t)(x - src.nre);
-            const float4 r0 = r[0];
-            const uint32_t og = __float_as_uint(r[1].w);
-            kn[j] = window_key(g, r0.x, r0.y, r0.z);
-            if (og == REC_NO_KEY) ko[j] = left ? 0u : g.ncells - 1u;
-            else ko[j] = og < key_base ? 0u : min(og - key_base, g.ncells - 1u);
-        } else {
-            const float4 p = src.pos[x + src.o_off];
-            kn[j] = window_key(g, p.x, p.y, p.z);
-            ko[j] = src.sk[x + src.o_off];
-        }
+        const bool rec = asm_rec(src, x);
+        const float4* r = x < src.nl ? src.rl + 2 * (size_t)x : src.rr + 2 * (size_t)(x - src.nre);
+        const float4* pp = rec ? r : src.pos + (x + src.o_off);
+        const uint32_t* kp = rec ? reinterpret_cast<const uint32_t*>(r + 1) + 3 : src.sk + (x + src.o_off);
+        pv[j] = *pp;
+        kv[j] = *kp;
+    }
+#pragma unroll
+    for (int j = 0; j < MV_DET_PER; ++j) {
+        const int32_t x = min(x0 + j * MV_BLK, n - 1);
+        kn[j] = window_key(g, pv[j].x, pv[j].y, pv[j].z);
+        const uint32_t og = kv[j];
+        uint32_t kr;
+        if (og == REC_NO_KEY) kr = x < src.nl ? 0u : g.ncells - 1u;
+        else kr = og < key_base ? 0u : min(og - key_base, g.ncells - 1u);
+        ko[j] = asm_rec(src, x) ? kr : og;
     }
     uint32_t mine = 0;   // bit j: slot x0 + j * MV_BLK moved
 #pragma unroll

@@ -126,25 +126,43 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_pack(const uint32_t* __restrict
                                                       int32_t col_le, int32_t col_ge,
                                                       const uint32_t* __restrict__ blk, int32_t nblk,
                                                       float4* __restrict__ out) {
-    __shared__ uint32_t wc[SL_WAVES];
+    __shared__ uint32_t wc[SL_PER][SL_WAVES];
+    const int w = threadIdx.x >> 6;
+    const int32_t i0 = b + blockIdx.x * SL_SEND + threadIdx.x;
+    // every key load issues before any is used; then one barrier for all sub-chunks' wave counts
+    uint32_t col[SL_PER];
+#pragma unroll
+    for (int j = 0; j < SL_PER; ++j) col[j] = keys[min(i0 + j * SL_BLK, e - 1)] / gyz;
+    uint32_t mine = 0;   // bit j: the slot of sub-chunk j is sent
+#pragma unroll
+    for (int j = 0; j < SL_PER; ++j) {
+        const bool pred = i0 + j * SL_BLK < e && (side == 0 ? (int32_t)col[j] <= col_le : (int32_t)col[j] >= col_ge);
+        const uint64_t m = __ballot(pred);
+        if ((threadIdx.x & 63) == 0) wc[j][w] = (uint32_t)__popcll(m);
+        mine |= (uint32_t)pred << j;
+    }
+    __syncthreads();
+    // sub-chunks in slot order, waves in order within a sub-chunk: the records keep slot order
     uint32_t run = blk[side * nblk + blockIdx.x];
-    for (int j = 0; j < SL_PER; ++j) {   // sub-chunks in slot order: the records keep slot order
-        const int32_t i = b + (blockIdx.x * SL_PER + j) * SL_BLK + threadIdx.x;
-        const bool in = i < e;
-        const int32_t col = in ? (int32_t)(keys[i] / gyz) : 0;
-        const bool pred = in && (side == 0 ? col <= col_le : col >= col_ge);
-        uint32_t wave_base;
-        const uint32_t tot = block_ballot_count(pred, wc, wave_base);
+#pragma unroll
+    for (int j = 0; j < SL_PER; ++j) {
+        uint32_t before = 0, tot = 0;
+#pragma unroll
+        for (int k = 0; k < SL_WAVES; ++k) {
+            before += k < w ? wc[j][k] : 0u;
+            tot += wc[j][k];
+        }
+        const bool pred = (mine >> j) & 1u;
         const uint64_t m = __ballot(pred);
         if (pred) {
-            const uint32_t r = run + wave_base + lane_prefix(m);
+            const int32_t i = i0 + j * SL_BLK;
+            const uint32_t r = run + before + lane_prefix(m);
             const float4 p = pos[i], v = vel[i];
             const uint32_t ok = sk ? sk[i] + key_base : SL_NO_KEY;
             out[2 * (size_t)r] = make_float4(p.x, p.y, p.z, __int_as_float(id[i]));
             out[2 * (size_t)r + 1] = make_float4(v.x, v.y, v.z, __uint_as_float(ok));
         }
         run += tot;
-        __syncthreads();   // wc is rewritten by the next sub-chunk
     }
 }
 
