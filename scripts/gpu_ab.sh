@@ -5,5 +5,5 @@ cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 V=${AB_VARIANTS:-1}
 for lib in "$@"; do
   echo "== $lib"
-  SPHHIP_LIB=$GRAFT_REPO_ROOT/$lib timeout -k 10 300 python3 scripts/nb_variants.py --variants $V --steps 20 --rounds 3
+  SPHHIP_LIB=$GRAFT_REPO_ROOT/$lib timeout -k 10 300 python3 scripts/nb_variants.py --variants $V --steps 20 --rounds ${AB_ROUNDS:-3}
 done

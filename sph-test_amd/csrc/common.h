@@ -96,12 +96,29 @@ __device__ __forceinline__ void cell_fracs(const GridDesc& g, float x, float y, 
 }
 
 // Workgroups are dispatched round-robin over the 8 XCDs, each with its own L2
-// (MI355X_MICROARCH.md). Remapped so that XCD x runs one contiguous range of logical blocks, in
-// order: blocks that stage the same neighbour rows then share one L2 instead of fetching them 8 times.
+// (MI355X_MICROARCH.md). Remapped so that each XCD runs groups of SPH_XCD_CHUNK consecutive logical
+// blocks: neighbouring blocks stage the same neighbour rows and then share one L2 instead of
+// fetching them 8 times, while dealing the runs round-robin keeps the eight XCDs on equally dense
+// parts of the fluid. One contiguous range per XCD (SPH_XCD_CHUNK=0) left XCDs with sparse or
+// surface-heavy ranges idle at the end: C3 force pass 250 -> 238 us with runs of 16
+// (profiles/r01_xcd_map_ab.log; 8 and 32 are within noise of 16, 4 and 64 are slower).
+#ifndef SPH_XCD_CHUNK
+#define SPH_XCD_CHUNK 16
+#endif
 __device__ __forceinline__ int32_t xcd_block(int32_t b, int32_t nb) {
     constexpr int32_t NX = 8;
+#if SPH_XCD_CHUNK < 0   // A/B: dispatch order
+    return b;
+#elif SPH_XCD_CHUNK > 0   // runs of C consecutive blocks dealt round-robin to the XCDs (the tail: dispatch order)
+    constexpr int32_t C = SPH_XCD_CHUNK;
+    const int32_t full = nb / (NX * C) * (NX * C);
+    if (b >= full) return b;
+    const int32_t x = b % NX, k = b / NX;
+    return ((k / C) * NX + x) * C + (k % C);
+#else   // A/B: one contiguous range per XCD
     const int32_t x = b % NX, k = b / NX, per = nb / NX, rem = nb % NX;
     return x * per + (x < rem ? x : rem) + k;
+#endif
 }
 
 __device__ __forceinline__ uint32_t lane_id() {
