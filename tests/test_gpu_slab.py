@@ -24,9 +24,9 @@ def _scenario(pkg):
     return pkg.make_scenario(0, 3, 48, 32, 32, 120, 48, 32, dx=0.01, seed=99)
 
 
-def _single(pkg, sc):
+def _single(pkg, sc, steps=STEPS):
     sim = pkg.SPHSim(sc)
-    sim.step(STEPS)
+    sim.step(steps)
     x, v = sim.positions(), sim.velocities()
     sim.close()
     return x, v
@@ -66,15 +66,16 @@ def _worker(rank, world, port, outdir, cuts=None, rebalance_every=0, steps=STEPS
     dist.destroy_process_group()
 
 
-def test_slab_world1_bitwise(pkg):
-    import torch
-    import torch.distributed as dist
+@pytest.mark.parametrize("steps", [STEPS, 300])
+def test_slab_world1_bitwise(pkg, steps):
+    """300 steps: the slab step's incremental re-sort (and its adaptive fallback) stays on the single
+    context's permutation over a long run."""
     from sph_test_amd import slab
     sc = _scenario(pkg)
-    xs, vs = _single(pkg, sc)
+    xs, vs = _single(pkg, sc, steps)
     runner = slab.SlabRunner("C3", 0, 1, device=0, scenario=sc)
     assert runner.cuts == [(0, runner.cuts[0][1])]
-    runner.step(STEPS)
+    runner.step(steps)
     rec = runner.owned()
     runner.close()
     ids = rec[:, 6].view(np.int32)
