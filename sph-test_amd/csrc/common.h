@@ -192,7 +192,11 @@ struct ResortScratch {
     uint64_t* ms;                    // movers by (new key, slot)
     uint32_t *mx, *mos;              // movers by slot: slot, old key
     uint32_t cap;
+    int32_t mi_off;                  // slab step: an own mover's slot is mi + mi_off (MV_REC: records' slot)
 };
+// a mover entry whose mi has this bit holds a slot of the assembled array (a halo record's);
+// without it, mi is the force pass's slot and the assembled slot is mi + mi_off
+constexpr uint32_t MV_REC = 0x80000000u;
 // The slot array the re-sort reads, slot x in [0, n). Single domain: pos/vel/id/sk[x]. Slab step:
 // the assembled [from left | own | from right] without copying it: x < nl is left record rl[x],
 // x >= nre is right record rr[x - nre] (32-B halo records, old keys in skr[x]), and the own block
@@ -201,21 +205,24 @@ struct AsmSrc {
     const float4* pos;
     const float4* vel;
     const int32_t* id;
-    const uint32_t* sk;
+    const uint32_t* sk;     // old (sorted) keys of the own slots
+    const uint32_t* keys;   // new keys of the own slots (the force pass's)
     int32_t o_off;
     const float4* rl;
     const float4* rr;
-    const uint32_t* skr;
+    const uint32_t* skr;    // records: old keys, by assembled slot
+    const uint32_t* keyr;   // records: new keys, by assembled slot
     int32_t nl, nre;
 };
-inline AsmSrc asm_plain(const float4* pos, const float4* vel, const int32_t* id, const uint32_t* sk, int32_t n) {
-    return AsmSrc{pos, vel, id, sk, 0, nullptr, nullptr, nullptr, 0, n};
+inline AsmSrc asm_plain(const float4* pos, const float4* vel, const int32_t* id, const uint32_t* sk,
+                        const uint32_t* keys, int32_t n) {
+    return AsmSrc{pos, vel, id, sk, keys, 0, nullptr, nullptr, nullptr, nullptr, 0, n};
 }
-// the slab step's assembled slots: new keys (window sentinel) into keys, the halo records' old keys
-// (moved into this window, clamped) into skr_out (= src.skr), and every slot whose key changed
-// appended to the sink (its counter must be zero)
-void launch_slab_keys(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base, uint32_t* keys, uint32_t* skr_out,
-                      MoverSink sink, hipStream_t s);
+// the slab step's halo records (slots [0, nl) and [nre, n)): new keys (window sentinel) into
+// src.keyr, old keys moved into this window and clamped into src.skr, and every record whose key
+// changed appended to the sink (mi = slot | MV_REC) after the own movers the force pass appended
+void launch_slab_rec(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base, uint32_t* keyr, uint32_t* skr,
+                     MoverSink sink, hipStream_t s);
 // cell-start values to pick once the table is final: out[t] = cs[idx[t]] (device), and the same
 // into out_host (mapped pinned memory) when given; m = 0: none
 struct CsPick {
@@ -224,7 +231,7 @@ struct CsPick {
     uint32_t* out;
     uint32_t* out_host;
 };
-void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* keys, const uint32_t* count,
+void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* count,
                    uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,
                    uint32_t* sk_o, hipStream_t s, CsPick pick = CsPick{{0}, 0, nullptr, nullptr});
 

@@ -41,6 +41,15 @@ static __device__ __forceinline__ uint32_t asm_sk(const AsmSrc& a, int32_t x) {
     return asm_rec(a, x) ? a.skr[x] : a.sk[x + a.o_off];
 }
 
+static __device__ __forceinline__ uint32_t asm_key(const AsmSrc& a, int32_t x) {
+    return asm_rec(a, x) ? a.keyr[x] : a.keys[x + a.o_off];
+}
+
+// a mover entry's slot in the array being re-sorted (see MV_REC)
+static __device__ __forceinline__ uint32_t mv_slot(const ResortScratch& w, uint32_t mi) {
+    return (mi & MV_REC) ? (mi & ~MV_REC) : mi + (uint32_t)w.mi_off;
+}
+
 // a halo record reads as the slab assemble's unpack wrote it: (x, y, z, 0), (u, v, w, 0), id
 static __device__ __forceinline__ void asm_load(const AsmSrc& a, int32_t x, float4& p, float4& v, int32_t& id) {
     if (asm_rec(a, x)) {
@@ -115,12 +124,12 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
         __syncthreads();
         for (int t = threadIdx.x; t < MV_TILE; t += MV_BLK) {
             const uint32_t y = it * MV_TILE + t;
-            tile[t] = y < m ? comp(w.mk[y], w.mi[y]) : ~0ull;
+            tile[t] = y < m ? comp(w.mk[y], mv_slot(w, w.mi[y])) : ~0ull;
         }
         __syncthreads();
         const uint32_t x = ir * MV_BLK + threadIdx.x;
         if (x < m) {
-            const uint32_t ix = w.mi[x], k = w.mk[x];
+            const uint32_t ix = mv_slot(w, w.mi[x]), k = w.mk[x];
             const uint64_t cx = comp(k, ix);
             const uint32_t c0 = cs_old[k], c1 = cs_old[k + 1];
             const uint32_t q = ix < c0 ? c0 : (ix > c1 ? c1 : ix);
@@ -146,7 +155,7 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_place(const uint32_t* __restrict_
                                                      int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o) {
     const uint32_t m = *mtotal;
     for (uint32_t r = blockIdx.x * MV_BLK + threadIdx.x; r < m; r += gridDim.x * MV_BLK) {
-        const uint32_t x = w.mi[r], k = w.mk[r];
+        const uint32_t x = mv_slot(w, w.mi[r]), k = w.mk[r];
         const uint32_t c0 = cs_old[k], c1 = cs_old[k + 1];
         const uint32_t q = x < c0 ? c0 : (x > c1 ? c1 : x);
         const uint32_t rk = w.rank[r], ri = w.rank[w.cap + r], aq = w.rank[2 * w.cap + r];
@@ -202,7 +211,7 @@ static __device__ void mv_cell_start(uint32_t* __restrict__ cs, uint32_t ncells,
     }
 }
 
-__global__ __launch_bounds__(MV_BLK) void k_mv_merge(const uint32_t* __restrict__ keys, AsmSrc src, int32_t n,
+__global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
                                                      const uint32_t* __restrict__ mtotal, ResortScratch w,
                                                      float4* __restrict__ pos_o,
                                                      float4* __restrict__ vel_o, int32_t* __restrict__ id_o,
@@ -230,7 +239,7 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(const uint32_t* __restrict_
         if (lane_id() == 0) b[wv] = p;
     }
     const uint32_t ko = i < n ? asm_sk(src, i) : 0u;
-    const bool stay = i < n && keys[i] == ko;
+    const bool stay = i < n && asm_key(src, i) == ko;
     __syncthreads();
     const uint32_t a = movers_before(i < n && !stay, b[0], wc);
     if (!stay) return;
@@ -246,58 +255,47 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(const uint32_t* __restrict_
     sk_o[dst] = ko;
 }
 
-// The slab step's keys and movers in one pass over the assembled slots [left | own | right] (the
-// force pass appends the movers in the single-domain path). New keys use the window sentinel (as
-// k_keys); a halo record's old key is its global old key moved into this window and clamped into
-// [0, ncells - 1]: the left neighbour's columns lie below this window's owned ones and the right
-// neighbour's above, so clamping keeps the assembled old keys sorted. A record without an old key
-// takes its side's bound (it then almost surely moves). The records' old keys go to skr_out, which
-// is src.skr. A workgroup takes MV_DET slots, counts its movers and reserves their entries with ONE
-// atomic: per-wave atomics on one counter serialise (~4,000 waves with a mover at C3).
+// The slab step's halo records: new keys (window sentinel, as k_keys) and old keys moved into this
+// window, clamped into [0, ncells - 1]. The left neighbour's columns lie below this window's owned
+// ones and the right neighbour's above, so clamping keeps the assembled old keys sorted. A record
+// without an old key takes its side's bound (it then almost surely moves). Changed records join the
+// movers the force pass appended for the own slots (mi = slot | MV_REC). A workgroup takes MV_DET
+// records and reserves its entries with one atomic.
 constexpr int MV_DET_PER = 4;
 constexpr int MV_DET = MV_BLK * MV_DET_PER;
 constexpr uint32_t REC_NO_KEY = 0xffffffffu;   // slab.hip SL_NO_KEY
 
-__global__ __launch_bounds__(MV_BLK) void k_slab_keys(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base,
-                                                      uint32_t* __restrict__ keys, uint32_t* __restrict__ skr_out,
-                                                      MoverSink sink) {
+__global__ __launch_bounds__(MV_BLK) void k_slab_rec(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base,
+                                                     uint32_t* __restrict__ keyr, uint32_t* __restrict__ skr,
+                                                     MoverSink sink) {
     __shared__ uint32_t wsum[MV_BLK / 64];
     __shared__ uint32_t base_s;
-    const int32_t x0 = blockIdx.x * MV_DET + threadIdx.x;
+    const int32_t nr = n - src.nre, nrec = src.nl + nr;
+    const int32_t r0 = blockIdx.x * MV_DET + threadIdx.x;
     uint32_t kn[MV_DET_PER], ko[MV_DET_PER];
-    // All loads first and unconditional (the source is picked by address, not by branch), stores
-    // after: a branch per slot, or a load below a store it may alias, serialises the round trips.
-    // A record's (x, y, z) sits where pos has it; its old key is the second float4's w.
+    int32_t xs[MV_DET_PER];
     float4 pv[MV_DET_PER];
-    uint32_t kv[MV_DET_PER];
+    uint32_t og[MV_DET_PER];
 #pragma unroll
-    for (int j = 0; j < MV_DET_PER; ++j) {
-        const int32_t x = min(x0 + j * MV_BLK, n - 1);
-        const bool rec = asm_rec(src, x);
-        const float4* r = x < src.nl ? src.rl + 2 * (size_t)x : src.rr + 2 * (size_t)(x - src.nre);
-        const float4* pp = rec ? r : src.pos + (x + src.o_off);
-        const uint32_t* kp = rec ? reinterpret_cast<const uint32_t*>(r + 1) + 3 : src.sk + (x + src.o_off);
-        pv[j] = *pp;
-        kv[j] = *kp;
+    for (int j = 0; j < MV_DET_PER; ++j) {   // loads first, unconditional
+        const int32_t r = min(r0 + j * MV_BLK, nrec - 1);
+        const float4* rec = r < src.nl ? src.rl + 2 * (size_t)r : src.rr + 2 * (size_t)(r - src.nl);
+        pv[j] = rec[0];
+        og[j] = __float_as_uint(rec[1].w);
+        xs[j] = r < src.nl ? r : src.nre + (r - src.nl);
     }
+    uint32_t mine = 0;   // bit j: record r0 + j * MV_BLK moved
 #pragma unroll
     for (int j = 0; j < MV_DET_PER; ++j) {
-        const int32_t x = min(x0 + j * MV_BLK, n - 1);
+        const bool left = xs[j] < src.nl;
         kn[j] = window_key(g, pv[j].x, pv[j].y, pv[j].z);
-        const uint32_t og = kv[j];
-        uint32_t kr;
-        if (og == REC_NO_KEY) kr = x < src.nl ? 0u : g.ncells - 1u;
-        else kr = og < key_base ? 0u : min(og - key_base, g.ncells - 1u);
-        ko[j] = asm_rec(src, x) ? kr : og;
-    }
-    uint32_t mine = 0;   // bit j: slot x0 + j * MV_BLK moved
-#pragma unroll
-    for (int j = 0; j < MV_DET_PER; ++j) {
-        const int32_t x = x0 + j * MV_BLK;
-        if (x >= n) continue;
-        keys[x] = kn[j];
-        if (asm_rec(src, x)) skr_out[x] = ko[j];
-        if (kn[j] != ko[j]) mine |= 1u << j;
+        if (og[j] == REC_NO_KEY) ko[j] = left ? 0u : g.ncells - 1u;
+        else ko[j] = og[j] < key_base ? 0u : min(og[j] - key_base, g.ncells - 1u);
+        if (r0 + j * MV_BLK < nrec) {
+            keyr[xs[j]] = kn[j];
+            skr[xs[j]] = ko[j];
+            if (kn[j] != ko[j]) mine |= 1u << j;
+        }
     }
     const uint32_t c = (uint32_t)__popc(mine);
     // exclusive prefix of c over the workgroup
@@ -319,26 +317,27 @@ __global__ __launch_bounds__(MV_BLK) void k_slab_keys(AsmSrc src, int32_t n, Gri
     }
     if (threadIdx.x == 0) base_s = tot ? atomicAdd(sink.count, tot) : 0u;
     __syncthreads();
-    uint32_t r = base_s + off + incl - c;
+    uint32_t q = base_s + off + incl - c;
 #pragma unroll
     for (int j = 0; j < MV_DET_PER; ++j) {
         if (!(mine >> j & 1u)) continue;
-        sink.mi[r] = (uint32_t)(x0 + j * MV_BLK);
-        sink.mk[r] = kn[j];
-        sink.mo[r] = ko[j];
-        sink.rank[r] = 0u;
-        sink.rank[sink.cap + r] = 0u;
-        sink.rank[2 * sink.cap + r] = 0u;
-        ++r;
+        sink.mi[q] = (uint32_t)xs[j] | MV_REC;
+        sink.mk[q] = kn[j];
+        sink.mo[q] = ko[j];
+        sink.rank[q] = 0u;
+        sink.rank[sink.cap + q] = 0u;
+        sink.rank[2 * sink.cap + q] = 0u;
+        ++q;
     }
 }
 
-void launch_slab_keys(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base, uint32_t* keys, uint32_t* skr_out,
-                      MoverSink sink, hipStream_t s) {
-    if (n > 0) k_slab_keys<<<(n + MV_DET - 1) / MV_DET, MV_BLK, 0, s>>>(src, n, g, key_base, keys, skr_out, sink);
+void launch_slab_rec(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base, uint32_t* keyr, uint32_t* skr,
+                     MoverSink sink, hipStream_t s) {
+    const int32_t nrec = src.nl + (n - src.nre);
+    if (nrec > 0) k_slab_rec<<<(nrec + MV_DET - 1) / MV_DET, MV_BLK, 0, s>>>(src, n, g, key_base, keyr, skr, sink);
 }
 
-void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* keys, const uint32_t* count,
+void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* count,
                    uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,
                    uint32_t* sk_o, hipStream_t s, CsPick pick) {
     if (n <= 0) return;
@@ -347,7 +346,7 @@ void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const u
     k_mv_place<<<std::min(nb, 1024), MV_BLK, 0, s>>>(count, cs, w, src, pos_o, vel_o, id_o, sk_o);
     // + the cell-start update, after every reader of cs_old (k_mv_rank, k_mv_place)
     const int32_t ncs = (int32_t)((ncells + MV_CS_CELLS) / MV_CS_CELLS);
-    k_mv_merge<<<nb + ncs, MV_BLK, 0, s>>>(keys, src, n, count, w, pos_o, vel_o, id_o, sk_o, nb, cs, ncells, pick);
+    k_mv_merge<<<nb + ncs, MV_BLK, 0, s>>>(src, n, count, w, pos_o, vel_o, id_o, sk_o, nb, cs, ncells, pick);
 }
 
 }  // namespace sph

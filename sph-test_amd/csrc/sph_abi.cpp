@@ -419,7 +419,7 @@ void force_range(sph_ctx* ctx, int32_t b, int32_t e, float dt, float fext, Mover
 
 ResortScratch resort_scratch(sph_ctx* ctx) {
     return ResortScratch{ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_rank, ctx->mv_ms, ctx->mv_mx, ctx->mv_mos,
-                         (uint32_t)std::max(ctx->capacity, 1)};
+                         (uint32_t)std::max(ctx->capacity, 1), 0};
 }
 
 // The force pass appends movers for the next step's incremental re-sort.
@@ -446,8 +446,8 @@ int sort_wcsph(sph_ctx* ctx) {
         {
             KTimer t(ctx, "resort", (double)n * (2 * 4 + 2 * 36));
             const int used = ctx->mv_par;
-            launch_resort(asm_plain(ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, n), ctx->cs, ctx->grid.ncells, n,
-                          ctx->keys, ctx->mv_count + used, ctx->mv_count + (1 - used), resort_scratch(ctx),
+            launch_resort(asm_plain(ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->keys, n), ctx->cs,
+                          ctx->grid.ncells, n, ctx->mv_count + used, ctx->mv_count + (1 - used), resort_scratch(ctx),
                           ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, ctx->stream);
             ctx->mv_par = 1 - used;
         }
@@ -1542,26 +1542,26 @@ int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void
     const int32_t idx[6] = {col_start(ctx, 0), col_start(ctx, lc_lo), col_start(ctx, lc_lo + 1),
                             col_start(ctx, lc_hi - 1), col_start(ctx, lc_hi), col_start(ctx, ctx->grid.gx)};
     if (ctx->resort_mode != 0 && !many && ctx->sk_valid && n > 0) {
-        // incremental: the re-sort reads [left records | own slots | right records] in place
-        const AsmSrc src{ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->o0 - nl, (const float4*)dev_left,
-                         (const float4*)dev_right, ctx->keys2, nl, nl + no};
-        const int used = ctx->mv_par;   // zeroed by the last re-sort's k_mv_rank, or by the full path
+        // incremental: the re-sort reads [left records | own slots | right records] in place. The force
+        // pass already appended the own movers (window keys); the records' keys and movers join here.
+        const AsmSrc src{ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->keys, ctx->o0 - nl, (const float4*)dev_left,
+                         (const float4*)dev_right, ctx->keys2, ctx->vals, nl, nl + no};
+        const int used = ctx->mv_par;
         const MoverSink mv{ctx->keys2, ctx->mv_count + used, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_rank,
                            (uint32_t)std::max(ctx->capacity, 1)};
         {
-            // new keys (own particles outside the held columns were sent away: they sort last and
-            // drop), the records' old keys, and the movers
-            KTimer t(ctx, "slab_assemble", 28.0 * (double)n);
-            launch_slab_keys(src, (int32_t)n, ctx->grid, key_base, ctx->keys, ctx->keys2, mv, s);
+            KTimer t(ctx, "slab_assemble", 40.0 * (double)(nl + nr));
+            launch_slab_rec(src, (int32_t)n, ctx->grid, key_base, ctx->vals, ctx->keys2, mv, s);
         }
         KTimer t(ctx, "resort", (double)n * (2 * 4 + 2 * 36));
         launch_slab_cs_old(ctx->cs, ctx->grid.ncells, gyz, (uint32_t)ctx->grid.gx, ctx->has_left, ctx->has_right,
                            nl - ctx->o0, ctx->keys2, nl, no, nr, s);
         CsPick pick{{0}, 6, ctx->sdev, ctx->rng_host};   // the ranges, read as the cell table completes
         for (int k = 0; k < 6; ++k) pick.idx[k] = idx[k];
-        launch_resort(src, ctx->cs, ctx->grid.ncells, (int32_t)n, ctx->keys, ctx->mv_count + used,
-                      ctx->mv_count + (1 - used), resort_scratch(ctx), ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, s,
-                      pick);
+        ResortScratch w = resort_scratch(ctx);
+        w.mi_off = nl - ctx->o0;   // own movers were appended by slot in the previous order
+        launch_resort(src, ctx->cs, ctx->grid.ncells, (int32_t)n, ctx->mv_count + used, ctx->mv_count + (1 - used), w,
+                      ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, s, pick);
         if ((ctx->steps & 7) == 0)
             HIPCHK(hipMemcpyAsync(ctx->mv_host, ctx->mv_count + used, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         ctx->mv_par = 1 - used;
@@ -1670,7 +1670,7 @@ static void slab_force_range(sph_ctx* ctx, float dt, int32_t b, int32_t e) {
     const float tt = (float)ctx->sim_time;
     const float fext = p.forcing_amp != 0.0f ? p.forcing_amp * sinf(6.28318530718f * p.forcing_freq * tt) : 0.0f;
     KTimer t(ctx, "force_integrate", 76.0 * (e - b));
-    force_range(ctx, b, e, dt, fext);
+    force_range(ctx, b, e, dt, fext, mover_sink(ctx));   // own movers for the next assemble's re-sort
 }
 
 int sph_slab_force(sph_ctx* ctx, float dt, int32_t part) {

@@ -146,7 +146,9 @@ __global__ __launch_bounds__(NB_BLK) void k_force_integrate(
     vel_o[i] = make_float4(nv[0], nv[1], nv[2], 0.f);
     const uint32_t key = cell_key(g, np[0], np[1], np[2]);
     keys_o[i] = key;
-    append_mover(mv, i, key);
+    // the mover list takes the window key: in a slab, a particle that left the held columns sorts
+    // last (window_key = cell_key in a single domain); it changed iff the clamped key changed
+    append_mover(mv, i, window_key(g, np[0], np[1], np[2]));
 }
 
 // dr set: [ib, ie) only sizes the grid (an upper bound); the kernel reads its bounds from dr
