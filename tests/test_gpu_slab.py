@@ -20,7 +20,10 @@ ROOT = Path(__file__).resolve().parent.parent
 STEPS = 8
 
 
-def _scenario(pkg):
+def _scenario(pkg, kind=0):
+    """kind 0: dam-break; 1: sloshing (lateral forcing from the simulated time)"""
+    if kind == 1:
+        return pkg.make_scenario(pkg.SPH_SCENARIO_SLOSHING, 3, 96, 24, 32, 96, 48, 64, dx=0.01, seed=99)
     return pkg.make_scenario(0, 3, 48, 32, 32, 120, 48, 32, dx=0.01, seed=99)
 
 
@@ -66,12 +69,12 @@ def _worker(rank, world, port, outdir, cuts=None, rebalance_every=0, steps=STEPS
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("steps", [STEPS, 300])
-def test_slab_world1_bitwise(pkg, steps):
+@pytest.mark.parametrize("steps,kind", [(STEPS, 0), (300, 0), (100, 1)])
+def test_slab_world1_bitwise(pkg, steps, kind):
     """300 steps: the slab step's incremental re-sort (and its adaptive fallback) stays on the single
-    context's permutation over a long run."""
+    context's permutation over a long run; sloshing: the forcing follows the same simulated time."""
     from sph_test_amd import slab
-    sc = _scenario(pkg)
+    sc = _scenario(pkg, kind)
     xs, vs = _single(pkg, sc, steps)
     runner = slab.SlabRunner("C3", 0, 1, device=0, scenario=sc)
     assert runner.cuts == [(0, runner.cuts[0][1])]
