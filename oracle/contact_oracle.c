@@ -22,6 +22,14 @@
 #define TORQUE_SCALE 10000
 #define ADHESION_DELTA_SCALE 1000000
 
+/* HLSL pow / exp / sin / cos / atan2 are approximations; evaluated in double and rounded once (as the
+ * GPU does, vec3.h), so the restatement and the GPU agree bit for bit. */
+static inline float powr(float x, float y) { return (float)pow((double)x, (double)y); }
+static inline float expr(float x) { return (float)exp((double)x); }
+static inline float sinr(float x) { return (float)sin((double)x); }
+static inline float cosr(float x) { return (float)cos((double)x); }
+static inline float atan2r(float y, float x) { return (float)atan2((double)y, (double)x); }
+
 typedef struct { float x, y, z; } f3;
 static inline f3 mk(float x, float y, float z) { f3 r = {x, y, z}; return r; }
 static inline f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
@@ -78,7 +86,7 @@ static inline pair_out contact_pair(const or_contact_params* P, const or_particl
     if (slipSpeed > 1e-4f) {                                    /* :274 */
         f3 frictionDir = divs(tangentVel, slipSpeed);
         float torqueInput = fabsf(slipSpeed * P->torque_factor);
-        float frictionMag = powf(torqueInput, 1.25f);
+        float frictionMag = powr(torqueInput, 1.25f);
         frictionMag = fminf(frictionMag, 10.0f);
         float torqueRadiusScale = overlapFalloff * overlapFalloff;          /* pow(x, 2.0) :282 */
         float effectiveRadiusTorqueA = torqueRadiusScale * effectiveRadiusA * P->roll_mult;
@@ -124,8 +132,8 @@ static void anchor_push(float strength, f4 q, f3 anchorLocal, f3 desiredMove, in
     float effectiveness = fabsf(dot(cross(rotAxis, rWorld), desiredMove));
     if (!(effectiveness > 1e-6f)) return;
     float rotAngle = strength * effectiveness * 5.0f;
-    f4 rotQuat = {rotAxis.x * sinf(rotAngle * 0.5f), rotAxis.y * sinf(rotAngle * 0.5f),
-                  rotAxis.z * sinf(rotAngle * 0.5f), cosf(rotAngle * 0.5f)};
+    f4 rotQuat = {rotAxis.x * sinr(rotAngle * 0.5f), rotAxis.y * sinr(rotAngle * 0.5f),
+                  rotAxis.z * sinr(rotAngle * 0.5f), cosr(rotAngle * 0.5f)};
     add_q(acc, qdiff(qmul(rotQuat, q), q));
 }
 
@@ -171,14 +179,14 @@ static void bond_terms(const or_adhesion84* c, int n, const or_particle84* in, c
     /* relative orientation :541-582 */
     f4 currentRel = qmul(qconj(rotA), rotB);
     f4 correction = qmul(q4(c->initialRelOrientation), qconj(currentRel));
-    float correctionAngle = 2.0f * atan2f(len(qv(correction)), fabsf(correction.w));
+    float correctionAngle = 2.0f * atan2r(len(qv(correction)), fabsf(correction.w));
     if (correctionAngle > 1e-6f) {
         f3 axis = nrm(qv(correction));
         float ocs = constraintStrength * 2.0f;
         float angA = -ocs * correctionAngle * 0.5f;
         float angB = ocs * correctionAngle * 0.5f;
-        f4 rqA = {axis.x * sinf(angA * 0.5f), axis.y * sinf(angA * 0.5f), axis.z * sinf(angA * 0.5f), cosf(angA * 0.5f)};
-        f4 rqB = {axis.x * sinf(angB * 0.5f), axis.y * sinf(angB * 0.5f), axis.z * sinf(angB * 0.5f), cosf(angB * 0.5f)};
+        f4 rqA = {axis.x * sinr(angA * 0.5f), axis.y * sinr(angA * 0.5f), axis.z * sinr(angA * 0.5f), cosr(angA * 0.5f)};
+        f4 rqB = {axis.x * sinr(angB * 0.5f), axis.y * sinr(angB * 0.5f), axis.z * sinr(angB * 0.5f), cosr(angB * 0.5f)};
         add_q(t + 8, qdiff(qmul(rqA, rotA), rotA));
         add_q(t + 12, qdiff(qmul(rqB, rotB), rotB));
     }
@@ -312,8 +320,8 @@ int or_contact_step_bonds(const or_contact_params* P, int n, or_particle84* part
             vel = add(vel, divs(force, p.mass));
         }
         /* UpdateMotion :332-354 */
-        float linearDamping = expf(-p.drag * P->global_drag * dt);
-        float angularDamping = expf(-P->torque_damping * dt);
+        float linearDamping = expr(-p.drag * P->global_drag * dt);
+        float angularDamping = expr(-P->torque_damping * dt);
         vel = mul(vel, linearDamping);
         omg = mul(omg, angularDamping);
         pos = add(pos, mul(vel, dt));
@@ -334,11 +342,11 @@ int or_contact_step_bonds(const or_contact_params* P, int n, or_particle84* part
                          (float)TORQUE_SCALE);
         f3 angAcc = divs(torque, p.momentOfInertia);
         omg = add(omg, angAcc);
-        omg = mul(omg, expf(-P->torque_damping * dt));
+        omg = mul(omg, expr(-P->torque_damping * dt));
         float angle = len(mul(omg, dt));
         if (angle > 0.00001f) {
             f3 axis = nrm(omg);
-            float s = sinf(angle * 0.5f), c = cosf(angle * 0.5f);
+            float s = sinr(angle * 0.5f), c = cosr(angle * 0.5f);
             float dq[4] = {axis.x * s, axis.y * s, axis.z * s, c};
             const float* q = p.rotation;
             /* quat_mul(dq, q) :359-365 */

@@ -7,6 +7,9 @@
 // bond's four int terms to its own 64-byte record (coalesced, no atomics) and the particle pass
 // gathers them through a CSR incidence list (bonds.h, k_contact_finish). int32 sums are
 // associative, so the totals equal the atomic ones bit for bit, in any order.
+// Every rounding is the one written (no fused multiply-adds), as in the oracle: with the double-evaluated
+// intrinsics (vec3.h) the Model R step is bit-identical to oracle/contact_oracle.c.
+#pragma clang fp contract(off)
 #include "common.h"
 #include "vec3.h"
 
@@ -40,7 +43,7 @@ __device__ __forceinline__ void anchor_push(float strength, float4 q, f3 anchor_
     const float effectiveness = fabsf(dot(cross(axis, r_world), desired));
     if (!(effectiveness > 1e-6f)) return;
     const float angle = strength * effectiveness * 5.0f;
-    const float s = sinf(angle * 0.5f), c = cosf(angle * 0.5f);
+    const float s = sin_r(angle * 0.5f), c = cos_r(angle * 0.5f);
     const float4 rq = make_float4(axis.x * s, axis.y * s, axis.z * s, c);
     add_q(dq, qsub(quat_mul(rq, q), q));
 }
@@ -91,14 +94,14 @@ __global__ __launch_bounds__(BD_BLK) void k_bond_terms(BondSet bs, const int32_t
             // --- relative orientation :541-582
             const float4 currentRel = quat_mul(quat_conjugate(qA), qB);
             const float4 corr = quat_mul(bs.relq[b], quat_conjugate(currentRel));
-            const float correctionAngle = 2.0f * atan2f(len(xyz(corr)), fabsf(corr.w));
+            const float correctionAngle = 2.0f * atan2_r(len(xyz(corr)), fabsf(corr.w));
             if (correctionAngle > 1e-6f) {
                 const f3 axis = normalize(xyz(corr));
                 const float ocs = constraintStrength * 2.0f;
                 const float angA = -ocs * correctionAngle * 0.5f;
                 const float angB = ocs * correctionAngle * 0.5f;
-                const float sA = sinf(angA * 0.5f), cA = cosf(angA * 0.5f);
-                const float sB = sinf(angB * 0.5f), cB = cosf(angB * 0.5f);
+                const float sA = sin_r(angA * 0.5f), cA = cos_r(angA * 0.5f);
+                const float sB = sin_r(angB * 0.5f), cB = cos_r(angB * 0.5f);
                 add_q(dqA, qsub(quat_mul(make_float4(axis.x * sA, axis.y * sA, axis.z * sA, cA), qA), qA));
                 add_q(dqB, qsub(quat_mul(make_float4(axis.x * sB, axis.y * sB, axis.z * sB, cB), qB), qB));
             }

@@ -13,6 +13,9 @@
 // second time from b's side and sums the same truncated int3 terms. int32 addition is
 // associative, so the sum is bit-identical to the atomic one, with no atomics and no
 // ordering dependence.
+// Every rounding is the one written (no fused multiply-adds), as in the oracle: with the double-evaluated
+// intrinsics (vec3.h) the Model R step is bit-identical to oracle/contact_oracle.c.
+#pragma clang fp contract(off)
 #include "bonds.h"
 #include "common.h"
 #include "vec3.h"
@@ -48,7 +51,7 @@ __device__ __forceinline__ int contact_pair(const ContactConst& c, const Body& A
     if (!(slipSpeed > 1e-4f)) return 1;
     const f3 frictionDir = tangentVel / slipSpeed;
     const float torqueInput = fabsf(slipSpeed * c.torque_factor);
-    float frictionMag = powf(torqueInput, 1.25f);
+    float frictionMag = pow_r(torqueInput, 1.25f);
     frictionMag = fminf(frictionMag, 10.0f);
     const float torqueRadiusScale = overlapFalloff * overlapFalloff;   // pow(x, 2.0) :282
     const float effectiveRadiusTorqueA = torqueRadiusScale * effectiveRadiusA * c.roll_mult;
@@ -216,8 +219,8 @@ __device__ __forceinline__ void contact_finish(const ContactConst& c, int32_t pi
     const float dt = c.dt;
     f3 p = xyz(pa);
     v = apply_drag(c, pid, p, v, mass);
-    const float linearDamping = expf(-drag * c.global_drag * dt);
-    const float angularDamping = expf(-c.torque_damping * dt);
+    const float linearDamping = exp_r(-drag * c.global_drag * dt);
+    const float angularDamping = exp_r(-c.torque_damping * dt);
     v = v * linearDamping;
     w = w * angularDamping;
     p = p + v * dt;
@@ -234,12 +237,12 @@ __device__ __forceinline__ void contact_finish(const ContactConst& c, int32_t pi
     }
     const f3 torque = mk((float)(int32_t)tq[0], (float)(int32_t)tq[1], (float)(int32_t)tq[2]) / TORQUE_SCALE;
     w = w + torque / inertia;
-    w = w * expf(-c.torque_damping * dt);
+    w = w * exp_r(-c.torque_damping * dt);
     float4 q = qa;
     const float angle = len(w * dt);
     if (angle > 0.00001f) {
         const f3 axis = normalize(w);
-        const float s = sinf(angle * 0.5f), co = cosf(angle * 0.5f);
+        const float s = sin_r(angle * 0.5f), co = cos_r(angle * 0.5f);
         const float4 r = quat_mul(make_float4(axis.x * s, axis.y * s, axis.z * s, co), qa);
         const float l = sqrtf(r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w);
         q = make_float4(r.x / l, r.y / l, r.z / l, r.w / l);

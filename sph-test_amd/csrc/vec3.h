@@ -31,6 +31,15 @@ __device__ __forceinline__ float saturate(float x) { return x > 0.0f ? (x < 1.0f
 __device__ __forceinline__ f3 normalize(f3 a) { return a / len(a); }
 __device__ __forceinline__ f3 xyz(float4 v) { return {v.x, v.y, v.z}; }
 
+// HLSL's pow / exp / sin / cos / atan2 are approximations (D3D allows a few ulp). Model R evaluates
+// them in double and rounds once, exactly as the oracle does (oracle/contact_oracle.c): both are then
+// correctly rounded but for results within ~1e-16 of a float tie, so GPU and oracle agree bit for bit.
+__device__ __forceinline__ float pow_r(float x, float y) { return (float)pow((double)x, (double)y); }
+__device__ __forceinline__ float exp_r(float x) { return (float)exp((double)x); }
+__device__ __forceinline__ float sin_r(float x) { return (float)sin((double)x); }
+__device__ __forceinline__ float cos_r(float x) { return (float)cos((double)x); }
+__device__ __forceinline__ float atan2_r(float y, float x) { return (float)atan2((double)y, (double)x); }
+
 __device__ __forceinline__ int32_t ftoi(float x) {   // D3D ftoi: truncate, saturate, NaN -> 0
     if (x != x) return 0;
     if (x >= 2147483648.0f) return 2147483647;

@@ -2,11 +2,9 @@
 
 Reference: ApplyAdhesionConstraints / ApplyAdhesionDeltas (SimulateParticles.compute:424-607),
 dispatched between ApplySPHForces and the drag (ParticleSystemController.cs:284-310).
-Tolerances: the per-bond fixed-point terms are int32 (×1e6, round half to even); GPU and glibc
-sin/cos/atan2 and fp contraction differ in the last ulp, which moves a term by one LSB only
-when the product sits on a .5 boundary, so terms must match exactly except for a small
-fraction off by a few LSB. Particle state: v, ω rtol 1e-4, x 1e-5, q 1e-5 (as Model R's
-one-step parity in test_gpu_parity.py).
+Bit-exact: the per-bond fixed-point terms (int32, ×1e6, round half to even) and the particle state
+match the oracle exactly, because both sides round identically (no contraction; sin / cos / atan2 /
+pow / exp in double, rounded once; see vec3.h and oracle/contact_oracle.c).
 """
 import numpy as np
 import pytest
@@ -18,14 +16,11 @@ pytestmark = pytest.mark.gpu
 
 def _check_terms(got, ref):
     diff = np.abs(got.astype(np.int64) - ref.astype(np.int64))
-    assert (diff > 0).mean() < 1e-2, f"{(diff > 0).sum()} of {diff.size} terms differ"
-    assert diff.max() <= 4, f"max term diff {diff.max()}"
+    assert diff.max() == 0, f"{(diff > 0).sum()} of {diff.size} terms differ (max {diff.max()})"
 
 
 def _check_parts(got, ref):
-    for f, rtol, atol in [("velocity", 1e-4, 1e-4), ("angularVelocity", 1e-4, 1e-3), ("position", 1e-5, 1e-5),
-                          ("rotation", 1e-4, 1e-5)]:
-        np.testing.assert_allclose(got[f], ref[f], rtol=rtol, atol=atol, err_msg=f)
+    assert got.tobytes() == ref.tobytes()
 
 
 class _Manager:
@@ -55,9 +50,7 @@ def test_adhesion_one_step(pkg, oracle, n):
     assert np.abs(terms_ref).max() > 1000           # the case exercises every term
     _check_terms(terms, terms_ref)
     _check_parts(got, ref)
-    tq = ctl.context.torque_int()
-    diff = np.abs(tq.astype(np.int64) - tq_ref)
-    assert (diff > 0).mean() < 1e-3 and diff.max() <= 4
+    assert np.array_equal(ctl.context.torque_int(), tq_ref)
     ctl.OnDestroy()
 
 
@@ -90,7 +83,6 @@ def test_adhesion_cap_and_removal(pkg, oracle):
                                           conns[:100].view(oracle.ADHESION84))
     got = ctl.GetParticles()
     _check_parts(got, ref)
-    assert got["rotation"][5][3] == pytest.approx(ref["rotation"][5][3], abs=1e-6)
     mgr.conns = conns[:0]
     ctl.SetParticles(parts)
     ctl.Update(dt)
