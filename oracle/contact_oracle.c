@@ -24,7 +24,8 @@
 
 /* HLSL pow / exp / sin / cos / atan2 are approximations; evaluated in double and rounded once (as the
  * GPU does, vec3.h), so the restatement and the GPU agree bit for bit. */
-static inline float powr(float x, float y) { return (float)pow((double)x, (double)y); }
+/* pow(x, 1.25), x >= 0 (compute:279, the model's only pow): x * sqrt(sqrt(x)) in double */
+static inline float pow125r(float x) { double d = (double)x; return (float)(d * sqrt(sqrt(d))); }
 static inline float expr(float x) { return (float)exp((double)x); }
 static inline float sinr(float x) { return (float)sin((double)x); }
 static inline float cosr(float x) { return (float)cos((double)x); }
@@ -86,7 +87,7 @@ static inline pair_out contact_pair(const or_contact_params* P, const or_particl
     if (slipSpeed > 1e-4f) {                                    /* :274 */
         f3 frictionDir = divs(tangentVel, slipSpeed);
         float torqueInput = fabsf(slipSpeed * P->torque_factor);
-        float frictionMag = powr(torqueInput, 1.25f);
+        float frictionMag = pow125r(torqueInput);
         frictionMag = fminf(frictionMag, 10.0f);
         float torqueRadiusScale = overlapFalloff * overlapFalloff;          /* pow(x, 2.0) :282 */
         float effectiveRadiusTorqueA = torqueRadiusScale * effectiveRadiusA * P->roll_mult;

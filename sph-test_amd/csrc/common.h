@@ -242,8 +242,9 @@ void launch_keys(const float4* pos, int32_t n, const int32_t* id, int32_t n_acti
 // cell_start[k] = lower_bound(sorted keys, k) for k = 0..ncells, every cell written once:
 // each particle boundary fills the cells up to its key; gaps longer than CS_SHORT cells are
 // queued (gap list + counter, zeroed by the call) and filled by whole workgroups.
+// gap_count: two counters used in turn (*par flips); each call zeroes the other one for the next call
 void launch_cell_start(const uint32_t* sorted_keys, int32_t n, uint32_t* cs, uint32_t ncells,
-                       uint4* gaps, uint32_t* gap_count, hipStream_t s);
+                       uint4* gaps, uint32_t* gap_count, int* par, hipStream_t s);
 // Model R's slot arrays (pos, vel, omg, rot, aux; id, mode) gathered by one launch
 struct GatherR {
     const float4* f4[5];

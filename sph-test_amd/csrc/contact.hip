@@ -51,7 +51,7 @@ __device__ __forceinline__ int contact_pair(const ContactConst& c, const Body& A
     if (!(slipSpeed > 1e-4f)) return 1;
     const f3 frictionDir = tangentVel / slipSpeed;
     const float torqueInput = fabsf(slipSpeed * c.torque_factor);
-    float frictionMag = pow_r(torqueInput, 1.25f);
+    float frictionMag = pow125_r(torqueInput);   // pow(x, 1.25) :279
     frictionMag = fminf(frictionMag, 10.0f);
     const float torqueRadiusScale = overlapFalloff * overlapFalloff;   // pow(x, 2.0) :282
     const float effectiveRadiusTorqueA = torqueRadiusScale * effectiveRadiusA * c.roll_mult;

@@ -34,8 +34,10 @@ constexpr uint32_t CS_CHUNK = 8192;   // long gaps are queued in chunks so no wo
 // thread i in [0, n]: cells (key[i-1], key[i]] start at slot i (key[-1] = -1, key[n] = ncells)
 __global__ __launch_bounds__(BLK) void k_cell_start(const uint32_t* __restrict__ sk, int32_t n,
                                                     uint32_t* __restrict__ cs, uint32_t ncells,
-                                                    uint4* __restrict__ gaps, uint32_t* __restrict__ gap_count) {
+                                                    uint4* __restrict__ gaps, uint32_t* __restrict__ gap_count,
+                                                    uint32_t* __restrict__ gap_next) {
     const int32_t i = blockIdx.x * BLK + threadIdx.x;
+    if (i == 0) *gap_next = 0u;   // the next call's counter (ping-pong: no memset launch)
     if (i > n) return;
     const int64_t kp = i > 0 ? (int64_t)sk[i - 1] : -1;
     const int64_t kc = i < n ? (int64_t)sk[i] : (int64_t)ncells;
@@ -218,10 +220,12 @@ void launch_keys(const float4* pos, int32_t n, const int32_t* id, int32_t n_acti
     if (n > 0) k_keys<<<nblk(n), BLK, 0, s>>>(pos, n, id, n_active_id, g, keys, window_sentinel);
 }
 void launch_cell_start(const uint32_t* sk, int32_t n, uint32_t* cs, uint32_t ncells, uint4* gaps,
-                       uint32_t* gap_count, hipStream_t s) {
-    (void)hipMemsetAsync(gap_count, 0, sizeof(uint32_t), s);
-    k_cell_start<<<nblk((int64_t)n + 1), BLK, 0, s>>>(sk, n, cs, ncells, gaps, gap_count);
-    k_cell_start_gaps<<<1024, BLK, 0, s>>>(gaps, gap_count, cs);
+                       uint32_t* gap_count, int* par, hipStream_t s) {
+    uint32_t* cur = gap_count + *par;
+    uint32_t* next = gap_count + (1 - *par);
+    k_cell_start<<<nblk((int64_t)n + 1), BLK, 0, s>>>(sk, n, cs, ncells, gaps, cur, next);
+    k_cell_start_gaps<<<1024, BLK, 0, s>>>(gaps, cur, cs);
+    *par = 1 - *par;
 }
 void launch_gather_r(const uint32_t* perm, const GatherR& g, int32_t n, hipStream_t s) {
     if (n > 0) k_gather_r<<<nblk(n), BLK, 0, s>>>(perm, g, n);

@@ -113,7 +113,8 @@ struct sph_ctx {
     int32_t rng[10] = {0};
     int32_t send_counts[2] = {0, 0};
     uint32_t* sblk = nullptr;    // compaction block counts [2][nblk]
-    uint32_t* sdev = nullptr;    // small device scratch (totals, picks)
+    uint32_t* sdev = nullptr;    // small device scratch (totals, picks; [8], [9]: cell-start gap counters)
+    int gap_par = 0;             // which of sdev[8], sdev[9] the next cell-start call uses
     uint32_t* rng_host = nullptr;   // pinned: column-start picks of the last assemble
     hipEvent_t rng_ev = nullptr;    // recorded after their device->host copy
     bool rng_pending = false;       // rng[] / o0 / o1 not yet updated from rng_host
@@ -204,6 +205,8 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
     AL(keys, n); AL(keys2, n); AL(vals, n); AL(vals2, n);
     AL(hist, radix_hist_elems((int32_t)n)); AL(bin_total, 256);
     AL(sblk, 2 * (size_t)slab_compact_blocks(0, (int32_t)n) + 2); AL(sdev, 16);
+    HIPCHK(hipMemset(ctx->sdev, 0, 16 * sizeof(uint32_t)));
+    ctx->gap_par = 0;
     if (is_contact(ctx)) {
         AL(omg, n); AL(rot, n); AL(aux, n); AL(omg2, n); AL(rot2, n); AL(aux2, n);
         AL(mode, n); AL(mode2, n); AL(torque, 3 * n); AL(slot_of, n);
@@ -395,7 +398,7 @@ int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id, const uint32_t** sorted_
     }
     {
         KTimer t(ctx, "cell_start", 4.0 * (ctx->grid.ncells + 1));
-        launch_cell_start(sk, n, ctx->cs, ctx->grid.ncells, ctx->gaps, ctx->sdev + 8, ctx->stream);
+        launch_cell_start(sk, n, ctx->cs, ctx->grid.ncells, ctx->gaps, ctx->sdev + 8, &ctx->gap_par, ctx->stream);
     }
     if (sorted_keys) *sorted_keys = sk;
     return SPH_OK;
@@ -1597,7 +1600,7 @@ int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void
         }
         {
             KTimer t(ctx, "cell_start", 4.0 * (ctx->grid.ncells + 1));
-            launch_cell_start(sk, (int32_t)n, ctx->cs, ctx->grid.ncells, ctx->gaps, ctx->sdev + 8, s);
+            launch_cell_start(sk, (int32_t)n, ctx->cs, ctx->grid.ncells, ctx->gaps, ctx->sdev + 8, &ctx->gap_par, s);
         }
         // the sorted keys of the new slot order: the next step's old keys
         if (ctx->resort_mode != 0 && n > 0)

@@ -34,7 +34,13 @@ __device__ __forceinline__ f3 xyz(float4 v) { return {v.x, v.y, v.z}; }
 // HLSL's pow / exp / sin / cos / atan2 are approximations (D3D allows a few ulp). Model R evaluates
 // them in double and rounds once, exactly as the oracle does (oracle/contact_oracle.c): both are then
 // correctly rounded but for results within ~1e-16 of a float tie, so GPU and oracle agree bit for bit.
-__device__ __forceinline__ float pow_r(float x, float y) { return (float)pow((double)x, (double)y); }
+// pow(x, 1.25) for x >= 0 (compute:279 is the only pow): x·sqrt(sqrt(x)) in double, every step
+// correctly rounded on both sides, so it matches the oracle bit for bit at a fraction of a general
+// double pow's cost (the contact pass evaluates it twice per touching pair)
+__device__ __forceinline__ float pow125_r(float x) {
+    const double d = (double)x;
+    return (float)(d * sqrt(sqrt(d)));
+}
 __device__ __forceinline__ float exp_r(float x) { return (float)exp((double)x); }
 __device__ __forceinline__ float sin_r(float x) { return (float)sin((double)x); }
 __device__ __forceinline__ float cos_r(float x) { return (float)cos((double)x); }
