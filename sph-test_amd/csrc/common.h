@@ -231,9 +231,17 @@ struct CsPick {
     uint32_t* out;
     uint32_t* out_host;
 };
+// Model R's further slot arrays, moved with pos / vel / id by the re-sort (all null for Model S)
+struct ResortExtra {
+    const float4 *omg, *rot, *aux;
+    const int32_t* mode;
+    float4 *omg_o, *rot_o, *aux_o;
+    int32_t* mode_o;
+};
 void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* count,
                    uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,
-                   uint32_t* sk_o, hipStream_t s, CsPick pick = CsPick{{0}, 0, nullptr, nullptr});
+                   uint32_t* sk_o, hipStream_t s, CsPick pick = CsPick{{0}, 0, nullptr, nullptr},
+                   ResortExtra ex = ResortExtra{});
 
 // grid / data movement (grid.hip)
 // window_sentinel (slab): a particle outside the held columns gets key ncells (sorts last)
@@ -362,7 +370,7 @@ void launch_contact_step(const float4* pos, const float4* vel, const float4* omg
                          const float4* aux, const int32_t* id, const uint32_t* cs, int32_t n_active,
                          int32_t n, GridDesc g, ContactConst c, float4* pos_o, float4* vel_o,
                          float4* omg_o, float4* rot_o, int32_t* torque_o, uint32_t* keys_o, int team,
-                         hipStream_t s);
+                         MoverSink mv, hipStream_t s);
 void launch_contact_forces(const float4* pos, const float4* vel, const float4* omg, const int32_t* id,
                            const uint32_t* cs, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
                            float4* vel_o, float4* omg_o, int32_t* torque_o, int32_t* slot_of, int team,
@@ -370,7 +378,7 @@ void launch_contact_forces(const float4* pos, const float4* vel, const float4* o
 void launch_contact_finish(const float4* pos, const float4* rot, const float4* aux, const int32_t* id,
                            const int32_t* torque, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
                            BondView b, float4* vel_io, float4* omg_io, float4* pos_o, float4* rot_o,
-                           uint32_t* keys_o, hipStream_t s);
+                           uint32_t* keys_o, MoverSink mv, hipStream_t s);
 // ApplyAdhesionConstraints (compute:424-584), one lane per bond: reads the start-of-step
 // position and rotation and the post-contact velocity, writes the bond's four int terms.
 void launch_bond_terms(BondSet bs, const int32_t* slot_of, int32_t n, const float4* pos, const float4* vel1,

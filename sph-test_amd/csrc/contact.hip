@@ -256,7 +256,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step(
     const float4* __restrict__ rot, const float4* __restrict__ aux, const int32_t* __restrict__ id,
     const uint32_t* __restrict__ cs, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
     float4* __restrict__ pos_o, float4* __restrict__ vel_o, float4* __restrict__ omg_o,
-    float4* __restrict__ rot_o, int32_t* __restrict__ torque_o, uint32_t* __restrict__ keys_o) {
+    float4* __restrict__ rot_o, int32_t* __restrict__ torque_o, uint32_t* __restrict__ keys_o, MoverSink mv) {
     const int32_t a = blockIdx.x * CT_BLK + threadIdx.x;
     if (a >= n) return;
     const float4 pa = pos[a], va = vel[a], wa = omg[a], qa = rot[a];
@@ -265,6 +265,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step(
         pos_o[a] = pa; vel_o[a] = make_float4(v.x, v.y, v.z, va.w); omg_o[a] = wa; rot_o[a] = qa;
         if (torque_o) { torque_o[3 * a] = 0; torque_o[3 * a + 1] = 0; torque_o[3 * a + 2] = 0; }
         keys_o[a] = g.ncells;
+        append_mover(mv, a, g.ncells);
         return;
     }
     f3 v, w;
@@ -281,6 +282,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step(
         torque_o[3 * a] = (int32_t)tq[0]; torque_o[3 * a + 1] = (int32_t)tq[1]; torque_o[3 * a + 2] = (int32_t)tq[2];
     }
     keys_o[a] = cell_key(g, p.x, p.y, p.z);
+    append_mover(mv, a, keys_o[a]);
 }
 
 // k_contact_step with T lanes per target (contact_accumulate_team); team lane 0 finishes and writes.
@@ -290,7 +292,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step_team(
     const float4* __restrict__ rot, const float4* __restrict__ aux, const int32_t* __restrict__ id,
     const uint32_t* __restrict__ cs, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
     float4* __restrict__ pos_o, float4* __restrict__ vel_o, float4* __restrict__ omg_o,
-    float4* __restrict__ rot_o, int32_t* __restrict__ torque_o, uint32_t* __restrict__ keys_o) {
+    float4* __restrict__ rot_o, int32_t* __restrict__ torque_o, uint32_t* __restrict__ keys_o, MoverSink mv) {
     const int32_t a = blockIdx.x * (CT_BLK / T) + (int32_t)(threadIdx.x / T);
     const bool lead = (threadIdx.x & (T - 1)) == 0;
     if (a >= n) return;                                                      // team-uniform
@@ -302,6 +304,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step_team(
         pos_o[a] = pa; vel_o[a] = make_float4(v.x, v.y, v.z, va.w); omg_o[a] = wa; rot_o[a] = qa;
         if (torque_o) { torque_o[3 * a] = 0; torque_o[3 * a + 1] = 0; torque_o[3 * a + 2] = 0; }
         keys_o[a] = g.ncells;
+        append_mover(mv, a, g.ncells);
         return;
     }
     f3 v, w;
@@ -319,6 +322,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step_team(
         torque_o[3 * a] = (int32_t)tq[0]; torque_o[3 * a + 1] = (int32_t)tq[1]; torque_o[3 * a + 2] = (int32_t)tq[2];
     }
     keys_o[a] = cell_key(g, p.x, p.y, p.z);
+    append_mover(mv, a, keys_o[a]);
 }
 
 // k_contact_forces with T lanes per target.
@@ -370,7 +374,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_finish(
     const float4* __restrict__ pos, const float4* __restrict__ rot, const float4* __restrict__ aux,
     const int32_t* __restrict__ id, const int32_t* __restrict__ torque, int32_t n_active, int32_t n,
     GridDesc g, ContactConst c, BondView b, float4* __restrict__ vel_io, float4* __restrict__ omg_io,
-    float4* __restrict__ pos_o, float4* __restrict__ rot_o, uint32_t* __restrict__ keys_o) {
+    float4* __restrict__ pos_o, float4* __restrict__ rot_o, uint32_t* __restrict__ keys_o, MoverSink mv) {
     const int32_t a = blockIdx.x * CT_BLK + threadIdx.x;
     if (a >= n) return;
     const float4 pa = pos[a], va = vel_io[a], wa = omg_io[a], qa = rot[a];
@@ -380,6 +384,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_finish(
         vel_io[a] = make_float4(v.x, v.y, v.z, va.w);
         pos_o[a] = pa; rot_o[a] = qa;
         keys_o[a] = g.ncells;
+        append_mover(mv, a, g.ncells);
         return;
     }
     f3 v = xyz(va);
@@ -393,6 +398,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_finish(
     omg_io[a] = make_float4(w.x, w.y, w.z, wa.w);
     rot_o[a] = q;
     keys_o[a] = cell_key(g, p.x, p.y, p.z);
+    append_mover(mv, a, keys_o[a]);
 }
 
 // Lanes per target: enough teams to fill the chip (256 CUs × 8 waves × 64 lanes ≈ 131k lanes) without
@@ -409,20 +415,20 @@ void launch_contact_step(const float4* pos, const float4* vel, const float4* omg
                          const float4* aux, const int32_t* id, const uint32_t* cs, int32_t n_active,
                          int32_t n, GridDesc g, ContactConst c, float4* pos_o, float4* vel_o,
                          float4* omg_o, float4* rot_o, int32_t* torque_o, uint32_t* keys_o, int team,
-                         hipStream_t s) {
+                         MoverSink mv, hipStream_t s) {
     if (n <= 0) return;
     switch (contact_team(n, team)) {
 #define SPH_CT_STEP(T)                                                                                        \
     case T:                                                                                                   \
         k_contact_step_team<T><<<(n + CT_BLK / T - 1) / (CT_BLK / T), CT_BLK, 0, s>>>(                          \
-            pos, vel, omg, rot, aux, id, cs, n_active, n, g, c, pos_o, vel_o, omg_o, rot_o, torque_o, keys_o);  \
+            pos, vel, omg, rot, aux, id, cs, n_active, n, g, c, pos_o, vel_o, omg_o, rot_o, torque_o, keys_o, mv);  \
         break;
         SPH_CT_STEP(64)
         SPH_CT_STEP(16)
 #undef SPH_CT_STEP
     default:
         k_contact_step<<<(n + CT_BLK - 1) / CT_BLK, CT_BLK, 0, s>>>(pos, vel, omg, rot, aux, id, cs, n_active, n, g,
-                                                                    c, pos_o, vel_o, omg_o, rot_o, torque_o, keys_o);
+                                                                    c, pos_o, vel_o, omg_o, rot_o, torque_o, keys_o, mv);
     }
 }
 
@@ -449,10 +455,10 @@ void launch_contact_forces(const float4* pos, const float4* vel, const float4* o
 void launch_contact_finish(const float4* pos, const float4* rot, const float4* aux, const int32_t* id,
                            const int32_t* torque, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
                            BondView b, float4* vel_io, float4* omg_io, float4* pos_o, float4* rot_o,
-                           uint32_t* keys_o, hipStream_t s) {
+                           uint32_t* keys_o, MoverSink mv, hipStream_t s) {
     if (n > 0)
         k_contact_finish<<<(n + CT_BLK - 1) / CT_BLK, CT_BLK, 0, s>>>(pos, rot, aux, id, torque, n_active, n, g, c,
-                                                                      b, vel_io, omg_io, pos_o, rot_o, keys_o);
+                                                                      b, vel_io, omg_io, pos_o, rot_o, keys_o, mv);
 }
 
 }  // namespace sph

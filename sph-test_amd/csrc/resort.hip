@@ -37,6 +37,15 @@ static __device__ __forceinline__ uint64_t comp(uint32_t key, uint32_t idx) { re
 
 static __device__ __forceinline__ bool asm_rec(const AsmSrc& a, int32_t x) { return x < a.nl || x >= a.nre; }
 
+// Model R's other slot arrays (single domain: slot x is x)
+static __device__ __forceinline__ void move_extra(const ResortExtra& ex, uint32_t x, uint32_t dst) {
+    if (!ex.omg) return;
+    ex.omg_o[dst] = ex.omg[x];
+    ex.rot_o[dst] = ex.rot[x];
+    ex.aux_o[dst] = ex.aux[x];
+    ex.mode_o[dst] = ex.mode[x];
+}
+
 static __device__ __forceinline__ uint32_t asm_sk(const AsmSrc& a, int32_t x) {
     return asm_rec(a, x) ? a.skr[x] : a.sk[x + a.o_off];
 }
@@ -152,7 +161,8 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
 __global__ __launch_bounds__(MV_BLK) void k_mv_place(const uint32_t* __restrict__ mtotal,
                                                      const uint32_t* __restrict__ cs_old, ResortScratch w, AsmSrc src,
                                                      float4* __restrict__ pos_o, float4* __restrict__ vel_o,
-                                                     int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o) {
+                                                     int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o,
+                                                     ResortExtra ex) {
     const uint32_t m = *mtotal;
     for (uint32_t r = blockIdx.x * MV_BLK + threadIdx.x; r < m; r += gridDim.x * MV_BLK) {
         const uint32_t x = mv_slot(w, w.mi[r]), k = w.mk[r];
@@ -167,6 +177,7 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_place(const uint32_t* __restrict_
         vel_o[dst] = v;
         id_o[dst] = pid;
         sk_o[dst] = k;
+        move_extra(ex, x, dst);
         w.ms[rk] = comp(k, x);
         w.mx[ri] = x;
         w.mos[ri] = w.mo[r];   // old keys by slot: ascending
@@ -216,7 +227,7 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
                                                      float4* __restrict__ pos_o,
                                                      float4* __restrict__ vel_o, int32_t* __restrict__ id_o,
                                                      uint32_t* __restrict__ sk_o, int32_t nb, uint32_t* __restrict__ cs,
-                                                     uint32_t ncells, CsPick pick) {
+                                                     uint32_t ncells, CsPick pick, ResortExtra ex) {
     __shared__ uint32_t wc[MV_BLK / 64];
     __shared__ uint32_t b[4];
     if ((int32_t)blockIdx.x >= nb) {   // the cell-start workgroups
@@ -253,6 +264,7 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
     vel_o[dst] = v;
     id_o[dst] = pid;
     sk_o[dst] = ko;
+    move_extra(ex, (uint32_t)i, dst);
 }
 
 // The slab step's halo records: new keys (window sentinel, as k_keys) and old keys moved into this
@@ -339,14 +351,14 @@ void launch_slab_rec(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base, uint3
 
 void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* count,
                    uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,
-                   uint32_t* sk_o, hipStream_t s, CsPick pick) {
+                   uint32_t* sk_o, hipStream_t s, CsPick pick, ResortExtra ex) {
     if (n <= 0) return;
     const int32_t nb = (n + MV_BLK - 1) / MV_BLK;
     k_mv_rank<<<MV_RANK_GRID, MV_BLK, 0, s>>>(count, count_other, cs, w);
-    k_mv_place<<<std::min(nb, 1024), MV_BLK, 0, s>>>(count, cs, w, src, pos_o, vel_o, id_o, sk_o);
+    k_mv_place<<<std::min(nb, 1024), MV_BLK, 0, s>>>(count, cs, w, src, pos_o, vel_o, id_o, sk_o, ex);
     // + the cell-start update, after every reader of cs_old (k_mv_rank, k_mv_place)
     const int32_t ncs = (int32_t)((ncells + MV_CS_CELLS) / MV_CS_CELLS);
-    k_mv_merge<<<nb + ncs, MV_BLK, 0, s>>>(src, n, count, w, pos_o, vel_o, id_o, sk_o, nb, cs, ncells, pick);
+    k_mv_merge<<<nb + ncs, MV_BLK, 0, s>>>(src, n, count, w, pos_o, vel_o, id_o, sk_o, nb, cs, ncells, pick, ex);
 }
 
 }  // namespace sph

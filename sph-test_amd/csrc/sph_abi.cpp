@@ -212,10 +212,12 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
         AL(mode, n); AL(mode2, n); AL(torque, 3 * n); AL(slot_of, n);
     } else {
         AL(rp, n);
-        AL(sk_cur, n); AL(sk_next, n);
-        AL(mv_mi, n); AL(mv_mk, n); AL(mv_mo, n); AL(mv_rank, 3 * n); AL(mv_mx, n); AL(mv_mos, n); AL(mv_ms, n);
-        AL(mv_count, 2);
     }
+    // incremental re-sort (both models)
+    AL(sk_cur, n); AL(sk_next, n);
+    AL(mv_mi, n); AL(mv_mk, n); AL(mv_mo, n); AL(mv_rank, 3 * n); AL(mv_mx, n); AL(mv_mos, n); AL(mv_ms, n);
+    AL(mv_count, 2);
+    HIPCHK(hipMemset(ctx->mv_count, 0, 2 * sizeof(uint32_t)));
 #undef AL
     ctx->staging_bytes = n * 84;
     HIPCHK(hipMalloc(&ctx->staging, ctx->staging_bytes));
@@ -546,11 +548,46 @@ int32_t contact_active(const sph_ctx* c) {
     return a;
 }
 
+// Model R's sort: the incremental re-sort (movers appended by the previous contact pass) while the
+// previous step's sorted keys describe the slot order, else the full sort. Both give the same
+// permutation (tests/test_gpu_resort.py), so results never depend on the choice.
+int sort_contact(sph_ctx* ctx, int32_t act) {
+    const int32_t n = ctx->n;
+    const bool many = ctx->resort_mode == 1 && *(volatile uint32_t*)ctx->mv_host > resort_limit(n);
+    if (ctx->resort_mode != 0 && !many && ctx->keys_valid && ctx->keys_active == act && ctx->sk_valid && n > 0) {
+        KTimer t(ctx, "resort", (double)n * (2 * 4 + 2 * 88));
+        const int used = ctx->mv_par;
+        const ResortExtra ex{ctx->omg, ctx->rot, ctx->aux, ctx->mode, ctx->omg2, ctx->rot2, ctx->aux2, ctx->mode2};
+        launch_resort(asm_plain(ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->keys, n), ctx->cs, ctx->grid.ncells, n,
+                      ctx->mv_count + used, ctx->mv_count + (1 - used), resort_scratch(ctx), ctx->pos2, ctx->vel2,
+                      ctx->id2, ctx->sk_next, ctx->stream, CsPick{{0}, 0, nullptr, nullptr}, ex);
+        ctx->mv_par = 1 - used;
+        swap_sv(ctx);
+        std::swap(ctx->id, ctx->id2);
+        std::swap(ctx->omg, ctx->omg2);
+        std::swap(ctx->rot, ctx->rot2);
+        std::swap(ctx->aux, ctx->aux2);
+        std::swap(ctx->mode, ctx->mode2);
+        std::swap(ctx->sk_cur, ctx->sk_next);
+        return SPH_OK;
+    }
+    const uint32_t* sk = nullptr;
+    int r = sort_and_reorder(ctx, act, &sk);
+    if (r != SPH_OK) return r;
+    if (ctx->resort_mode != 0 && n > 0) {
+        HIPCHK(hipMemcpyAsync(ctx->sk_cur, sk, (size_t)n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+        HIPCHK(hipMemsetAsync(ctx->mv_count, 0, 2 * sizeof(uint32_t), ctx->stream));
+    }
+    ctx->sk_valid = ctx->resort_mode != 0;
+    return SPH_OK;
+}
+
 int step_contact(sph_ctx* ctx, float dt) {
     const int32_t n = ctx->n;
     const int32_t act = contact_active(ctx);
-    int r = sort_and_reorder(ctx, act);
+    int r = sort_contact(ctx, act);
     if (r != SPH_OK) return r;
+    const MoverSink mv = mover_sink(ctx);
     const sph_params& p = ctx->prm;
     ContactConst c{};
     c.dt = dt;
@@ -569,7 +606,7 @@ int step_contact(sph_ctx* ctx, float dt) {
     if (ctx->nbonds == 0) {
         KTimer t(ctx, "contact_step", (double)n * (2 * 64 + 4 + 12 + 4));
         launch_contact_step(ctx->pos, ctx->vel, ctx->omg, ctx->rot, ctx->aux, ctx->id, ctx->cs, act, n, ctx->grid,
-                            c, ctx->pos2, ctx->vel2, ctx->omg2, ctx->rot2, ctx->torque, ctx->keys, ctx->ct_team,
+                            c, ctx->pos2, ctx->vel2, ctx->omg2, ctx->rot2, ctx->torque, ctx->keys, ctx->ct_team, mv,
                             ctx->stream);
     } else {
         // adhesion (controller:284-310): forces, bond terms, then deltas + drag + motion + rotation
@@ -589,9 +626,11 @@ int step_contact(sph_ctx* ctx, float dt) {
             KTimer t(ctx, "contact_finish", (double)n * (5 * 16 + 4 + 12 + 8 + 4 * 16 + 4) + 4.0 * ctx->nbonds * 36);
             BondView bv{ctx->nbonds, ctx->b_index_n, ctx->b_off, ctx->b_ent, ctx->b_terms};
             launch_contact_finish(ctx->pos, ctx->rot, ctx->aux, ctx->id, ctx->torque, act, n, ctx->grid, c, bv,
-                                  ctx->vel2, ctx->omg2, ctx->pos2, ctx->rot2, ctx->keys, ctx->stream);
+                                  ctx->vel2, ctx->omg2, ctx->pos2, ctx->rot2, ctx->keys, mv, ctx->stream);
         }
     }
+    if (mv.sk && (ctx->steps & 7) == 0)   // the mover count for the next steps' sort choice (no wait)
+        HIPCHK(hipMemcpyAsync(ctx->mv_host, mv.count, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
     swap_sv(ctx);
     std::swap(ctx->omg, ctx->omg2);
     std::swap(ctx->rot, ctx->rot2);

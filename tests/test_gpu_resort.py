@@ -127,3 +127,44 @@ def test_resort_adaptive_falls_back_when_many_move(pkg, monkeypatch):
         assert ks["resort"]["launches"] == 20 and ks["radix_sort"]["launches"] == 1
     finally:
         quiet.close()
+
+
+# ------------------------------------------------------------------ Model R
+def _contact_run(pkg, monkeypatch, flag, parts, steps, conns=None, change_active=None):
+    from test_gpu_contact_team import _Manager
+    monkeypatch.setenv("SPH_RESORT", flag)
+    ctl = pkg.ParticleSystemController(particleCount=len(parts))
+    if conns is not None:
+        ctl.adhesionManager = _Manager(conns)
+    ctl.Start(parts.copy())
+    ctl.drag.selectedID = 3
+    ctl.drag.targetPosition = (2.0, 1.0, -1.0)
+    ctl.drag.strength = 50.0
+    for s in range(steps):
+        if change_active is not None and s == steps // 2:
+            ctl.activeParticleCount = change_active
+        ctl.Update(0.01)
+    out = (ctl.GetParticles().tobytes(), ctl.context.torque_int().tobytes(), ctl.context.sorted_ids().tobytes(),
+           ctl.context.cell_start().tobytes(), ctl.context.kernel_stats() if hasattr(ctl.context, "kernel_stats") else {})
+    ctl.OnDestroy()
+    monkeypatch.delenv("SPH_RESORT")
+    return out
+
+
+@pytest.mark.parametrize("case", ["plain", "bonds", "active_change"])
+def test_resort_bitwise_contact(pkg, monkeypatch, case):
+    """Model R: the incremental re-sort (movers appended by the contact pass; all seven slot arrays
+    moved) against the full sort, bit for bit over 20 steps, with drag, adhesion bonds, and a change
+    of activeParticleCount mid-run (which forces one full sort)."""
+    from adhesion_cases import bonded_sphere
+    from test_gpu_parity import random_sphere
+    conns = None
+    if case == "bonds":
+        parts, conns = bonded_sphere(pkg.PARTICLE84, pkg.ADHESION84, 2048, seed=21)
+    else:
+        parts = random_sphere(pkg.PARTICLE84, 4096, seed=21)
+    act = 3000 if case == "active_change" else None
+    full = _contact_run(pkg, monkeypatch, "0", parts, 20, conns, act)
+    inc = _contact_run(pkg, monkeypatch, "2", parts, 20, conns, act)
+    for a, b, what in zip(full[:4], inc[:4], ("particles", "torque", "sorted ids", "cell starts")):
+        assert a == b, what
