@@ -196,6 +196,7 @@ int sph_read_rotations(sph_ctx* ctx, float* xyzw, int32_t count);
 int sph_read_velocities(sph_ctx* ctx, float* xyz, int32_t count);
 int sph_read_angular_velocities(sph_ctx* ctx, float* xyz, int32_t count);
 int sph_read_density(sph_ctx* ctx, float* rho, int32_t count);   /* Model S, pass-1 ρ */
+int sph_read_pressure_term(sph_ctx* ctx, float* prho, int32_t count);   /* Model S, pass-1 P/ρ² */
 int sph_synchronize(sph_ctx* ctx);
 
 /* replaces: AsyncGPUReadback.Request(buffer, callback) + r.GetData<T>() (controller:1115-1159).
@@ -230,6 +231,11 @@ int sph_reset_kernel_stats(sph_ctx* ctx);
 int sph_read_sorted_ids(sph_ctx* ctx, int32_t* ids, int32_t count);
 int sph_read_cell_start(sph_ctx* ctx, uint32_t* cell_start, int32_t count);
 int sph_read_torque_int(sph_ctx* ctx, int32_t* xyz, int32_t count);  /* Model R, index order */
+/* Model S neighbour passes: how often a workgroup left the LDS-staged fast path since the last
+ * reset (sparse or splashing regions): [0] density planes processed row by row in chunks, [1] density
+ * rows gathered straight from global memory, [2] / [3] the same for the force pass. reset != 0
+ * zeroes them after the read. */
+int sph_read_path_counts(sph_ctx* ctx, uint32_t counts[4], int32_t reset);
 /* stable LSD radix sort of (key, index) on the device: the sort of the step, exposed for
  * bit-exact parity tests. perm[i] = source index of sorted slot i. */
 int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int32_t key_bits,

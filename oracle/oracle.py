@@ -84,6 +84,12 @@ def lib():
         L.or_sph_derive.argtypes = [P(OrSphParams)]
         L.or_sph_step.argtypes = [P(OrSphParams), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                   C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.or_sph_step_diag.argtypes = [P(OrSphParams), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_int]
+        L.or_sph_force_range_diag.argtypes = [P(OrSphParams), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                              C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_float,
+                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         L.or_sph_lattice.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
                                      C.c_float, C.c_float, C.c_uint32, C.c_float, C.c_void_p]
         L.or_contact_step.argtypes = [P(OrContactParams), C.c_int, C.c_void_p, C.c_void_p, C.c_int]
@@ -137,6 +143,42 @@ def sph_step(p: OrSphParams, pos, vel, ids, dt, t=0.0, nthreads=0):
     lib().or_sph_step(C.byref(p), n, _ptr(pos), _ptr(vel), _ptr(ids), dt, t, _ptr(rho), _ptr(prho),
                       _ptr(cs), nthreads)
     return pos, vel, ids, rho, prho, cs
+
+
+def sph_step_diag(p: OrSphParams, pos, vel, ids, dt, t=0.0, nthreads=0):
+    """sph_step plus, in the same sorted order, acc (n,3): the pair sum a_i without gravity or
+    forcing, and mag (n,2): Σ|pair acceleration term| and Σ|pair XSPH term| (error scales).
+    Returns (pos, vel, ids, rho, prho, cell_start, acc, mag)."""
+    pos = np.ascontiguousarray(pos, dtype=np.float32).copy()
+    vel = np.ascontiguousarray(vel, dtype=np.float32).copy()
+    ids = np.ascontiguousarray(ids, dtype=np.int32).copy()
+    n = pos.shape[0]
+    rho = np.empty(n, np.float32)
+    prho = np.empty(n, np.float32)
+    cs = np.empty(ncells(p) + 1, np.uint32)
+    acc = np.empty((n, 3), np.float32)
+    mag = np.empty((n, 3), np.float32)
+    lib().or_sph_step_diag(C.byref(p), n, _ptr(pos), _ptr(vel), _ptr(ids), dt, t, _ptr(rho), _ptr(prho),
+                           _ptr(cs), _ptr(acc), _ptr(mag), nthreads)
+    return pos, vel, ids, rho, prho, cs, acc, mag
+
+
+def force_range_diag(p: OrSphParams, pos, vel, rho, prho, sk, cs, dt, t=0.0, nthreads=0):
+    """Pass 2 + integrate over ALL sorted slots of (pos, vel) with the given (rho, prho) (e.g. the
+    GPU's pass-1 output): returns (pos_out, vel_out, acc, mag) in the same sorted order."""
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    vel = np.ascontiguousarray(vel, dtype=np.float32)
+    rho = np.ascontiguousarray(rho, dtype=np.float32)
+    prho = np.ascontiguousarray(prho, dtype=np.float32)
+    sk = np.ascontiguousarray(sk, dtype=np.uint32)
+    cs = np.ascontiguousarray(cs, dtype=np.uint32)
+    n = pos.shape[0]
+    po, vo = np.empty_like(pos), np.empty_like(vel)
+    acc = np.empty((n, 3), np.float32)
+    mag = np.empty((n, 3), np.float32)
+    lib().or_sph_force_range_diag(C.byref(p), _ptr(pos), _ptr(vel), _ptr(rho), _ptr(prho), _ptr(sk), _ptr(cs), 0, n,
+                                  dt, t, _ptr(po), _ptr(vo), _ptr(acc), _ptr(mag), nthreads)
+    return po, vo, acc, mag
 
 
 def density_range(p: OrSphParams, pos, sk, cs, i0, i1, rho, prho, nthreads=0):

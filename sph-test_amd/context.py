@@ -192,6 +192,10 @@ class Context:
     def density(self) -> np.ndarray:
         return self._read("sph_read_density", 1)
 
+    def pressure_term(self) -> np.ndarray:
+        """P/ρ² of the last step's pass 1 (index order)."""
+        return self._read("sph_read_pressure_term", 1)
+
     def torque_int(self) -> np.ndarray:
         return self._read("sph_read_torque_int", 3, np.int32)
 
@@ -203,6 +207,13 @@ class Context:
         nc = st.grid[0] * st.grid[1] * st.grid[2] + 1
         out = np.empty(nc, np.uint32)
         self._chk("sph_read_cell_start", self._L.sph_read_cell_start(self._h, A.ptr(out), nc))
+        return out
+
+    def path_counts(self, reset: bool = True) -> np.ndarray:
+        """Sparse-path counters of the neighbour passes (sph_read_path_counts): density chunked,
+        density global, force chunked, force global."""
+        out = np.zeros(4, np.uint32)
+        self._chk("sph_read_path_counts", self._L.sph_read_path_counts(self._h, A.ptr(out), 1 if reset else 0))
         return out
 
     def radix_sort(self, keys: np.ndarray, key_bits: int):

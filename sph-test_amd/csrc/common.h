@@ -21,7 +21,7 @@ struct GridDesc {
     uint32_t ncells;     // gx*gy*gz (keys == ncells mark inactive particles)
     int32_t cx0;         // first global column held (0 without decomposition)
     int32_t gx_all;      // global column count (== gx without decomposition)
-    int32_t zsub;        // z sub-cells per cell (Model S 4, Model R 1)
+    int32_t zsub;        // z sub-cells per cell (Model S 3D 6, Model R and 2D 1)
     int32_t zwin;        // max |Δ z sub-cell| of a neighbour (zsub + 1; Model R 1)
 };
 
@@ -265,7 +265,9 @@ void launch_gather_s(const uint32_t* perm, const float4* pos, const float4* vel,
                      float4* pos_o, float4* vel_o, int32_t* id_o, int32_t n, hipStream_t s);
 void launch_scatter_f4_by_id(const float4* src, const int32_t* id, int32_t n, float* dst,
                              int32_t comps, hipStream_t s);
-void launch_scatter_f2x_by_id(const float2* src, const int32_t* id, int32_t n, float* dst, hipStream_t s);
+// dst[id[i]] = src[i].x (comp 0) or .y (comp 1)
+void launch_scatter_f2x_by_id(const float2* src, const int32_t* id, int32_t n, float* dst, hipStream_t s,
+                              int32_t comp = 0);
 void launch_scatter_i3_by_id(const int32_t* src, const int32_t* id, int32_t n, int32_t* dst, hipStream_t s);
 void launch_aos84_to_soa(const void* aos, int32_t n, float4* pos, float4* vel, float4* omg,
                          float4* rot, float4* aux, int32_t* mode, int32_t* id, hipStream_t s);
@@ -279,20 +281,13 @@ void launch_lattice(int32_t dim, int32_t nx, int32_t ny, int32_t nz, float dx, f
                     hipStream_t s);
 void launch_iota(uint32_t* v, int32_t n, hipStream_t s);
 
-// Model S (wcsph.hip): targets are the sorted slots [ib, ie)
-void launch_density(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g,
-                    SphConst c, float2* rp, hipStream_t s, DevRange dr = DevRange{});
-void launch_force_integrate(const float4* pos, const float4* vel, const float2* rp,
-                            const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
-                            float dt, float fext_x, float4* pos_o, float4* vel_o, uint32_t* keys_o,
-                            MoverSink mv, hipStream_t s);
-
-// Model S, LDS-tiled (wcsph_tiled.hip)
+// Model S, LDS-tiled (wcsph_tiled.hip): targets are the sorted slots [ib, ie). paths: 4 sparse-path
+// counters (density chunked / global, force chunked / global), incremented once per block and event.
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g,
-                          SphConst c, float2* rp, hipStream_t s, DevRange dr = DevRange{});
+                          SphConst c, float2* rp, uint32_t* paths, hipStream_t s, DevRange dr = DevRange{});
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs,
                         int32_t ib, int32_t ie, GridDesc g, SphConst c, float dt, float fext_x,
-                        float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv, hipStream_t s);
+                        float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv, uint32_t* paths, hipStream_t s);
 
 // slab decomposition (slab.hip)
 // Order-preserving compaction of the sorted slots [b, e) whose key column satisfies

@@ -31,7 +31,9 @@ __global__ __launch_bounds__(BLK) void k_keys(const float4* __restrict__ pos, in
 constexpr uint32_t CS_SHORT = 32;
 constexpr uint32_t CS_CHUNK = 8192;   // long gaps are queued in chunks so no workgroup fills more
 
-// thread i in [0, n]: cells (key[i-1], key[i]] start at slot i (key[-1] = -1, key[n] = ncells)
+// thread i in [0, n]: cells (key[i-1], key[i]] start at slot i (key[-1] = -1, key[n] = ncells).
+// Thread n also writes cs[ncells + 1] = n: the re-sort reads cs_old[k + 1] for a mover whose key is
+// the inactive sentinel ncells.
 __global__ __launch_bounds__(BLK) void k_cell_start(const uint32_t* __restrict__ sk, int32_t n,
                                                     uint32_t* __restrict__ cs, uint32_t ncells,
                                                     uint4* __restrict__ gaps, uint32_t* __restrict__ gap_count,
@@ -39,6 +41,7 @@ __global__ __launch_bounds__(BLK) void k_cell_start(const uint32_t* __restrict__
     const int32_t i = blockIdx.x * BLK + threadIdx.x;
     if (i == 0) *gap_next = 0u;   // the next call's counter (ping-pong: no memset launch)
     if (i > n) return;
+    if (i == n) cs[ncells + 1] = (uint32_t)n;
     const int64_t kp = i > 0 ? (int64_t)sk[i - 1] : -1;
     const int64_t kc = i < n ? (int64_t)sk[i] : (int64_t)ncells;
     if (kc <= kp) return;
@@ -104,9 +107,9 @@ __global__ __launch_bounds__(BLK) void k_scatter_f4_by_id(const float4* __restri
 
 __global__ __launch_bounds__(BLK) void k_scatter_f2x_by_id(const float2* __restrict__ src,
                                                            const int32_t* __restrict__ id, int32_t n,
-                                                           float* __restrict__ dst) {
+                                                           float* __restrict__ dst, int32_t comp) {
     const int32_t i = blockIdx.x * BLK + threadIdx.x;
-    if (i < n) dst[id[i]] = src[i].x;
+    if (i < n) dst[id[i]] = comp ? src[i].y : src[i].x;
 }
 
 __global__ __launch_bounds__(BLK) void k_scatter_i3_by_id(const int32_t* __restrict__ src,
@@ -238,8 +241,8 @@ void launch_scatter_f4_by_id(const float4* src, const int32_t* id, int32_t n, fl
                              hipStream_t s) {
     if (n > 0) k_scatter_f4_by_id<<<nblk(n), BLK, 0, s>>>(src, id, n, dst, comps);
 }
-void launch_scatter_f2x_by_id(const float2* src, const int32_t* id, int32_t n, float* dst, hipStream_t s) {
-    if (n > 0) k_scatter_f2x_by_id<<<nblk(n), BLK, 0, s>>>(src, id, n, dst);
+void launch_scatter_f2x_by_id(const float2* src, const int32_t* id, int32_t n, float* dst, hipStream_t s, int32_t comp) {
+    if (n > 0) k_scatter_f2x_by_id<<<nblk(n), BLK, 0, s>>>(src, id, n, dst, comp);
 }
 void launch_scatter_i3_by_id(const int32_t* src, const int32_t* id, int32_t n, int32_t* dst, hipStream_t s) {
     if (n > 0) k_scatter_i3_by_id<<<nblk(n), BLK, 0, s>>>(src, id, n, dst);

@@ -1,0 +1,225 @@
+// host.h — host-side state of libsphhip.so: the context behind the C ABI (include/sphhip.h) and the
+// helpers the ABI files share (host_ctx.cpp: memory and profiling; host_step.cpp: the per-step
+// launch sequences; abi.cpp: the single-domain ABI; abi_slab.cpp: the slab decomposition and
+// the multi-GPU step).
+//
+// Host orchestration of the reference's per-frame GPU work, MI355X-first:
+//   ParticleSystemController.Update() (ParticleSystemController.cs:244-351) issues
+//   ~9 Dispatches plus two full-buffer H2D clears and two synchronous D2H readbacks every
+//   frame. sph_step() issues hash → radix sort → reorder → cell-start → pass 1 → pass 2
+//   on one HIP stream with no host synchronisation, no per-step allocation and no
+//   readback. Readback is an explicit call (sph_read_*).
+// Device memory is owned here and sized once per capacity (InitializeBuffers :373-451).
+#pragma once
+#include "common.h"
+#include "sphhip.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace sph {
+
+// z sub-cells per 2h cell (SPEC_SPH.md §0). 6 trims the neighbour windows closer than 4 (C3: both passes
+// −8 us each) while the sub-cell crossings it adds cost the re-sort 2 us; 8 costs it 14 us
+// (profiles/r01_zsub_ab.log).
+static const int32_t SPH_ZSUB = 6;
+
+struct KStat {
+    std::string name;
+    int64_t launches = 0;
+    double total_ms = 0.0;
+    double bytes = 0.0;
+};
+
+struct Pending {
+    int k;
+    hipEvent_t a, b;
+};
+
+}  // namespace sph
+
+struct sph_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    sph_config cfg{};
+    sph_params prm{};
+    bool params_set = false;
+    int32_t capacity = 0;
+    int32_t n = 0;
+    sph::GridDesc grid{};
+    int32_t key_bits = 1;
+    sph::SphConst sc{};
+    // particle state, cell-sorted slot order; *2 = ping-pong partner
+    float4 *pos = nullptr, *vel = nullptr, *pos2 = nullptr, *vel2 = nullptr;
+    float4 *omg = nullptr, *rot = nullptr, *aux = nullptr, *omg2 = nullptr, *rot2 = nullptr, *aux2 = nullptr;
+    int32_t *id = nullptr, *id2 = nullptr, *mode = nullptr, *mode2 = nullptr;
+    float2* rp = nullptr;        // Model S (ρ, P/ρ²)
+    int32_t* torque = nullptr;   // Model R int torque of the last step (slot order)
+    int32_t* slot_of = nullptr;  // Model R particle index -> slot (bond pass)
+    // adhesion bonds (Model R, §8f-1): device SoA, host copy of the ends for the incidence lists
+    int32_t nbonds = 0, bond_cap = 0;
+    int2* b_ends = nullptr;
+    float4 *b_spring = nullptr, *b_relq = nullptr, *b_anc_a = nullptr, *b_anc_b = nullptr;
+    int4* b_terms = nullptr;
+    uint32_t *b_off = nullptr, *b_ent = nullptr;
+    int32_t b_off_cap = 0;
+    std::vector<int2> bonds_host;
+    std::vector<uint32_t> b_off_host, b_ent_host;
+    int32_t b_index_n = -1;      // particle count the incidence lists were built for (-1: stale)
+    // sort / grid
+    uint32_t *keys = nullptr, *keys2 = nullptr, *vals = nullptr, *vals2 = nullptr;
+    uint32_t *hist = nullptr, *bin_total = nullptr;
+    uint32_t* cs = nullptr;
+    uint32_t cs_cap = 0;
+    uint4* gaps = nullptr;       // cell-start long-gap queue
+    uint32_t gaps_cap = 0;
+    void* staging = nullptr;
+    size_t staging_bytes = 0;
+    bool keys_valid = false;
+    int32_t keys_active = -1;
+    // incremental re-sort (resort.hip): sorted keys of the current slot order, and scratch
+    uint32_t *sk_cur = nullptr, *sk_next = nullptr;
+    uint32_t *mv_mi = nullptr, *mv_mk = nullptr, *mv_mo = nullptr, *mv_rank = nullptr, *mv_mx = nullptr, *mv_mos = nullptr;
+    uint64_t* mv_ms = nullptr;
+    uint32_t* mv_count = nullptr;   // [2] mover counters, ping-pong by step
+    int mv_par = 0;                 // counter the next force pass appends into
+    bool sk_valid = false;       // sk_cur matches the slot order and cs (set by a Model S sort)
+    // env SPH_RESORT: 0 full radix sort every step, 1 (default) incremental re-sort unless the last
+    // seen mover count exceeds resort_limit(n), 2 incremental whenever possible (tests)
+    int resort_mode = 1;
+    int ct_team = 0;                // env SPH_CT_TEAM: Model R lanes per target (0 = by size; tests)
+    uint32_t* mv_host = nullptr;    // pinned: the mover count of the latest step copied back
+    int64_t steps = 0;
+    double sim_time = 0.0;
+    sph_drag_input drag{-1, {0.f, 0.f, 0.f}, 0.f};
+    std::string err;
+    bool profiling = false;
+    std::vector<sph::KStat> kstats;
+    std::vector<sph::Pending> pending;
+    std::vector<hipEvent_t> ev_pool;
+    int64_t device_bytes = 0;
+    uint32_t* paths = nullptr;   // [4] sparse-path counters of the neighbour passes (sph_read_path_counts)
+    // slab decomposition (SPEC_SPH.md §3)
+    bool slab = false;
+    sph_slab sl{};
+    bool has_left = false, has_right = false;
+    sph::GridDesc gglobal{};
+    int32_t o0 = 0, o1 = 0;      // owned sorted slots
+    int32_t rng[10] = {0};
+    int32_t send_counts[2] = {0, 0};
+    uint32_t* sblk = nullptr;    // compaction block counts [2][nblk]
+    uint32_t* sdev = nullptr;    // small device scratch (totals, picks; [8], [9]: cell-start gap counters)
+    int gap_par = 0;             // which of sdev[8], sdev[9] the next cell-start call uses
+    uint32_t* rng_host = nullptr;   // pinned: column-start picks of the last assemble
+    hipEvent_t rng_ev = nullptr;    // recorded after their device->host copy
+    bool rng_pending = false;       // rng[] / o0 / o1 not yet updated from rng_host
+    int32_t dropped = 0;            // own particles the last assemble dropped (outside the window)
+    // asynchronous readback (AsyncGPUReadback, controller:1115-1159): index-order copies on the
+    // device, D2H on a side stream into pinned host buffers
+    hipStream_t rb_stream = nullptr;
+    hipEvent_t rb_src = nullptr, rb_ready = nullptr;
+    void* rb_dev[3] = {nullptr, nullptr, nullptr};
+    void* rb_host[3] = {nullptr, nullptr, nullptr};
+    size_t rb_cap[3] = {0, 0, 0};
+    int32_t rb_fields = 0;          // fields of the outstanding request (0: none)
+    int32_t rb_count = 0;           // particles it holds
+};
+
+namespace sph {
+
+inline int fail(sph_ctx* c, int code, const char* fmt, ...) {
+    if (c) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        c->err = buf;
+    }
+    return code;
+}
+
+#define HIPCHK(call)                                                                            \
+    do {                                                                                        \
+        hipError_t e_ = (call);                                                                 \
+        if (e_ != hipSuccess) return fail(ctx, SPH_ERR_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+int dalloc(sph_ctx* ctx, T** p, size_t count) {
+    if (*p) { (void)hipFree(*p); *p = nullptr; }
+    if (count == 0) return SPH_OK;
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, count * sizeof(T));
+    if (e != hipSuccess) return fail(ctx, SPH_ERR_NOMEM, "hipMalloc(%zu): %s", count * sizeof(T), hipGetErrorString(e));
+    *p = (T*)q;
+    ctx->device_bytes += (int64_t)(count * sizeof(T));
+    return SPH_OK;
+}
+
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+void free_all(sph_ctx* c);
+int bit_width(uint32_t v);
+inline bool is_contact(const sph_ctx* c) { return c->cfg.model == SPH_MODEL_CONTACT; }
+int alloc_particles(sph_ctx* ctx, int32_t cap);
+int ensure_cells(sph_ctx* ctx);
+int derive(sph_ctx* ctx);
+// Every mutation of the particle slots (upload, init, split, index-range set, resize, window change)
+// makes the sorted keys, the old-key table of the incremental re-sort and the movers stale: the next
+// step runs the full radix sort.
+void invalidate_sort(sph_ctx* c);
+int kstat_index(sph_ctx* c, const char* name);
+hipEvent_t take_event(sph_ctx* c);
+void resolve_pending(sph_ctx* c);
+
+struct KTimer {
+    sph_ctx* c;
+    int k;
+    hipEvent_t a = nullptr;
+    KTimer(sph_ctx* ctx, const char* name, double bytes) : c(ctx), k(kstat_index(ctx, name)) {
+        c->kstats[k].launches++;
+        c->kstats[k].bytes = bytes;
+        if (c->profiling) {
+            a = take_event(c);
+            (void)hipEventRecord(a, c->stream);
+        }
+    }
+    ~KTimer() {
+        if (c->profiling) {
+            hipEvent_t b = take_event(c);
+            (void)hipEventRecord(b, c->stream);
+            c->pending.push_back({k, a, b});
+            if (c->pending.size() > 8192) resolve_pending(c);
+        }
+    }
+};
+
+// per-step launch sequences (host_step.cpp)
+void swap_sv(sph_ctx* c);
+int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id, const uint32_t** sorted_keys = nullptr);
+void density_range(sph_ctx* ctx, int32_t b, int32_t e);
+void force_range(sph_ctx* ctx, int32_t b, int32_t e, float dt, float fext, MoverSink mv = MoverSink{});
+ResortScratch resort_scratch(sph_ctx* ctx);
+MoverSink mover_sink(sph_ctx* ctx);
+uint32_t resort_limit(int32_t n);
+float forcing(const sph_ctx* ctx);
+int step_wcsph(sph_ctx* ctx, float dt);
+void free_bonds(sph_ctx* c);
+int32_t contact_active(const sph_ctx* c);
+int step_contact(sph_ctx* ctx, float dt);
+// slab window of the global grid (abi_slab.cpp)
+int slab_local_grid(sph_ctx* ctx);
+
+}  // namespace sph

@@ -30,12 +30,10 @@
 namespace sph {
 
 constexpr int MV_BLK = 256;
-// movers per rank tile: 64 gives ~4x the work items of 256 for a few more atomics (C3 re-sort
-// 42.6 -> 39.3 us; 32: 40.5, 128: 39.9, 512: 49.8; profiles/r01_mv_tile_ab.log)
-#ifndef SPH_MV_TILE
-#define SPH_MV_TILE 64
-#endif
-constexpr int MV_TILE = SPH_MV_TILE;
+// movers per rank tile: 64 gives ~4x the work items of 256 for a few more atomics (256 -> 64 was
+// faster in every paired round, C3 re-sort ~42 -> ~39 us; 32 and 128 are within the run-to-run noise
+// of 64, profiles/r01_mv_tile_ab.log)
+constexpr int MV_TILE = 64;
 constexpr int MV_RANK_GRID = 2048;
 
 static __device__ __forceinline__ uint64_t comp(uint32_t key, uint32_t idx) { return (uint64_t)key << 32 | idx; }
@@ -123,8 +121,8 @@ static __device__ __forceinline__ uint32_t movers_before(bool mv, uint32_t block
 }
 
 // Per mover x (append order): rank[x] = #{y : (k_y, i_y) < (k_x, i_x)}, rank[cap + x] =
-// #{y : i_y < i_x}, rank[2cap + x] = A(q_x) = #{y : i_y < q_x}. Work items = (256 movers) x
-// (256-mover tile); partial counts are added atomically (integers: order-independent).
+// #{y : i_y < i_x}, rank[2cap + x] = A(q_x) = #{y : i_y < q_x}. Work items = (MV_BLK movers) x
+// (MV_TILE-mover tile); partial counts are added atomically (integers: order-independent).
 // Also zeroes the next step's mover counter.
 __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__ mtotal,
                                                     uint32_t* __restrict__ next_count,

@@ -20,37 +20,15 @@
 
 namespace sph {
 
-#ifndef SPH_FLUSH_BATCH
-#define SPH_FLUSH_BATCH 0   // 4-hit batched flush: measured 3% slower (kept for A/B)
-#endif
-#ifndef SPH_FORCE_QUAD
-#define SPH_FORCE_QUAD 0   // quadrant lanes: measured neutral on the force pass (kept for density)
-#endif
-#ifndef SPH_FORCE_ABL
-#define SPH_FORCE_ABL 0   // ablation builds for profiling only (scripts/gpu_ablate.sh)
-#endif
-
-#ifndef SPH_TT_BLK
-#define SPH_TT_BLK 256
-#endif
-#ifndef SPH_TT_GCAP
-#define SPH_TT_GCAP 1024
-#endif
-constexpr int TT_BLK = SPH_TT_BLK;    // targets per workgroup
-constexpr int TT_GCAP = SPH_TT_GCAP;  // candidates staged per plane (LDS)
-#ifndef SPH_TT_CAP
-#define SPH_TT_CAP 16
-#endif
-constexpr int TT_CAP = SPH_TT_CAP;  // per-lane hit list (force)
+constexpr int TT_BLK = 256;     // targets per workgroup (128 / 192 / 512 measured 13-25% slower)
+constexpr int TT_GCAP = 1024;   // candidates staged per plane (LDS), density pass
+constexpr int TT_CAP = 16;      // per-lane hit list (force)
 constexpr int TT_FALLBACK = 4 * TT_GCAP;
 // The force pass stages 32 B per candidate and keeps per-lane hit lists in LDS. Its flush loop is
 // latency-bound (LDS list read -> candidate reads -> body), so occupancy pays: 704 candidates and
 // 16-entry lists keep a workgroup under 32 KiB, 5 workgroups per CU instead of 3 (C3, MI355X:
 // force pass 305 -> 258 us; 1024/32 and 768/16 measured 305 and 282).
-#ifndef SPH_TF_GCAP
-#define SPH_TF_GCAP 704
-#endif
-constexpr int TF_GCAP = SPH_TF_GCAP;
+constexpr int TF_GCAP = 704;
 constexpr int TF_FALLBACK = 4 * TF_GCAP;
 
 struct BlockRows {
@@ -101,6 +79,12 @@ __device__ __forceinline__ void lane_window(const GridDesc& g, const uint32_t* _
         r0 = (int32_t)cs[rowk + (uint32_t)zlo];
         r1 = (int32_t)cs[rowk + (uint32_t)zhi + 1u];
     }
+}
+
+// Sparse-path counters (tests: sph_read_path_counts): [0] density planes chunked, [1] density rows
+// gathered from global memory, [2] / [3] the same for the force pass. One atomic per block and event.
+__device__ __forceinline__ void count_path(uint32_t* paths, int k) {
+    if (threadIdx.x == 0) atomicAdd(paths + k, 1u);
 }
 
 __device__ __forceinline__ float dist2(float4 a, float4 b) {
@@ -178,7 +162,7 @@ __device__ __forceinline__ int32_t quadrant_target(const GridDesc& g, const floa
 __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restrict__ pos,
                                                           const uint32_t* __restrict__ cs, int32_t ib, int32_t n,
                                                           GridDesc g, SphConst c, float2* __restrict__ rp,
-                                                          DevRange dr) {
+                                                          DevRange dr, uint32_t* __restrict__ paths) {
     __shared__ float4 sp[TT_GCAP + 4];
     __shared__ int32_t perm[TT_BLK];
     __shared__ uint32_t qcnt[TT_BLK / 64][5];
@@ -229,9 +213,11 @@ __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restri
             continue;
         }
         // sparse block: offset by offset, in chunks, or straight from global memory
+        count_path(paths, 0);
 #pragma unroll 1
         for (int r = 0; r < 3; ++r) {
             if (len[r] > TT_FALLBACK) {
+                count_path(paths, 1);
                 for (int32_t j = r0[r]; j < r1[r]; ++j) s += spline_w4(c, dist2(pi, pos[j]));
                 continue;
             }
@@ -279,10 +265,8 @@ static PairK pair_constants(const SphConst& c) {
 
 // Pair body (SPEC_SPH.md §2). pj = (x, y, z, ρ_j), vj = (u, v, w, P_j/ρ_j²). Branchless, for
 // pairs with r < 2h: one rsq gives r and 1/r; r = 0 (coincident, distinct particles) gives q = 0.
-// live = false adds exact zeros (selected contributions, so a garbage slot cannot leak NaN): the two-hit flush
-// computes both bodies unconditionally and the compiler interleaves their chains.
 __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi, float rhoi, float prhoi, float4 pj,
-                                           float4 vj, ForceAcc& a, bool live = true) {
+                                           float4 vj, ForceAcc& a) {
     const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
     const float r2 = dx * dx + dy * dy + dz * dz;
     const float rs = __builtin_amdgcn_rsqf(fmaxf(r2, 1e-30f));
@@ -303,27 +287,22 @@ __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi,
     const float inv_s = e * inv_es;
     const float pij = fminf(vr, 0.0f) * k.kvisc * inv_es;
     const float cf = (prhoi + vj.w + pij) * G;
-    a.ax += live ? cf * dx : 0.0f; a.ay += live ? cf * dy : 0.0f; a.az += live ? cf * dz : 0.0f;
+    a.ax += cf * dx; a.ay += cf * dy; a.az += cf * dz;
     const float cx = k.kx * inv_s * w4;
-    a.sx -= live ? cx * du : 0.0f; a.sy -= live ? cx * dv : 0.0f; a.sz -= live ? cx * dw : 0.0f;
+    a.sx -= cx * du; a.sy -= cx * dv; a.sz -= cx * dw;
 }
 
 __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
     const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, PairK pk, float dt,
-    float fext_x, float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o, MoverSink mv) {
+    float fext_x, float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o, MoverSink mv,
+    uint32_t* __restrict__ paths) {
     __shared__ float4 sp[TF_GCAP + 4];     // (x, y, z, ρ)
     __shared__ float4 sv[TF_GCAP + 4];     // (u, v, w, P/ρ²)
     __shared__ uint16_t lst[TT_CAP][TT_BLK];
     const int tid = threadIdx.x;
     const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
-#if SPH_FORCE_QUAD
-    __shared__ int32_t perm[TT_BLK];
-    __shared__ uint32_t qcnt[TT_BLK / 64][5];
-    const int32_t i = quadrant_target(g, pos, i0, n, perm, qcnt);
-#else
     const int32_t i = i0 + tid;
-#endif
     const bool valid = i < n;
     const int32_t ilast = min(i0 + TT_BLK, n) - 1;
     const int32_t ii = valid ? i : ilast;
@@ -337,46 +316,16 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + off);
     };
     auto flush = [&]() {
-#if SPH_FORCE_ABL == 2   // measurement build: scan only, hits dropped
-        acc.ax += 1e-30f * (float)cnt;
-        cnt = 0;
-        return;
-#endif
-#if SPH_FLUSH_BATCH
-        // two hits per iteration, both bodies unconditional (the second masked by a select when
-        // q + 1 >= cnt), so their dependency chains interleave. Slots past cnt hold stale in-range
-        // offsets or are clamped into the padded array.
-        constexpr uint32_t OMAX = 16u * TF_GCAP;
-        for (int q = 0; __any(q < cnt); q += 2) {
-            const uint32_t o0 = min((uint32_t)lst[q][tid], OMAX);
-            const uint32_t o1 = min((uint32_t)lst[min(q + 1, TT_CAP - 1)][tid], OMAX);
-            const float4 p0 = at(sp, o0), v0 = at(sv, o0), p1 = at(sp, o1), v1 = at(sv, o1);
-            pair_force(pk, pi, vi, ri.x, ri.y, p0, v0, acc, q < cnt);
-            pair_force(pk, pi, vi, ri.x, ri.y, p1, v1, acc, q + 1 < cnt);
-        }
-#else
         for (int q = 0; __any(q < cnt); ++q) {
             if (q < cnt) {
                 const uint32_t off = lst[q][tid];
-#if SPH_FORCE_ABL == 1   // measurement build: trivial pair body
-                acc.ax += 1e-30f * at(sp, off).x; acc.sx += 1e-30f * at(sv, off).w;
-#elif SPH_FORCE_ABL == 4   // measurement build: list read only
-                acc.ax += 1e-30f * (float)off;
-#elif SPH_FORCE_ABL == 5   // measurement build: one 16-B hit read
-                acc.ax += 1e-30f * at(sp, off).x;
-#else
                 pair_force(pk, pi, vi, ri.x, ri.y, at(sp, off), at(sv, off), acc);
-#endif
             }
         }
-#endif
         cnt = 0;
     };
     // scan LDS slots [lo, lo+ln), appending hits
     auto scan = [&](int32_t lo, int32_t ln) {
-#if SPH_FORCE_ABL == 3   // measurement build: staging only
-        return;
-#endif
         for (int t = 0; __any(t < ln); t += 4) {
             const int32_t j = min(lo + t, TF_GCAP);   // lanes past their range stay in the array
             const float4 a = sp[j], bb = sp[j + 1], cc = sp[j + 2], d = sp[j + 3];
@@ -426,9 +375,11 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
             continue;
         }
         // sparse block: offset by offset, in chunks, or straight from global memory
+        count_path(paths, 2);
 #pragma unroll 1
         for (int r = 0; r < 3; ++r) {
             if (len[r] > TF_FALLBACK) {
+                count_path(paths, 3);
                 for (int32_t j = r0[r]; j < r1[r]; ++j) {
                     const float4 pj = pos[j];
                     if (j != i && dist2(pi, pj) < c.four_h2) {
@@ -472,16 +423,16 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
 
 // dr set: [ib, ie) only sizes the grid (an upper bound); the kernel reads its bounds from dr
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
-                          float2* rp, hipStream_t s, DevRange dr) {
-    if (ie > ib) k_density_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, cs, ib, ie, g, c, rp, dr);
+                          float2* rp, uint32_t* paths, hipStream_t s, DevRange dr) {
+    if (ie > ib) k_density_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, cs, ib, ie, g, c, rp, dr, paths);
 }
 
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,
                         int32_t ie, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o,
-                        uint32_t* keys_o, MoverSink mv, hipStream_t s) {
+                        uint32_t* keys_o, MoverSink mv, uint32_t* paths, hipStream_t s) {
     if (ie > ib)
         k_force_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt, fext_x,
-                                                                         pos_o, vel_o, keys_o, mv);
+                                                                         pos_o, vel_o, keys_o, mv, paths);
 }
 
 }  // namespace sph
