@@ -47,19 +47,43 @@ def parse():
     ap.add_argument("--strong", action="store_true",
                     help="decompose --config itself over the N ranks (strong scaling: C4 on 4 GPUs, C5 on 8) "
                          "instead of stretching it xN")
+    ap.add_argument("--mid-steps", type=int, default=200,
+                    help="N=1: also time this many steps from a mid-collapse state (0: skip)")
+    ap.add_argument("--mid-at", type=int, default=5000,
+                    help="step count (from the lattice) at which the mid-collapse timing starts")
     ap.add_argument("--table", action="store_true",
                     help="print the GPU / 1-thread / all-thread CPU rate table (SURVEY §8d) instead of the bench line")
     return ap.parse_args()
 
 
-# VALU issue peak, MEASURED on MI355X (scripts/valu_peak.hip, profiles/r01_valu_peak.log): independent
-# f32 FMA chains at 8 waves per SIMD issue 891.9 G wave64-instructions/s chip-wide (114 TFLOP/s);
-# 2 waves/SIMD 778, 4 waves 861. Packed f32 (v_pk_fma_f32) issues 473 G/s, 121 TFLOP/s: no faster per flop.
-PEAK_VALU_WAVE_INSTR_PER_S = 891.9e9
+# VALU issue peak, MEASURED on MI355X (scripts/valu_peak.hip, profiles/r02_valu_peak_long.log): independent
+# f32 FMA chains at 8 waves per SIMD in ~3.7 ms dispatches issue 1,153.8 G wave64-instructions/s chip-wide
+# (148 TFLOP/s) at an in-kernel clock of 2.39 GHz, 94% of the spec issue rate at that clock (256 CUs x 4
+# SIMDs x 1/2 wave-instruction per cycle). Round 1's 891.9 G came from 0.3 ms dispatches, whose ramp and
+# tail hid a quarter of the rate. Packed f32 (v_pk_fma_f32) issues ~584 G/s: no faster per flop.
+PEAK_VALU_WAVE_INSTR_PER_S = 1153.8e9
 
 
 def force_kernel_name() -> str:
-    return "k_force_integrate" if os.environ.get("SPH_NB_VARIANT", "1") == "0" else "k_force_tiled"
+    return "k_force_tiled"
+
+
+def load_clock():
+    """Effective shader clocks from the committed rocprofv3 GRBM passes (profiles/clock_*.json,
+    scripts/gpu_clock.sh): the force pass on its longest dispatches (C5) and the VALU microbenchmark."""
+    out = {}
+    for f in sorted((ROOT / "profiles").glob("clock_*.json")):
+        try:
+            d = json.loads(f.read_text())
+        except Exception:
+            continue
+        if "k_force_tiled" in d.get("C5", {}):
+            out["force_ghz"] = d["C5"]["k_force_tiled"]["clock_ghz_median"]
+            out["force_src"] = f"{f.name}: C5 k_force_tiled, {d['C5']['k_force_tiled']['mean_us']:.0f} us dispatches"
+        if "k_fma" in d.get("valu", {}):
+            out["micro_ghz"] = d["valu"]["k_fma"]["clock_ghz_median"]
+        out["file"] = f.name
+    return out
 
 
 def load_pmc(config: str):
@@ -287,12 +311,47 @@ def main():
                     "bytes_per_launch": bytes_per_launch}
         if "valu_instr" in pmc:
             # what bounds the neighbour pass in practice: VALU issue, from the same
-            # kernel's committed PMC pass and this run's kernel time
+            # kernel's committed PMC pass and this run's kernel time, priced two ways: against the
+            # microbenchmark's measured issue rate, and against the spec issue rate (256 CUs × 4 SIMDs
+            # × ½ wave64-instruction per cycle) at the clock the chip held during the force pass
             va = pmc["valu_instr"] / avg_s
             roofline["valu"] = {"achieved": round(va / 1e9, 2), "peak": round(PEAK_VALU_WAVE_INSTR_PER_S / 1e9, 1),
                                 "unit": "G wave-instr/s", "frac": round(va / PEAK_VALU_WAVE_INSTR_PER_S, 4),
                                 "source": "rocprofv3 SQ_INSTS_VALU per launch (profiles/pmc_C3.json); peak measured by "
-                                          "scripts/valu_peak.hip (profiles/r01_valu_peak.log)"}
+                                          "scripts/valu_peak.hip, long dispatches (profiles/r02_valu_peak_long.log)"}
+            clk = load_clock()
+            if "force_ghz" in clk:
+                spec = 256 * 4 * 0.5 * clk["force_ghz"] * 1e9
+                roofline["valu"].update({
+                    "force_clock_ghz": round(clk["force_ghz"], 3),
+                    "spec_peak_at_force_clock": round(spec / 1e9, 1),
+                    "frac_of_spec_at_clock": round(va / spec, 4),
+                    "clock_source": clk["force_src"]})
+            if "micro_ghz" in clk:
+                roofline["valu"]["microbench_clock_ghz"] = round(clk["micro_ghz"], 3)
+                roofline["valu"]["microbench_frac_of_spec_at_its_clock"] = round(
+                    PEAK_VALU_WAVE_INSTR_PER_S / (256 * 4 * 0.5 * clk["micro_ghz"] * 1e9), 4)
+
+    mid = None
+    if isinstance(runner, SingleRunner) and args.mid_steps > 0:
+        # a representative state beside the driver's line: the timed region above starts a few steps
+        # after the lattice, before the column moves; this one starts mid-collapse (untimed advance)
+        done = args.warmup + args.steps
+        if done < args.mid_at:
+            runner.step(args.mid_at - done)
+        barrier()
+        runner.reset_stats()
+        barrier()
+        t0 = time.perf_counter()
+        runner.step(args.mid_steps)
+        barrier()
+        mwall = time.perf_counter() - t0
+        mks = runner.kernel_stats()
+        mid = {"ms_per_step_mid_collapse": round(mwall * 1e3 / args.mid_steps, 4),
+               "value_mid_collapse": round(runner.total_particles() * args.mid_steps / mwall, 1),
+               "mid_collapse_state": runner.mid_state(max(done, args.mid_at), args.mid_steps),
+               "kernels_ms_per_step_mid_collapse": {k: round(v["total_ms"] / max(1, args.mid_steps), 4)
+                                                    for k, v in mks.items() if v["total_ms"] > 0}}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -321,6 +380,8 @@ def main():
             "kernels_ms_per_step": {k: round(v["total_ms"] / max(1, args.steps), 4) for k, v in kstats.items()
                                     if v["total_ms"] > 0},
         }
+        if mid:
+            line.update(mid)
         print(json.dumps(line), flush=True)
     runner.close()
     if world > 1:
@@ -350,6 +411,13 @@ class SingleRunner:
 
     def local_particles(self):
         return self.sim.n
+
+    def mid_state(self, start: int, steps: int) -> str:
+        sc = self.sim.scenario
+        L = sc.nx * sc.dx
+        T = start * self.sim.dt * (2 * 9.81 / L) ** 0.5
+        return (f"{self.config} steps {start}-{start + steps} from the lattice: t = {start * self.sim.dt:.3f} s, "
+                f"T = t*sqrt(2g/L) = {T:.2f} (surge front running along the floor)")
 
     def workload(self, scaling: str = "weak"):
         sc = self.sim.scenario

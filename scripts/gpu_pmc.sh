@@ -2,13 +2,12 @@
 set +e
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-V=${SPH_NB_VARIANT:-1}
 rocprofv3 -L > gpurun_out/pmc/counters_list.txt 2>&1
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  for v in ${PMC_VARIANTS:-0 1}; do
-    SPH_NB_VARIANT=$v timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp -d "$GRAFT_REPO_ROOT/gpurun_out/pmc/v${v}_g$i" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/scripts/run_steps.py" --config C3 --steps 10 --warmup 2 > gpurun_out/pmc/v${v}_g$i.log 2>&1; rc=$?
+  for v in 1; do
+    timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp -d "$GRAFT_REPO_ROOT/gpurun_out/pmc/v${v}_g$i" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/scripts/run_steps.py" --config C3 --steps 10 --warmup 2 > gpurun_out/pmc/v${v}_g$i.log 2>&1; rc=$?
     echo "group $i v$v rc=$rc"
     if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/v${v}_g$i.log; exit $rc; fi
   done

@@ -15,9 +15,9 @@ export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline > gpurun_out/prof.log 2>&1; rc=$?
 echo "rocprof rc=$rc"; tail -1 gpurun_out/prof.log
 [ $rc -ne 0 ] && exit $rc
-PMC_VARIANTS=1 bash scripts/gpu_pmc.sh; rc=$?
+bash scripts/gpu_pmc.sh; rc=$?
 echo "pmc rc=$rc"
 [ $rc -ne 0 ] && exit $rc
-SPH_NB_VARIANT=1 python3 scripts/pmc_summary.py gpurun_out/pmc gpurun_out/pmc_C3.json C3 > gpurun_out/pmc_summary.log 2>&1
+python3 scripts/pmc_summary.py gpurun_out/pmc gpurun_out/pmc_C3.json C3 > gpurun_out/pmc_summary.log 2>&1
 echo "pmc_summary rc=$?"
 exit 0

@@ -34,7 +34,7 @@ def main(root, out, config):
             if k in ks and "hbm_bytes_per_launch" in ks[k]:
                 force[var] = ks[k]["hbm_bytes_per_launch"]
     # bench.py reads kernel_bytes.force_integrate for the default variant
-    default = os.environ.get("SPH_NB_VARIANT", "1")
+    default = "1"
     if f"v{default}" in force:
         doc["kernel_bytes"] = {"force_integrate": force[f"v{default}"]}
     json.dump(doc, open(out, "w"), indent=1)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Plain step driver for rocprofv3 runs: `python scripts/run_steps.py --config C3 --steps 20`.
-SPH_NB_VARIANT in the environment selects the neighbour-pass kernels. `--model-r N` steps the
+`--model-r N` steps the
 reference controller instead (Model R, N particles from its InitParticles, dt = 1/144)."""
 import argparse
 import sys

@@ -78,3 +78,36 @@ def test_controller_async_readback(pkg):
     ctl.Update(0.01)                                   # delivers the request made after frame 1
     assert ctl.CpuParticlePositions[: len(parts)].tobytes() == after1.tobytes()
     ctl.OnDestroy()
+
+
+def test_readback_and_export_match_the_oracle(pkg, oracle):
+    """The delivery paths against the CPU oracle, not against another GPU read: after one Model R step
+    (SimulateParticles.compute:211-408, bit-exact, test_gpu_parity.py), the asynchronous readback
+    (ParticleSystemController.cs:1115-1159: particles, positions, rotations) and the device AoS-84 export
+    (the renderer's particleBuffer, InstancedParticles.shader:27-44) hold the oracle's step output byte
+    for byte, with drag and inactive particles (export covers the whole buffer, as the reference's)."""
+    import torch
+    from sph_test_amd import _abi as A
+    from test_gpu_parity import random_sphere
+    n, act = 6000, 5000
+    parts = random_sphere(pkg.PARTICLE84, n, seed=17)
+    ctl = pkg.ParticleSystemController(particleCount=n)
+    ctl.Start(parts)
+    ctl.activeParticleCount = act
+    ctl.drag.selectedID, ctl.drag.targetPosition, ctl.drag.strength = 9, (1.0, 2.0, -3.0), 80.0
+    ctl.Update(0.01)
+    cp = oracle.contact_params(0.01, drag_id=9, drag_target=(1.0, 2.0, -3.0), drag_strength=80.0)
+    ref_act, _ = oracle.contact_step(cp, parts[:act].view(oracle.PARTICLE84))
+    ref = parts.copy()
+    ref[:act] = ref_act.view(pkg.PARTICLE84)
+    ctx = ctl.context
+    ctx.request_readback(A.SPH_READBACK_PARTICLES | A.SPH_READBACK_POSITIONS | A.SPH_READBACK_ROTATIONS)
+    got = ctx.readback_get(A.SPH_READBACK_PARTICLES)
+    assert got.tobytes() == ref.tobytes()
+    assert ctx.readback_get(A.SPH_READBACK_POSITIONS).tobytes() == np.ascontiguousarray(ref["position"]).tobytes()
+    assert ctx.readback_get(A.SPH_READBACK_ROTATIONS).tobytes() == np.ascontiguousarray(ref["rotation"]).tobytes()
+    buf = torch.zeros(n * 84, dtype=torch.uint8, device="cuda")
+    ctx.export_aos84_device(buf.data_ptr(), n)
+    ctx.synchronize()
+    assert buf.cpu().numpy().tobytes() == ref.tobytes()
+    ctl.OnDestroy()
