@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event pass")
     ap.add_argument("--slab", action="store_true", help="run the multi-GPU slab step even at N=1 (rehearsal)")
     ap.add_argument("--rebalance", type=int, default=50, help="slab cut re-balancing interval in steps (0: off)")
+    ap.add_argument("--transport", choices=("library", "python"), default="library",
+                    help="N>1: the decomposed step inside libsphhip.so over RCCL (sph_comm_init), or the per-phase "
+                         "slab ABI driven from Python over torch.distributed")
     ap.add_argument("--strong", action="store_true",
                     help="decompose --config itself over the N ranks (strong scaling: C4 on 4 GPUs, C5 on 8) "
                          "instead of stretching it xN")
@@ -259,12 +262,21 @@ def main():
         torch.cuda.set_device(0)
     pkg = GE.load_package()
 
-    if world > 1 or args.slab or args.strong:
+    runner = None
+    if (world > 1 or args.slab) and args.transport == "library" and not (world == 1 and args.strong):
+        # the decomposed step inside libsphhip.so: one RCCL communicator, no host read per step
+        try:
+            runner = LibraryRankRunner(pkg, args.config, rank, world, local, profile=not args.no_profile,
+                                       rebalance_every=args.rebalance, strong=args.strong)
+        except Exception as e:   # noqa: BLE001 - reported, then the torch.distributed slab path (also RCCL)
+            print(json.dumps({"rank": rank, "library_transport_failed": str(e)}), file=sys.stderr, flush=True)
+            runner = None
+    if runner is None and (world > 1 or args.slab or args.strong):
         from sph_test_amd import slab
         runner = slab.SlabRunner(args.config, rank, world, device=local, profile=not args.no_profile,
                                  rebalance_every=args.rebalance,
                                  scenario=pkg.config_scenario(args.config) if args.strong else None)
-    else:
+    elif runner is None:
         runner = SingleRunner(pkg, args.config, local, profile=not args.no_profile)
 
     # one explicit HIP stream shared by torch (events, RCCL ordering) and libsphhip
@@ -373,7 +385,8 @@ def main():
             "data": "synthetic (dam-break lattice, seed 1234)",
             "config": {"workload": runner.workload("strong" if args.strong else "weak"), "particles": n_total,
                        "particles_per_gpu": runner.local_particles(), "h_over_dx": 1.2,
-                       "parallelism": f"slab{world}" if world > 1 else "single"},
+                       "parallelism": f"slab{world}" if world > 1 else "single",
+                       "transport": getattr(runner, "transport", "single" if world == 1 else "python")},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
@@ -386,6 +399,64 @@ def main():
     runner.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+class LibraryRankRunner:
+    """One rank of the in-library decomposed step (sphhip.h sph_comm_init): rank 0 makes the RCCL
+    unique id, torch.distributed hands its 128 bytes to every rank, and from then on sph_step runs the
+    whole decomposed step (halos, re-sort, density, ρ halo overlapped with the interior force pass,
+    re-balancing) with no host read per step."""
+    transport = "library-rccl"
+
+    def __init__(self, pkg, config, rank, world, device, profile, rebalance_every, strong):
+        import torch
+        import torch.distributed as dist
+        from sph_test_amd import slab
+        from sph_test_amd.context import comm_unique_id
+        self.pkg, self.config, self.world = pkg, config, world
+        self.scenario = pkg.config_scenario(config) if strong else slab.weak_scenario(config, world)
+        self.params, self.dt = pkg.scenario_params(self.scenario)
+        buf = torch.zeros(128, dtype=torch.uint8, device=torch.device("cuda", device))
+        if rank == 0:
+            buf.copy_(torch.frombuffer(bytearray(comm_unique_id()), dtype=torch.uint8))
+        if world > 1:
+            dist.broadcast(buf, 0)
+        torch.cuda.synchronize()
+        self.ctx = pkg.Context(pkg.SPH_MODEL_WCSPH, self.scenario.dim, 1024, device=device, profile=profile)
+        self.ctx.comm_init(bytes(buf.cpu().numpy().tobytes()), world, rank)
+        self.ctx.set_params(self.params)
+        self.ctx.set_rebalance(rebalance_every)
+        self.ctx.init_scenario(self.scenario)
+        d = self.ctx.decomposition()
+        self.n_total, self.cut = d.total, (d.cut.cx_lo, d.cut.cx_hi)
+
+    def bind_stream(self, handle):
+        self.ctx.set_stream(handle)
+
+    def step(self, k):
+        self.ctx.step(self.dt, k)
+
+    def reset_stats(self):
+        self.ctx.reset_kernel_stats()
+
+    def kernel_stats(self):
+        return self.ctx.kernel_stats()
+
+    def total_particles(self):
+        return self.n_total
+
+    def local_particles(self):
+        return int(self.ctx.decomposition().owned)
+
+    def workload(self, scaling: str = "weak"):
+        sc = self.scenario
+        kind = "sloshing" if sc.kind == self.pkg.SPH_SCENARIO_SLOSHING else "dam-break"
+        name = f"{self.config}x{self.world} weak" if scaling == "weak" else f"{self.config} on {self.world} GPUs"
+        return (f"{name}: {self.n_total} particles, {sc.dim}D {kind}, column {sc.nx}x{sc.ny}x{sc.nz}, "
+                f"tank {sc.tx}x{sc.ty}x{sc.tz} dx, x-slabs (rank 0 {self.cut})")
+
+    def close(self):
+        self.ctx.close()
 
 
 class SingleRunner:

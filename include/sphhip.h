@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define SPH_ABI_VERSION 1
+#define SPH_ABI_VERSION 2
 
 typedef struct sph_ctx sph_ctx;
 
@@ -41,13 +41,18 @@ typedef enum sph_model {
 } sph_model;
 
 #define SPH_FLAG_PROFILE 1  /* time every kernel launch with HIP events (sph_get_kernel_stat) */
+#define SPH_FLAG_VALIDATE 2 /* multi-GPU step: wait after every step and check every slab's device sizes */
 
 /* replaces: new ComputeBuffer(particleCount, 84) … (ParticleSystemController.cs:373-388) */
 typedef struct sph_config {
     int32_t model;          /* sph_model */
     int32_t dim;            /* 2 or 3 (Model R: 3) */
-    int32_t capacity;       /* particleCount (ParticleSystemController.cs:12) */
+    int32_t capacity;       /* particleCount (ParticleSystemController.cs:12); ndev > 1: per-GPU minimum */
     int32_t flags;          /* SPH_FLAG_* */
+    int32_t ndev;           /* GPUs this context drives (0 or 1: one). ndev > 1 (Model S): the domain is
+                               cut into x-slabs over devices device, device+1, ... (modulo the visible
+                               count), one slab context per GPU, halos moved by device-to-device copies
+                               over xGMI; sph_init_scenario / sph_step / sph_read_* work as for one GPU */
 } sph_config;
 
 /* replaces: computeShader.SetFloat/SetInt uniforms (ParticleSystemController.cs:255-263,
@@ -286,6 +291,34 @@ int sph_slab_force(sph_ctx* ctx, float dt, int32_t part);   /* 0 all, 1 interior
 int sph_slab_finish_step(sph_ctx* ctx, float dt);
 /* owned particles as 8-float records (x, y, z, u, v, w, id-bits, ρ); count >= owned */
 int sph_slab_read_owned(sph_ctx* ctx, float* records, int32_t count, int32_t* n_owned);
+
+/* ---- the multi-GPU step inside the library (SPEC_SPH.md §3). A multi-GPU
+ *      context (sph_config.ndev > 1, or one context per process joined by sph_comm_init) runs the
+ *      whole decomposed step in sph_step: migration + x,v halo, incremental re-sort across the halo,
+ *      density, ρ halo overlapped with the interior force pass, boundary force pass, and the
+ *      re-balancing of the cuts every sph_set_rebalance steps. Every per-step size stays on the device
+ *      (message headers; no host read per step): halo messages have capacities both neighbours derive
+ *      from the counts of two steps before; an overflow is detected on the device and reported by a
+ *      later sph_step as SPH_ERR_CAPACITY. ---- */
+typedef struct sph_comm_id {
+    char internal[128];         /* an RCCL unique id (ncclUniqueId) */
+} sph_comm_id;
+/* rank 0 creates the id; the host hands the 128 bytes to every rank (any channel) */
+int sph_comm_unique_id(sph_comm_id* out);
+/* one process per GPU: this context is rank `rank` of `nranks`, exchanging over RCCL (xGMI). Model S,
+ * before sph_init_scenario, which then keeps this rank's slab of the scenario (equal-count cuts). */
+int sph_comm_init(sph_ctx* ctx, const sph_comm_id* id, int32_t nranks, int32_t rank);
+/* re-balancing interval of the multi-GPU step in steps (default 50; 0: off) */
+int sph_set_rebalance(sph_ctx* ctx, int32_t every);
+/* the decomposition: this process's rank and the world size, its (first local) slab, the particles
+ * it owns (ndev > 1: all of them), and the global particle count */
+typedef struct sph_decomp {
+    int32_t rank, world, local_ranks;
+    sph_slab cut;
+    int64_t owned, total;
+    int32_t rebalances;
+} sph_decomp;
+int sph_get_decomposition(sph_ctx* ctx, sph_decomp* out);
 
 #ifdef __cplusplus
 }

@@ -28,6 +28,7 @@ _STATUS = {0: "SPH_OK", -1: "SPH_ERR_INVALID", -2: "SPH_ERR_HIP", -3: "SPH_ERR_C
 SPH_MODEL_CONTACT = 0
 SPH_MODEL_WCSPH = 1
 SPH_FLAG_PROFILE = 1
+SPH_FLAG_VALIDATE = 2
 SPH_SCENARIO_DAMBREAK = 0
 SPH_SCENARIO_SLOSHING = 1
 SPH_SCENARIO_SPHERE = 2
@@ -66,7 +67,8 @@ assert SPLIT92.itemsize == 92
 
 
 class SphConfig(C.Structure):
-    _fields_ = [("model", C.c_int32), ("dim", C.c_int32), ("capacity", C.c_int32), ("flags", C.c_int32)]
+    _fields_ = [("model", C.c_int32), ("dim", C.c_int32), ("capacity", C.c_int32), ("flags", C.c_int32),
+                ("ndev", C.c_int32)]
 
 
 class SphParams(C.Structure):
@@ -108,10 +110,21 @@ class SphSlab(C.Structure):
     _fields_ = [("cx_lo", C.c_int32), ("cx_hi", C.c_int32)]
 
 
+class SphCommId(C.Structure):
+    _fields_ = [("internal", C.c_char * 128)]
+
+
+class SphDecomp(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("world", C.c_int32), ("local_ranks", C.c_int32), ("cut", SphSlab),
+                ("owned", C.c_int64), ("total", C.c_int64), ("rebalances", C.c_int32)]
+
+
 SPH_SLAB_RECORD_BYTES = 32
+SPH_ABI_VERSION = 2
 
 assert C.sizeof(SphDragInput) == 20
-assert C.sizeof(SphConfig) == 16
+assert C.sizeof(SphConfig) == 20
+assert C.sizeof(SphCommId) == 128
 
 # every entry point declared in include/sphhip.h, with its ctypes signature
 _P = C.c_void_p
@@ -176,6 +189,10 @@ SIGNATURES = {
     "sph_slab_force": ([_P, C.c_float, _I], C.c_int),
     "sph_slab_finish_step": ([_P, C.c_float], C.c_int),
     "sph_slab_read_owned": ([_P, _P, _I, C.POINTER(C.c_int32)], C.c_int),
+    "sph_comm_unique_id": ([C.POINTER(SphCommId)], C.c_int),
+    "sph_comm_init": ([_P, C.POINTER(SphCommId), _I, _I], C.c_int),
+    "sph_set_rebalance": ([_P, _I], C.c_int),
+    "sph_get_decomposition": ([_P, C.POINTER(SphDecomp)], C.c_int),
 }
 
 

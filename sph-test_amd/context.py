@@ -12,15 +12,17 @@ from . import _abi as A
 class Context:
     """A device context: particle buffers, grid, stream (include/sphhip.h)."""
 
-    def __init__(self, model: int, dim: int, capacity: int, device: int = 0, profile: bool = False):
+    def __init__(self, model: int, dim: int, capacity: int, device: int = 0, profile: bool = False, ndev: int = 1,
+                 validate: bool = False):
         self._L = A.lib()
-        cfg = A.SphConfig(model, dim, capacity, A.SPH_FLAG_PROFILE if profile else 0)
+        flags = (A.SPH_FLAG_PROFILE if profile else 0) | (A.SPH_FLAG_VALIDATE if validate else 0)
+        cfg = A.SphConfig(model, dim, capacity, flags, ndev)
         h = C.c_void_p()
         st = self._L.sph_create(C.byref(cfg), device, C.byref(h))
         if st != A.SPH_OK:
             raise A.SphError("sph_create", st, f"model={model} dim={dim} capacity={capacity} device={device}")
         self._h = h
-        self.model, self.dim, self.capacity, self.device = model, dim, capacity, device
+        self.model, self.dim, self.capacity, self.device, self.ndev = model, dim, capacity, device, ndev
         self.n = 0
         self.nbonds = 0
 
@@ -61,6 +63,21 @@ class Context:
         s = C.c_void_p()
         self._chk("sph_get_stream", self._L.sph_get_stream(self._h, C.byref(s)))
         return int(s.value or 0)
+
+    # -------------------------------------------------------------- multi-GPU (sphhip.h: the decomposed step)
+    def comm_init(self, comm_id: bytes, nranks: int, rank: int) -> None:
+        """Join an RCCL communicator (one process per GPU): rank `rank` of `nranks`."""
+        cid = A.SphCommId()
+        C.memmove(C.byref(cid), comm_id, 128)
+        self._chk("sph_comm_init", self._L.sph_comm_init(self._h, C.byref(cid), nranks, rank))
+
+    def set_rebalance(self, every: int) -> None:
+        self._chk("sph_set_rebalance", self._L.sph_set_rebalance(self._h, every))
+
+    def decomposition(self) -> A.SphDecomp:
+        d = A.SphDecomp()
+        self._chk("sph_get_decomposition", self._L.sph_get_decomposition(self._h, C.byref(d)))
+        return d
 
     def set_params(self, params: A.SphParams) -> None:
         self._chk("sph_set_params", self._L.sph_set_params(self._h, C.byref(params)))
@@ -252,6 +269,13 @@ def scenario_params(sc: A.SphScenario):
     dt = C.c_float()
     A.check("sph_scenario_params", A.lib().sph_scenario_params(C.byref(sc), C.byref(p), C.byref(dt)))
     return p, float(dt.value)
+
+
+def comm_unique_id() -> bytes:
+    """A new RCCL unique id (rank 0); the caller hands the 128 bytes to every rank."""
+    cid = A.SphCommId()
+    A.check("sph_comm_unique_id", A.lib().sph_comm_unique_id(C.byref(cid)))
+    return C.string_at(C.byref(cid), 128)
 
 
 def make_scenario(kind: int, dim: int, nx: int, ny: int, nz: int, tx: int, ty: int, tz: int,

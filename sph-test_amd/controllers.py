@@ -40,12 +40,18 @@ class SPHSim:
     """Weakly-compressible SPH simulation on one GPU (Model S)."""
 
     def __init__(self, scenario: A.SphScenario, device: int = 0, capacity: Optional[int] = None,
-                 profile: bool = False):
+                 profile: bool = False, ndev: int = 1, rebalance_every: Optional[int] = None,
+                 validate: bool = False):
+        """ndev > 1: the domain is cut into x-slabs over ndev GPUs (device, device+1, ...) inside the
+        library; positions() / velocities() / density() still return every particle in index order."""
         self.scenario = scenario
         self.params, self.dt = scenario_params(scenario)
         n = scenario.nx * scenario.ny * (scenario.nz if scenario.dim == 3 else 1)
-        self.ctx = Context(A.SPH_MODEL_WCSPH, scenario.dim, capacity or n, device=device, profile=profile)
+        self.ctx = Context(A.SPH_MODEL_WCSPH, scenario.dim, capacity or (0 if ndev > 1 else n), device=device,
+                           profile=profile, ndev=ndev, validate=validate)
         self.ctx.set_params(self.params)
+        if ndev > 1 and rebalance_every is not None:
+            self.ctx.set_rebalance(rebalance_every)
         self.ctx.init_scenario(scenario)
 
     @classmethod

@@ -17,7 +17,9 @@ int sph_create(const sph_config* cfg, int32_t device, sph_ctx** out) {
     if (cfg->model != SPH_MODEL_CONTACT && cfg->model != SPH_MODEL_WCSPH) return SPH_ERR_INVALID;
     if (cfg->dim != 2 && cfg->dim != 3) return SPH_ERR_INVALID;
     if (cfg->model == SPH_MODEL_CONTACT && cfg->dim != 3) return SPH_ERR_INVALID;
-    if (cfg->capacity < 0) return SPH_ERR_INVALID;
+    if (cfg->capacity < 0 || cfg->ndev < 0) return SPH_ERR_INVALID;
+    const bool group = cfg->ndev > 1;
+    if (group && cfg->model != SPH_MODEL_WCSPH) return SPH_ERR_INVALID;   // the decomposed step is Model S
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SPH_ERR_HIP;
     if (device < 0 || device >= ndev) return SPH_ERR_INVALID;
@@ -35,8 +37,8 @@ int sph_create(const sph_config* cfg, int32_t device, sph_ctx** out) {
     }
     *ctx->mv_host = 0u;
     ctx->own_stream = true;
-    ctx->capacity = cfg->capacity;
-    int r = alloc_particles(ctx, cfg->capacity);
+    ctx->capacity = group ? 0 : cfg->capacity;   // a group's slots live in its per-GPU slab contexts
+    int r = alloc_particles(ctx, ctx->capacity);
     if (r != SPH_OK) {
         free_all(ctx);
         (void)hipStreamDestroy(ctx->stream);
@@ -54,12 +56,18 @@ int sph_create(const sph_config* cfg, int32_t device, sph_ctx** out) {
         if (r != SPH_OK) { sph_destroy(ctx); return r; }
         ctx->params_set = true;
     }
+    if (group && (r = multi_create_group(ctx)) != SPH_OK) { sph_destroy(ctx); return r; }
     *out = ctx;
     return SPH_OK;
 }
 
+// the entry points that address one GPU's slot arrays directly have no meaning on a group
+#define NOT_GROUP(ctx) \
+    if (is_group(ctx)) return fail(ctx, SPH_ERR_STATE, "%s: not available on a multi-GPU (ndev > 1) context", __func__)
+
 void sph_destroy(sph_ctx* ctx) {
     if (!ctx) return;
+    multi_free(ctx);
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     resolve_pending(ctx);
@@ -82,6 +90,7 @@ void sph_destroy(sph_ctx* ctx) {
 
 int sph_set_stream(sph_ctx* ctx, void* s) {
     if (!ctx) return SPH_ERR_INVALID;
+    NOT_GROUP(ctx);
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (s == nullptr) {
         if (!ctx->own_stream) {
@@ -105,6 +114,15 @@ int sph_get_stream(sph_ctx* ctx, void** s) {
 int sph_set_params(sph_ctx* ctx, const sph_params* params) {
     if (!ctx || !params) return SPH_ERR_INVALID;
     HIPCHK(hipSetDevice(ctx->device));
+    if (is_group(ctx)) {   // kept for the slab contexts (made at sph_init_scenario), applied to existing ones
+        if (!(params->h > 0.f) || !(params->dx > 0.f) || !(params->rho0 > 0.f))
+            return fail(ctx, SPH_ERR_INVALID, "Model S needs dx, h, rho0 > 0");
+        ctx->prm = *params;
+        ctx->params_set = true;
+        for (sph_ctx* k : multi_kids(ctx))
+            if (int r = sph_set_params(k, params)) return fail(ctx, r, "%s", sph_last_error(k));
+        return SPH_OK;
+    }
     const sph_params old = ctx->prm;
     ctx->prm = *params;
     int r = derive(ctx);
@@ -158,6 +176,7 @@ int sph_scenario_params(const sph_scenario* sc, sph_params* out, float* dt_out) 
 
 int sph_upload_particles_aos84(sph_ctx* ctx, const void* src, int32_t count) {
     if (!ctx || (!src && count > 0) || count < 0) return SPH_ERR_INVALID;
+    NOT_GROUP(ctx);
     if (count > ctx->capacity) return fail(ctx, SPH_ERR_CAPACITY, "count %d > capacity %d", count, ctx->capacity);
     HIPCHK(hipSetDevice(ctx->device));
     if (count > 0) {
@@ -176,6 +195,7 @@ int sph_upload_particles_aos84(sph_ctx* ctx, const void* src, int32_t count) {
 
 int sph_download_particles_aos84(sph_ctx* ctx, void* dst, int32_t count) {
     if (!ctx || (!dst && count > 0)) return SPH_ERR_INVALID;
+    NOT_GROUP(ctx);
     if (count < ctx->n) return fail(ctx, SPH_ERR_INVALID, "count %d < active particles %d", count, ctx->n);
     HIPCHK(hipSetDevice(ctx->device));
     if (ctx->n > 0) {
@@ -190,6 +210,7 @@ int sph_download_particles_aos84(sph_ctx* ctx, void* dst, int32_t count) {
 
 int sph_upload_state(sph_ctx* ctx, const float* pos3, const float* vel3, int32_t count) {
     if (!ctx || (!pos3 && count > 0) || count < 0) return SPH_ERR_INVALID;
+    NOT_GROUP(ctx);
     if (is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "sph_upload_state is Model S only; use aos84");
     if (count > ctx->capacity) return fail(ctx, SPH_ERR_CAPACITY, "count %d > capacity %d", count, ctx->capacity);
     HIPCHK(hipSetDevice(ctx->device));
@@ -211,6 +232,10 @@ int sph_upload_state(sph_ctx* ctx, const float* pos3, const float* vel3, int32_t
 
 int sph_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
     if (!ctx || !sc) return SPH_ERR_INVALID;
+    if (ctx->mg) {   // multi-GPU: this process's slabs of the scenario
+        HIPCHK(hipSetDevice(ctx->device));
+        return is_group(ctx) ? multi_init_scenario(ctx, sc) : multi_init_rank(ctx, sc);
+    }
     if (is_contact(ctx)) {
         if (sc->kind != SPH_SCENARIO_SPHERE) return fail(ctx, SPH_ERR_INVALID, "Model R scenarios: SPH_SCENARIO_SPHERE");
         return sph_init_particles(ctx, sc->nx, sc->nx, 0, 0);
@@ -370,6 +395,7 @@ int sph_set_particles_aos84(sph_ctx* ctx, int32_t first, int32_t count, const vo
 
 int sph_step(sph_ctx* ctx, float dt, int32_t nsteps) {
     if (!ctx || nsteps < 0 || !(dt >= 0.f)) return SPH_ERR_INVALID;
+    if (ctx->mg) return multi_step(ctx, dt, nsteps);
     if (ctx->slab) return fail(ctx, SPH_ERR_STATE, "slab mode: the host drives sph_slab_* phases");
     if (!ctx->params_set) return fail(ctx, SPH_ERR_STATE, "sph_set_params first");
     HIPCHK(hipSetDevice(ctx->device));
@@ -475,9 +501,11 @@ static int read_f4(sph_ctx* ctx, const float4* src, float* dst, int32_t count, i
 }
 
 int sph_read_positions(sph_ctx* ctx, float* xyz, int32_t count) {
+    if (ctx && is_group(ctx)) return (!xyz && count > 0) ? SPH_ERR_INVALID : multi_read(ctx, 0, xyz, count);
     return ctx ? read_f4(ctx, ctx->pos, xyz, count, 3) : SPH_ERR_INVALID;
 }
 int sph_read_velocities(sph_ctx* ctx, float* xyz, int32_t count) {
+    if (ctx && is_group(ctx)) return (!xyz && count > 0) ? SPH_ERR_INVALID : multi_read(ctx, 1, xyz, count);
     return ctx ? read_f4(ctx, ctx->vel, xyz, count, 3) : SPH_ERR_INVALID;
 }
 int sph_read_rotations(sph_ctx* ctx, float* xyzw, int32_t count) {
@@ -503,9 +531,15 @@ static int read_rp(sph_ctx* ctx, float* dst, int32_t count, int32_t comp) {
     return SPH_OK;
 }
 
-int sph_read_density(sph_ctx* ctx, float* rho, int32_t count) { return read_rp(ctx, rho, count, 0); }
+int sph_read_density(sph_ctx* ctx, float* rho, int32_t count) {
+    if (ctx && is_group(ctx)) return (!rho && count > 0) ? SPH_ERR_INVALID : multi_read(ctx, 2, rho, count);
+    return read_rp(ctx, rho, count, 0);
+}
 
-int sph_read_pressure_term(sph_ctx* ctx, float* prho, int32_t count) { return read_rp(ctx, prho, count, 1); }
+int sph_read_pressure_term(sph_ctx* ctx, float* prho, int32_t count) {
+    if (ctx && is_group(ctx)) return fail(ctx, SPH_ERR_STATE, "not available on a multi-GPU context");
+    return read_rp(ctx, prho, count, 1);
+}
 
 int sph_read_torque_int(sph_ctx* ctx, int32_t* xyz, int32_t count) {
     if (!ctx || (!xyz && count > 0)) return SPH_ERR_INVALID;
@@ -527,6 +561,7 @@ static const size_t RB_BYTES[3] = {12, 16, 84};   // positions, rotations, 84-by
 int sph_request_readback(sph_ctx* ctx, int32_t fields) {
     if (!ctx || fields <= 0 || (fields & ~(SPH_READBACK_POSITIONS | SPH_READBACK_ROTATIONS | SPH_READBACK_PARTICLES)))
         return SPH_ERR_INVALID;
+    NOT_GROUP(ctx);
     if (ctx->slab) return fail(ctx, SPH_ERR_STATE, "slab mode: use sph_slab_read_owned");
     if ((fields & (SPH_READBACK_ROTATIONS | SPH_READBACK_PARTICLES)) && !is_contact(ctx))
         return fail(ctx, SPH_ERR_STATE, "rotations / 84-byte particles are Model R fields");
@@ -602,6 +637,7 @@ int sph_readback_count(sph_ctx* ctx, int32_t* count) {
 
 int sph_export_aos84_device(sph_ctx* ctx, void* dev_dst, int32_t count) {
     if (!ctx || (!dev_dst && count > 0)) return SPH_ERR_INVALID;
+    NOT_GROUP(ctx);
     if (ctx->slab) return fail(ctx, SPH_ERR_STATE, "slab mode");
     if (count < ctx->n) return fail(ctx, SPH_ERR_INVALID, "count %d < particles %d", count, ctx->n);
     HIPCHK(hipSetDevice(ctx->device));
@@ -614,6 +650,7 @@ int sph_export_aos84_device(sph_ctx* ctx, void* dev_dst, int32_t count) {
 
 int sph_write_draw_args(sph_ctx* ctx, void* dev_args) {
     if (!ctx || !dev_args) return SPH_ERR_INVALID;
+    NOT_GROUP(ctx);
     HIPCHK(hipSetDevice(ctx->device));
     const int32_t inst = is_contact(ctx) ? contact_active(ctx) : ctx->n;
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)((uint32_t*)dev_args + 1), inst, 1, ctx->stream));
@@ -622,6 +659,8 @@ int sph_write_draw_args(sph_ctx* ctx, void* dev_args) {
 
 int sph_synchronize(sph_ctx* ctx) {
     if (!ctx) return SPH_ERR_INVALID;
+    for (sph_ctx* k : multi_kids(ctx))
+        if (int r = sph_synchronize(k)) return fail(ctx, r, "%s", sph_last_error(k));
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return SPH_OK;
@@ -636,12 +675,43 @@ int sph_get_stats(sph_ctx* ctx, sph_stats* out) {
     out->grid[0] = ctx->grid.gx; out->grid[1] = ctx->grid.gy; out->grid[2] = ctx->grid.gz;
     out->key_bits = ctx->key_bits;
     out->device_bytes = ctx->device_bytes;
+    const std::vector<sph_ctx*> kids = multi_kids(ctx);
+    if (!kids.empty()) {   // a group: the global grid, every slab's slots and memory
+        sph_decomp d;
+        if (int r = sph_get_decomposition(ctx, &d)) return r;
+        out->active = (int32_t)d.total;
+        out->capacity = 0;
+        out->device_bytes = 0;
+        for (sph_ctx* k : kids) {
+            out->capacity += k->capacity;
+            out->device_bytes += k->device_bytes;
+        }
+        out->grid[0] = kids[0]->gglobal.gx; out->grid[1] = kids[0]->gglobal.gy; out->grid[2] = kids[0]->gglobal.gz;
+        out->key_bits = kids[0]->key_bits;
+    }
     return SPH_OK;
+}
+
+// a group's kernel statistics: its slab contexts' merged by kernel name
+static void merge_kid_stats(sph_ctx* ctx) {
+    const std::vector<sph_ctx*> kids = multi_kids(ctx);
+    if (kids.empty()) return;
+    ctx->kstats.clear();
+    for (sph_ctx* k : kids) {
+        if (!k->pending.empty()) resolve_pending(k);
+        for (const KStat& s : k->kstats) {
+            const int i = kstat_index(ctx, s.name.c_str());
+            ctx->kstats[i].launches += s.launches;
+            ctx->kstats[i].total_ms += s.total_ms;
+            ctx->kstats[i].bytes = s.bytes;
+        }
+    }
 }
 
 int sph_get_kernel_stat(sph_ctx* ctx, int32_t index, sph_kernel_stat* out) {
     if (!ctx || !out) return SPH_ERR_INVALID;
     if (!ctx->pending.empty()) resolve_pending(ctx);
+    merge_kid_stats(ctx);
     if (index < 0 || index >= (int32_t)ctx->kstats.size()) return SPH_ERR_INVALID;
     const KStat& k = ctx->kstats[index];
     std::memset(out, 0, sizeof *out);
@@ -654,6 +724,7 @@ int sph_get_kernel_stat(sph_ctx* ctx, int32_t index, sph_kernel_stat* out) {
 
 int sph_reset_kernel_stats(sph_ctx* ctx) {
     if (!ctx) return SPH_ERR_INVALID;
+    for (sph_ctx* k : multi_kids(ctx)) sph_reset_kernel_stats(k);
     if (!ctx->pending.empty()) resolve_pending(ctx);
     for (auto& k : ctx->kstats) { k.launches = 0; k.total_ms = 0.0; }
     return SPH_OK;
@@ -661,6 +732,7 @@ int sph_reset_kernel_stats(sph_ctx* ctx) {
 
 int sph_read_sorted_ids(sph_ctx* ctx, int32_t* ids, int32_t count) {
     if (!ctx || (!ids && count > 0)) return SPH_ERR_INVALID;
+    NOT_GROUP(ctx);
     if (count < ctx->n) return fail(ctx, SPH_ERR_INVALID, "count %d < active particles %d", count, ctx->n);
     HIPCHK(hipSetDevice(ctx->device));
     if (ctx->n > 0) HIPCHK(hipMemcpyAsync(ids, ctx->id, (size_t)ctx->n * 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -670,6 +742,7 @@ int sph_read_sorted_ids(sph_ctx* ctx, int32_t* ids, int32_t count) {
 
 int sph_read_cell_start(sph_ctx* ctx, uint32_t* cs, int32_t count) {
     if (!ctx || (!cs && count > 0)) return SPH_ERR_INVALID;
+    NOT_GROUP(ctx);
     if ((uint32_t)count < ctx->grid.ncells + 1)
         return fail(ctx, SPH_ERR_INVALID, "count %d < ncells+1 = %u", count, ctx->grid.ncells + 1);
     HIPCHK(hipSetDevice(ctx->device));
@@ -680,6 +753,16 @@ int sph_read_cell_start(sph_ctx* ctx, uint32_t* cs, int32_t count) {
 
 int sph_read_path_counts(sph_ctx* ctx, uint32_t counts[4], int32_t reset) {
     if (!ctx || !counts) return SPH_ERR_INVALID;
+    const std::vector<sph_ctx*> kids = multi_kids(ctx);
+    if (!kids.empty()) {
+        for (int k = 0; k < 4; ++k) counts[k] = 0;
+        for (sph_ctx* kc : kids) {
+            uint32_t c[4];
+            if (int r = sph_read_path_counts(kc, c, reset)) return r;
+            for (int k = 0; k < 4; ++k) counts[k] += c[k];
+        }
+        return SPH_OK;
+    }
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipMemcpyAsync(counts, ctx->paths, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
     if (reset) HIPCHK(hipMemsetAsync(ctx->paths, 0, 4 * sizeof(uint32_t), ctx->stream));
@@ -718,6 +801,7 @@ int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int3
 
 int sph_resize(sph_ctx* ctx, int32_t capacity) {
     if (!ctx || capacity < 0) return SPH_ERR_INVALID;
+    NOT_GROUP(ctx);
     if (capacity < ctx->n) return fail(ctx, SPH_ERR_CAPACITY, "capacity %d < active particles %d", capacity, ctx->n);
     if (ctx->slab) return fail(ctx, SPH_ERR_STATE, "slab mode");
     HIPCHK(hipSetDevice(ctx->device));

@@ -1,0 +1,976 @@
+// abi_multi.cpp — the decomposed Model S step inside the library (SPEC_SPH.md §3).
+//
+// The reference has one GPU and one host thread (ParticleSystemController.cs:244-351, InitializeBuffers
+// :373-451). Here one sph_step drives an x-slab decomposition over several GPUs, in two forms:
+//   * sph_config.ndev > 1: one context in one process owns a slab context per GPU (a "local group");
+//     the halos move by device-to-device copies (hipMemcpyPeerAsync: xGMI between GPUs, a plain copy
+//     when two slabs share a device, as on a one-GPU test box);
+//   * sph_comm_init: one context per process (one process per GPU, as torchrun launches), the halos
+//     move over RCCL (ncclSend / ncclRecv in one group per exchange, so both neighbours at once).
+// Both run the same per-rank phases (the kernels of the per-phase ABI in abi_slab.cpp), phase-major
+// over the ranks this process drives:
+//   A  send counts + packing of migrants / x,v halo into capacity-sized messages (header = count)
+//   X1 exchange 1
+//   B  sizes from the headers → incremental re-sort over [left | own | right] (device sizes), or the
+//      full radix sort (after a re-cut: a host-sized step) → ranges → density → ρ of the boundary columns
+//   X2 exchange 2 on the comm stream, in flight while the interior columns' force pass runs
+//   C  ghost densities in → boundary columns' force pass → finish
+// No host read happens in a steady-state step. Message capacities come from the counts of two steps
+// before (a kernel writes them to mapped pinned memory; both neighbours read the same numbers, so they
+// agree on every message size), with a margin far above what particles moving < 0.1 h per step can add.
+// A larger count is caught on the device (SZ_* flags) and the next sph_step fails with SPH_ERR_CAPACITY.
+// The first two steps after the initial cut and after every re-cut size the messages exactly (a count
+// exchange and one host read per exchange), as the lagged counts then describe other columns.
+#include "host.h"
+
+#include <rccl/rccl.h>
+
+namespace sph {
+
+constexpr int LAG_SLOTS = 4;
+constexpr int LAG_WORDS = 16;
+constexpr int SDEV_TOTALS = 10;   // sdev[10..11]: this step's send counts (sdev[0..5] picks, [8..9] gap counters)
+
+struct RankState {
+    sph_ctx* c = nullptr;
+    int rank = 0, world = 1, left = -1, right = -1;
+    hipStream_t comm = nullptr;                       // exchange 2 (overlaps the interior force pass)
+    hipEvent_t ev_packed = nullptr, ev_in = nullptr;  // exchange 1: messages packed / received
+    hipEvent_t ev_rho_packed = nullptr, ev_rho_recv = nullptr;
+    SlabSizes* dz = nullptr;
+    float4* msg_out[2] = {nullptr, nullptr};
+    float4* msg_in[2] = {nullptr, nullptr};
+    int32_t mcap_out[2] = {0, 0}, mcap_in[2] = {0, 0};   // allocated records
+    float2* rho_out[2] = {nullptr, nullptr};
+    float2* rho_in[2] = {nullptr, nullptr};
+    int32_t rcap_out[2] = {0, 0}, rcap_in[2] = {0, 0};
+    int32_t c1o[2] = {0, 0}, c1i[2] = {0, 0}, c2o[2] = {0, 0}, c2i[2] = {0, 0};   // this step's capacities
+    uint32_t* cnt_dev = nullptr;   // [4] received counts (exact-size steps over RCCL)
+    uint32_t* lag = nullptr;       // pinned, mapped: LAG_SLOTS x LAG_WORDS (launch_slab_lag)
+    hipEvent_t lag_ev[LAG_SLOTS] = {};
+    int64_t cin_hist[LAG_SLOTS] = {};   // Σ records received per step (slot bound bookkeeping)
+    int64_t since_cut = 0;              // steps since the initial cut or the last re-cut
+    int64_t n_prev_ub = 0;              // upper bound of the previous step's assembled slots
+    int64_t n_ub = 0;                   // this step's
+    int32_t nb_send = 1;                // count / pack blocks of this step
+};
+
+struct Multi {
+    int mode = 0;                    // 1: local group (ndev), 2: RCCL
+    std::vector<sph_ctx*> kids;      // local group: one slab context per GPU (owned)
+    std::vector<RankState> ranks;    // the ranks this process drives
+    int world = 1;
+    ncclComm_t comm = nullptr;
+    int64_t* hist_dev = nullptr;     // RCCL: the re-balancing histogram
+    int32_t hist_cap = 0;
+    int rebalance_every = 50;
+    int rebalances = 0;
+    std::vector<sph_slab> cuts;      // every rank's owned columns
+    int64_t n_total = 0;
+    bool ready = false;
+    int64_t steps = 0;
+};
+
+namespace {
+
+#define NCCLCHK(call)                                                                                  \
+    do {                                                                                               \
+        ncclResult_t r_ = (call);                                                                      \
+        if (r_ != ncclSuccess) return fail(ctx, SPH_ERR_HIP, "%s: %s", #call, ncclGetErrorString(r_)); \
+    } while (0)
+
+int32_t cap_of(uint32_t cnt) {
+    // the count two steps ago + 25% + 512 (a one-column halo changes by far less in two steps), whole 256s
+    const int64_t c = (int64_t)cnt + cnt / 4 + 512;
+    return (int32_t)std::min<int64_t>((c + 255) / 256 * 256, INT32_MAX / 4);
+}
+
+int global_columns(const sph_params& p) {
+    const float cell = 2.0f * p.h;
+    return (int)floorf(p.box[0] / cell) + 1;
+}
+
+// Lattice x-indices per global column of a scenario (jitter ignored; slab.py balanced_cuts). Times
+// ny·nz: the initial particles per column.
+std::vector<int64_t> lattice_columns(const sph_scenario& sc, const sph_params& p) {
+    const float cell = 2.0f * p.h, inv = 1.0f / cell;
+    const int G = global_columns(p);
+    std::vector<int64_t> per(G, 0);
+    for (int i = 0; i < sc.nx; ++i) {
+        const float x = ((float)i + 0.5f) * sc.dx;
+        int c = (int)floorf(x * inv);
+        c = std::min(std::max(c, 0), G - 1);
+        per[c] += 1;
+    }
+    return per;
+}
+
+// Equal-count cuts (slab.py balanced_cuts): cut r at the first column whose cumulative count reaches r/world.
+std::vector<sph_slab> balanced_cuts(const std::vector<int64_t>& per, int world) {
+    const int G = (int)per.size();
+    std::vector<double> cum(G);
+    double t = 0;
+    for (int c = 0; c < G; ++c) cum[c] = (t += (double)per[c]);
+    std::vector<int> b{0};
+    for (int r = 1; r < world; ++r) {
+        const double target = t * r / world;
+        int c = (int)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin()) + 1;
+        c = std::max(c, b.back() + 1);
+        c = std::min(c, G - (world - r));
+        b.push_back(c);
+    }
+    b.push_back(G);
+    std::vector<sph_slab> out(world);
+    for (int r = 0; r < world; ++r) out[r] = sph_slab{b[r], b[r + 1]};
+    return out;
+}
+
+// slab.py rebalance_cuts: every inner cut moves at most one column toward equal counts; moves that
+// would leave a slab narrower than two columns are dropped. A pure function: every rank agrees.
+std::vector<sph_slab> rebalance_cuts(const std::vector<sph_slab>& cuts, const std::vector<int64_t>& hist) {
+    const int world = (int)cuts.size();
+    std::vector<int> b, nb;
+    for (auto& c : cuts) b.push_back(c.cx_lo);
+    b.push_back(cuts.back().cx_hi);
+    nb = b;
+    std::vector<double> cum(hist.size());
+    double t = 0;
+    for (size_t c = 0; c < hist.size(); ++c) cum[c] = (t += (double)hist[c]);
+    if (t > 0)
+        for (int r = 1; r < world; ++r) {
+            const int ideal = (int)(std::lower_bound(cum.begin(), cum.end(), t * r / world) - cum.begin()) + 1;
+            nb[r] = b[r] + std::max(-1, std::min(1, ideal - b[r]));
+        }
+    for (bool changed = true; changed;) {
+        changed = false;
+        for (int r = 1; r < world; ++r)
+            if (nb[r] != b[r] && (nb[r] - nb[r - 1] < 2 || nb[r + 1] - nb[r] < 2)) {
+                nb[r] = b[r];
+                changed = true;
+            }
+    }
+    std::vector<sph_slab> out(world);
+    for (int r = 0; r < world; ++r) out[r] = sph_slab{nb[r], nb[r + 1]};
+    return out;
+}
+
+// Every stream of the ranks this process drives: a message buffer is about to be reallocated and a
+// neighbour's copy may still read it (rare: capacities only grow).
+int sync_all(Multi& M, sph_ctx* ctx) {
+    for (auto& R : M.ranks) {
+        if (!R.c) continue;
+        HIPCHK(hipSetDevice(R.c->device));
+        HIPCHK(hipStreamSynchronize(R.c->stream));
+        if (R.comm) HIPCHK(hipStreamSynchronize(R.comm));
+    }
+    HIPCHK(hipSetDevice(ctx->device));
+    return SPH_OK;
+}
+
+template <class T>
+int ensure_buf(Multi& M, sph_ctx* ctx, T** p, int32_t* cap, int32_t need) {
+    if (need <= *cap && *p) return SPH_OK;
+    int r = sync_all(M, ctx);
+    if (r != SPH_OK) return r;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    const int32_t n = std::max(need + need / 2, 4096);
+    HIPCHK(hipMalloc((void**)p, (size_t)n * sizeof(T)));
+    *cap = n;
+    return SPH_OK;
+}
+
+int rank_init(RankState& R) {
+    sph_ctx* ctx = R.c;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamCreateWithFlags(&R.comm, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&R.ev_packed, &R.ev_in, &R.ev_rho_packed, &R.ev_rho_recv})
+        HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    for (auto& e : R.lag_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipMalloc((void**)&R.dz, sizeof(SlabSizes)));
+    HIPCHK(hipMemset(R.dz, 0, sizeof(SlabSizes)));
+    R.c->dz = R.dz;
+    HIPCHK(hipMalloc((void**)&R.cnt_dev, 4 * sizeof(uint32_t)));
+    HIPCHK(hipMemset(R.c->sdev + SDEV_TOTALS, 0, 2 * sizeof(uint32_t)));
+    HIPCHK(hipHostMalloc((void**)&R.lag, LAG_SLOTS * LAG_WORDS * sizeof(uint32_t), hipHostMallocMapped));
+    std::memset(R.lag, 0, LAG_SLOTS * LAG_WORDS * sizeof(uint32_t));
+    return SPH_OK;
+}
+
+void rank_free(RankState& R) {
+    if (!R.c) return;
+    (void)hipSetDevice(R.c->device);
+    if (R.comm) (void)hipStreamSynchronize(R.comm);
+    for (hipEvent_t e : {R.ev_packed, R.ev_in, R.ev_rho_packed, R.ev_rho_recv})
+        if (e) (void)hipEventDestroy(e);
+    for (auto e : R.lag_ev)
+        if (e) (void)hipEventDestroy(e);
+    for (int s = 0; s < 2; ++s) {
+        dfree(R.msg_out[s]); dfree(R.msg_in[s]); dfree(R.rho_out[s]); dfree(R.rho_in[s]);
+    }
+    R.c->dz = nullptr;
+    R.c->dz_ahead = false;
+    dfree(R.dz);
+    dfree(R.cnt_dev);
+    if (R.lag) (void)hipHostFree(R.lag);
+    if (R.comm) (void)hipStreamDestroy(R.comm);
+    R = RankState{};
+}
+
+// The host copies of the slab ranges from the device sizes (after device-sized steps), with one wait.
+int sync_dz(RankState& R) {
+    sph_ctx* ctx = R.c;
+    ctx->dz_ahead = true;
+    int r = slab_sync_ranges(ctx);
+    if (r != SPH_OK) return r;
+    R.n_prev_ub = ctx->n;
+    return SPH_OK;
+}
+
+// device sizes from the host's (after init or a host-sized step's bookkeeping)
+int put_dz(RankState& R) {
+    sph_ctx* ctx = R.c;
+    SlabSizes h{};
+    HIPCHK(hipMemcpy(&h, R.dz, sizeof h, hipMemcpyDeviceToHost));
+    h.o0 = (uint32_t)ctx->o0;
+    h.o1 = (uint32_t)ctx->o1;
+    h.no = h.o1 - h.o0;
+    h.n = (uint32_t)ctx->n;
+    HIPCHK(hipMemcpy(R.dz, &h, sizeof h, hipMemcpyHostToDevice));
+    R.n_prev_ub = ctx->n;
+    return SPH_OK;
+}
+
+int col_le(const sph_ctx* c) { return c->has_left ? c->sl.cx_lo - c->grid.cx0 : -1; }
+int col_ge(const sph_ctx* c) { return c->has_right ? c->sl.cx_hi - 1 - c->grid.cx0 : 0x7fffffff; }
+uint32_t gyz(const sph_ctx* c) { return (uint32_t)c->grid.gy * (uint32_t)c->grid.gz; }
+
+const uint32_t* lag_slot(RankState& R, int64_t step, sph_ctx* ctx, int* rc) {
+    const int k = (int)(step % LAG_SLOTS);
+    const hipError_t e = hipEventSynchronize(R.lag_ev[k]);   // done long ago unless the host runs 2 steps ahead
+    if (e != hipSuccess) *rc = fail(ctx, SPH_ERR_HIP, "lag event: %s", hipGetErrorString(e));
+    return R.lag + k * LAG_WORDS;
+}
+
+// SPH_FLAG_VALIDATE: wait for the rank's streams after a launch group and name it in the error
+int checkpoint(RankState& R, const char* what) {
+    sph_ctx* ctx = R.c;
+    if (!(ctx->cfg.flags & SPH_FLAG_VALIDATE)) return SPH_OK;
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess && R.comm) e = hipStreamSynchronize(R.comm);
+    if (e != hipSuccess) return fail(ctx, SPH_ERR_HIP, "rank %d, %s: %s", R.rank, what, hipGetErrorString(e));
+    return SPH_OK;
+}
+#define CKPT(R, what) \
+    do { if (int rc_ = checkpoint(R, what)) return rc_; } while (0)
+
+// ---------------------------------------------------------------- phase A: counts and messages
+int phase_count(RankState& R) {
+    sph_ctx* ctx = R.c;
+    HIPCHK(hipSetDevice(ctx->device));
+    if (!ctx->keys_valid) {   // after init or a re-cut: keys of the owned slots in the (new) window
+        const int32_t no = ctx->o1 - ctx->o0;
+        if (no > 0) {
+            KTimer t(ctx, "keys", 20.0 * no);
+            launch_keys(ctx->pos + ctx->o0, no, nullptr, 0, ctx->grid, ctx->keys + ctx->o0, ctx->stream);
+        }
+        ctx->keys_valid = true;
+    }
+    if (R.left < 0 && R.right < 0) return SPH_OK;
+    // the count blocks over the owned slots of the previous order (within its slot bound); the pack
+    // reads the per-block counts with this same block count
+    R.nb_send = slab_send_blocks(0, (int32_t)std::max<int64_t>(R.n_prev_ub, 1));
+    KTimer t(ctx, "slab_count", 4.0 * R.n_prev_ub);
+    launch_slab_count_dev(ctx->keys, R.dz, R.nb_send, gyz(ctx), col_le(ctx), col_ge(ctx), ctx->sblk,
+                          ctx->sdev + SDEV_TOTALS, ctx->stream);
+    CKPT(R, "count");
+    return SPH_OK;
+}
+
+int phase_pack(RankState& R, Multi& M) {
+    sph_ctx* ctx = R.c;
+    HIPCHK(hipSetDevice(ctx->device));
+    for (int s = 0; s < 2; ++s) {
+        const int peer = s == 0 ? R.left : R.right;
+        if (peer < 0) continue;
+        int r = ensure_buf(M, ctx, &R.msg_out[s], &R.mcap_out[s], MSG_HDR_F4 + 2 * R.c1o[s]);
+        if (r != SPH_OK) return r;
+        r = ensure_buf(M, ctx, &R.msg_in[s], &R.mcap_in[s], MSG_HDR_F4 + 2 * R.c1i[s]);
+        if (r != SPH_OK) return r;
+        // the neighbour's copy of last step's message must be done before it is overwritten
+        if (M.mode == 1) HIPCHK(hipStreamWaitEvent(ctx->stream, M.ranks[peer - M.ranks[0].rank].ev_in, 0));
+        KTimer t(ctx, "slab_pack", 36.0 * R.c1o[s]);
+        launch_slab_pack_dev(ctx->keys, ctx->pos, ctx->vel, ctx->id, ctx->sk_valid ? ctx->sk_cur : nullptr,
+                             (uint32_t)ctx->grid.cx0 * gyz(ctx), R.dz,
+                             R.nb_send, gyz(ctx), s, col_le(ctx),
+                             col_ge(ctx), ctx->sblk, R.msg_out[s], R.c1o[s], ctx->sdev + SDEV_TOTALS + s, ctx->stream);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(R.ev_packed, ctx->stream));
+    CKPT(R, "pack");
+    return SPH_OK;
+}
+
+// ---------------------------------------------------------------- exchanges
+int exchange_counts(Multi& M, sph_ctx* pctx) {
+    // exact-size steps: the host reads every local rank's send counts, then learns the neighbours'
+    for (auto& R : M.ranks) {
+        sph_ctx* ctx = R.c;
+        HIPCHK(hipSetDevice(ctx->device));
+        uint32_t t[2] = {0, 0};
+        if (R.left >= 0 || R.right >= 0) {
+            HIPCHK(hipMemcpyAsync(t, ctx->sdev + SDEV_TOTALS, 8, hipMemcpyDeviceToHost, ctx->stream));
+            HIPCHK(hipStreamSynchronize(ctx->stream));
+        }
+        R.c1o[0] = R.left >= 0 ? (int32_t)t[0] : 0;
+        R.c1o[1] = R.right >= 0 ? (int32_t)t[1] : 0;
+    }
+    if (M.mode == 1) {
+        const int r0 = M.ranks[0].rank;
+        for (auto& R : M.ranks) {
+            R.c1i[0] = R.left >= 0 ? M.ranks[R.left - r0].c1o[1] : 0;
+            R.c1i[1] = R.right >= 0 ? M.ranks[R.right - r0].c1o[0] : 0;
+        }
+        return SPH_OK;
+    }
+    RankState& R = M.ranks[0];
+    sph_ctx* ctx = R.c;
+    (void)pctx;
+    NCCLCHK(ncclGroupStart());
+    if (R.left >= 0) {
+        NCCLCHK(ncclSend(ctx->sdev + SDEV_TOTALS, 1, ncclUint32, R.left, M.comm, ctx->stream));
+        NCCLCHK(ncclRecv(R.cnt_dev + 0, 1, ncclUint32, R.left, M.comm, ctx->stream));
+    }
+    if (R.right >= 0) {
+        NCCLCHK(ncclSend(ctx->sdev + SDEV_TOTALS + 1, 1, ncclUint32, R.right, M.comm, ctx->stream));
+        NCCLCHK(ncclRecv(R.cnt_dev + 1, 1, ncclUint32, R.right, M.comm, ctx->stream));
+    }
+    NCCLCHK(ncclGroupEnd());
+    uint32_t in[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(in, R.cnt_dev, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    R.c1i[0] = R.left >= 0 ? (int32_t)in[0] : 0;
+    R.c1i[1] = R.right >= 0 ? (int32_t)in[1] : 0;
+    return SPH_OK;
+}
+
+int exchange1(Multi& M) {
+    if (M.mode == 1) {
+        const int r0 = M.ranks[0].rank;
+        for (auto& R : M.ranks) {
+            sph_ctx* ctx = R.c;
+            HIPCHK(hipSetDevice(ctx->device));
+            for (int s = 0; s < 2; ++s) {
+                const int peer = s == 0 ? R.left : R.right;
+                if (peer < 0) continue;
+                RankState& S = M.ranks[peer - r0];
+                const size_t bytes = (size_t)(MSG_HDR_F4 + 2 * R.c1i[s]) * sizeof(float4);
+                HIPCHK(hipStreamWaitEvent(ctx->stream, S.ev_packed, 0));
+                HIPCHK(hipMemcpyPeerAsync(R.msg_in[s], ctx->device, S.msg_out[1 - s], S.c->device, bytes, ctx->stream));
+            }
+            HIPCHK(hipEventRecord(R.ev_in, ctx->stream));
+        }
+        return SPH_OK;
+    }
+    RankState& R = M.ranks[0];
+    sph_ctx* ctx = R.c;
+    NCCLCHK(ncclGroupStart());
+    for (int s = 0; s < 2; ++s) {
+        const int peer = s == 0 ? R.left : R.right;
+        if (peer < 0) continue;
+        NCCLCHK(ncclSend(R.msg_out[s], (size_t)(MSG_HDR_F4 + 2 * R.c1o[s]) * sizeof(float4), ncclUint8, peer, M.comm,
+                         ctx->stream));
+        NCCLCHK(ncclRecv(R.msg_in[s], (size_t)(MSG_HDR_F4 + 2 * R.c1i[s]) * sizeof(float4), ncclUint8, peer, M.comm,
+                         ctx->stream));
+    }
+    NCCLCHK(ncclGroupEnd());
+    return SPH_OK;
+}
+
+constexpr int RHO_HDR = 4;   // slab.hip: 32-byte header of a ρ message, in float2
+
+int exchange2_start(Multi& M) {
+    if (M.mode == 1) {
+        const int r0 = M.ranks[0].rank;
+        for (auto& R : M.ranks) {
+            sph_ctx* ctx = R.c;
+            HIPCHK(hipSetDevice(ctx->device));
+            for (int s = 0; s < 2; ++s) {
+                const int peer = s == 0 ? R.left : R.right;
+                if (peer < 0) continue;
+                RankState& S = M.ranks[peer - r0];
+                HIPCHK(hipStreamWaitEvent(R.comm, S.ev_rho_packed, 0));
+                HIPCHK(hipMemcpyPeerAsync(R.rho_in[s], ctx->device, S.rho_out[1 - s], S.c->device,
+                                          (size_t)(RHO_HDR + R.c2i[s]) * sizeof(float2), R.comm));
+            }
+            HIPCHK(hipEventRecord(R.ev_rho_recv, R.comm));
+        }
+        return SPH_OK;
+    }
+    RankState& R = M.ranks[0];
+    sph_ctx* ctx = R.c;
+    HIPCHK(hipStreamWaitEvent(R.comm, R.ev_rho_packed, 0));
+    NCCLCHK(ncclGroupStart());
+    for (int s = 0; s < 2; ++s) {
+        const int peer = s == 0 ? R.left : R.right;
+        if (peer < 0) continue;
+        NCCLCHK(ncclSend(R.rho_out[s], (size_t)(RHO_HDR + R.c2o[s]) * sizeof(float2), ncclUint8, peer, M.comm, R.comm));
+        NCCLCHK(ncclRecv(R.rho_in[s], (size_t)(RHO_HDR + R.c2i[s]) * sizeof(float2), ncclUint8, peer, M.comm, R.comm));
+    }
+    NCCLCHK(ncclGroupEnd());
+    HIPCHK(hipEventRecord(R.ev_rho_recv, R.comm));
+    return SPH_OK;
+}
+
+// ---------------------------------------------------------------- phase B: assemble, density, ρ out
+int phase_assemble(RankState& R, bool exact) {
+    sph_ctx* ctx = R.c;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    launch_slab_sizes(R.dz, R.left >= 0 ? R.msg_in[0] : nullptr, R.right >= 0 ? R.msg_in[1] : nullptr, R.c1i[0],
+                      R.c1i[1], ctx->capacity, s);
+    R.n_ub = std::min<int64_t>(R.c1i[0] + R.n_prev_ub + R.c1i[1], ctx->capacity);
+    const bool many = ctx->resort_mode == 1 && *(volatile uint32_t*)ctx->mv_host > resort_limit((int32_t)R.n_ub);
+    if (ctx->resort_mode != 0 && !many && ctx->sk_valid && R.n_ub > 0) {
+        // incremental re-sort over [left records | own slots | right records], sizes on the device
+        const int32_t nl_ub = R.c1i[0], nr_ub = R.c1i[1], n_ub = (int32_t)R.n_ub;
+        const AsmSrc src{ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->keys, 0,
+                         R.left >= 0 ? (const float4*)(R.msg_in[0] + MSG_HDR_F4) : nullptr,
+                         R.right >= 0 ? (const float4*)(R.msg_in[1] + MSG_HDR_F4) : nullptr,
+                         ctx->keys2, ctx->vals, nl_ub, n_ub - nr_ub, R.dz};
+        const int used = ctx->mv_par;
+        const MoverSink mv{ctx->keys2, ctx->mv_count + used, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_rank,
+                           (uint32_t)std::max(ctx->capacity, 1), &R.dz->flags};
+        const uint32_t key_base = (uint32_t)ctx->grid.cx0 * gyz(ctx);
+        CKPT(R, "exchange 1 + sizes");
+        if (nl_ub + nr_ub > 0) {
+            KTimer t(ctx, "slab_assemble", 40.0 * (double)(nl_ub + nr_ub));
+            launch_slab_rec(src, n_ub, ctx->grid, key_base, ctx->vals, ctx->keys2, mv, s);  // grid: nl_ub + nr_ub
+        }
+        CKPT(R, "slab_rec");
+        KTimer t(ctx, "resort", (double)R.n_ub * (2 * 4 + 2 * 36));
+        if (ctx->has_left || ctx->has_right)   // without neighbours the own block keeps its cell starts
+            launch_slab_cs_old(ctx->cs, ctx->grid.ncells, gyz(ctx), (uint32_t)ctx->grid.gx, ctx->has_left,
+                               ctx->has_right, 0, ctx->keys2, 0, 0, 0, s, R.dz);
+        CKPT(R, "cs_old");
+        const int32_t lc_lo = ctx->sl.cx_lo - ctx->grid.cx0, lc_hi = ctx->sl.cx_hi - ctx->grid.cx0;
+        CsPick pick{{col_start(ctx, 0), col_start(ctx, lc_lo), col_start(ctx, lc_lo + 1), col_start(ctx, lc_hi - 1),
+                     col_start(ctx, lc_hi), col_start(ctx, ctx->grid.gx)},
+                    6, R.dz->pick, nullptr};
+        ResortScratch w = resort_scratch(ctx);
+        w.dz = R.dz;
+        w.err = &R.dz->flags;
+        launch_resort(src, ctx->cs, ctx->grid.ncells, n_ub, ctx->mv_count + used, ctx->mv_count + (1 - used), w,
+                      ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, s, pick);
+        CKPT(R, "resort");
+        if ((ctx->steps & 7) == 0)
+            HIPCHK(hipMemcpyAsync(ctx->mv_host, ctx->mv_count + used, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        ctx->mv_par = 1 - used;
+        swap_sv(ctx);
+        std::swap(ctx->id, ctx->id2);
+        std::swap(ctx->sk_cur, ctx->sk_next);
+        ctx->keys_valid = false;
+        ctx->sk_valid = true;
+        ctx->n = n_ub;
+    } else {
+        // the full radix sort: host-sized (after a re-cut, or while many particles move)
+        HIPCHK(hipStreamSynchronize(s));
+        SlabSizes h;
+        HIPCHK(hipMemcpy(&h, R.dz, sizeof h, hipMemcpyDeviceToHost));
+        if (h.flags & (SZ_OVF_MSG | SZ_OVF_CAP))
+            return fail(ctx, SPH_ERR_CAPACITY, "slab step: halo message overflow or slots over capacity (rank %d)", R.rank);
+        ctx->dz_ahead = false;
+        ctx->o0 = (int32_t)h.o0;
+        ctx->o1 = (int32_t)h.o1;
+        int r = slab_assemble(ctx, R.left >= 0 ? (const void*)(R.msg_in[0] + MSG_HDR_F4) : nullptr, (int32_t)h.nl,
+                              R.right >= 0 ? (const void*)(R.msg_in[1] + MSG_HDR_F4) : nullptr, (int32_t)h.nr, true);
+        if (r != SPH_OK) return r;
+        ctx->rng_pending = false;
+        // the picked column starts (sdev[0..5]) and the slot count into the device sizes
+        HIPCHK(hipMemcpyAsync(R.dz->pick, ctx->sdev, 6 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+        const uint32_t nn = (uint32_t)ctx->n;
+        HIPCHK(hipMemcpyAsync(&R.dz->n, &nn, sizeof nn, hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));   // nn lives on this stack frame
+        R.n_ub = ctx->n;
+    }
+    launch_slab_ranges(R.dz, ctx->has_left ? 1 : 0, ctx->has_right ? 1 : 0, s);
+    CKPT(R, "ranges");
+    {
+        KTimer t(ctx, "density", 24.0 * (double)R.n_ub);
+        launch_density_tiled(ctx->pos, ctx->cs, 0, (int32_t)R.n_ub, ctx->grid, ctx->sc, ctx->rp, ctx->paths, s,
+                             DevRange{&R.dz->rg[2], &R.dz->rg[3]});
+    }
+    CKPT(R, "density");
+    if (exact && (R.left >= 0 || R.right >= 0)) {   // exact ρ message sizes: this rank's own columns
+        HIPCHK(hipStreamSynchronize(s));
+        SlabSizes h;
+        HIPCHK(hipMemcpy(&h, R.dz, sizeof h, hipMemcpyDeviceToHost));
+        R.c2o[0] = R.left >= 0 ? (int32_t)(h.rg[7] - h.rg[6]) : 0;
+        R.c2o[1] = R.right >= 0 ? (int32_t)(h.rg[9] - h.rg[8]) : 0;
+        R.c2i[0] = R.left >= 0 ? (int32_t)(h.rg[1] - h.rg[0]) : 0;
+        R.c2i[1] = R.right >= 0 ? (int32_t)(h.rg[5] - h.rg[4]) : 0;
+    }
+    return SPH_OK;
+}
+
+int phase_rho_out(RankState& R, Multi& M) {
+    sph_ctx* ctx = R.c;
+    HIPCHK(hipSetDevice(ctx->device));
+    for (int s = 0; s < 2; ++s) {
+        const int peer = s == 0 ? R.left : R.right;
+        if (peer < 0) continue;
+        int r = ensure_buf(M, ctx, &R.rho_out[s], &R.rcap_out[s], RHO_HDR + R.c2o[s]);
+        if (r != SPH_OK) return r;
+        r = ensure_buf(M, ctx, &R.rho_in[s], &R.rcap_in[s], RHO_HDR + R.c2i[s]);
+        if (r != SPH_OK) return r;
+        if (M.mode == 1) HIPCHK(hipStreamWaitEvent(ctx->stream, M.ranks[peer - M.ranks[0].rank].ev_rho_recv, 0));
+        launch_slab_pack_rho(ctx->rp, R.dz, s, R.rho_out[s], R.c2o[s], ctx->stream);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(R.ev_rho_packed, ctx->stream));
+    CKPT(R, "rho pack");
+    return SPH_OK;
+}
+
+// ---------------------------------------------------------------- phase C: force passes, finish
+void force_dev(sph_ctx* ctx, const uint32_t* lo, const uint32_t* hi, int64_t grid_ub, float dt) {
+    if (grid_ub <= 0) return;
+    KTimer t(ctx, "force_integrate", 76.0 * (double)grid_ub);
+    MoverSink mv = mover_sink(ctx);
+    mv.err = &ctx->dz->flags;
+    launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, (int32_t)grid_ub, ctx->grid, ctx->sc, dt, forcing(ctx),
+                       ctx->pos2, ctx->vel2, ctx->keys, mv, ctx->paths, ctx->stream, DevRange{lo, hi});
+}
+
+int phase_interior(RankState& R, float dt) {
+    sph_ctx* ctx = R.c;
+    HIPCHK(hipSetDevice(ctx->device));
+    force_dev(ctx, &R.dz->fr[0], &R.dz->fr[1], R.n_ub, dt);
+    CKPT(R, "interior force");
+    return SPH_OK;
+}
+
+int phase_finish(RankState& R, float dt, int64_t step) {
+    sph_ctx* ctx = R.c;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    if (R.left >= 0 || R.right >= 0) HIPCHK(hipStreamWaitEvent(s, R.ev_rho_recv, 0));
+    CKPT(R, "exchange 2");
+    for (int side = 0; side < 2; ++side)
+        if ((side == 0 ? R.left : R.right) >= 0) launch_slab_unpack_rho(ctx->rp, R.dz, side, R.rho_in[side], R.c2i[side], s);
+    CKPT(R, "rho unpack");
+    const bool one_col = ctx->sl.cx_hi - ctx->sl.cx_lo == 1;
+    if (one_col && (ctx->has_left || ctx->has_right)) {
+        force_dev(ctx, &R.dz->fr[2], &R.dz->fr[3], R.n_ub, dt);
+    } else {
+        if (ctx->has_left) force_dev(ctx, &R.dz->fr[2], &R.dz->fr[3], std::min<int64_t>(R.c2o[0], R.n_ub), dt);
+        if (ctx->has_right) force_dev(ctx, &R.dz->fr[4], &R.dz->fr[5], std::min<int64_t>(R.c2o[1], R.n_ub), dt);
+    }
+    CKPT(R, "boundary force");
+    swap_sv(ctx);
+    ctx->keys_valid = true;
+    ctx->steps++;
+    ctx->sim_time += (double)dt;
+    const int k = (int)(step % LAG_SLOTS);
+    launch_slab_lag(R.dz, ctx->sdev + SDEV_TOTALS, R.left >= 0 ? R.msg_in[0] : nullptr, R.right >= 0 ? R.msg_in[1] : nullptr,
+                    R.left >= 0 ? R.rho_in[0] : nullptr, R.right >= 0 ? R.rho_in[1] : nullptr, R.lag + k * LAG_WORDS, s);
+    HIPCHK(hipEventRecord(R.lag_ev[k], s));
+    R.cin_hist[k] = R.c1i[0] + R.c1i[1];
+    R.n_prev_ub = R.n_ub;
+    R.since_cut++;
+    ctx->dz_ahead = true;   // o0 / o1 / n / rng on the host are last step's until slab_sync_ranges
+    HIPCHK(hipGetLastError());
+    return SPH_OK;
+}
+
+// ---------------------------------------------------------------- re-balancing
+int rebalance(Multi& M, sph_ctx* pctx) {
+    sph_ctx* ctx = pctx;
+    const int G = global_columns(M.ranks[0].c->prm);
+    std::vector<int64_t> hist(G, 0), part(G);
+    for (auto& R : M.ranks) {
+        int r = sync_dz(R);
+        if (r != SPH_OK) return r;
+        r = sph_slab_column_counts(R.c, part.data(), G);
+        if (r != SPH_OK) return r;
+        for (int c = 0; c < G; ++c) hist[c] += part[c];
+    }
+    if (M.mode == 2 && M.world > 1) {
+        sph_ctx* rc = M.ranks[0].c;
+        HIPCHK(hipSetDevice(rc->device));
+        if (M.hist_cap < G) {
+            dfree(M.hist_dev);
+            HIPCHK(hipMalloc((void**)&M.hist_dev, (size_t)G * sizeof(int64_t)));
+            M.hist_cap = G;
+        }
+        HIPCHK(hipMemcpyAsync(M.hist_dev, hist.data(), (size_t)G * 8, hipMemcpyHostToDevice, rc->stream));
+        NCCLCHK(ncclAllReduce(M.hist_dev, M.hist_dev, (size_t)G, ncclInt64, ncclSum, M.comm, rc->stream));
+        HIPCHK(hipMemcpyAsync(hist.data(), M.hist_dev, (size_t)G * 8, hipMemcpyDeviceToHost, rc->stream));
+        HIPCHK(hipStreamSynchronize(rc->stream));
+    }
+    const std::vector<sph_slab> nc = rebalance_cuts(M.cuts, hist);
+    bool changed = false;
+    for (int r = 0; r < M.world; ++r) changed |= nc[r].cx_lo != M.cuts[r].cx_lo || nc[r].cx_hi != M.cuts[r].cx_hi;
+    if (!changed) return SPH_OK;
+    M.cuts = nc;
+    M.rebalances++;
+    for (auto& R : M.ranks) {
+        int r = sph_slab_recut(R.c, &M.cuts[R.rank]);
+        if (r != SPH_OK) return r;
+        R.since_cut = 0;
+    }
+    return SPH_OK;
+}
+
+// SPH_FLAG_VALIDATE, after the assemble: the sizes the density and force passes will use
+int validate_mid(Multi& M, sph_ctx* pctx) {
+    for (auto& R : M.ranks) {
+        sph_ctx* ctx = R.c;
+        HIPCHK(hipSetDevice(ctx->device));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        SlabSizes h;
+        HIPCHK(hipMemcpy(&h, R.dz, sizeof h, hipMemcpyDeviceToHost));
+        bool ok = h.flags == 0 && h.n <= (uint32_t)ctx->capacity && (int64_t)h.n <= R.n_ub && h.rg[0] <= h.rg[1] &&
+                  h.rg[1] <= h.rg[3] && h.rg[3] <= h.rg[5] && h.rg[5] <= h.n && h.nl <= (uint32_t)R.c1i[0] &&
+                  h.nr <= (uint32_t)R.c1i[1] && h.rg[7] - h.rg[6] <= (uint32_t)std::max(R.c2o[0], 0) + (R.left < 0 ? h.n : 0) &&
+                  h.rg[9] - h.rg[8] <= (uint32_t)std::max(R.c2o[1], 0) + (R.right < 0 ? h.n : 0);
+        for (int k = 0; k < 6; k += 2) ok = ok && h.fr[k] <= h.fr[k + 1] && h.fr[k + 1] <= h.n;
+        // the cell-start table the neighbour passes will walk: monotone, within the assembled slots
+        std::vector<uint32_t> cs(ctx->grid.ncells + 2);
+        HIPCHK(hipMemcpy(cs.data(), ctx->cs, cs.size() * 4, hipMemcpyDeviceToHost));
+        int64_t bad_at = -1;
+        for (size_t k = 0; k + 1 < cs.size() && bad_at < 0; ++k)
+            if (cs[k] > cs[k + 1] || cs[k + 1] > h.n + h.dropped) bad_at = (int64_t)k;
+        if (cs[0] != 0 || cs[ctx->grid.ncells] != h.n) bad_at = bad_at < 0 ? (int64_t)ctx->grid.ncells : bad_at;
+        if (bad_at >= 0)
+            return fail(pctx, SPH_ERR_STATE, "validate(mid) rank %d step %lld: cell starts broken at %lld (%u %u, n %u, ncells %u)",
+                        R.rank, (long long)M.steps, (long long)bad_at, cs[bad_at], cs[bad_at + 1], h.n, ctx->grid.ncells);
+        if (!ok)
+            return fail(pctx, SPH_ERR_STATE,
+                        "validate(mid) rank %d step %lld: flags %u n %u (ub %lld) rg %u %u %u %u %u %u %u %u %u %u "
+                        "fr %u %u %u %u %u %u nl %u nr %u no %u c1i %d %d c2o %d %d",
+                        R.rank, (long long)M.steps, h.flags, h.n, (long long)R.n_ub, h.rg[0], h.rg[1], h.rg[2], h.rg[3],
+                        h.rg[4], h.rg[5], h.rg[6], h.rg[7], h.rg[8], h.rg[9], h.fr[0], h.fr[1], h.fr[2], h.fr[3],
+                        h.fr[4], h.fr[5], h.nl, h.nr, h.no, R.c1i[0], R.c1i[1], R.c2o[0], R.c2o[1]);
+    }
+    return SPH_OK;
+}
+
+int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
+    if (M.rebalance_every > 0 && M.world > 1 && M.steps > 0 && M.steps % M.rebalance_every == 0) {
+        int r = rebalance(M, pctx);
+        if (r != SPH_OK) return r;
+    }
+    const bool exact = M.ranks[0].since_cut < 2;   // the same on every rank
+    int r;
+    for (auto& R : M.ranks)
+        if ((r = phase_count(R)) != SPH_OK) return r;
+    if (exact) {
+        if ((r = exchange_counts(M, pctx)) != SPH_OK) return r;
+    } else {
+        for (auto& R : M.ranks) {
+            // the counts of two steps before: both neighbours read the same numbers
+            const uint32_t* L = lag_slot(R, M.steps - 2, R.c, &r);
+            if (r != SPH_OK) return r;
+            if (L[9]) return sync_dz(R);   // an overflow flagged two steps ago: report it
+            R.c1o[0] = R.left >= 0 ? cap_of(L[0]) : 0;
+            R.c1o[1] = R.right >= 0 ? cap_of(L[1]) : 0;
+            R.c1i[0] = R.left >= 0 ? cap_of(L[2]) : 0;
+            R.c1i[1] = R.right >= 0 ? cap_of(L[3]) : 0;
+            R.c2o[0] = R.left >= 0 ? cap_of(L[4]) : 0;
+            R.c2o[1] = R.right >= 0 ? cap_of(L[5]) : 0;
+            R.c2i[0] = R.left >= 0 ? cap_of(L[6]) : 0;
+            R.c2i[1] = R.right >= 0 ? cap_of(L[7]) : 0;
+            // slot bound: the assembled count two steps ago plus every record received since
+            const int64_t km1 = (M.steps - 1) % LAG_SLOTS;
+            R.n_prev_ub = std::min<int64_t>(R.n_prev_ub, (int64_t)L[8] + R.cin_hist[km1]);
+        }
+    }
+    for (auto& R : M.ranks)
+        if ((r = phase_pack(R, M)) != SPH_OK) return r;
+    if ((r = exchange1(M)) != SPH_OK) return r;
+    for (auto& R : M.ranks)
+        if ((r = phase_assemble(R, exact)) != SPH_OK) return r;
+    if ((pctx->cfg.flags & SPH_FLAG_VALIDATE) && (r = validate_mid(M, pctx)) != SPH_OK) return r;
+    for (auto& R : M.ranks)
+        if ((r = phase_rho_out(R, M)) != SPH_OK) return r;
+    if (M.world > 1 && (r = exchange2_start(M)) != SPH_OK) return r;
+    for (auto& R : M.ranks)
+        if ((r = phase_interior(R, dt)) != SPH_OK) return r;
+    for (auto& R : M.ranks)
+        if ((r = phase_finish(R, dt, M.steps)) != SPH_OK) return r;
+    M.steps++;
+    return SPH_OK;
+}
+
+int rank_setup(Multi& M, RankState& R, sph_ctx* c, int rank) {
+    R.c = c;
+    R.rank = rank;
+    R.world = M.world;
+    R.left = rank > 0 ? rank - 1 : -1;
+    R.right = rank + 1 < M.world ? rank + 1 : -1;
+    return rank_init(R);
+}
+
+}  // namespace
+
+void multi_free(sph_ctx* ctx) {
+    Multi* M = ctx->mg;
+    if (!M) return;
+    for (auto& R : M->ranks) rank_free(R);
+    if (M->hist_dev) (void)hipFree(M->hist_dev);
+    if (M->comm) (void)ncclCommDestroy(M->comm);
+    for (sph_ctx* k : M->kids) sph_destroy(k);
+    delete M;
+    ctx->mg = nullptr;
+}
+
+bool is_group(const sph_ctx* ctx) { return ctx->mg && ctx->mg->mode == 1; }
+
+std::vector<sph_ctx*> multi_kids(const sph_ctx* ctx) { return ctx->mg ? ctx->mg->kids : std::vector<sph_ctx*>{}; }
+
+int multi_create_group(sph_ctx* ctx) {
+    Multi* M = new Multi();
+    M->mode = 1;
+    M->world = ctx->cfg.ndev;
+    ctx->mg = M;
+    return SPH_OK;
+}
+
+// Distribute a scenario over a local group: equal-count cuts, one slab context per GPU.
+int multi_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
+    Multi& M = *ctx->mg;
+    if (sc->dim != ctx->cfg.dim) return fail(ctx, SPH_ERR_INVALID, "scenario dim %d != context dim %d", sc->dim, ctx->cfg.dim);
+    if (!ctx->params_set) return fail(ctx, SPH_ERR_STATE, "sph_set_params first");
+    const sph_params& p = ctx->prm;
+    const int G = global_columns(p);
+    if (G < 2 * M.world) return fail(ctx, SPH_ERR_INVALID, "%d columns cannot be cut into %d slabs", G, M.world);
+    const std::vector<int64_t> per = lattice_columns(*sc, p);
+    M.cuts = balanced_cuts(per, M.world);
+    M.n_total = (int64_t)sc->nx * sc->ny * (sc->dim == 3 ? sc->nz : 1);
+    const int64_t per_x = (int64_t)sc->ny * (sc->dim == 3 ? sc->nz : 1);
+    int64_t maxcol = 0;
+    for (int64_t v : per) maxcol = std::max(maxcol, v * per_x);
+    auto need_cap = [&](int r) {   // an even share or this rank's initial share, plus a halo column per side, x1.5
+        int64_t own = 0;
+        for (int c = M.cuts[r].cx_lo; c < M.cuts[r].cx_hi; ++c) own += per[c] * per_x;
+        const double share = std::max((double)M.n_total / M.world, (double)own);
+        return (int64_t)((share + 2.0 * (double)maxcol) * 1.5) + 4096;
+    };
+    for (auto& R : M.ranks) rank_free(R);
+    M.ranks.clear();
+    {
+        for (sph_ctx* k : M.kids) sph_destroy(k);
+        M.kids.clear();
+        int nvis = 0;
+        HIPCHK(hipGetDeviceCount(&nvis));
+        for (int r = 0; r < M.world; ++r) {
+            const int64_t cap = std::max<int64_t>(need_cap(r), ctx->cfg.capacity);
+            if (cap > INT32_MAX) return fail(ctx, SPH_ERR_CAPACITY, "slab %d needs %lld slots", r, (long long)cap);
+            sph_config kc = ctx->cfg;
+            kc.ndev = 1;
+            kc.capacity = (int32_t)cap;
+            sph_ctx* k = nullptr;
+            int rc = sph_create(&kc, (ctx->device + r) % nvis, &k);
+            if (rc != SPH_OK) return fail(ctx, rc, "slab context %d on device %d", r, (ctx->device + r) % nvis);
+            M.kids.push_back(k);
+        }
+        M.ranks.resize(M.world);
+        for (int r = 0; r < M.world; ++r) {
+            sph_ctx* k = M.kids[r];
+            int rc = sph_set_params(k, &p);
+            if (rc == SPH_OK) rc = sph_slab_set(k, &M.cuts[r]);
+            if (rc == SPH_OK) rc = sph_slab_init_scenario(k, sc);
+            if (rc == SPH_OK) rc = rank_setup(M, M.ranks[r], k, r);
+            if (rc == SPH_OK) rc = put_dz(M.ranks[r]);
+            if (rc != SPH_OK) return fail(ctx, rc, "slab %d: %s", r, sph_last_error(k));
+        }
+    }
+    M.steps = 0;
+    M.ready = true;
+    return SPH_OK;
+}
+
+// SPH_FLAG_VALIDATE: after every step, one wait and a check of every rank's device sizes
+int validate(Multi& M, sph_ctx* pctx) {
+    for (auto& R : M.ranks) {
+        sph_ctx* ctx = R.c;
+        HIPCHK(hipSetDevice(ctx->device));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        HIPCHK(hipStreamSynchronize(R.comm));
+        SlabSizes h;
+        HIPCHK(hipMemcpy(&h, R.dz, sizeof h, hipMemcpyDeviceToHost));
+        const uint32_t cap = (uint32_t)ctx->capacity;
+        bool ok = h.flags == 0 && h.n <= cap && h.o0 <= h.o1 && h.o1 <= h.n && h.rg[0] <= h.rg[1] &&
+                  h.rg[1] <= h.rg[3] && h.rg[3] <= h.rg[5] && h.rg[5] <= h.n && (int64_t)h.n <= R.n_ub;
+        for (int k = 0; k < 6; k += 2) ok = ok && h.fr[k] <= h.fr[k + 1] && h.fr[k + 1] <= h.n;
+        if (!ok)
+            return fail(pctx, SPH_ERR_STATE,
+                        "validate rank %d step %lld: flags %u n %u (ub %lld, cap %u) o %u..%u rg %u %u %u %u %u %u "
+                        "fr %u %u %u %u %u %u nl %u nr %u no %u c1i %d %d c2i %d %d",
+                        R.rank, (long long)M.steps, h.flags, h.n, (long long)R.n_ub, cap, h.o0, h.o1, h.rg[0], h.rg[1],
+                        h.rg[2], h.rg[3], h.rg[4], h.rg[5], h.fr[0], h.fr[1], h.fr[2], h.fr[3], h.fr[4], h.fr[5], h.nl,
+                        h.nr, h.no, R.c1i[0], R.c1i[1], R.c2i[0], R.c2i[1]);
+    }
+    return SPH_OK;
+}
+
+int multi_step(sph_ctx* ctx, float dt, int32_t nsteps) {
+    Multi& M = *ctx->mg;
+    if (!M.ready) return fail(ctx, SPH_ERR_STATE, "multi-GPU context: sph_init_scenario first");
+    for (int32_t k = 0; k < nsteps; ++k) {
+        if ((ctx->cfg.flags & SPH_FLAG_VALIDATE) && M.steps > 0) {
+            int r = validate(M, ctx);
+            if (r != SPH_OK) return r;
+        }
+        int r = multi_one_step(M, ctx, dt);
+        if (r != SPH_OK) {
+            if (M.mode == 1)   // a slab context's message on the group
+                for (auto& R : M.ranks)
+                    if (R.c && !R.c->err.empty()) ctx->err = R.c->err;
+            return r;
+        }
+    }
+    if (M.mode == 1) {
+        ctx->steps = M.ranks[0].c->steps;
+        ctx->sim_time = M.ranks[0].c->sim_time;
+    }
+    return SPH_OK;
+}
+
+// owned particles of every local rank -> index-order host arrays (comps of the 8-float record)
+int multi_read(sph_ctx* ctx, int field, float* dst, int32_t count) {
+    Multi& M = *ctx->mg;
+    if (!M.ready) return fail(ctx, SPH_ERR_STATE, "no scenario");
+    if (count < M.n_total) return fail(ctx, SPH_ERR_INVALID, "count %d < particles %lld", count, (long long)M.n_total);
+    std::vector<float> rec;
+    int64_t seen = 0;
+    for (auto& R : M.ranks) {
+        int r = sync_dz(R);
+        if (r != SPH_OK) return fail(ctx, r, "%s", R.c->err.c_str());
+        const int32_t no = R.c->o1 - R.c->o0;
+        rec.resize((size_t)std::max(no, 1) * 8);
+        int32_t got = 0;
+        r = sph_slab_read_owned(R.c, rec.data(), no, &got);
+        if (r != SPH_OK) return fail(ctx, r, "%s", R.c->err.c_str());
+        for (int32_t i = 0; i < got; ++i) {
+            const float* q = rec.data() + 8 * (size_t)i;
+            int32_t id;
+            std::memcpy(&id, q + 6, 4);
+            if (id < 0 || id >= count) return fail(ctx, SPH_ERR_STATE, "particle id %d out of range", id);
+            if (field == 0) { dst[3 * (size_t)id] = q[0]; dst[3 * (size_t)id + 1] = q[1]; dst[3 * (size_t)id + 2] = q[2]; }
+            if (field == 1) { dst[3 * (size_t)id] = q[3]; dst[3 * (size_t)id + 1] = q[4]; dst[3 * (size_t)id + 2] = q[5]; }
+            if (field == 2) dst[id] = q[7];
+        }
+        seen += got;
+    }
+    if (seen != M.n_total) return fail(ctx, SPH_ERR_STATE, "ranks own %lld particles, expected %lld", (long long)seen, (long long)M.n_total);
+    return SPH_OK;
+}
+
+}  // namespace sph
+
+using namespace sph;
+
+extern "C" {
+
+int sph_comm_unique_id(sph_comm_id* out) {
+    if (!out) return SPH_ERR_INVALID;
+    static_assert(sizeof(sph_comm_id) == sizeof(ncclUniqueId), "sph_comm_id is an ncclUniqueId");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return SPH_ERR_HIP;
+    std::memcpy(out, &id, sizeof id);
+    return SPH_OK;
+}
+
+int sph_comm_init(sph_ctx* ctx, const sph_comm_id* id, int32_t nranks, int32_t rank) {
+    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return SPH_ERR_INVALID;
+    if (is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "the multi-GPU step is Model S only");
+    if (ctx->mg) return fail(ctx, SPH_ERR_STATE, "context already multi-GPU");
+    HIPCHK(hipSetDevice(ctx->device));
+    Multi* M = new Multi();
+    M->mode = 2;
+    M->world = nranks;
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof uid);
+    const ncclResult_t r = ncclCommInitRank(&M->comm, nranks, uid, rank);
+    if (r != ncclSuccess) {
+        delete M;
+        return fail(ctx, SPH_ERR_HIP, "ncclCommInitRank(%d of %d): %s", rank, nranks, ncclGetErrorString(r));
+    }
+    M->ranks.resize(1);
+    M->ranks[0].rank = rank;
+    ctx->mg = M;
+    return SPH_OK;
+}
+
+int sph_set_rebalance(sph_ctx* ctx, int32_t every) {
+    if (!ctx || every < 0) return SPH_ERR_INVALID;
+    if (!ctx->mg) return fail(ctx, SPH_ERR_STATE, "not a multi-GPU context");
+    ctx->mg->rebalance_every = every;
+    return SPH_OK;
+}
+
+int sph_get_decomposition(sph_ctx* ctx, sph_decomp* out) {
+    if (!ctx || !out) return SPH_ERR_INVALID;
+    std::memset(out, 0, sizeof *out);
+    if (!ctx->mg) {
+        out->world = out->local_ranks = 1;
+        out->owned = out->total = ctx->n;
+        return SPH_OK;
+    }
+    Multi& M = *ctx->mg;
+    out->world = M.world;
+    out->local_ranks = (int32_t)M.ranks.size();
+    out->rank = M.ranks.empty() ? 0 : M.ranks[0].rank;
+    out->total = M.n_total;
+    out->rebalances = M.rebalances;
+    if (!M.cuts.empty()) out->cut = M.cuts[out->rank];
+    for (auto& R : M.ranks) {
+        if (!R.c) continue;
+        int r = sync_dz(R);
+        if (r != SPH_OK) return r;
+        out->owned += R.c->o1 - R.c->o0;
+    }
+    return SPH_OK;
+}
+
+}  // extern "C"
+
+// RCCL rank: this process's slab of the scenario (called by sph_init_scenario)
+int sph::multi_init_rank(sph_ctx* ctx, const sph_scenario* sc) {
+    Multi& M = *ctx->mg;
+    const int rank = M.ranks[0].rank;
+    if (sc->dim != ctx->cfg.dim) return fail(ctx, SPH_ERR_INVALID, "scenario dim %d != context dim %d", sc->dim, ctx->cfg.dim);
+    if (!ctx->params_set) return fail(ctx, SPH_ERR_STATE, "sph_set_params first");
+    const sph_params& p = ctx->prm;
+    const int G = global_columns(p);
+    if (G < 2 * M.world) return fail(ctx, SPH_ERR_INVALID, "%d columns cannot be cut into %d slabs", G, M.world);
+    const std::vector<int64_t> per = lattice_columns(*sc, p);
+    M.cuts = balanced_cuts(per, M.world);
+    M.n_total = (int64_t)sc->nx * sc->ny * (sc->dim == 3 ? sc->nz : 1);
+    const int64_t per_x = (int64_t)sc->ny * (sc->dim == 3 ? sc->nz : 1);
+    int64_t maxcol = 0, own = 0;
+    for (int64_t v : per) maxcol = std::max(maxcol, v * per_x);
+    for (int c = M.cuts[rank].cx_lo; c < M.cuts[rank].cx_hi; ++c) own += per[c] * per_x;
+    const double share = std::max((double)M.n_total / M.world, (double)own);
+    const int64_t cap = (int64_t)((share + 2.0 * (double)maxcol) * 1.5) + 4096;
+    if (cap > INT32_MAX) return fail(ctx, SPH_ERR_CAPACITY, "slab needs %lld slots", (long long)cap);
+    rank_free(M.ranks[0]);
+    if (ctx->slab) {   // a second scenario: start from a plain context again
+        ctx->slab = false;
+        ctx->grid = ctx->gglobal;
+    }
+    if (cap > ctx->capacity) {
+        int r = sph_resize(ctx, (int32_t)cap);
+        if (r != SPH_OK) return r;
+    }
+    int r = sph_slab_set(ctx, &M.cuts[rank]);
+    if (r == SPH_OK) r = sph_slab_init_scenario(ctx, sc);
+    if (r == SPH_OK) r = rank_setup(M, M.ranks[0], ctx, rank);
+    if (r == SPH_OK) r = put_dz(M.ranks[0]);
+    if (r != SPH_OK) return r;
+    M.steps = 0;
+    M.ready = true;
+    return SPH_OK;
+}

@@ -6,7 +6,26 @@ using namespace sph;
 
 // ---------------------------------------------------------------- slab decomposition
 // Wait for the last assemble's range copy and publish rng / o0 / o1 (no-op when up to date).
-static int slab_sync_ranges(sph_ctx* ctx) {
+int sph::slab_sync_ranges(sph_ctx* ctx) {
+    if (ctx->dz_ahead) {   // after the in-library step's device-sized steps: one wait, then the device sizes
+        ctx->dz_ahead = false;
+        HIPCHK(hipSetDevice(ctx->device));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        SlabSizes h;
+        HIPCHK(hipMemcpy(&h, ctx->dz, sizeof h, hipMemcpyDeviceToHost));
+        if (h.flags)
+            return fail(ctx, SPH_ERR_CAPACITY, "slab step:%s%s%s%s", (h.flags & SZ_OVF_MSG) ? " halo message overflow" : "",
+                        (h.flags & SZ_OVF_CAP) ? " slots over capacity" : "",
+                        (h.flags & SZ_RHO_MISMATCH) ? " ghost density count mismatch" : "",
+                        (h.flags & SZ_OVF_MOVERS) ? " mover list / re-sort destination out of range" : "");
+        for (int k = 0; k < 10; ++k) ctx->rng[k] = (int32_t)h.rg[k];
+        ctx->o0 = (int32_t)h.o0;
+        ctx->o1 = (int32_t)h.o1;
+        ctx->n = (int32_t)h.n;
+        ctx->dropped = (int32_t)h.dropped;
+        ctx->rng_pending = false;
+        return SPH_OK;
+    }
     if (!ctx->rng_pending) return SPH_OK;
     HIPCHK(hipEventSynchronize(ctx->rng_ev));
     ctx->rng_pending = false;
@@ -40,7 +59,7 @@ int sph::slab_local_grid(sph_ctx* ctx) {
     return ensure_cells(ctx);
 }
 
-static inline int32_t col_start(const sph_ctx* c, int32_t local_col) {
+int32_t sph::col_start(const sph_ctx* c, int32_t local_col) {
     return local_col * c->grid.gy * c->grid.gz;
 }
 
@@ -48,6 +67,7 @@ extern "C" {
 
 int sph_slab_set(sph_ctx* ctx, const sph_slab* slab) {
     if (!ctx || !slab) return SPH_ERR_INVALID;
+    if (is_group(ctx)) return fail(ctx, SPH_ERR_STATE, "a multi-GPU (ndev > 1) context cuts its own slabs");
     if (is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "slab decomposition is Model S only");
     if (!ctx->params_set) return fail(ctx, SPH_ERR_STATE, "sph_set_params first");
     HIPCHK(hipSetDevice(ctx->device));
@@ -219,6 +239,15 @@ int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void
     if (!ctx || nl < 0 || nr < 0 || (nl > 0 && !dev_left) || (nr > 0 && !dev_right)) return SPH_ERR_INVALID;
     if (!ctx->slab) return fail(ctx, SPH_ERR_STATE, "not in slab mode");
     HIPCHK(hipSetDevice(ctx->device));
+    return slab_assemble(ctx, dev_left, nl, dev_right, nr, false);
+}
+
+}  // extern "C"
+
+// The assemble with host-known record counts (the per-phase ABI above, and the in-library step's
+// full-sort steps). force_full: take the full radix sort even when the incremental one is possible.
+int sph::slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void* dev_right, int32_t nr,
+                       bool force_full) {
     const int32_t no = ctx->o1 - ctx->o0;
     const int64_t n = (int64_t)nl + no + nr;
     if (n > ctx->capacity) return fail(ctx, SPH_ERR_CAPACITY, "slab needs %lld slots > capacity %d", (long long)n, ctx->capacity);
@@ -231,7 +260,7 @@ int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void
     const int32_t lc_lo = ctx->sl.cx_lo - ctx->grid.cx0, lc_hi = ctx->sl.cx_hi - ctx->grid.cx0;
     const int32_t idx[6] = {col_start(ctx, 0), col_start(ctx, lc_lo), col_start(ctx, lc_lo + 1),
                             col_start(ctx, lc_hi - 1), col_start(ctx, lc_hi), col_start(ctx, ctx->grid.gx)};
-    if (ctx->resort_mode != 0 && !many && ctx->sk_valid && n > 0) {
+    if (ctx->resort_mode != 0 && !many && !force_full && ctx->sk_valid && n > 0) {
         // incremental: the re-sort reads [left records | own slots | right records] in place. The force
         // pass already appended the own movers (window keys); the records' keys and movers join here.
         const AsmSrc src{ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->keys, ctx->o0 - nl, (const float4*)dev_left,
@@ -302,6 +331,8 @@ int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void
     ctx->sk_valid = ctx->resort_mode != 0;
     return SPH_OK;
 }
+
+extern "C" {
 
 int sph_slab_ranges(sph_ctx* ctx, int32_t ranges[10]) {
     if (!ctx || !ranges) return SPH_ERR_INVALID;

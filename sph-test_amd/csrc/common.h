@@ -133,6 +133,26 @@ struct DevRange {
     const uint32_t* hi = nullptr;
 };
 
+// The in-library slab step (abi_multi.cpp) keeps every per-step size on the device: the counts of
+// the halo messages arrive in their headers, the slot ranges come out of the re-sort's cell table,
+// and every kernel reads them here (launch grids are host upper bounds). No host read per step.
+struct SlabSizes {
+    uint32_t nl, nr;          // records taken from the left / right message (clamped to capacity)
+    uint32_t o0, o1;          // owned slots of the previous sorted order
+    uint32_t no, n;           // o1 - o0; assembled slots nl + no + nr
+    uint32_t pick[6];         // column starts of the new order (launch_resort's CsPick)
+    uint32_t rg[10];          // ghost-left [0,1), owned [2,3), ghost-right [4,5), boundary columns [6,7), [8,9)
+    uint32_t fr[6];           // force pass: interior [0,1), boundary [2,3) and [4,5)
+    uint32_t dropped;         // own particles the assemble dropped (left the held window)
+    uint32_t flags;           // sticky: SZ_* bits
+};
+constexpr uint32_t SZ_OVF_MSG = 1u;     // a halo message held more records than its capacity
+constexpr uint32_t SZ_OVF_CAP = 2u;     // the assembled slots exceed the context's capacity
+constexpr uint32_t SZ_RHO_MISMATCH = 4u;  // a ghost column and the densities received differ in count
+constexpr uint32_t SZ_OVF_MOVERS = 8u;    // a mover list or a re-sort destination past the slot capacity
+// Halo messages: one 32-byte header record, then the records. Header: (count, capacity, 0, 0 | 0...)
+constexpr int MSG_HDR_F4 = 2;
+
 // Movers of a Model S step (resort.hip): particles whose new cell key differs from the sorted key
 // of their slot. The force pass appends them (any order) for the incremental re-sort.
 struct MoverSink {
@@ -143,6 +163,7 @@ struct MoverSink {
     uint32_t* mo;         // old key
     uint32_t* rank;       // 3 x cap rank accumulators, zeroed here
     uint32_t cap;
+    uint32_t* err = nullptr;   // SZ_OVF_MOVERS is or-ed here if the list would pass cap (entries dropped)
 };
 
 #if defined(__HIPCC__)
@@ -159,6 +180,10 @@ __device__ __forceinline__ void append_mover(const MoverSink& s, int32_t i, uint
     base = __shfl(base, leader, 64);
     if (mv) {
         const uint32_t r = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        if (r >= s.cap) {   // a corrupted counter: never write past the lists
+            if (s.err) atomicOr(s.err, SZ_OVF_MOVERS);
+            return;
+        }
         s.mi[r] = (uint32_t)i;
         s.mk[r] = key;
         s.mo[r] = ko;
@@ -193,6 +218,8 @@ struct ResortScratch {
     uint32_t *mx, *mos;              // movers by slot: slot, old key
     uint32_t cap;
     int32_t mi_off;                  // slab step: an own mover's slot is mi + mi_off (MV_REC: records' slot)
+    const SlabSizes* dz = nullptr;   // non-null: mi_off = nl - o0 from the device sizes
+    uint32_t* err = nullptr;         // SZ_OVF_MOVERS if a destination would pass cap (never written)
 };
 // a mover entry whose mi has this bit holds a slot of the assembled array (a halo record's);
 // without it, mi is the force pass's slot and the assembled slot is mi + mi_off
@@ -213,10 +240,23 @@ struct AsmSrc {
     const uint32_t* skr;    // records: old keys, by assembled slot
     const uint32_t* keyr;   // records: new keys, by assembled slot
     int32_t nl, nre;
+    const SlabSizes* dz;    // non-null: nl, nre, o_off (and the slot count) live on the device
 };
+#if defined(__HIPCC__)
+// the device-sized slab step: the assembled array's layout from SlabSizes (see AsmSrc)
+__device__ __forceinline__ void resolve_sizes(AsmSrc& a, ResortScratch& w, int32_t& n) {
+    if (!a.dz) return;
+    const uint32_t nl = a.dz->nl, no = a.dz->no;
+    a.nl = (int32_t)nl;
+    a.nre = (int32_t)(nl + no);
+    a.o_off = (int32_t)a.dz->o0 - (int32_t)nl;
+    w.mi_off = -a.o_off;
+    n = (int32_t)a.dz->n;
+}
+#endif
 inline AsmSrc asm_plain(const float4* pos, const float4* vel, const int32_t* id, const uint32_t* sk,
                         const uint32_t* keys, int32_t n) {
-    return AsmSrc{pos, vel, id, sk, keys, 0, nullptr, nullptr, nullptr, nullptr, 0, n};
+    return AsmSrc{pos, vel, id, sk, keys, 0, nullptr, nullptr, nullptr, nullptr, 0, n, nullptr};
 }
 // the slab step's halo records (slots [0, nl) and [nre, n)): new keys (window sentinel) into
 // src.keyr, old keys moved into this window and clamped into src.skr, and every record whose key
@@ -287,7 +327,8 @@ void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int
                           SphConst c, float2* rp, uint32_t* paths, hipStream_t s, DevRange dr = DevRange{});
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs,
                         int32_t ib, int32_t ie, GridDesc g, SphConst c, float dt, float fext_x,
-                        float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv, uint32_t* paths, hipStream_t s);
+                        float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv, uint32_t* paths, hipStream_t s,
+                        DevRange dr = DevRange{});
 
 // slab decomposition (slab.hip)
 // Order-preserving compaction of the sorted slots [b, e) whose key column satisfies
@@ -304,10 +345,38 @@ void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel
 void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, int32_t* id, hipStream_t s);
 // cell starts of the assembled old keys, in place from the previous table (ncells + 2 entries)
 void launch_slab_cs_old(uint32_t* cs, uint32_t ncells, uint32_t gyz, uint32_t gx, bool has_left, bool has_right,
-                        int32_t shift, const uint32_t* sk, int32_t nl, int32_t no, int32_t nr, hipStream_t s);
+                        int32_t shift, const uint32_t* sk, int32_t nl, int32_t no, int32_t nr, hipStream_t s,
+                        const SlabSizes* dz = nullptr);
 void launch_column_starts(const uint32_t* cs, uint32_t gyz, int32_t c0, int32_t m, uint32_t* out, hipStream_t s);
 void launch_pick(const uint32_t* cs, const int32_t* idx, int32_t m, uint32_t* out, hipStream_t s,
                  uint32_t* out_host = nullptr);
+// ---- the device-sized slab step (slab.hip; abi_multi.cpp drives it)
+// count + pack over the owned slots [dz->o0, dz->o1): the same order-preserving compaction as above,
+// into messages of a header and `cap[side]` records (header = true count; records past cap dropped and
+// flagged by the receiver). nb_ub: count-block upper bound (slab_send_blocks of the slot bound).
+void launch_slab_count_dev(const uint32_t* keys, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz, int32_t col_le,
+                           int32_t col_ge, uint32_t* blk, uint32_t* totals, hipStream_t s);
+// total: the side's count from launch_slab_count_dev, written into the message header
+void launch_slab_pack_dev(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
+                          const uint32_t* sk, uint32_t key_base, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz,
+                          int32_t side, int32_t col_le, int32_t col_ge, const uint32_t* blk, float4* msg, int32_t cap,
+                          const uint32_t* total, hipStream_t s);
+int32_t slab_send_blocks(int32_t b, int32_t e);
+// the received messages' counts -> dz (nl, nr clamped to the capacities, no, n, overflow flags)
+void launch_slab_sizes(SlabSizes* dz, const float4* msg_l, const float4* msg_r, int32_t cap_l, int32_t cap_r,
+                       int32_t capacity, hipStream_t s);
+// after the re-sort: dz->pick -> the ranges (rg, fr, o0/o1 of the new order, n and dropped)
+void launch_slab_ranges(SlabSizes* dz, int32_t has_left, int32_t has_right, hipStream_t s);
+// ρ, P/ρ² of boundary column `side` (rg[6+2side], rg[7+2side]) -> message (header + cap entries)
+void launch_slab_pack_rho(const float2* rp, SlabSizes* dz, int32_t side, float2* msg, int32_t cap, hipStream_t s);
+// received densities -> the ghost column of `side` (rg[4side], rg[4side+1]); mismatch -> SZ_RHO_MISMATCH
+void launch_slab_unpack_rho(float2* rp, SlabSizes* dz, int32_t side, const float2* msg, int32_t cap, hipStream_t s);
+// per-step counts for the host's lagged capacity choice, written to mapped pinned memory:
+// out[0..1] sent records (left, right), out[2..3] received headers, out[4..5] ρ sent, out[6..7] ρ received,
+// out[8] assembled slots, out[9] flags
+void launch_slab_lag(const SlabSizes* dz, const uint32_t* totals, const float4* msg_in_l, const float4* msg_in_r,
+                     const float2* rho_in_l, const float2* rho_in_r, uint32_t* out, hipStream_t s);
+
 // owned slots [o0, o0+n) -> records of 8 floats (x,y,z,u,v,w,id-bits,ρ)
 void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, const float2* rp,
                        int32_t o0, int32_t n, float* out, hipStream_t s);

@@ -25,6 +25,7 @@
 
 namespace sph {
 
+struct Multi;   // the multi-GPU step's state (abi_multi.cpp)
 // z sub-cells per 2h cell (SPEC_SPH.md §0). 6 trims the neighbour windows closer than 4 (C3: both passes
 // −8 us each) while the sub-cell crossings it adds cost the re-sort 2 us; 8 costs it 14 us
 // (profiles/r01_zsub_ab.log).
@@ -130,6 +131,10 @@ struct sph_ctx {
     size_t rb_cap[3] = {0, 0, 0};
     int32_t rb_fields = 0;          // fields of the outstanding request (0: none)
     int32_t rb_count = 0;           // particles it holds
+    // multi-GPU (abi_multi.cpp): a local group (sph_config.ndev > 1) or an RCCL rank (sph_comm_init)
+    sph::Multi* mg = nullptr;
+    sph::SlabSizes* dz = nullptr;   // a rank of the in-library step: its sizes on the device
+    bool dz_ahead = false;          // the device sizes are newer than o0 / o1 / n / rng (slab_sync_ranges reads them)
 };
 
 namespace sph {
@@ -219,7 +224,19 @@ int step_wcsph(sph_ctx* ctx, float dt);
 void free_bonds(sph_ctx* c);
 int32_t contact_active(const sph_ctx* c);
 int step_contact(sph_ctx* ctx, float dt);
-// slab window of the global grid (abi_slab.cpp)
+// slab decomposition (abi_slab.cpp)
 int slab_local_grid(sph_ctx* ctx);
+int slab_sync_ranges(sph_ctx* ctx);   // waits for the ranges of the last assemble (host or device sized)
+int32_t col_start(const sph_ctx* c, int32_t local_col);
+int slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void* dev_right, int32_t nr, bool force_full);
+// multi-GPU step (abi_multi.cpp)
+void multi_free(sph_ctx* ctx);
+bool is_group(const sph_ctx* ctx);   // sph_config.ndev > 1: the context holds one slab context per GPU
+int multi_create_group(sph_ctx* ctx);
+int multi_init_scenario(sph_ctx* ctx, const sph_scenario* sc);   // local group
+int multi_init_rank(sph_ctx* ctx, const sph_scenario* sc);       // RCCL rank
+int multi_step(sph_ctx* ctx, float dt, int32_t nsteps);
+int multi_read(sph_ctx* ctx, int field, float* dst, int32_t count);   // 0 positions, 1 velocities, 2 density
+std::vector<sph_ctx*> multi_kids(const sph_ctx* ctx);
 
 }  // namespace sph

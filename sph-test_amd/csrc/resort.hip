@@ -128,6 +128,7 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
                                                     uint32_t* __restrict__ next_count,
                                                     const uint32_t* __restrict__ cs_old, ResortScratch w) {
     __shared__ uint64_t tile[MV_TILE];
+    if (w.dz) w.mi_off = (int32_t)w.dz->nl - (int32_t)w.dz->o0;
     if (blockIdx.x == 0 && threadIdx.x == 0) *next_count = 0u;
     const uint32_t m = *mtotal;
     const uint64_t nr = (m + MV_BLK - 1) / MV_BLK, nt = (m + MV_TILE - 1) / MV_TILE;
@@ -166,6 +167,8 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_place(const uint32_t* __restrict_
                                                      float4* __restrict__ pos_o, float4* __restrict__ vel_o,
                                                      int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o,
                                                      ResortExtra ex) {
+    int32_t n_unused = 0;
+    resolve_sizes(src, w, n_unused);
     const uint32_t m = *mtotal;
     for (uint32_t r = blockIdx.x * MV_BLK + threadIdx.x; r < m; r += gridDim.x * MV_BLK) {
         const uint32_t x = mv_slot(w, w.mi[r]), k = w.mk[r];
@@ -173,6 +176,10 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_place(const uint32_t* __restrict_
         const uint32_t q = x < c0 ? c0 : (x > c1 ? c1 : x);
         const uint32_t rk = w.rank[r], ri = w.rank[w.cap + r], aq = w.rank[2 * w.cap + r];
         const uint32_t dst = (q - aq) + rk;
+        if (dst >= w.cap || rk >= w.cap || ri >= w.cap) {   // inconsistent tables: flag, never write past them
+            if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
+            continue;
+        }
         float4 p, v;
         int32_t pid;
         asm_load(src, (int32_t)x, p, v, pid);
@@ -237,7 +244,9 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
         mv_cell_start(cs, ncells, *mtotal, w, blockIdx.x - nb, b, pick);
         return;
     }
+    resolve_sizes(src, w, n);          // device-sized slab step: nb is an upper bound
     const int32_t i0 = xcd_block(blockIdx.x, nb) * MV_BLK;
+    if (i0 >= n) return;               // whole workgroup, before any barrier
     const int32_t i = i0 + threadIdx.x;
     const int32_t ilast = min(i0 + MV_BLK, n) - 1;
     const uint32_t m = *mtotal;
@@ -260,6 +269,10 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
     const uint32_t lo = b[1], hi = b[2];
     const uint32_t below = lo + lower_bound(w.ms + lo, hi - lo, comp(ko, (uint32_t)i));
     const uint32_t dst = ((uint32_t)i - a) + below;
+    if (dst >= w.cap) {
+        if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
+        return;
+    }
     float4 p, v;
     int32_t pid;
     asm_load(src, i, p, v, pid);
@@ -285,7 +298,13 @@ __global__ __launch_bounds__(MV_BLK) void k_slab_rec(AsmSrc src, int32_t n, Grid
                                                      MoverSink sink) {
     __shared__ uint32_t wsum[MV_BLK / 64];
     __shared__ uint32_t base_s;
+    if (src.dz) {   // device-sized slab step: the launch covers the message capacities
+        src.nl = (int32_t)src.dz->nl;
+        src.nre = (int32_t)(src.dz->nl + src.dz->no);
+        n = (int32_t)src.dz->n;
+    }
     const int32_t nr = n - src.nre, nrec = src.nl + nr;
+    if ((int32_t)(blockIdx.x * MV_DET) >= nrec) return;   // whole workgroup, before any barrier
     const int32_t r0 = blockIdx.x * MV_DET + threadIdx.x;
     uint32_t kn[MV_DET_PER], ko[MV_DET_PER];
     int32_t xs[MV_DET_PER];
@@ -336,6 +355,10 @@ __global__ __launch_bounds__(MV_BLK) void k_slab_rec(AsmSrc src, int32_t n, Grid
 #pragma unroll
     for (int j = 0; j < MV_DET_PER; ++j) {
         if (!(mine >> j & 1u)) continue;
+        if (q >= sink.cap) {
+            if (sink.err) atomicOr(sink.err, SZ_OVF_MOVERS);
+            break;
+        }
         sink.mi[q] = (uint32_t)xs[j] | MV_REC;
         sink.mk[q] = kn[j];
         sink.mo[q] = ko[j];

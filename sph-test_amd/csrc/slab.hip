@@ -45,8 +45,13 @@ int32_t slab_send_blocks(int32_t b, int32_t e) { return e > b ? (e - b + SL_SEND
 
 __global__ __launch_bounds__(SL_BLK) void k_slab_count(const uint32_t* __restrict__ keys, int32_t b, int32_t e,
                                                        uint32_t gyz, int32_t col_le, int32_t col_ge,
-                                                       uint32_t* __restrict__ blk, int32_t nblk) {
+                                                       uint32_t* __restrict__ blk, int32_t nblk,
+                                                       const SlabSizes* __restrict__ dz) {
     __shared__ uint32_t wl[SL_WAVES], wr[SL_WAVES];
+    if (dz) {   // device-sized step: the owned slots of the previous order; nblk is an upper bound
+        b = (int32_t)dz->o0;
+        e = (int32_t)dz->o1;
+    }
     uint32_t cl = 0, cr = 0;
     const int32_t i0 = b + blockIdx.x * SL_SEND + threadIdx.x;
 #pragma unroll
@@ -77,8 +82,17 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_count(const uint32_t* __restric
 // same totals as int64 into totals64 when given (the async send counts)
 constexpr int SL_SCAN = 1024;
 
+// Message header (MSG_HDR_F4 float4s): (count, capacity, 0, 0 | 0, 0, 0, 0) as uint32 bits.
+__device__ __forceinline__ void write_header(float4* msg, uint32_t count, uint32_t cap) {
+    msg[0] = make_float4(__uint_as_float(count), __uint_as_float(cap), 0.f, 0.f);
+    msg[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+__device__ __forceinline__ uint32_t header_count(const float4* msg) { return __float_as_uint(msg[0].x); }
+
 __global__ __launch_bounds__(SL_SCAN) void k_slab_scan(uint32_t* __restrict__ blk, int32_t nblk,
-                                                       uint32_t* __restrict__ totals, int64_t* __restrict__ totals64) {
+                                                       uint32_t* __restrict__ totals, int64_t* __restrict__ totals64,
+                                                       float4* __restrict__ hdr_l, float4* __restrict__ hdr_r,
+                                                       int32_t cap_l, int32_t cap_r) {
     __shared__ uint32_t ws[SL_SCAN / 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int side = 0; side < 2; ++side) {
@@ -108,6 +122,8 @@ __global__ __launch_bounds__(SL_SCAN) void k_slab_scan(uint32_t* __restrict__ bl
         if (threadIdx.x == 0) {
             totals[side] = carry;
             if (totals64) totals64[side] = (int64_t)carry;
+            float4* h = side == 0 ? hdr_l : hdr_r;
+            if (h) write_header(h, carry, (uint32_t)(side == 0 ? cap_l : cap_r));
         }
     }
 }
@@ -125,9 +141,15 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_pack(const uint32_t* __restrict
                                                       int32_t b, int32_t e, uint32_t gyz, int32_t side,
                                                       int32_t col_le, int32_t col_ge,
                                                       const uint32_t* __restrict__ blk, int32_t nblk,
-                                                      float4* __restrict__ out) {
+                                                      float4* __restrict__ out, const SlabSizes* __restrict__ dz,
+                                                      uint32_t cap) {
     __shared__ uint32_t wc[SL_PER][SL_WAVES];
     const int w = threadIdx.x >> 6;
+    if (dz) {   // device-sized step (see k_slab_count)
+        b = (int32_t)dz->o0;
+        e = (int32_t)dz->o1;
+    }
+    if (b + (int32_t)blockIdx.x * SL_SEND >= e) return;   // whole workgroup, before the barrier
     const int32_t i0 = b + blockIdx.x * SL_SEND + threadIdx.x;
     // every key load issues before any is used; then one barrier for all sub-chunks' wave counts
     uint32_t col[SL_PER];
@@ -154,9 +176,9 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_pack(const uint32_t* __restrict
         }
         const bool pred = (mine >> j) & 1u;
         const uint64_t m = __ballot(pred);
-        if (pred) {
+        const uint32_t r = run + before + lane_prefix(m);
+        if (pred && r < cap) {   // past the message capacity: dropped; the header's count tells the receiver
             const int32_t i = i0 + j * SL_BLK;
-            const uint32_t r = run + before + lane_prefix(m);
             const float4 p = pos[i], v = vel[i];
             const uint32_t ok = sk ? sk[i] + key_base : SL_NO_KEY;
             out[2 * (size_t)r] = make_float4(p.x, p.y, p.z, __int_as_float(id[i]));
@@ -184,9 +206,16 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_unpack(const float4* __restrict
 __global__ __launch_bounds__(SL_BLK) void k_slab_cs_old(uint32_t* __restrict__ cs, uint32_t ncells, uint32_t gyz,
                                                         uint32_t gx, int32_t has_left, int32_t has_right,
                                                         int32_t shift, const uint32_t* __restrict__ sk,
-                                                        int32_t nl, int32_t no, int32_t nr) {
+                                                        int32_t nl, int32_t no, int32_t nr,
+                                                        const SlabSizes* __restrict__ dz) {
     const uint32_t k = blockIdx.x * SL_BLK + threadIdx.x;
     if (k > ncells + 1u) return;
+    if (dz) {
+        nl = (int32_t)dz->nl;
+        no = (int32_t)dz->no;
+        nr = (int32_t)dz->nr;
+        shift = nl - (int32_t)dz->o0;
+    }
     const uint32_t n = (uint32_t)(nl + no + nr);
     if (k >= ncells) {
         cs[k] = n;
@@ -303,8 +332,8 @@ void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, 
 void launch_slab_count(const uint32_t* keys, int32_t b, int32_t e, uint32_t gyz, int32_t col_le, int32_t col_ge,
                        uint32_t* blk, uint32_t* totals, hipStream_t s, int64_t* totals64) {
     const int32_t nb = slab_send_blocks(b, e);
-    k_slab_count<<<nb, SL_BLK, 0, s>>>(keys, b, e, gyz, col_le, col_ge, blk, nb);
-    k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb, totals, totals64);
+    k_slab_count<<<nb, SL_BLK, 0, s>>>(keys, b, e, gyz, col_le, col_ge, blk, nb, nullptr);
+    k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb, totals, totals64, nullptr, nullptr, 0, 0);
 }
 
 void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
@@ -313,7 +342,130 @@ void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel
     const int32_t nb = slab_send_blocks(b, e);
     if (e > b)
         k_slab_pack<<<nb, SL_BLK, 0, s>>>(keys, pos, vel, id, sk, key_base, b, e, gyz, side, col_le, col_ge, blk, nb,
-                                          out);
+                                          out, nullptr, 0xffffffffu);
+}
+
+void launch_slab_count_dev(const uint32_t* keys, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz, int32_t col_le,
+                           int32_t col_ge, uint32_t* blk, uint32_t* totals, hipStream_t s) {
+    k_slab_count<<<nb_ub, SL_BLK, 0, s>>>(keys, 0, 0, gyz, col_le, col_ge, blk, nb_ub, dz);
+    k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb_ub, totals, nullptr, nullptr, nullptr, 0, 0);
+}
+
+__global__ void k_msg_header(float4* __restrict__ msg, const uint32_t* __restrict__ total, int32_t cap) {
+    if (threadIdx.x == 0) write_header(msg, *total, (uint32_t)cap);
+}
+
+void launch_slab_pack_dev(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
+                          const uint32_t* sk, uint32_t key_base, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz,
+                          int32_t side, int32_t col_le, int32_t col_ge, const uint32_t* blk, float4* msg, int32_t cap,
+                          const uint32_t* total, hipStream_t s) {
+    k_msg_header<<<1, 64, 0, s>>>(msg, total, cap);
+    k_slab_pack<<<nb_ub, SL_BLK, 0, s>>>(keys, pos, vel, id, sk, key_base, 0, 0, gyz, side, col_le, col_ge, blk,
+                                         nb_ub, msg + MSG_HDR_F4, dz, (uint32_t)cap);
+}
+
+__global__ void k_slab_sizes(SlabSizes* __restrict__ dz, const float4* __restrict__ msg_l,
+                             const float4* __restrict__ msg_r, int32_t cap_l, int32_t cap_r, int32_t capacity) {
+    if (threadIdx.x != 0) return;
+    const uint32_t hl = msg_l ? header_count(msg_l) : 0u, hr = msg_r ? header_count(msg_r) : 0u;
+    uint32_t nl = min(hl, (uint32_t)cap_l), nr = min(hr, (uint32_t)cap_r);
+    uint32_t f = dz->flags;
+    if (hl > (uint32_t)cap_l || hr > (uint32_t)cap_r) f |= SZ_OVF_MSG;
+    uint32_t no = dz->o1 >= dz->o0 ? dz->o1 - dz->o0 : 0u;
+    if ((uint64_t)nl + no + nr > (uint64_t)capacity) {   // never address past the slot arrays
+        f |= SZ_OVF_CAP;
+        nl = nr = 0;
+        if (no > (uint32_t)capacity) no = 0;
+    }
+    dz->nl = nl;
+    dz->nr = nr;
+    dz->no = no;
+    dz->n = nl + no + nr;
+    dz->flags = f;
+}
+
+void launch_slab_sizes(SlabSizes* dz, const float4* msg_l, const float4* msg_r, int32_t cap_l, int32_t cap_r,
+                       int32_t capacity, hipStream_t s) {
+    k_slab_sizes<<<1, 64, 0, s>>>(dz, msg_l, msg_r, cap_l, cap_r, capacity);
+}
+
+// ranges of the new order from the picked column starts (as slab_sync_ranges does on the host)
+__global__ void k_slab_ranges(SlabSizes* __restrict__ dz, int32_t has_left, int32_t has_right) {
+    if (threadIdx.x != 0) return;
+    const uint32_t* v = dz->pick;
+    const uint32_t rg[10] = {v[0], v[1], v[1], v[4], v[4], v[5], v[1], v[2], v[3], v[4]};
+    for (int k = 0; k < 10; ++k) dz->rg[k] = rg[k];
+    const uint32_t ib = has_left ? v[2] : v[1], ie = has_right ? v[3] : v[4];
+    dz->fr[0] = ib;
+    dz->fr[1] = ie > ib ? ie : ib;
+    if (ie < ib) {   // one-column slab: both boundary columns are the owned column
+        dz->fr[2] = v[1]; dz->fr[3] = v[4]; dz->fr[4] = 0u; dz->fr[5] = 0u;
+    } else {
+        dz->fr[2] = v[1]; dz->fr[3] = ib; dz->fr[4] = ie; dz->fr[5] = v[4];
+    }
+    dz->dropped = dz->n - v[5];
+    dz->n = v[5];
+    dz->o0 = v[1];
+    dz->o1 = v[4];
+}
+
+void launch_slab_ranges(SlabSizes* dz, int32_t has_left, int32_t has_right, hipStream_t s) {
+    k_slab_ranges<<<1, 64, 0, s>>>(dz, has_left, has_right);
+}
+
+// ρ messages: a 32-byte header (count, capacity) = 4 float2, then the entries
+constexpr int RHO_HDR = 4;
+
+__global__ __launch_bounds__(SL_BLK) void k_slab_pack_rho(const float2* __restrict__ rp, const SlabSizes* __restrict__ dz,
+                                                          int32_t side, float2* __restrict__ msg, int32_t cap) {
+    const uint32_t b = dz->rg[6 + 2 * side], e = dz->rg[7 + 2 * side];
+    const uint32_t cnt = e - b;
+    const uint32_t t = blockIdx.x * SL_BLK + threadIdx.x;
+    if (t == 0) {
+        msg[0] = make_float2(__uint_as_float(cnt), __uint_as_float((uint32_t)cap));
+        msg[1] = msg[2] = msg[3] = make_float2(0.f, 0.f);
+    }
+    if (t < cnt && t < (uint32_t)cap) msg[RHO_HDR + t] = rp[b + t];
+}
+
+__global__ __launch_bounds__(SL_BLK) void k_slab_unpack_rho(float2* __restrict__ rp, SlabSizes* __restrict__ dz,
+                                                            int32_t side, const float2* __restrict__ msg, int32_t cap) {
+    const uint32_t b = dz->rg[4 * side], e = dz->rg[4 * side + 1];
+    const uint32_t cnt = __float_as_uint(msg[0].x);
+    const uint32_t m = min(min(cnt, (uint32_t)cap), e - b);
+    const uint32_t t = blockIdx.x * SL_BLK + threadIdx.x;
+    if (t == 0 && (cnt != e - b || cnt > (uint32_t)cap)) atomicOr(&dz->flags, SZ_RHO_MISMATCH);
+    if (t < m) rp[b + t] = msg[RHO_HDR + t];
+}
+
+void launch_slab_pack_rho(const float2* rp, SlabSizes* dz, int32_t side, float2* msg, int32_t cap, hipStream_t s) {
+    k_slab_pack_rho<<<cap / SL_BLK + 1, SL_BLK, 0, s>>>(rp, dz, side, msg, cap);
+}
+
+void launch_slab_unpack_rho(float2* rp, SlabSizes* dz, int32_t side, const float2* msg, int32_t cap, hipStream_t s) {
+    k_slab_unpack_rho<<<cap / SL_BLK + 1, SL_BLK, 0, s>>>(rp, dz, side, msg, cap);
+}
+
+__global__ void k_slab_lag(const SlabSizes* __restrict__ dz, const uint32_t* __restrict__ totals,
+                           const float4* __restrict__ msg_in_l, const float4* __restrict__ msg_in_r,
+                           const float2* __restrict__ rho_in_l, const float2* __restrict__ rho_in_r,
+                           uint32_t* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    out[0] = totals[0];
+    out[1] = totals[1];
+    out[2] = msg_in_l ? header_count(msg_in_l) : 0u;
+    out[3] = msg_in_r ? header_count(msg_in_r) : 0u;
+    out[4] = dz->rg[7] - dz->rg[6];
+    out[5] = dz->rg[9] - dz->rg[8];
+    out[6] = rho_in_l ? __float_as_uint(rho_in_l[0].x) : 0u;
+    out[7] = rho_in_r ? __float_as_uint(rho_in_r[0].x) : 0u;
+    out[8] = dz->n;
+    out[9] = dz->flags;
+}
+
+void launch_slab_lag(const SlabSizes* dz, const uint32_t* totals, const float4* msg_in_l, const float4* msg_in_r,
+                     const float2* rho_in_l, const float2* rho_in_r, uint32_t* out, hipStream_t s) {
+    k_slab_lag<<<1, 64, 0, s>>>(dz, totals, msg_in_l, msg_in_r, rho_in_l, rho_in_r, out);
 }
 
 void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, int32_t* id, hipStream_t s) {
@@ -321,10 +473,11 @@ void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, 
 }
 
 void launch_slab_cs_old(uint32_t* cs, uint32_t ncells, uint32_t gyz, uint32_t gx, bool has_left, bool has_right,
-                        int32_t shift, const uint32_t* sk, int32_t nl, int32_t no, int32_t nr, hipStream_t s) {
+                        int32_t shift, const uint32_t* sk, int32_t nl, int32_t no, int32_t nr, hipStream_t s,
+                        const SlabSizes* dz) {
     const uint32_t m = ncells + 2u;
     k_slab_cs_old<<<(m + SL_BLK - 1) / SL_BLK, SL_BLK, 0, s>>>(cs, ncells, gyz, gx, has_left ? 1 : 0,
-                                                               has_right ? 1 : 0, shift, sk, nl, no, nr);
+                                                               has_right ? 1 : 0, shift, sk, nl, no, nr, dz);
 }
 
 void launch_slab_select_columns(const float4* pos, const float4* vel, const int32_t* id, int32_t n, GridDesc g,
@@ -334,7 +487,7 @@ void launch_slab_select_columns(const float4* pos, const float4* vel, const int3
     k_sel_count<<<nb, SL_BLK, 0, s>>>(pos, n, g, lo, hi, blk);
     // reuse the two-row scan: row 1 is a dummy of zeros
     (void)hipMemsetAsync(blk + nb, 0, sizeof(uint32_t) * nb, s);
-    k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb, total, nullptr);
+    k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb, total, nullptr, nullptr, nullptr, 0, 0);
     if (n > 0 && pos_o != nullptr) k_sel_scatter<<<nb, SL_BLK, 0, s>>>(pos, vel, id, n, g, lo, hi, blk, pos_o, vel_o, id_o);
 }
 

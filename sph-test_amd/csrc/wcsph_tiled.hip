@@ -296,12 +296,17 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
     const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, PairK pk, float dt,
     float fext_x, float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o, MoverSink mv,
-    uint32_t* __restrict__ paths) {
+    uint32_t* __restrict__ paths, DevRange dr) {
     __shared__ float4 sp[TF_GCAP + 4];     // (x, y, z, ρ)
     __shared__ float4 sv[TF_GCAP + 4];     // (u, v, w, P/ρ²)
     __shared__ uint16_t lst[TT_CAP][TT_BLK];
     const int tid = threadIdx.x;
+    if (dr.lo) {   // device-resident bounds (slab step); the grid is an upper bound
+        ib = (int32_t)*dr.lo;
+        n = (int32_t)*dr.hi;
+    }
     const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
+    if (i0 >= n) return;   // whole workgroup: before any barrier
     const int32_t i = i0 + tid;
     const bool valid = i < n;
     const int32_t ilast = min(i0 + TT_BLK, n) - 1;
@@ -421,7 +426,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     append_mover(mv, i, window_key(g, np[0], np[1], np[2]));
 }
 
-// dr set: [ib, ie) only sizes the grid (an upper bound); the kernel reads its bounds from dr
+// dr set: [ib, ie) only sizes the grid (an upper bound); the kernels read their bounds from dr
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
                           float2* rp, uint32_t* paths, hipStream_t s, DevRange dr) {
     if (ie > ib) k_density_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, cs, ib, ie, g, c, rp, dr, paths);
@@ -429,10 +434,10 @@ void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int
 
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,
                         int32_t ie, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o,
-                        uint32_t* keys_o, MoverSink mv, uint32_t* paths, hipStream_t s) {
+                        uint32_t* keys_o, MoverSink mv, uint32_t* paths, hipStream_t s, DevRange dr) {
     if (ie > ib)
         k_force_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt, fext_x,
-                                                                         pos_o, vel_o, keys_o, mv, paths);
+                                                                         pos_o, vel_o, keys_o, mv, paths, dr);
 }
 
 }  // namespace sph

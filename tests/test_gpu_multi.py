@@ -1,0 +1,111 @@
+"""The decomposed step inside the library (sph_config.ndev > 1 / sph_comm_init; abi_multi.cpp).
+
+On the one-GPU test box every slab context of a local group sits on device 0 (the halo copies are
+then plain device copies instead of xGMI peer copies; the step is otherwise the same code).
+
+  * ndev = 2 / 3 against the single-context step (the decomposition changes only who computes what:
+    positions within 2e-6, as tests/test_gpu_slab.py);
+  * ndev = 3 with re-balancing against the per-phase slab ABI driven from Python over gloo
+    (tests/test_gpu_slab.py's harness, sph_test_amd.slab.SlabRunner): the same kernels on the same data
+    in the same order, so every rank's owned particles are BIT-identical, over 60 steps that take the
+    exact-size steps (after each re-cut) and the lag-sized steps (device sizes, no host read);
+  * an RCCL communicator of one rank (sph_comm_init): the in-library step equals the single context bit
+    for bit (world 1 has no halo; RCCL between ranks needs two GPUs and runs in the driver's 8-GPU bench).
+"""
+import numpy as np
+import pytest
+
+from test_gpu_slab import _run_ranks, _scenario, _single
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(x, v, xs, vs):
+    np.testing.assert_allclose(x, xs, rtol=0, atol=2e-6)
+    np.testing.assert_allclose(v, vs, rtol=1e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize("ndev", [2, 3])
+def test_group_matches_single(pkg, ndev):
+    sc = _scenario(pkg)
+    xs, vs = _single(pkg, sc)
+    sim = pkg.SPHSim(sc, ndev=ndev, rebalance_every=0)
+    try:
+        d = sim.ctx.decomposition()
+        assert d.world == ndev and d.local_ranks == ndev and d.total == len(xs)
+        sim.step(8)
+        _check(sim.positions(), sim.velocities(), xs, vs)
+        st = sim.ctx.stats()
+        assert st.active == len(xs) and st.steps == 8
+        assert sim.ctx.decomposition().owned == len(xs)   # every particle owned once
+    finally:
+        sim.close()
+
+
+def test_group_bitwise_vs_python_slab_path(pkg, tmp_path):
+    """The in-library step (device sizes, lagged message capacities, RCCL-free local copies) against
+    SlabRunner's per-phase ABI over gloo: bit-identical owned particles after 60 steps with re-balancing
+    every 20 steps (3 re-cuts, each followed by two exact-size steps)."""
+    sc = _scenario(pkg)
+    steps, every = 60, 20
+    rec = _run_ranks(3, tmp_path, rebalance_every=every, steps=steps)
+    ref = {int(i): r for i, r in zip(rec[:, 6].view(np.int32), rec)}
+    sim = pkg.SPHSim(sc, ndev=3, rebalance_every=every, profile=True)
+    try:
+        sim.step(steps)
+        x, v, rho = sim.positions(), sim.velocities(), sim.density()
+        ids = np.arange(len(x))
+        want = np.stack([ref[i] for i in ids])
+        assert x.tobytes() == np.ascontiguousarray(want[:, 0:3]).tobytes()
+        assert v.tobytes() == np.ascontiguousarray(want[:, 3:6]).tobytes()
+        assert rho.tobytes() == np.ascontiguousarray(want[:, 7]).tobytes()
+        cuts = [tuple(int(v) for v in c) for c in np.load(tmp_path / "cuts0.npy")]
+        d = sim.ctx.decomposition()
+        assert (d.cut.cx_lo, d.cut.cx_hi) == cuts[0]   # rank 0's slab after re-balancing, as the Python run's
+        ks = sim.ctx.kernel_stats()
+        assert ks["resort"]["launches"] > 0          # the device-sized incremental re-sort ran
+    finally:
+        sim.close()
+
+
+def test_group_long_run_lag_sizes(pkg):
+    """300 steps of a 2-slab group with re-balancing every 50: the lag-sized messages never overflow
+    (a flagged overflow would fail sph_step with SPH_ERR_CAPACITY), no particle is lost, and the result
+    stays within the decomposition tolerance of the single context after the first 8 steps."""
+    sc = _scenario(pkg)
+    sim = pkg.SPHSim(sc, ndev=2, rebalance_every=50, validate=True)
+    try:
+        sim.step(300)
+        x = sim.positions()
+        assert np.isfinite(x).all()
+        assert (x >= 0).all() and (x <= np.array(sim.params.box, np.float32)).all()
+        assert sim.ctx.decomposition().owned == len(x)
+    finally:
+        sim.close()
+
+
+def test_rccl_world1_bitwise(pkg):
+    """One RCCL rank: sph_comm_init + sph_init_scenario + sph_step give the single context's bits."""
+    from sph_test_amd.context import comm_unique_id
+    sc = _scenario(pkg)
+    xs, vs = _single(pkg, sc, 50)
+    p, dt = pkg.scenario_params(sc)
+    ctx = pkg.Context(pkg.SPH_MODEL_WCSPH, 3, 1000)
+    try:
+        ctx.comm_init(comm_unique_id(), 1, 0)
+        ctx.set_params(p)
+        ctx.init_scenario(sc)
+        ctx.step(dt, 50)
+        d = ctx.decomposition()
+        assert d.world == 1 and d.owned == len(xs)
+        rec = np.empty((ctx.stats().capacity, 8), np.float32)
+        import ctypes as C
+        from sph_test_amd import _abi as A
+        n = C.c_int32()
+        A.check("sph_slab_read_owned", ctx._L.sph_slab_read_owned(ctx.handle, A.ptr(rec), len(rec), C.byref(n)), ctx.handle)
+        rec = rec[: n.value]
+        order = np.argsort(rec[:, 6].view(np.int32))
+        assert np.array_equal(rec[order, 0:3], xs)
+        assert np.array_equal(rec[order, 3:6], vs)
+    finally:
+        ctx.close()
