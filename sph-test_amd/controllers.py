@@ -107,7 +107,8 @@ class ParticleSystemController:
     buffer edit to the device (`sph_split_particles`), so the particle buffer never makes the
     host round trip the reference's ProcessPendingSplits does (:793-794, :959)."""
 
-    def __init__(self, particleCount: int = 10000, device: int = 0):
+    def __init__(self, particleCount: int = 10000, device: int = 0, backend=None):
+        """backend: a factory (model, dim, capacity, device) -> context (default: the libsphhip Context)."""
         # [Header("Particle Configuration")]  ParticleSystemController.cs:11-15
         self.particleCount = particleCount
         self.minRadius = 1.5
@@ -146,14 +147,16 @@ class ParticleSystemController:
         self.ParticleIDs: List[ParticleIDData] = []          # :118-119
         self._bonds_uploaded: Optional[bytes] = None
         self._rb_requested = False
+        self._backend = backend if backend is not None else (lambda m, d, c, dev: Context(m, d, c, device=dev))
         self._ctx: Optional[Context] = None
+        self.frameCount = 0                     # Unity's Time.frameCount: +1 per Update
 
     @classmethod
-    def from_scene(cls, scene_path, genome_path=None, device: int = 0) -> "ParticleSystemController":
+    def from_scene(cls, scene_path, genome_path=None, device: int = 0, backend=None) -> "ParticleSystemController":
         """The controller as a Unity scene serializes it (e.g. Particle Simulation.unity:151-178),
         with an optional genome asset (e.g. NewCellGenome.asset)."""
         vals = load_scene_controller(scene_path)
-        ctl = cls(particleCount=vals.pop("particleCount"), device=device)
+        ctl = cls(particleCount=vals.pop("particleCount"), device=device, backend=backend)
         for k, v in vals.items():
             setattr(ctl, k, float(v))
         if genome_path is not None:
@@ -166,7 +169,7 @@ class ParticleSystemController:
         AoS-84 particles (PARTICLE84) uploaded as they are."""
         if self.genome is not None:
             self.genome.ValidateForSimulation()             # :216-226 (raises on several initial modes)
-        self._ctx = Context(A.SPH_MODEL_CONTACT, 3, self.particleCount, device=self.device)
+        self._ctx = self._backend(A.SPH_MODEL_CONTACT, 3, self.particleCount, self.device)
         if particles is not None:
             self._ctx.upload_aos84(particles)
             self.activeParticleCount = len(particles)
@@ -229,9 +232,22 @@ class ParticleSystemController:
             self.CpuParticleRotations[: len(rot)] = rot
             self._rb_requested = False
 
+    def Frame(self, dt: float) -> None:
+        """One Unity frame of the scene: this Update, then the adhesion manager's LateUpdate (Unity runs
+        every script's LateUpdate after all Updates; CellAdhesionManager.cs:72-75)."""
+        self.Update(dt)
+        late = getattr(self.adhesionManager, "LateUpdate", None)
+        if late is not None:
+            late()
+
+    def cached_mode_indices(self) -> np.ndarray:
+        """modeIndex of every particle (CellAdhesionManager reads the controller's cachedParticleData)."""
+        return self._ctx.get_particles(0, self._ctx.n)["modeIndex"]
+
     def Update(self, dt: float) -> None:
         """One frame (:244-351): readback delivery (:250), division (:253), uniforms (:255-263), the
         step with adhesion (:265-331), readback (:332-333)."""
+        self.frameCount += 1
         if not self.immediateReadback:
             self.RequestParticleDataAsync()
         self.UpdateCellDivisionTimers(dt)
@@ -313,6 +329,8 @@ class ParticleSystemController:
         cap = self._ctx.stats().capacity
         if cap > self.particleCount:                        # the device grew the buffers (:788-792)
             self._grow_host(cap)
+        handle = getattr(self.adhesionManager, "HandleCellSplit", None)
+        g = self.genome
         for k, sp in enumerate(splits):
             pidx = int(sp["parentIndex"])
             parent_uid = self.ParticleIDs[pidx].uniqueID
@@ -322,6 +340,14 @@ class ParticleSystemController:
             self.nextUniqueIDCounter += 2
             self.cellSplitTimers[pidx] = 0.0
             self.cellSplitTimers[b_idx] = 0.0
+            if handle is not None and g is not None:   # :929-951
+                # "the parent's mode" is read after the parent's record became child A's (:854-857, :933)
+                pm = int(sp["childAModeIndex"])
+                mode = g.modes[pm if 0 <= pm < len(g.modes) else 0]
+                handle(pidx, pidx, b_idx, mode.parentSplitYaw, mode.parentSplitPitch, self.CpuParticleRotations[pidx],
+                       self.CpuParticlePositions[pidx], int(sp["childAModeIndex"]), int(sp["childBModeIndex"]),
+                       mode.parentMakeAdhesion, mode.childA_KeepAdhesion, mode.childB_KeepAdhesion)
+            self.activeParticleCount = act0 + k + 1
         self.activeParticleCount = new_active
 
     def _grow_host(self, cap: int) -> None:

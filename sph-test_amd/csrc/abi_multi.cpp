@@ -19,8 +19,9 @@
 // before (a kernel writes them to mapped pinned memory; both neighbours read the same numbers, so they
 // agree on every message size), with a margin far above what particles moving < 0.1 h per step can add.
 // A larger count is caught on the device (SZ_* flags) and the next sph_step fails with SPH_ERR_CAPACITY.
-// The first two steps after the initial cut and after every re-cut size the messages exactly (a count
-// exchange and one host read per exchange), as the lagged counts then describe other columns.
+// The first three steps after the initial cut and after every re-cut size the messages exactly (a count
+// exchange and one host read per exchange): the lagged counts would describe the old cut's columns, or
+// the one-off migration exchange of the first step after the re-cut.
 #include "host.h"
 
 #include <rccl/rccl.h>
@@ -264,6 +265,95 @@ int checkpoint(RankState& R, const char* what) {
 #define CKPT(R, what) \
     do { if (int rc_ = checkpoint(R, what)) return rc_; } while (0)
 
+// SPH_FLAG_VALIDATE, before the incremental re-sort: the mover lists and the old cell starts it reads
+int validate_movers(RankState& R, int used) {
+    sph_ctx* ctx = R.c;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    SlabSizes h;
+    HIPCHK(hipMemcpy(&h, R.dz, sizeof h, hipMemcpyDeviceToHost));
+    uint32_t m = 0;
+    HIPCHK(hipMemcpy(&m, ctx->mv_count + used, 4, hipMemcpyDeviceToHost));
+    const uint32_t cap = (uint32_t)ctx->capacity, ncells = ctx->grid.ncells;
+    if (m > cap) return fail(ctx, SPH_ERR_STATE, "validate(movers) rank %d: %u movers > cap %u", R.rank, m, cap);
+    std::vector<uint32_t> mi(m), mk(m), mo(m), cs(ncells + 2);
+    if (m) {
+        HIPCHK(hipMemcpy(mi.data(), ctx->mv_mi, m * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(mk.data(), ctx->mv_mk, m * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(mo.data(), ctx->mv_mo, m * 4, hipMemcpyDeviceToHost));
+    }
+    HIPCHK(hipMemcpy(cs.data(), ctx->cs, cs.size() * 4, hipMemcpyDeviceToHost));
+    const int64_t mi_off = (int64_t)h.nl - (int64_t)h.o0;
+    struct Ent { uint32_t slot, mo, r; bool operator<(const Ent& o) const { return slot < o.slot; } };
+    std::vector<Ent> by_slot;
+    for (uint32_t r = 0; r < m; ++r) {
+        const int64_t x = (mi[r] & MV_REC) ? (int64_t)(mi[r] & ~MV_REC) : (int64_t)mi[r] + mi_off;
+        const bool rec = (mi[r] & MV_REC) != 0;
+        const bool slot_ok = x >= 0 && x < (int64_t)h.n && (rec ? (x < h.nl || x >= h.nl + h.no) : (x >= h.nl && x < h.nl + h.no));
+        if (!slot_ok || mk[r] > ncells || mo[r] > ncells)
+            return fail(ctx, SPH_ERR_STATE,
+                        "validate(movers) rank %d step %lld: entry %u of %u: mi %#x (slot %lld) mk %u mo %u; nl %u no %u nr %u "
+                        "n %u o0 %u o1 %u ncells %u",
+                        R.rank, (long long)ctx->steps, r, m, mi[r], (long long)x, mk[r], mo[r], h.nl, h.no, h.nr, h.n, h.o0,
+                        h.o1, ncells);
+        by_slot.push_back(Ent{(uint32_t)x, mo[r], r});
+    }
+    // the assembled old keys (records: keys2, own: sk_cur) and new keys (records: vals, own: keys)
+    const uint32_t n = h.n;
+    std::vector<uint32_t> skr(n), keyr(n), sko(h.no), keyo(h.no);
+    if (n) {
+        HIPCHK(hipMemcpy(skr.data(), ctx->keys2, n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(keyr.data(), ctx->vals, n * 4, hipMemcpyDeviceToHost));
+    }
+    if (h.no) {
+        HIPCHK(hipMemcpy(sko.data(), ctx->sk_cur + h.o0, h.no * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(keyo.data(), ctx->keys + h.o0, h.no * 4, hipMemcpyDeviceToHost));
+    }
+    std::sort(by_slot.begin(), by_slot.end());
+    uint32_t nrec = 0;
+    for (uint32_t r = 0; r < m; ++r) nrec += (mi[r] & MV_REC) != 0;
+    for (size_t k = 1; k < by_slot.size(); ++k)
+        if (by_slot[k].slot == by_slot[k - 1].slot || by_slot[k].mo < by_slot[k - 1].mo) {
+            const Ent& a = by_slot[k - 1];
+            const Ent& b = by_slot[k];
+            float4 rec[4] = {};
+            if (R.left >= 0) HIPCHK(hipMemcpy(rec, R.msg_in[0], sizeof rec, hipMemcpyDeviceToHost));
+            uint32_t u[16];
+            std::memcpy(u, rec, sizeof u);
+            return fail(ctx, SPH_ERR_STATE,
+                        "validate(movers) rank %d step %lld: slot %u (entry %u: mi %#x mk %u mo %u) before slot %u (entry %u: "
+                        "mi %#x mk %u mo %u); %u movers (%u records); nl %u no %u nr %u n %u o0 %u o1 %u ncells %u; "
+                        "left hdr %u %u rec0 pos %g %g %g id %d og %u; c1i %d %d c1o %d %d mcap_in %d; skr0 %u keyr0 %u "
+                        "cx0 %d gyz %u",
+                        R.rank, (long long)ctx->steps, a.slot, a.r, mi[a.r], mk[a.r], mo[a.r], b.slot, b.r, mi[b.r], mk[b.r],
+                        mo[b.r], m, nrec, h.nl, h.no, h.nr, h.n, h.o0, h.o1, ncells, u[0], u[1], rec[2].x, rec[2].y, rec[2].z,
+                        (int)u[11], u[15], R.c1i[0], R.c1i[1], R.c1o[0], R.c1o[1], R.mcap_in[0], n ? skr[0] : 0u,
+                        n ? keyr[0] : 0u, ctx->grid.cx0, gyz(ctx));
+        }
+    for (uint32_t k = 0; k <= ncells; ++k)
+        if (cs[k] > cs[k + 1] || (k == ncells && cs[k] != h.n))
+            return fail(ctx, SPH_ERR_STATE, "validate(movers) rank %d: old cell starts broken at %u (%u %u, n %u)", R.rank,
+                        k, cs[k], cs[k + 1], h.n);
+    auto ask = [&](uint32_t x) { return (x < h.nl || x >= h.nl + h.no) ? skr[x] : sko[x - h.nl]; };
+    auto akey = [&](uint32_t x) { return (x < h.nl || x >= h.nl + h.no) ? keyr[x] : keyo[x - h.nl]; };
+    uint32_t moved = 0;
+    for (uint32_t x = 0; x < n; ++x) {
+        const uint32_t k = ask(x);
+        if (k >= ncells || (x && ask(x - 1) > k) || x < cs[k] || x >= cs[k + 1])
+            return fail(ctx, SPH_ERR_STATE, "validate(movers) rank %d: old key %u of slot %u (prev %u) vs cs %u %u; nl %u no %u n %u",
+                        R.rank, k, x, x ? ask(x - 1) : 0u, k < ncells ? cs[k] : 0u, k < ncells ? cs[k + 1] : 0u, h.nl, h.no, n);
+        moved += akey(x) != k;
+    }
+    if (moved != m)
+        return fail(ctx, SPH_ERR_STATE, "validate(movers) rank %d: %u slots changed key, %u movers listed", R.rank, moved, m);
+    for (uint32_t r = 0; r < m; ++r) {
+        const uint32_t x = by_slot[r].slot;
+        if (ask(x) != by_slot[r].mo)
+            return fail(ctx, SPH_ERR_STATE, "validate(movers) rank %d: mover slot %u old key %u, slot holds %u", R.rank, x,
+                        by_slot[r].mo, ask(x));
+    }
+    return SPH_OK;
+}
+
 // ---------------------------------------------------------------- phase A: counts and messages
 int phase_count(RankState& R) {
     sph_ctx* ctx = R.c;
@@ -453,6 +543,10 @@ int phase_assemble(RankState& R, bool exact) {
             launch_slab_cs_old(ctx->cs, ctx->grid.ncells, gyz(ctx), (uint32_t)ctx->grid.gx, ctx->has_left,
                                ctx->has_right, 0, ctx->keys2, 0, 0, 0, s, R.dz);
         CKPT(R, "cs_old");
+        if (ctx->cfg.flags & SPH_FLAG_VALIDATE) {
+            int r = validate_movers(R, used);
+            if (r != SPH_OK) return r;
+        }
         const int32_t lc_lo = ctx->sl.cx_lo - ctx->grid.cx0, lc_hi = ctx->sl.cx_hi - ctx->grid.cx0;
         CsPick pick{{col_start(ctx, 0), col_start(ctx, lc_lo), col_start(ctx, lc_lo + 1), col_start(ctx, lc_hi - 1),
                      col_start(ctx, lc_hi), col_start(ctx, ctx->grid.gx)},
@@ -661,7 +755,9 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
         int r = rebalance(M, pctx);
         if (r != SPH_OK) return r;
     }
-    const bool exact = M.ranks[0].since_cut < 2;   // the same on every rank
+    // exact sizes for three steps after a cut: the lagged counts of step s come from step s - 2, and the
+    // first step after a re-cut carries the migration to the new cut, not the new steady halo
+    const bool exact = M.ranks[0].since_cut < 3;   // the same on every rank
     int r;
     for (auto& R : M.ranks)
         if ((r = phase_count(R)) != SPH_OK) return r;
@@ -824,6 +920,16 @@ int multi_step(sph_ctx* ctx, float dt, int32_t nsteps) {
             if (r != SPH_OK) return r;
         }
         int r = multi_one_step(M, ctx, dt);
+        static const bool trace = std::getenv("SPH_TRACE_LAG") != nullptr;
+        if (r == SPH_OK && trace && (ctx->cfg.flags & SPH_FLAG_VALIDATE))
+            for (auto& R : M.ranks) {
+                (void)hipStreamSynchronize(R.c->stream);
+                const uint32_t* L = R.lag + ((M.steps - 1) % LAG_SLOTS) * LAG_WORDS;
+                std::fprintf(stderr, "[lag] step %lld rank %d: sent %u %u recv %u %u rho sent %u %u recv %u %u n %u flags %u | "
+                             "c1o %d %d c1i %d %d n_ub %lld since_cut %lld\n", (long long)(M.steps - 1), R.rank, L[0], L[1],
+                             L[2], L[3], L[4], L[5], L[6], L[7], L[8], L[9], R.c1o[0], R.c1o[1], R.c1i[0], R.c1i[1],
+                             (long long)R.n_ub, (long long)R.since_cut);
+            }
         if (r != SPH_OK) {
             if (M.mode == 1)   // a slab context's message on the group
                 for (auto& R : M.ranks)

@@ -324,7 +324,11 @@ __global__ __launch_bounds__(MV_BLK) void k_slab_rec(AsmSrc src, int32_t n, Grid
         const bool left = xs[j] < src.nl;
         kn[j] = window_key(g, pv[j].x, pv[j].y, pv[j].z);
         if (og[j] == REC_NO_KEY) ko[j] = left ? 0u : g.ncells - 1u;
-        else ko[j] = og[j] < key_base ? 0u : min(og[j] - key_base, g.ncells - 1u);
+        else {   // clamp og - key_base into [0, ncells - 1] in 64-bit (the u32 form `og < base ? 0 : min(og - base,
+                 // ncells - 1)` compiled to a plain subtract + min on ROCm 7.2, so keys below the window wrapped)
+            const int64_t d = (int64_t)og[j] - (int64_t)key_base;
+            ko[j] = (uint32_t)(d < 0 ? 0 : (d > (int64_t)g.ncells - 1 ? (int64_t)g.ncells - 1 : d));
+        }
         if (r0 + j * MV_BLK < nrec) {
             keyr[xs[j]] = kn[j];
             skr[xs[j]] = ko[j];

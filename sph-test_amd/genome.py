@@ -167,6 +167,32 @@ def rotate(q, v):
     return (v + w * t + np.cross(u, t)).astype(f32)
 
 
+def q_inverse(q):
+    """Quaternion.Inverse of a rotation: the conjugate (Unity's native code is closed; rotations are unit)."""
+    x, y, z, w = (f32(v) for v in q)
+    return np.array([-x, -y, -z, w], f32)
+
+
+def normalized(v):
+    """Vector3.normalized: v / |v| when |v| > 1e-5, else zero."""
+    v = np.asarray(v, f32)
+    m = f32(math.sqrt(float(np.dot(v, v).astype(f32))))
+    return (v / m).astype(f32) if m > f32(1e-5) else np.zeros(3, f32)
+
+
+def dot(a, b):
+    """Vector3.Dot in float32."""
+    a = np.asarray(a, f32)
+    b = np.asarray(b, f32)
+    return f32(a[0] * b[0] + a[1] * b[1] + a[2] * b[2])
+
+
+def distance(a, b):
+    """Vector3.Distance."""
+    d = (np.asarray(a, f32) - np.asarray(b, f32)).astype(f32)
+    return f32(math.sqrt(float(dot(d, d))))
+
+
 def _axis_angle(axis, deg):
     h = math.radians(float(deg)) * 0.5
     s = math.sin(h)

@@ -21,6 +21,7 @@ backend over gloo to check the decomposition against the single-domain oracle.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 from typing import List, Optional, Tuple
 
@@ -114,6 +115,14 @@ class GpuSlabBackend:
         self.torch = torch
         self.device = torch.device("cuda", device)
         self.ctx = Context(A.SPH_MODEL_WCSPH, sc.dim, capacity, device=device, profile=profile)
+        # the counts, records and ρ halos the library writes are handed to torch p2p / .cpu(): the library
+        # and torch share one stream by default (torch's current one; a new one if that is the legacy
+        # null stream, which sph_set_stream cannot name). SlabRunner.step runs on it; bind_stream rebinds.
+        cur = torch.cuda.current_stream(self.device)
+        if cur.cuda_stream == 0:
+            cur = torch.cuda.Stream(self.device)
+        self.stream = cur
+        self.ctx.set_stream(cur.cuda_stream)
         self.ctx.set_params(params)
         L, h = self.ctx._L, self.ctx.handle
         A.check("sph_slab_set", L.sph_slab_set(h, C.byref(A.SphSlab(cut[0], cut[1]))), h)
@@ -125,6 +134,7 @@ class GpuSlabBackend:
 
     def bind_stream(self, handle: int) -> None:
         self.ctx.set_stream(handle)
+        self.stream = self.torch.cuda.ExternalStream(handle, device=self.device)
 
     def empty(self, n: int, width: int):
         return self.torch.empty((max(n, 1), width), dtype=self.torch.float32, device=self.device)
@@ -286,11 +296,13 @@ class SlabRunner:
 
     # ----------------------------------------------------------------- step
     def step(self, k: int = 1) -> None:
-        for _ in range(k):
-            if self.rebalance_every and self.steps_done and self.steps_done % self.rebalance_every == 0:
-                self._rebalance()
-            self._one_step()
-            self.steps_done += 1
+        stream = getattr(self.be, "stream", None)   # torch work of the step on the library's stream
+        with self.torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            for _ in range(k):
+                if self.rebalance_every and self.steps_done and self.steps_done % self.rebalance_every == 0:
+                    self._rebalance()
+                self._one_step()
+                self.steps_done += 1
 
     def _rebalance(self) -> None:
         """All-reduce the per-column owned counts, move the cuts (identically on every rank), and

@@ -21,10 +21,14 @@ def shipped_genome(pkg):
     return g
 
 
-def shipped_controller(pkg, device=0):
-    ctl = pkg.ParticleSystemController(particleCount=SCENE_CONTROLLER["particleCount"], device=device)
+def shipped_controller(pkg, device=0, backend=None, bonds=False):
+    """The scene's controller; bonds=True also attaches the CellAdhesionManager mirror (the scene's
+    manager object, `Particle Simulation.unity`), so divisions create the genome's bonds."""
+    ctl = pkg.ParticleSystemController(particleCount=SCENE_CONTROLLER["particleCount"], device=device, backend=backend)
     for k, v in SCENE_CONTROLLER.items():
         if k != "particleCount":
             setattr(ctl, k, float(v))
     ctl.genome = shipped_genome(pkg)
+    if bonds:
+        ctl.adhesionManager = pkg.CellAdhesionManager(ctl)
     return ctl
