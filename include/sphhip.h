@@ -239,8 +239,14 @@ int sph_read_torque_int(sph_ctx* ctx, int32_t* xyz, int32_t count);  /* Model R,
 /* Model S neighbour passes: how often a workgroup left the LDS-staged fast path since the last
  * reset (sparse or splashing regions): [0] density planes processed row by row in chunks, [1] density
  * rows gathered straight from global memory, [2] / [3] the same for the force pass. reset != 0
- * zeroes them after the read. */
+ * zeroes them after the read. The passes count only after the first call of this function or of
+ * sph_read_hit_mask_counts on the context (counting costs atomics on one address). */
 int sph_read_path_counts(sph_ctx* ctx, uint32_t counts[4], int32_t reset);
+/* Model S pass 2 takes its hits from pass 1's hit mask (8 words = 256 candidates per target):
+ * [0] wave-planes (one wave, one dx plane) that scanned by distance instead, because a lane's
+ * candidates passed the mask or the plane took a sparse path, [1] waves run (3 planes each).
+ * reset != 0 zeroes them after the read. */
+int sph_read_hit_mask_counts(sph_ctx* ctx, uint32_t counts[2], int32_t reset);
 /* stable LSD radix sort of (key, index) on the device: the sort of the step, exposed for
  * bit-exact parity tests. perm[i] = source index of sorted slot i. */
 int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int32_t key_bits,

@@ -233,6 +233,13 @@ class Context:
         self._chk("sph_read_path_counts", self._L.sph_read_path_counts(self._h, A.ptr(out), 1 if reset else 0))
         return out
 
+    def hit_mask_counts(self, reset: bool = True) -> np.ndarray:
+        """(wave-planes of the force pass scanned by distance instead of the hit mask, waves run)
+        (sph_read_hit_mask_counts)."""
+        out = np.zeros(2, np.uint32)
+        self._chk("sph_read_hit_mask_counts", self._L.sph_read_hit_mask_counts(self._h, A.ptr(out), 1 if reset else 0))
+        return out
+
     def radix_sort(self, keys: np.ndarray, key_bits: int):
         keys = np.ascontiguousarray(keys, dtype=np.uint32)
         perm = np.empty_like(keys)

@@ -751,23 +751,38 @@ int sph_read_cell_start(sph_ctx* ctx, uint32_t* cs, int32_t count) {
     return SPH_OK;
 }
 
-int sph_read_path_counts(sph_ctx* ctx, uint32_t counts[4], int32_t reset) {
-    if (!ctx || !counts) return SPH_ERR_INVALID;
-    const std::vector<sph_ctx*> kids = multi_kids(ctx);
+}  // extern "C"
+
+// counters [first, first + m) of ctx->paths (summed over a local group's slab contexts)
+static int read_paths(sph_ctx* ctx, int first, int m, uint32_t* counts, int32_t reset) {
+    const std::vector<sph_ctx*> kids = sph::multi_kids(ctx);
     if (!kids.empty()) {
-        for (int k = 0; k < 4; ++k) counts[k] = 0;
+        for (int k = 0; k < m; ++k) counts[k] = 0;
         for (sph_ctx* kc : kids) {
-            uint32_t c[4];
-            if (int r = sph_read_path_counts(kc, c, reset)) return r;
-            for (int k = 0; k < 4; ++k) counts[k] += c[k];
+            uint32_t c[8];
+            if (int r = read_paths(kc, first, m, c, reset)) return r;
+            for (int k = 0; k < m; ++k) counts[k] += c[k];
         }
         return SPH_OK;
     }
+    ctx->count_paths = true;   // from now on the neighbour passes count
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipMemcpyAsync(counts, ctx->paths, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-    if (reset) HIPCHK(hipMemsetAsync(ctx->paths, 0, 4 * sizeof(uint32_t), ctx->stream));
+    HIPCHK(hipMemcpyAsync(counts, ctx->paths + first, m * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    if (reset) HIPCHK(hipMemsetAsync(ctx->paths + first, 0, m * sizeof(uint32_t), ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return SPH_OK;
+}
+
+extern "C" {
+
+int sph_read_path_counts(sph_ctx* ctx, uint32_t counts[4], int32_t reset) {
+    if (!ctx || !counts) return SPH_ERR_INVALID;
+    return read_paths(ctx, 0, 4, counts, reset);
+}
+
+int sph_read_hit_mask_counts(sph_ctx* ctx, uint32_t counts[2], int32_t reset) {
+    if (!ctx || !counts) return SPH_ERR_INVALID;
+    return read_paths(ctx, 4, 2, counts, reset);
 }
 
 int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int32_t key_bits, uint32_t* perm_out,

@@ -591,7 +591,7 @@ int phase_assemble(RankState& R, bool exact) {
     CKPT(R, "ranges");
     {
         KTimer t(ctx, "density", 24.0 * (double)R.n_ub);
-        launch_density_tiled(ctx->pos, ctx->cs, 0, (int32_t)R.n_ub, ctx->grid, ctx->sc, ctx->rp, ctx->paths, s,
+        launch_density_tiled(ctx->pos, ctx->cs, 0, (int32_t)R.n_ub, ctx->grid, ctx->sc, ctx->rp, hit_mask(ctx), path_ctr(ctx), s,
                              DevRange{&R.dz->rg[2], &R.dz->rg[3]});
     }
     CKPT(R, "density");
@@ -633,7 +633,7 @@ void force_dev(sph_ctx* ctx, const uint32_t* lo, const uint32_t* hi, int64_t gri
     MoverSink mv = mover_sink(ctx);
     mv.err = &ctx->dz->flags;
     launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, (int32_t)grid_ub, ctx->grid, ctx->sc, dt, forcing(ctx),
-                       ctx->pos2, ctx->vel2, ctx->keys, mv, ctx->paths, ctx->stream, DevRange{lo, hi});
+                       ctx->pos2, ctx->vel2, ctx->keys, mv, hit_mask(ctx), path_ctr(ctx), ctx->stream, DevRange{lo, hi});
 }
 
 int phase_interior(RankState& R, float dt) {

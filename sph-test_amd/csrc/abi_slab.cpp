@@ -349,7 +349,7 @@ int sph_slab_density(sph_ctx* ctx) {
     if (ctx->rng_pending) {   // owned range [sdev[1], sdev[4]) on the device; grid sized for all slots
         KTimer t(ctx, "density", 24.0 * ctx->n);
         const DevRange dr{ctx->sdev + 1, ctx->sdev + 4};
-        launch_density_tiled(ctx->pos, ctx->cs, 0, ctx->n, ctx->grid, ctx->sc, ctx->rp, ctx->paths, ctx->stream, dr);
+        launch_density_tiled(ctx->pos, ctx->cs, 0, ctx->n, ctx->grid, ctx->sc, ctx->rp, hit_mask(ctx), path_ctr(ctx), ctx->stream, dr);
         HIPCHK(hipGetLastError());
         return SPH_OK;
     }

@@ -321,14 +321,25 @@ void launch_lattice(int32_t dim, int32_t nx, int32_t ny, int32_t nz, float dx, f
                     hipStream_t s);
 void launch_iota(uint32_t* v, int32_t n, hipStream_t s);
 
-// Model S, LDS-tiled (wcsph_tiled.hip): targets are the sorted slots [ib, ie). paths: 4 sparse-path
-// counters (density chunked / global, force chunked / global), incremented once per block and event.
+// Model S, LDS-tiled (wcsph_tiled.hip): targets are the sorted slots [ib, ie). paths: 6 counters
+// (density planes chunked / rows gathered from global memory, the same for the force pass, force
+// planes scanned by distance because a target's candidates passed the hit mask, force blocks), once per
+// block and event.
+// The hit mask: pass 1 evaluates every candidate of a target's trimmed windows anyway, and writes
+// bit k = "candidate k of the visit order is within 2h" (HM_WORDS words per target, word-major: word w
+// of slot i at w[w * stride + i]). Pass 2 runs on the same positions and windows, so it reads its hits
+// from the mask instead of recomputing every candidate's distance.
+constexpr int HM_WORDS = 8;
+struct HitMask {
+    uint32_t* w = nullptr;   // HM_WORDS * stride words; nullptr: no mask (pass 2 scans by distance)
+    uint32_t stride = 0;
+};
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g,
-                          SphConst c, float2* rp, uint32_t* paths, hipStream_t s, DevRange dr = DevRange{});
+                          SphConst c, float2* rp, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr = DevRange{});
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs,
                         int32_t ib, int32_t ie, GridDesc g, SphConst c, float dt, float fext_x,
-                        float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv, uint32_t* paths, hipStream_t s,
-                        DevRange dr = DevRange{});
+                        float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths,
+                        hipStream_t s, DevRange dr = DevRange{});
 
 // slab decomposition (slab.hip)
 // Order-preserving compaction of the sorted slots [b, e) whose key column satisfies

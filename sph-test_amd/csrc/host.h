@@ -106,7 +106,9 @@ struct sph_ctx {
     std::vector<sph::Pending> pending;
     std::vector<hipEvent_t> ev_pool;
     int64_t device_bytes = 0;
-    uint32_t* paths = nullptr;   // [4] sparse-path counters of the neighbour passes (sph_read_path_counts)
+    uint32_t* paths = nullptr;   // [8] path counters of the neighbour passes (sph_read_path_counts, _mask_counts)
+    bool count_paths = false;    // armed by the first counter read: counted launches pay for atomics
+    uint32_t* hmask = nullptr;   // Model S: HM_WORDS x capacity hit-mask words (pass 1 -> pass 2)
     // slab decomposition (SPEC_SPH.md §3)
     bool slab = false;
     sph_slab sl{};
@@ -214,6 +216,8 @@ struct KTimer {
 // per-step launch sequences (host_step.cpp)
 void swap_sv(sph_ctx* c);
 int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id, const uint32_t** sorted_keys = nullptr);
+HitMask hit_mask(const sph_ctx* ctx);   // Model S pass 1 -> pass 2 (common.h)
+inline uint32_t* path_ctr(const sph_ctx* ctx) { return ctx->count_paths ? ctx->paths : nullptr; }
 void density_range(sph_ctx* ctx, int32_t b, int32_t e);
 void force_range(sph_ctx* ctx, int32_t b, int32_t e, float dt, float fext, MoverSink mv = MoverSink{});
 ResortScratch resort_scratch(sph_ctx* ctx);

@@ -11,7 +11,7 @@ void free_all(sph_ctx* c) {
     dfree(c->keys); dfree(c->keys2); dfree(c->vals); dfree(c->vals2); dfree(c->hist); dfree(c->bin_total);
     dfree(c->cs); dfree(c->gaps);
     c->gaps_cap = 0;
-    dfree(c->sblk); dfree(c->sdev); dfree(c->paths);
+    dfree(c->sblk); dfree(c->sdev); dfree(c->paths); dfree(c->hmask);
     dfree(c->sk_cur); dfree(c->sk_next);
     dfree(c->mv_mi); dfree(c->mv_mk); dfree(c->mv_mo); dfree(c->mv_rank); dfree(c->mv_mx); dfree(c->mv_mos);
     dfree(c->mv_ms); dfree(c->mv_count);
@@ -38,15 +38,16 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
     AL(id, n); AL(id2, n);
     AL(keys, n); AL(keys2, n); AL(vals, n); AL(vals2, n);
     AL(hist, radix_hist_elems((int32_t)n)); AL(bin_total, 256);
-    AL(sblk, 2 * (size_t)slab_compact_blocks(0, (int32_t)n) + 2); AL(sdev, 16); AL(paths, 4);
+    AL(sblk, 2 * (size_t)slab_compact_blocks(0, (int32_t)n) + 2); AL(sdev, 16); AL(paths, 8);
     HIPCHK(hipMemset(ctx->sdev, 0, 16 * sizeof(uint32_t)));
-    HIPCHK(hipMemset(ctx->paths, 0, 4 * sizeof(uint32_t)));
+    HIPCHK(hipMemset(ctx->paths, 0, 8 * sizeof(uint32_t)));
     ctx->gap_par = 0;
     if (is_contact(ctx)) {
         AL(omg, n); AL(rot, n); AL(aux, n); AL(omg2, n); AL(rot2, n); AL(aux2, n);
         AL(mode, n); AL(mode2, n); AL(torque, 3 * n); AL(slot_of, n);
     } else {
         AL(rp, n);
+        AL(hmask, (size_t)HM_WORDS * n);
     }
     // incremental re-sort (both models)
     AL(sk_cur, n); AL(sk_next, n);

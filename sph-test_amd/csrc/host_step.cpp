@@ -51,13 +51,22 @@ int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id, const uint32_t** sorted_
     return SPH_OK;
 }
 
+HitMask hit_mask(const sph_ctx* ctx) {
+#ifdef SPH_HM_OFF
+    (void)ctx;
+    return HitMask{};
+#else
+    return HitMask{ctx->hmask, (uint32_t)std::max(ctx->capacity, 1)};
+#endif
+}
+
 void density_range(sph_ctx* ctx, int32_t b, int32_t e) {
-    launch_density_tiled(ctx->pos, ctx->cs, b, e, ctx->grid, ctx->sc, ctx->rp, ctx->paths, ctx->stream);
+    launch_density_tiled(ctx->pos, ctx->cs, b, e, ctx->grid, ctx->sc, ctx->rp, hit_mask(ctx), path_ctr(ctx), ctx->stream);
 }
 
 void force_range(sph_ctx* ctx, int32_t b, int32_t e, float dt, float fext, MoverSink mv) {
     launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, b, e, ctx->grid, ctx->sc, dt, fext, ctx->pos2, ctx->vel2,
-                       ctx->keys, mv, ctx->paths, ctx->stream);
+                       ctx->keys, mv, hit_mask(ctx), path_ctr(ctx), ctx->stream);
 }
 
 // f_ext(t) of SPEC_SPH.md §2 at the context's simulated time (sloshing; 0 otherwise)

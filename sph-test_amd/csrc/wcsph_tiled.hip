@@ -16,6 +16,13 @@
 // A plane whose intervals exceed TT_GCAP candidates (sparse blocks spanning many rows) is
 // processed offset by offset in chunks, and an offset beyond TT_FALLBACK is gathered directly
 // from global memory.
+//
+// Hit mask (common.h HitMask): pass 1 computes every candidate's r² anyway; it also records
+// r² < 4h² as one bit per candidate, in visit order (the sign bit of r² − 4h²: exact). Pass 2 then
+// takes its hits from the mask (a bit reader and a find-first-set loop that appends only hits) instead
+// of re-reading every candidate from LDS and recomputing its distance. A target with more than
+// HM_WORDS·32 candidates, and the sparse paths, fall back to the distance scan for the plane in
+// question (wave-uniform); both give the same hits, so results do not depend on the path.
 #include "common.h"
 
 namespace sph {
@@ -84,7 +91,11 @@ __device__ __forceinline__ void lane_window(const GridDesc& g, const uint32_t* _
 // Sparse-path counters (tests: sph_read_path_counts): [0] density planes chunked, [1] density rows
 // gathered from global memory, [2] / [3] the same for the force pass. One atomic per block and event.
 __device__ __forceinline__ void count_path(uint32_t* paths, int k) {
-    if (threadIdx.x == 0) atomicAdd(paths + k, 1u);
+    if (paths && threadIdx.x == 0) atomicAdd(paths + k, 1u);
+}
+// per wave; paths is null unless a test armed the counters (one address: contended atomics)
+__device__ __forceinline__ void count_wave(uint32_t* paths, int k) {
+    if (paths && lane_id() == 0) atomicAdd(paths + k, 1u);
 }
 
 __device__ __forceinline__ float dist2(float4 a, float4 b) {
@@ -162,7 +173,7 @@ __device__ __forceinline__ int32_t quadrant_target(const GridDesc& g, const floa
 __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restrict__ pos,
                                                           const uint32_t* __restrict__ cs, int32_t ib, int32_t n,
                                                           GridDesc g, SphConst c, float2* __restrict__ rp,
-                                                          DevRange dr, uint32_t* __restrict__ paths) {
+                                                          DevRange dr, HitMask hm, uint32_t* __restrict__ paths) {
     __shared__ float4 sp[TT_GCAP + 4];
     __shared__ int32_t perm[TT_BLK];
     __shared__ uint32_t qcnt[TT_BLK / 64][5];
@@ -178,17 +189,42 @@ __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restri
     const float4 pi = pos[valid ? i : ilast];
     const BlockRows b = block_rows(g, pos, i0, ilast, pi);
     float s = 0.0f;
+    // hit-mask writer: the newest bit enters at bit 63, so after m bits the oldest unwritten one sits
+    // at 64 − m; a word leaves once 32 are pending
+    uint64_t mb = 0;
+    int32_t mn = 0, mw = 0;
+    const bool rec = valid && hm.w != nullptr;
+    auto bit = [&](float r2) {
+        mb = (mb >> 1) | ((uint64_t)(__float_as_uint(r2 - c.four_h2) & 0x80000000u) << 32);
+    };
+    auto emit = [&]() {
+        if (mn >= 32) {
+            if (rec && mw < HM_WORDS) hm.w[(size_t)mw * hm.stride + i] = (uint32_t)(mb >> (64 - mn));
+            ++mw;
+            mn -= 32;
+        }
+    };
     auto scan = [&](int32_t lo, int32_t ln) {
         int32_t t = 0;
         for (; t + 4 <= ln; t += 4) {
             const float4 a = sp[lo + t], bb = sp[lo + t + 1], cc = sp[lo + t + 2], d = sp[lo + t + 3];
-            s += spline_w4(c, dist2(pi, a));
-            s += spline_w4(c, dist2(pi, bb));
-            s += spline_w4(c, dist2(pi, cc));
-            s += spline_w4(c, dist2(pi, d));
+            const float ra = dist2(pi, a), rb = dist2(pi, bb), rc = dist2(pi, cc), rd = dist2(pi, d);
+            s += spline_w4(c, ra);
+            s += spline_w4(c, rb);
+            s += spline_w4(c, rc);
+            s += spline_w4(c, rd);
+            bit(ra); bit(rb); bit(rc); bit(rd);
+            mn += 4;
+            emit();
             keep_b128(a, bb, cc, d);
         }
-        for (; t < ln; ++t) s += spline_w4(c, dist2(pi, sp[lo + t]));
+        for (; t < ln; ++t) {
+            const float r2 = dist2(pi, sp[lo + t]);
+            s += spline_w4(c, r2);
+            bit(r2);
+            ++mn;
+            emit();
+        }
     };
 #pragma unroll 1
     for (int p = 0; p < 3; ++p) {
@@ -218,7 +254,13 @@ __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restri
         for (int r = 0; r < 3; ++r) {
             if (len[r] > TT_FALLBACK) {
                 count_path(paths, 1);
-                for (int32_t j = r0[r]; j < r1[r]; ++j) s += spline_w4(c, dist2(pi, pos[j]));
+                for (int32_t j = r0[r]; j < r1[r]; ++j) {
+                    const float r2 = dist2(pi, pos[j]);
+                    s += spline_w4(c, r2);
+                    bit(r2);
+                    ++mn;
+                    emit();
+                }
                 continue;
             }
 #pragma unroll 1
@@ -233,6 +275,8 @@ __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restri
         }
     }
     if (!valid) return;
+    if (rec && mn > 0 && mw < HM_WORDS)   // the last, partial word (its bits above mn are stale)
+        hm.w[(size_t)mw * hm.stride + i] = (uint32_t)(mb >> (64 - mn)) & ((1u << mn) - 1u);
     const float d = c.mass * (c.sigma * (0.25f * s));
     const float tr = d * c.inv_rho0;
     const float t2 = tr * tr, t4 = t2 * t2;
@@ -292,11 +336,18 @@ __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi,
     a.sx -= cx * du; a.sy -= cx * dv; a.sz -= cx * dw;
 }
 
+#ifndef SPH_HM_READER
+#define SPH_HM_READER 0
+#endif
+#if SPH_FORCE_WPE
+__global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_FORCE_WPE))) void k_force_tiled(
+#else
 __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
+#endif
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
     const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, PairK pk, float dt,
     float fext_x, float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o, MoverSink mv,
-    uint32_t* __restrict__ paths, DevRange dr) {
+    HitMask hm, uint32_t* __restrict__ paths, DevRange dr) {
     __shared__ float4 sp[TF_GCAP + 4];     // (x, y, z, ρ)
     __shared__ float4 sv[TF_GCAP + 4];     // (u, v, w, P/ρ²)
     __shared__ uint16_t lst[TT_CAP][TT_BLK];
@@ -328,6 +379,72 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
             }
         }
         cnt = 0;
+    };
+    // hit-mask reader (pass 1's bits of this target, in visit order): rb holds rn bits, LSB next;
+    // the remaining words wait in a queue of registers (static indices only)
+#if SPH_HM_READER == 1
+    const uint32_t* hmw = hm.w ? hm.w + ii : nullptr;   // word w of this target at hmw[w * stride]
+    uint64_t rb = 0;
+    uint32_t nxt = 0;
+    int32_t rn = 64, wi = 3, kb = 0;   // kb: candidates of this target so far
+    if (valid && hmw) {
+        rb = (uint64_t)hmw[0] | ((uint64_t)hmw[hm.stride] << 32);
+        nxt = hmw[2 * (size_t)hm.stride];
+    }
+    auto take = [&](int32_t len) -> uint32_t {   // the next len (0..32) bits
+        const uint32_t v = (uint32_t)rb & (len >= 32 ? 0xffffffffu : ((1u << len) - 1u));
+        rb >>= len;
+        rn -= len;
+        if (rn <= 32) {   // the prefetched word joins; the one after it is fetched now
+            rb |= (uint64_t)nxt << rn;
+            rn += 32;
+            nxt = (valid && hmw && wi < HM_WORDS) ? hmw[(size_t)wi * hm.stride] : 0u;
+            ++wi;
+        }
+        return v;
+    };
+#else
+    uint32_t q[HM_WORDS];
+#pragma unroll
+    for (int w = 0; w < HM_WORDS; ++w) q[w] = (valid && hm.w) ? hm.w[(size_t)w * hm.stride + i] : 0u;
+    uint64_t rb = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
+    int32_t rn = 64, kb = 0;   // kb: candidates of this target so far (the bit index of the next window)
+    auto take = [&](int32_t len) -> uint32_t {   // the next len (0..32) bits
+        const uint32_t v = (uint32_t)rb & (len >= 32 ? 0xffffffffu : ((1u << len) - 1u));
+        rb >>= len;
+        rn -= len;
+        if (rn <= 32) {
+            rb |= (uint64_t)q[2] << rn;
+            rn += 32;
+#pragma unroll
+            for (int w = 2; w + 1 < HM_WORDS; ++w) q[w] = q[w + 1];
+            q[HM_WORDS - 1] = 0u;
+        }
+        return v;
+    };
+#endif
+    // the hits of LDS slots [lo, lo+ln) from the mask, 16 candidates at a time: at most 16 hits, so
+    // one list check per piece; then two hits per iteration with unconditional stores (a lane out of
+    // hits stores to its next free entry without advancing, as the distance scan does)
+    auto hits = [&](int32_t lo, int32_t ln) {
+        for (int32_t off = 0; __any(off < ln); off += 16) {
+            uint32_t m = take(max(0, min(16, ln - off)));
+            if (__any(cnt + (int)__popc(m) > TT_CAP)) flush();
+            const uint32_t base = (uint32_t)(lo + off) * 16u;
+            while (__any(m != 0u)) {
+                const int c0i = min(cnt, TT_CAP - 1);
+                lst[c0i][tid] = (uint16_t)(base + 16u * (uint32_t)__builtin_ctz(m | 0x10000u));
+                cnt += m != 0u;
+                m &= m - 1u;
+                const int c1i = min(cnt, TT_CAP - 1);
+                lst[c1i][tid] = (uint16_t)(base + 16u * (uint32_t)__builtin_ctz(m | 0x10000u));
+                cnt += m != 0u;
+                m &= m - 1u;
+            }
+        }
+    };
+    auto skip = [&](int32_t ln) {
+        for (int32_t off = 0; __any(off < ln); off += 32) (void)take(max(0, min(32, ln - off)));
     };
     // scan LDS slots [lo, lo+ln), appending hits
     auto scan = [&](int32_t lo, int32_t ln) {
@@ -366,6 +483,14 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
             lane_window(g, cs, b, valid, 3 * p + r, r0[r], r1[r]);
         }
         const int32_t total = len[0] + len[1] + len[2];
+        const int32_t plen = (r1[0] - r0[0]) + (r1[1] - r0[1]) + (r1[2] - r0[2]);
+        // the mask covers this plane for every lane of the wave (wave-uniform)
+        const bool by_mask = hm.w != nullptr && !__any(kb + plen > HM_WORDS * 32);
+        kb += plen;
+        if (hm.w != nullptr && !by_mask) {   // this plane scans by distance: its bits are passed over
+            count_wave(paths, 4);
+            skip(plen);
+        }
         if (total <= TF_GCAP) {
             __syncthreads();
             stage_plane(c0, len, total, put);
@@ -373,18 +498,23 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
             int32_t o = 0;
 #pragma unroll
             for (int r = 0; r < 3; ++r) {
-                scan(o + (r0[r] - c0[r]), r1[r] - r0[r]);
+                if (by_mask)
+                    hits(o + (r0[r] - c0[r]), r1[r] - r0[r]);
+                else
+                    scan(o + (r0[r] - c0[r]), r1[r] - r0[r]);
                 o += len[r];
             }
             flush();
             continue;
         }
-        // sparse block: offset by offset, in chunks, or straight from global memory
+        // sparse block: offset by offset, in chunks (the chunks of a row take its bits in order), or
+        // straight from global memory
         count_path(paths, 2);
 #pragma unroll 1
         for (int r = 0; r < 3; ++r) {
             if (len[r] > TF_FALLBACK) {
                 count_path(paths, 3);
+                if (by_mask) skip(r1[r] - r0[r]);
                 for (int32_t j = r0[r]; j < r1[r]; ++j) {
                     const float4 pj = pos[j];
                     if (j != i && dist2(pi, pj) < c.four_h2) {
@@ -403,11 +533,16 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
                 for (int32_t t = tid; t < ln; t += TT_BLK) put(t, base + t);
                 __syncthreads();
                 const int32_t lo = max(r0[r], base) - base;
-                scan(lo, max(min(r1[r], base + ln) - base - lo, 0));
+                const int32_t wl = max(min(r1[r], base + ln) - base - lo, 0);
+                if (by_mask)
+                    hits(lo, wl);
+                else
+                    scan(lo, wl);
                 flush();
             }
         }
     }
+    count_wave(paths, 5);   // waves (3 planes each)
     if (!valid) return;
     float nv[3] = {vi.x + (acc.ax + c.gx + fext_x) * dt, vi.y + (acc.ay + c.gy) * dt, vi.z + (acc.az + c.gz) * dt};
     float np[3] = {pi.x + (nv[0] + acc.sx) * dt, pi.y + (nv[1] + acc.sy) * dt, pi.z + (nv[2] + acc.sz) * dt};
@@ -428,16 +563,17 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
 
 // dr set: [ib, ie) only sizes the grid (an upper bound); the kernels read their bounds from dr
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
-                          float2* rp, uint32_t* paths, hipStream_t s, DevRange dr) {
-    if (ie > ib) k_density_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, cs, ib, ie, g, c, rp, dr, paths);
+                          float2* rp, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr) {
+    if (ie > ib)
+        k_density_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, cs, ib, ie, g, c, rp, dr, hm, paths);
 }
 
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,
                         int32_t ie, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o,
-                        uint32_t* keys_o, MoverSink mv, uint32_t* paths, hipStream_t s, DevRange dr) {
+                        uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr) {
     if (ie > ib)
         k_force_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt, fext_x,
-                                                                         pos_o, vel_o, keys_o, mv, paths, dr);
+                                                                         pos_o, vel_o, keys_o, mv, hm, paths, dr);
 }
 
 }  // namespace sph
