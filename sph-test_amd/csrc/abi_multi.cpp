@@ -517,8 +517,10 @@ int phase_assemble(RankState& R, bool exact) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
-    launch_slab_sizes(R.dz, R.left >= 0 ? R.msg_in[0] : nullptr, R.right >= 0 ? R.msg_in[1] : nullptr, R.c1i[0],
-                      R.c1i[1], ctx->capacity, s);
+    // the layout [left | own | right] from the message headers: in k_slab_rec on device-sized steps
+    // (a rank without neighbours has it from the previous step's k_slab_lag), k_slab_sizes otherwise
+    const SizesIn sizes{R.left >= 0 ? R.msg_in[0] : nullptr, R.right >= 0 ? R.msg_in[1] : nullptr, R.c1i[0], R.c1i[1],
+                        ctx->capacity};
     R.n_ub = std::min<int64_t>(R.c1i[0] + R.n_prev_ub + R.c1i[1], ctx->capacity);
     const bool many = ctx->resort_mode == 1 && *(volatile uint32_t*)ctx->mv_host > resort_limit((int32_t)R.n_ub);
     if (ctx->resort_mode != 0 && !many && ctx->sk_valid && R.n_ub > 0) {
@@ -532,12 +534,12 @@ int phase_assemble(RankState& R, bool exact) {
         const MoverSink mv{ctx->keys2, ctx->mv_count + used, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_rank,
                            (uint32_t)std::max(ctx->capacity, 1), &R.dz->flags};
         const uint32_t key_base = (uint32_t)ctx->grid.cx0 * gyz(ctx);
-        CKPT(R, "exchange 1 + sizes");
-        if (nl_ub + nr_ub > 0) {
+        CKPT(R, "exchange 1");
+        if (nl_ub + nr_ub > 0) {   // every rank with a neighbour (capacities are >= 512)
             KTimer t(ctx, "slab_assemble", 40.0 * (double)(nl_ub + nr_ub));
-            launch_slab_rec(src, n_ub, ctx->grid, key_base, ctx->vals, ctx->keys2, mv, s);  // grid: nl_ub + nr_ub
+            launch_slab_rec(src, n_ub, ctx->grid, key_base, ctx->vals, ctx->keys2, mv, s, &sizes);  // grid: nl_ub + nr_ub
         }
-        CKPT(R, "slab_rec");
+        CKPT(R, "sizes + slab_rec");
         KTimer t(ctx, "resort", (double)R.n_ub * (2 * 4 + 2 * 36));
         if (ctx->has_left || ctx->has_right)   // without neighbours the own block keeps its cell starts
             launch_slab_cs_old(ctx->cs, ctx->grid.ncells, gyz(ctx), (uint32_t)ctx->grid.gx, ctx->has_left,
@@ -568,6 +570,7 @@ int phase_assemble(RankState& R, bool exact) {
         ctx->n = n_ub;
     } else {
         // the full radix sort: host-sized (after a re-cut, or while many particles move)
+        launch_slab_sizes(R.dz, sizes.hl, sizes.hr, sizes.cap_l, sizes.cap_r, sizes.capacity, s);
         HIPCHK(hipStreamSynchronize(s));
         SlabSizes h;
         HIPCHK(hipMemcpy(&h, R.dz, sizeof h, hipMemcpyDeviceToHost));
@@ -587,22 +590,21 @@ int phase_assemble(RankState& R, bool exact) {
         HIPCHK(hipStreamSynchronize(s));   // nn lives on this stack frame
         R.n_ub = ctx->n;
     }
-    launch_slab_ranges(R.dz, ctx->has_left ? 1 : 0, ctx->has_right ? 1 : 0, s);
-    CKPT(R, "ranges");
-    {
+    {   // the owned slots of the new order: the column starts the re-sort picked (k_slab_lag copies the
+        // ranges for the host at the end of the step)
         KTimer t(ctx, "density", 24.0 * (double)R.n_ub);
         launch_density_tiled(ctx->pos, ctx->cs, 0, (int32_t)R.n_ub, ctx->grid, ctx->sc, ctx->rp, hit_mask(ctx), path_ctr(ctx), s,
-                             DevRange{&R.dz->rg[2], &R.dz->rg[3]});
+                             DevRange{&R.dz->pick[1], &R.dz->pick[4]});
     }
     CKPT(R, "density");
     if (exact && (R.left >= 0 || R.right >= 0)) {   // exact ρ message sizes: this rank's own columns
         HIPCHK(hipStreamSynchronize(s));
         SlabSizes h;
         HIPCHK(hipMemcpy(&h, R.dz, sizeof h, hipMemcpyDeviceToHost));
-        R.c2o[0] = R.left >= 0 ? (int32_t)(h.rg[7] - h.rg[6]) : 0;
-        R.c2o[1] = R.right >= 0 ? (int32_t)(h.rg[9] - h.rg[8]) : 0;
-        R.c2i[0] = R.left >= 0 ? (int32_t)(h.rg[1] - h.rg[0]) : 0;
-        R.c2i[1] = R.right >= 0 ? (int32_t)(h.rg[5] - h.rg[4]) : 0;
+        R.c2o[0] = R.left >= 0 ? (int32_t)(h.pick[2] - h.pick[1]) : 0;
+        R.c2o[1] = R.right >= 0 ? (int32_t)(h.pick[4] - h.pick[3]) : 0;
+        R.c2i[0] = R.left >= 0 ? (int32_t)(h.pick[1] - h.pick[0]) : 0;
+        R.c2i[1] = R.right >= 0 ? (int32_t)(h.pick[5] - h.pick[4]) : 0;
     }
     return SPH_OK;
 }
@@ -639,7 +641,10 @@ void force_dev(sph_ctx* ctx, const uint32_t* lo, const uint32_t* hi, int64_t gri
 int phase_interior(RankState& R, float dt) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
-    force_dev(ctx, &R.dz->fr[0], &R.dz->fr[1], R.n_ub, dt);
+    // interior columns: [pick[2] or pick[1], pick[3] or pick[4]) (empty when a one-column slab has both
+    // neighbours: then the bound is below the start and every workgroup exits)
+    const uint32_t* pk = R.dz->pick;
+    force_dev(ctx, ctx->has_left ? &pk[2] : &pk[1], ctx->has_right ? &pk[3] : &pk[4], R.n_ub, dt);
     CKPT(R, "interior force");
     return SPH_OK;
 }
@@ -654,11 +659,12 @@ int phase_finish(RankState& R, float dt, int64_t step) {
         if ((side == 0 ? R.left : R.right) >= 0) launch_slab_unpack_rho(ctx->rp, R.dz, side, R.rho_in[side], R.c2i[side], s);
     CKPT(R, "rho unpack");
     const bool one_col = ctx->sl.cx_hi - ctx->sl.cx_lo == 1;
-    if (one_col && (ctx->has_left || ctx->has_right)) {
-        force_dev(ctx, &R.dz->fr[2], &R.dz->fr[3], R.n_ub, dt);
+    const uint32_t* pk = R.dz->pick;
+    if (one_col && (ctx->has_left || ctx->has_right)) {   // the owned column is both boundary columns
+        force_dev(ctx, &pk[1], &pk[4], R.n_ub, dt);
     } else {
-        if (ctx->has_left) force_dev(ctx, &R.dz->fr[2], &R.dz->fr[3], std::min<int64_t>(R.c2o[0], R.n_ub), dt);
-        if (ctx->has_right) force_dev(ctx, &R.dz->fr[4], &R.dz->fr[5], std::min<int64_t>(R.c2o[1], R.n_ub), dt);
+        if (ctx->has_left) force_dev(ctx, &pk[1], &pk[2], std::min<int64_t>(R.c2o[0], R.n_ub), dt);
+        if (ctx->has_right) force_dev(ctx, &pk[3], &pk[4], std::min<int64_t>(R.c2o[1], R.n_ub), dt);
     }
     CKPT(R, "boundary force");
     swap_sv(ctx);
@@ -666,7 +672,8 @@ int phase_finish(RankState& R, float dt, int64_t step) {
     ctx->steps++;
     ctx->sim_time += (double)dt;
     const int k = (int)(step % LAG_SLOTS);
-    launch_slab_lag(R.dz, ctx->sdev + SDEV_TOTALS, R.left >= 0 ? R.msg_in[0] : nullptr, R.right >= 0 ? R.msg_in[1] : nullptr,
+    launch_slab_lag(R.dz, ctx->has_left ? 1 : 0, ctx->has_right ? 1 : 0, ctx->sdev + SDEV_TOTALS,
+                    R.left >= 0 ? R.msg_in[0] : nullptr, R.right >= 0 ? R.msg_in[1] : nullptr,
                     R.left >= 0 ? R.rho_in[0] : nullptr, R.right >= 0 ? R.rho_in[1] : nullptr, R.lag + k * LAG_WORDS, s);
     HIPCHK(hipEventRecord(R.lag_ev[k], s));
     R.cin_hist[k] = R.c1i[0] + R.c1i[1];
@@ -724,28 +731,29 @@ int validate_mid(Multi& M, sph_ctx* pctx) {
         HIPCHK(hipStreamSynchronize(ctx->stream));
         SlabSizes h;
         HIPCHK(hipMemcpy(&h, R.dz, sizeof h, hipMemcpyDeviceToHost));
-        bool ok = h.flags == 0 && h.n <= (uint32_t)ctx->capacity && (int64_t)h.n <= R.n_ub && h.rg[0] <= h.rg[1] &&
-                  h.rg[1] <= h.rg[3] && h.rg[3] <= h.rg[5] && h.rg[5] <= h.n && h.nl <= (uint32_t)R.c1i[0] &&
-                  h.nr <= (uint32_t)R.c1i[1] && h.rg[7] - h.rg[6] <= (uint32_t)std::max(R.c2o[0], 0) + (R.left < 0 ? h.n : 0) &&
-                  h.rg[9] - h.rg[8] <= (uint32_t)std::max(R.c2o[1], 0) + (R.right < 0 ? h.n : 0);
-        for (int k = 0; k < 6; k += 2) ok = ok && h.fr[k] <= h.fr[k + 1] && h.fr[k + 1] <= h.n;
+        const uint32_t* v = h.pick;   // the column starts every kernel of the rest of the step reads
+        bool ok = h.flags == 0 && h.n <= (uint32_t)ctx->capacity && (int64_t)h.n <= R.n_ub && h.nl <= (uint32_t)R.c1i[0] &&
+                  h.nr <= (uint32_t)R.c1i[1] && v[5] <= h.n &&
+                  v[2] - v[1] <= (uint32_t)std::max(R.c2o[0], 0) + (R.left < 0 ? h.n : 0) &&
+                  v[4] - v[3] <= (uint32_t)std::max(R.c2o[1], 0) + (R.right < 0 ? h.n : 0);
+        for (int k = 0; k < 5; ++k) ok = ok && v[k] <= v[k + 1];
         // the cell-start table the neighbour passes will walk: monotone, within the assembled slots
         std::vector<uint32_t> cs(ctx->grid.ncells + 2);
         HIPCHK(hipMemcpy(cs.data(), ctx->cs, cs.size() * 4, hipMemcpyDeviceToHost));
         int64_t bad_at = -1;
         for (size_t k = 0; k + 1 < cs.size() && bad_at < 0; ++k)
-            if (cs[k] > cs[k + 1] || cs[k + 1] > h.n + h.dropped) bad_at = (int64_t)k;
-        if (cs[0] != 0 || cs[ctx->grid.ncells] != h.n) bad_at = bad_at < 0 ? (int64_t)ctx->grid.ncells : bad_at;
+            if (cs[k] > cs[k + 1] || cs[k + 1] > h.n) bad_at = (int64_t)k;   // h.n: the assembled slots
+        // cs[ncells]: the slots kept (the dropped ones, which left the window, sort after it)
+        if (cs[0] != 0 || cs[ctx->grid.ncells] != v[5]) bad_at = bad_at < 0 ? (int64_t)ctx->grid.ncells : bad_at;
         if (bad_at >= 0)
             return fail(pctx, SPH_ERR_STATE, "validate(mid) rank %d step %lld: cell starts broken at %lld (%u %u, n %u, ncells %u)",
                         R.rank, (long long)M.steps, (long long)bad_at, cs[bad_at], cs[bad_at + 1], h.n, ctx->grid.ncells);
         if (!ok)
             return fail(pctx, SPH_ERR_STATE,
-                        "validate(mid) rank %d step %lld: flags %u n %u (ub %lld) rg %u %u %u %u %u %u %u %u %u %u "
-                        "fr %u %u %u %u %u %u nl %u nr %u no %u c1i %d %d c2o %d %d",
-                        R.rank, (long long)M.steps, h.flags, h.n, (long long)R.n_ub, h.rg[0], h.rg[1], h.rg[2], h.rg[3],
-                        h.rg[4], h.rg[5], h.rg[6], h.rg[7], h.rg[8], h.rg[9], h.fr[0], h.fr[1], h.fr[2], h.fr[3],
-                        h.fr[4], h.fr[5], h.nl, h.nr, h.no, R.c1i[0], R.c1i[1], R.c2o[0], R.c2o[1]);
+                        "validate(mid) rank %d step %lld: flags %u n %u (ub %lld) picks %u %u %u %u %u %u "
+                        "nl %u nr %u no %u c1i %d %d c2o %d %d",
+                        R.rank, (long long)M.steps, h.flags, h.n, (long long)R.n_ub, v[0], v[1], v[2], v[3], v[4], v[5],
+                        h.nl, h.nr, h.no, R.c1i[0], R.c1i[1], R.c2o[0], R.c2o[1]);
     }
     return SPH_OK;
 }

@@ -152,6 +152,38 @@ constexpr uint32_t SZ_RHO_MISMATCH = 4u;  // a ghost column and the densities re
 constexpr uint32_t SZ_OVF_MOVERS = 8u;    // a mover list or a re-sort destination past the slot capacity
 // Halo messages: one 32-byte header record, then the records. Header: (count, capacity, 0, 0 | 0...)
 constexpr int MSG_HDR_F4 = 2;
+// What the assembled layout is computed from: the two message headers (null: no neighbour), the
+// capacities they were sent with, and the context's slot capacity.
+struct SizesIn {
+    const float4* hl;
+    const float4* hr;
+    int32_t cap_l, cap_r, capacity;
+};
+#if defined(__HIPCC__)
+__device__ __forceinline__ uint32_t header_count(const float4* msg) { return __float_as_uint(msg[0].x); }
+// nl, no, nr and the flags of the assembled [left | own | right] (slab.hip k_slab_sizes; k_slab_rec)
+__device__ __forceinline__ void slab_sizes_from(const SlabSizes* dz, const SizesIn& in, uint32_t& nl, uint32_t& no,
+                                                uint32_t& nr, uint32_t& f) {
+    const uint32_t hl = in.hl ? header_count(in.hl) : 0u, hr = in.hr ? header_count(in.hr) : 0u;
+    nl = min(hl, (uint32_t)in.cap_l);
+    nr = min(hr, (uint32_t)in.cap_r);
+    f = dz->flags;
+    if (hl > (uint32_t)in.cap_l || hr > (uint32_t)in.cap_r) f |= SZ_OVF_MSG;
+    no = dz->o1 >= dz->o0 ? dz->o1 - dz->o0 : 0u;
+    if ((uint64_t)nl + no + nr > (uint64_t)in.capacity) {   // never address past the slot arrays
+        f |= SZ_OVF_CAP;
+        nl = nr = 0;
+        if (no > (uint32_t)in.capacity) no = 0;
+    }
+}
+__device__ __forceinline__ void slab_sizes_store(SlabSizes* dz, uint32_t nl, uint32_t no, uint32_t nr, uint32_t f) {
+    dz->nl = nl;
+    dz->nr = nr;
+    dz->no = no;
+    dz->n = nl + no + nr;
+    dz->flags = f;
+}
+#endif
 
 // Movers of a Model S step (resort.hip): particles whose new cell key differs from the sorted key
 // of their slot. The force pass appends them (any order) for the incremental re-sort.
@@ -262,7 +294,7 @@ inline AsmSrc asm_plain(const float4* pos, const float4* vel, const int32_t* id,
 // src.keyr, old keys moved into this window and clamped into src.skr, and every record whose key
 // changed appended to the sink (mi = slot | MV_REC) after the own movers the force pass appended
 void launch_slab_rec(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base, uint32_t* keyr, uint32_t* skr,
-                     MoverSink sink, hipStream_t s);
+                     MoverSink sink, hipStream_t s, const SizesIn* sizes = nullptr);
 // cell-start values to pick once the table is final: out[t] = cs[idx[t]] (device), and the same
 // into out_host (mapped pinned memory) when given; m = 0: none
 struct CsPick {
@@ -377,16 +409,16 @@ int32_t slab_send_blocks(int32_t b, int32_t e);
 void launch_slab_sizes(SlabSizes* dz, const float4* msg_l, const float4* msg_r, int32_t cap_l, int32_t cap_r,
                        int32_t capacity, hipStream_t s);
 // after the re-sort: dz->pick -> the ranges (rg, fr, o0/o1 of the new order, n and dropped)
-void launch_slab_ranges(SlabSizes* dz, int32_t has_left, int32_t has_right, hipStream_t s);
-// ρ, P/ρ² of boundary column `side` (rg[6+2side], rg[7+2side]) -> message (header + cap entries)
+// ρ, P/ρ² of boundary column `side` ([pick[1+2side], pick[2+2side])) -> message (header + cap entries)
 void launch_slab_pack_rho(const float2* rp, SlabSizes* dz, int32_t side, float2* msg, int32_t cap, hipStream_t s);
-// received densities -> the ghost column of `side` (rg[4side], rg[4side+1]); mismatch -> SZ_RHO_MISMATCH
+// received densities -> the ghost column of `side` ([pick[4side], pick[4side+1])); mismatch -> SZ_RHO_MISMATCH
 void launch_slab_unpack_rho(float2* rp, SlabSizes* dz, int32_t side, const float2* msg, int32_t cap, hipStream_t s);
 // per-step counts for the host's lagged capacity choice, written to mapped pinned memory:
 // out[0..1] sent records (left, right), out[2..3] received headers, out[4..5] ρ sent, out[6..7] ρ received,
 // out[8] assembled slots, out[9] flags
-void launch_slab_lag(const SlabSizes* dz, const uint32_t* totals, const float4* msg_in_l, const float4* msg_in_r,
-                     const float2* rho_in_l, const float2* rho_in_r, uint32_t* out, hipStream_t s);
+void launch_slab_lag(SlabSizes* dz, int32_t has_left, int32_t has_right, const uint32_t* totals,
+                     const float4* msg_in_l, const float4* msg_in_r, const float2* rho_in_l, const float2* rho_in_r,
+                     uint32_t* out, hipStream_t s);
 
 // owned slots [o0, o0+n) -> records of 8 floats (x,y,z,u,v,w,id-bits,ρ)
 void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, const float2* rp,

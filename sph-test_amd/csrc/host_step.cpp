@@ -52,12 +52,7 @@ int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id, const uint32_t** sorted_
 }
 
 HitMask hit_mask(const sph_ctx* ctx) {
-#ifdef SPH_HM_OFF
-    (void)ctx;
-    return HitMask{};
-#else
     return HitMask{ctx->hmask, (uint32_t)std::max(ctx->capacity, 1)};
-#endif
 }
 
 void density_range(sph_ctx* ctx, int32_t b, int32_t e) {

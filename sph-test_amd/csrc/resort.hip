@@ -295,10 +295,17 @@ constexpr uint32_t REC_NO_KEY = 0xffffffffu;   // slab.hip SL_NO_KEY
 
 __global__ __launch_bounds__(MV_BLK) void k_slab_rec(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base,
                                                      uint32_t* __restrict__ keyr, uint32_t* __restrict__ skr,
-                                                     MoverSink sink) {
+                                                     MoverSink sink, SizesIn in, int32_t from_headers) {
     __shared__ uint32_t wsum[MV_BLK / 64];
     __shared__ uint32_t base_s;
-    if (src.dz) {   // device-sized slab step: the launch covers the message capacities
+    if (from_headers) {   // device-sized slab step: every workgroup derives the layout from the headers,
+        uint32_t nl, no, nr, f;   // the first stores it for the kernels after this one
+        slab_sizes_from(src.dz, in, nl, no, nr, f);
+        if (blockIdx.x == 0 && threadIdx.x == 0) slab_sizes_store(const_cast<SlabSizes*>(src.dz), nl, no, nr, f);
+        src.nl = (int32_t)nl;
+        src.nre = (int32_t)(nl + no);
+        n = (int32_t)(nl + no + nr);
+    } else if (src.dz) {   // sizes already on the device; the launch covers the message capacities
         src.nl = (int32_t)src.dz->nl;
         src.nre = (int32_t)(src.dz->nl + src.dz->no);
         n = (int32_t)src.dz->n;
@@ -374,9 +381,11 @@ __global__ __launch_bounds__(MV_BLK) void k_slab_rec(AsmSrc src, int32_t n, Grid
 }
 
 void launch_slab_rec(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base, uint32_t* keyr, uint32_t* skr,
-                     MoverSink sink, hipStream_t s) {
+                     MoverSink sink, hipStream_t s, const SizesIn* sizes) {
     const int32_t nrec = src.nl + (n - src.nre);
-    if (nrec > 0) k_slab_rec<<<(nrec + MV_DET - 1) / MV_DET, MV_BLK, 0, s>>>(src, n, g, key_base, keyr, skr, sink);
+    if (nrec > 0)
+        k_slab_rec<<<(nrec + MV_DET - 1) / MV_DET, MV_BLK, 0, s>>>(src, n, g, key_base, keyr, skr, sink,
+                                                                  sizes ? *sizes : SizesIn{}, sizes ? 1 : 0);
 }
 
 void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* count,

@@ -87,7 +87,6 @@ __device__ __forceinline__ void write_header(float4* msg, uint32_t count, uint32
     msg[0] = make_float4(__uint_as_float(count), __uint_as_float(cap), 0.f, 0.f);
     msg[1] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
-__device__ __forceinline__ uint32_t header_count(const float4* msg) { return __float_as_uint(msg[0].x); }
 
 __global__ __launch_bounds__(SL_SCAN) void k_slab_scan(uint32_t* __restrict__ blk, int32_t nblk,
                                                        uint32_t* __restrict__ totals, int64_t* __restrict__ totals64,
@@ -364,53 +363,18 @@ void launch_slab_pack_dev(const uint32_t* keys, const float4* pos, const float4*
                                          nb_ub, msg + MSG_HDR_F4, dz, (uint32_t)cap);
 }
 
-__global__ void k_slab_sizes(SlabSizes* __restrict__ dz, const float4* __restrict__ msg_l,
-                             const float4* __restrict__ msg_r, int32_t cap_l, int32_t cap_r, int32_t capacity) {
+// The assembled layout from the message headers and the owned range of the previous order (a
+// host-sized step; device-sized steps compute it in k_slab_rec).
+__global__ void k_slab_sizes(SlabSizes* __restrict__ dz, SizesIn in) {
     if (threadIdx.x != 0) return;
-    const uint32_t hl = msg_l ? header_count(msg_l) : 0u, hr = msg_r ? header_count(msg_r) : 0u;
-    uint32_t nl = min(hl, (uint32_t)cap_l), nr = min(hr, (uint32_t)cap_r);
-    uint32_t f = dz->flags;
-    if (hl > (uint32_t)cap_l || hr > (uint32_t)cap_r) f |= SZ_OVF_MSG;
-    uint32_t no = dz->o1 >= dz->o0 ? dz->o1 - dz->o0 : 0u;
-    if ((uint64_t)nl + no + nr > (uint64_t)capacity) {   // never address past the slot arrays
-        f |= SZ_OVF_CAP;
-        nl = nr = 0;
-        if (no > (uint32_t)capacity) no = 0;
-    }
-    dz->nl = nl;
-    dz->nr = nr;
-    dz->no = no;
-    dz->n = nl + no + nr;
-    dz->flags = f;
+    uint32_t nl, no, nr, f;
+    slab_sizes_from(dz, in, nl, no, nr, f);
+    slab_sizes_store(dz, nl, no, nr, f);
 }
 
 void launch_slab_sizes(SlabSizes* dz, const float4* msg_l, const float4* msg_r, int32_t cap_l, int32_t cap_r,
                        int32_t capacity, hipStream_t s) {
-    k_slab_sizes<<<1, 64, 0, s>>>(dz, msg_l, msg_r, cap_l, cap_r, capacity);
-}
-
-// ranges of the new order from the picked column starts (as slab_sync_ranges does on the host)
-__global__ void k_slab_ranges(SlabSizes* __restrict__ dz, int32_t has_left, int32_t has_right) {
-    if (threadIdx.x != 0) return;
-    const uint32_t* v = dz->pick;
-    const uint32_t rg[10] = {v[0], v[1], v[1], v[4], v[4], v[5], v[1], v[2], v[3], v[4]};
-    for (int k = 0; k < 10; ++k) dz->rg[k] = rg[k];
-    const uint32_t ib = has_left ? v[2] : v[1], ie = has_right ? v[3] : v[4];
-    dz->fr[0] = ib;
-    dz->fr[1] = ie > ib ? ie : ib;
-    if (ie < ib) {   // one-column slab: both boundary columns are the owned column
-        dz->fr[2] = v[1]; dz->fr[3] = v[4]; dz->fr[4] = 0u; dz->fr[5] = 0u;
-    } else {
-        dz->fr[2] = v[1]; dz->fr[3] = ib; dz->fr[4] = ie; dz->fr[5] = v[4];
-    }
-    dz->dropped = dz->n - v[5];
-    dz->n = v[5];
-    dz->o0 = v[1];
-    dz->o1 = v[4];
-}
-
-void launch_slab_ranges(SlabSizes* dz, int32_t has_left, int32_t has_right, hipStream_t s) {
-    k_slab_ranges<<<1, 64, 0, s>>>(dz, has_left, has_right);
+    k_slab_sizes<<<1, 64, 0, s>>>(dz, SizesIn{msg_l, msg_r, cap_l, cap_r, capacity});
 }
 
 // ρ messages: a 32-byte header (count, capacity) = 4 float2, then the entries
@@ -418,7 +382,7 @@ constexpr int RHO_HDR = 4;
 
 __global__ __launch_bounds__(SL_BLK) void k_slab_pack_rho(const float2* __restrict__ rp, const SlabSizes* __restrict__ dz,
                                                           int32_t side, float2* __restrict__ msg, int32_t cap) {
-    const uint32_t b = dz->rg[6 + 2 * side], e = dz->rg[7 + 2 * side];
+    const uint32_t b = dz->pick[1 + 2 * side], e = dz->pick[2 + 2 * side];   // boundary column of `side`
     const uint32_t cnt = e - b;
     const uint32_t t = blockIdx.x * SL_BLK + threadIdx.x;
     if (t == 0) {
@@ -430,7 +394,7 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_pack_rho(const float2* __restri
 
 __global__ __launch_bounds__(SL_BLK) void k_slab_unpack_rho(float2* __restrict__ rp, SlabSizes* __restrict__ dz,
                                                             int32_t side, const float2* __restrict__ msg, int32_t cap) {
-    const uint32_t b = dz->rg[4 * side], e = dz->rg[4 * side + 1];
+    const uint32_t b = dz->pick[4 * side], e = dz->pick[4 * side + 1];   // ghost column of `side`
     const uint32_t cnt = __float_as_uint(msg[0].x);
     const uint32_t m = min(min(cnt, (uint32_t)cap), e - b);
     const uint32_t t = blockIdx.x * SL_BLK + threadIdx.x;
@@ -446,26 +410,53 @@ void launch_slab_unpack_rho(float2* rp, SlabSizes* dz, int32_t side, const float
     k_slab_unpack_rho<<<cap / SL_BLK + 1, SL_BLK, 0, s>>>(rp, dz, side, msg, cap);
 }
 
-__global__ void k_slab_lag(const SlabSizes* __restrict__ dz, const uint32_t* __restrict__ totals,
-                           const float4* __restrict__ msg_in_l, const float4* __restrict__ msg_in_r,
-                           const float2* __restrict__ rho_in_l, const float2* __restrict__ rho_in_r,
-                           uint32_t* __restrict__ out) {
+// End of a device-sized step: the slot ranges of the new order from the picked column starts (the
+// kernels of this step read the picks themselves; these copies are for the host and the next step),
+// the next step's owned range, the sizes of a rank without neighbours (no message will set them), and
+// this step's counts for the capacities two steps on (mapped pinned memory).
+__global__ void k_slab_lag(SlabSizes* __restrict__ dz, int32_t has_left, int32_t has_right,
+                           const uint32_t* __restrict__ totals, const float4* __restrict__ msg_in_l,
+                           const float4* __restrict__ msg_in_r, const float2* __restrict__ rho_in_l,
+                           const float2* __restrict__ rho_in_r, uint32_t* __restrict__ out) {
     if (threadIdx.x != 0) return;
+    const uint32_t* v = dz->pick;
+    const uint32_t rg[10] = {v[0], v[1], v[1], v[4], v[4], v[5], v[1], v[2], v[3], v[4]};
+    for (int k = 0; k < 10; ++k) dz->rg[k] = rg[k];
+    const uint32_t ib = has_left ? v[2] : v[1], ie = has_right ? v[3] : v[4];
+    dz->fr[0] = ib;
+    dz->fr[1] = ie > ib ? ie : ib;
+    if (ie < ib) {   // one-column slab: both boundary columns are the owned column
+        dz->fr[2] = v[1]; dz->fr[3] = v[4]; dz->fr[4] = 0u; dz->fr[5] = 0u;
+    } else {
+        dz->fr[2] = v[1]; dz->fr[3] = ib; dz->fr[4] = ie; dz->fr[5] = v[4];
+    }
+    dz->dropped = dz->n - v[5];
+    dz->o0 = v[1];
+    dz->o1 = v[4];
+    const uint32_t f = dz->flags;
+    if (!has_left && !has_right) {   // the next step's layout: the owned slots alone
+        dz->nl = dz->nr = 0u;
+        dz->no = v[4] - v[1];
+        dz->n = v[4] - v[1];
+    } else {
+        dz->n = v[5];
+    }
     out[0] = totals[0];
     out[1] = totals[1];
     out[2] = msg_in_l ? header_count(msg_in_l) : 0u;
     out[3] = msg_in_r ? header_count(msg_in_r) : 0u;
-    out[4] = dz->rg[7] - dz->rg[6];
-    out[5] = dz->rg[9] - dz->rg[8];
+    out[4] = v[2] - v[1];
+    out[5] = v[4] - v[3];
     out[6] = rho_in_l ? __float_as_uint(rho_in_l[0].x) : 0u;
     out[7] = rho_in_r ? __float_as_uint(rho_in_r[0].x) : 0u;
-    out[8] = dz->n;
-    out[9] = dz->flags;
+    out[8] = v[5];
+    out[9] = f;
 }
 
-void launch_slab_lag(const SlabSizes* dz, const uint32_t* totals, const float4* msg_in_l, const float4* msg_in_r,
-                     const float2* rho_in_l, const float2* rho_in_r, uint32_t* out, hipStream_t s) {
-    k_slab_lag<<<1, 64, 0, s>>>(dz, totals, msg_in_l, msg_in_r, rho_in_l, rho_in_r, out);
+void launch_slab_lag(SlabSizes* dz, int32_t has_left, int32_t has_right, const uint32_t* totals,
+                     const float4* msg_in_l, const float4* msg_in_r, const float2* rho_in_l, const float2* rho_in_r,
+                     uint32_t* out, hipStream_t s) {
+    k_slab_lag<<<1, 64, 0, s>>>(dz, has_left, has_right, totals, msg_in_l, msg_in_r, rho_in_l, rho_in_r, out);
 }
 
 void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, int32_t* id, hipStream_t s) {

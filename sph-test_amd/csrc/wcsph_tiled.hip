@@ -336,21 +336,14 @@ __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi,
     a.sx -= cx * du; a.sy -= cx * dv; a.sz -= cx * dw;
 }
 
-#ifndef SPH_HM_READER
-#define SPH_HM_READER 0
-#endif
-#if SPH_FORCE_WPE
-__global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_FORCE_WPE))) void k_force_tiled(
-#else
 __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
-#endif
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
     const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, PairK pk, float dt,
     float fext_x, float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o, MoverSink mv,
     HitMask hm, uint32_t* __restrict__ paths, DevRange dr) {
     __shared__ float4 sp[TF_GCAP + 4];     // (x, y, z, ρ)
     __shared__ float4 sv[TF_GCAP + 4];     // (u, v, w, P/ρ²)
-    __shared__ uint16_t lst[TT_CAP][TT_BLK];
+    __shared__ uint16_t lst[TT_CAP + 1][TT_BLK];   // + a row for the stores of lanes out of hits
     const int tid = threadIdx.x;
     if (dr.lo) {   // device-resident bounds (slab step); the grid is an upper bound
         ib = (int32_t)*dr.lo;
@@ -381,29 +374,9 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         cnt = 0;
     };
     // hit-mask reader (pass 1's bits of this target, in visit order): rb holds rn bits, LSB next;
-    // the remaining words wait in a queue of registers (static indices only)
-#if SPH_HM_READER == 1
-    const uint32_t* hmw = hm.w ? hm.w + ii : nullptr;   // word w of this target at hmw[w * stride]
-    uint64_t rb = 0;
-    uint32_t nxt = 0;
-    int32_t rn = 64, wi = 3, kb = 0;   // kb: candidates of this target so far
-    if (valid && hmw) {
-        rb = (uint64_t)hmw[0] | ((uint64_t)hmw[hm.stride] << 32);
-        nxt = hmw[2 * (size_t)hm.stride];
-    }
-    auto take = [&](int32_t len) -> uint32_t {   // the next len (0..32) bits
-        const uint32_t v = (uint32_t)rb & (len >= 32 ? 0xffffffffu : ((1u << len) - 1u));
-        rb >>= len;
-        rn -= len;
-        if (rn <= 32) {   // the prefetched word joins; the one after it is fetched now
-            rb |= (uint64_t)nxt << rn;
-            rn += 32;
-            nxt = (valid && hmw && wi < HM_WORDS) ? hmw[(size_t)wi * hm.stride] : 0u;
-            ++wi;
-        }
-        return v;
-    };
-#else
+    // the remaining words wait in a queue of registers (static indices only). Measured against a
+    // one-word prefetch from global memory (with and without 5 waves per SIMD): the queue is 2-3%
+    // faster on the force pass (profiles/r02_hitmask_ab.log).
     uint32_t q[HM_WORDS];
 #pragma unroll
     for (int w = 0; w < HM_WORDS; ++w) q[w] = (valid && hm.w) ? hm.w[(size_t)w * hm.stride + i] : 0u;
@@ -422,22 +395,19 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         }
         return v;
     };
-#endif
     // the hits of LDS slots [lo, lo+ln) from the mask, 16 candidates at a time: at most 16 hits, so
     // one list check per piece; then two hits per iteration with unconditional stores (a lane out of
-    // hits stores to its next free entry without advancing, as the distance scan does)
+    // hits stores to its next free entry, at most row TT_CAP, without advancing)
     auto hits = [&](int32_t lo, int32_t ln) {
         for (int32_t off = 0; __any(off < ln); off += 16) {
             uint32_t m = take(max(0, min(16, ln - off)));
             if (__any(cnt + (int)__popc(m) > TT_CAP)) flush();
             const uint32_t base = (uint32_t)(lo + off) * 16u;
             while (__any(m != 0u)) {
-                const int c0i = min(cnt, TT_CAP - 1);
-                lst[c0i][tid] = (uint16_t)(base + 16u * (uint32_t)__builtin_ctz(m | 0x10000u));
+                lst[cnt][tid] = (uint16_t)(base + 16u * (uint32_t)__builtin_ctz(m | 0x10000u));
                 cnt += m != 0u;
                 m &= m - 1u;
-                const int c1i = min(cnt, TT_CAP - 1);
-                lst[c1i][tid] = (uint16_t)(base + 16u * (uint32_t)__builtin_ctz(m | 0x10000u));
+                lst[cnt][tid] = (uint16_t)(base + 16u * (uint32_t)__builtin_ctz(m | 0x10000u));
                 cnt += m != 0u;
                 m &= m - 1u;
             }
