@@ -396,7 +396,9 @@ int phase_pack(RankState& R, Multi& M) {
                              col_ge(ctx), ctx->sblk, R.msg_out[s], R.c1o[s], ctx->sdev + SDEV_TOTALS + s, ctx->stream);
     }
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(R.ev_packed, ctx->stream));
+    // the peer copies of a local group wait for it (RCCL orders its sends on this stream itself); a
+    // marker costs the stream a few microseconds, so none without a neighbour
+    if (M.mode == 1 && (R.left >= 0 || R.right >= 0)) HIPCHK(hipEventRecord(R.ev_packed, ctx->stream));
     CKPT(R, "pack");
     return SPH_OK;
 }
@@ -458,7 +460,7 @@ int exchange1(Multi& M) {
                 HIPCHK(hipStreamWaitEvent(ctx->stream, S.ev_packed, 0));
                 HIPCHK(hipMemcpyPeerAsync(R.msg_in[s], ctx->device, S.msg_out[1 - s], S.c->device, bytes, ctx->stream));
             }
-            HIPCHK(hipEventRecord(R.ev_in, ctx->stream));
+            if (R.left >= 0 || R.right >= 0) HIPCHK(hipEventRecord(R.ev_in, ctx->stream));
         }
         return SPH_OK;
     }
@@ -623,7 +625,7 @@ int phase_rho_out(RankState& R, Multi& M) {
         launch_slab_pack_rho(ctx->rp, R.dz, s, R.rho_out[s], R.c2o[s], ctx->stream);
     }
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(R.ev_rho_packed, ctx->stream));
+    if (R.left >= 0 || R.right >= 0) HIPCHK(hipEventRecord(R.ev_rho_packed, ctx->stream));
     CKPT(R, "rho pack");
     return SPH_OK;
 }
@@ -675,7 +677,7 @@ int phase_finish(RankState& R, float dt, int64_t step) {
     launch_slab_lag(R.dz, ctx->has_left ? 1 : 0, ctx->has_right ? 1 : 0, ctx->sdev + SDEV_TOTALS,
                     R.left >= 0 ? R.msg_in[0] : nullptr, R.right >= 0 ? R.msg_in[1] : nullptr,
                     R.left >= 0 ? R.rho_in[0] : nullptr, R.right >= 0 ? R.rho_in[1] : nullptr, R.lag + k * LAG_WORDS, s);
-    HIPCHK(hipEventRecord(R.lag_ev[k], s));
+    if (R.left >= 0 || R.right >= 0) HIPCHK(hipEventRecord(R.lag_ev[k], s));   // read two steps on
     R.cin_hist[k] = R.c1i[0] + R.c1i[1];
     R.n_prev_ub = R.n_ub;
     R.since_cut++;
@@ -773,6 +775,7 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
         if ((r = exchange_counts(M, pctx)) != SPH_OK) return r;
     } else {
         for (auto& R : M.ranks) {
+            if (R.left < 0 && R.right < 0) continue;   // no messages: nothing to size
             // the counts of two steps before: both neighbours read the same numbers
             const uint32_t* L = lag_slot(R, M.steps - 2, R.c, &r);
             if (r != SPH_OK) return r;
