@@ -271,6 +271,21 @@ def main():
         except Exception as e:   # noqa: BLE001 - reported, then the torch.distributed slab path (also RCCL)
             print(json.dumps({"rank": rank, "library_transport_failed": str(e)}), file=sys.stderr, flush=True)
             runner = None
+    if runner is not None and world > 1:
+        # every rank checks one step of the in-library path; if any rank failed, all take the
+        # torch.distributed slab path instead (the same kernels, RCCL through torch)
+        ok = 1
+        try:
+            runner.step(1)
+            torch.cuda.synchronize()
+        except Exception as e:   # noqa: BLE001 - reported
+            ok = 0
+            print(json.dumps({"rank": rank, "library_step_failed": str(e)}), file=sys.stderr, flush=True)
+        flag = torch.tensor([ok], dtype=torch.int32, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            runner.close()
+            runner = None
     if runner is None and (world > 1 or args.slab or args.strong):
         from sph_test_amd import slab
         runner = slab.SlabRunner(args.config, rank, world, device=local, profile=not args.no_profile,

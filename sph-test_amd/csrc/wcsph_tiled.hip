@@ -31,11 +31,13 @@ constexpr int TT_BLK = 256;     // targets per workgroup (128 / 192 / 512 measur
 constexpr int TT_GCAP = 1024;   // candidates staged per plane (LDS), density pass
 constexpr int TT_CAP = 16;      // per-lane hit list (force)
 constexpr int TT_FALLBACK = 4 * TT_GCAP;
-// The force pass stages 32 B per candidate and keeps per-lane hit lists in LDS. Its flush loop is
-// latency-bound (LDS list read -> candidate reads -> body), so occupancy pays: 704 candidates and
-// 16-entry lists keep a workgroup under 32 KiB, 5 workgroups per CU instead of 3 (C3, MI355X:
-// force pass 305 -> 258 us; 1024/32 and 768/16 measured 305 and 282).
-constexpr int TF_GCAP = 704;
+// The force pass stages 32 B per candidate and keeps per-lane hit lists in LDS. With the hit mask
+// (117 VGPRs) four workgroups fit a CU by registers, so the plane budget takes what four leave of the
+// LDS: 1000 candidates (40.8 KB), and most planes (~840 candidates at C3) are staged at once instead of
+// row by row in chunks. Measured against 704 / 832 / 960 (profiles/r02_force_budget_ab.log): force pass
+// 241 -> 232 us from rest, 314 -> 287 us mid-collapse. (Before the mask, 704 with 16-entry lists kept a
+// workgroup under 32 KiB for five per CU: 305 -> 258 us then.)
+constexpr int TF_GCAP = 1000;
 constexpr int TF_FALLBACK = 4 * TF_GCAP;
 
 struct BlockRows {
