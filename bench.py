@@ -28,9 +28,10 @@ sys.path.insert(0, str(ROOT))
 import __graft_entry__ as GE  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
-# SURVEY.md §8d, algorithmic bytes per particle-step of the force+visc+XSPH+KDK pass
-# (read x,v,ρ,P 32 B + write x,v 24 B, SoA fp32, neighbour reads counted once)
-FORCE_BYTES_PER_PARTICLE = 56.0
+# SURVEY.md §8d, algorithmic bytes per particle-step of the force+visc+XSPH+KDK pass: read x,v,ρ,P 32 B
+# + write x,v 24 B (SoA fp32, neighbour reads counted once) + this design's hit mask, 8 words read 32 B
+# (pass 1 writes it)
+FORCE_BYTES_PER_PARTICLE = 88.0
 
 
 def parse():
