@@ -3,8 +3,8 @@
 On the one-GPU test box every slab context of a local group sits on device 0 (the halo copies are
 then plain device copies instead of xGMI peer copies; the step is otherwise the same code).
 
-  * ndev = 2 / 3 against the single-context step (the decomposition changes only who computes what:
-    positions within 2e-6, as tests/test_gpu_slab.py);
+  * ndev = 2 / 3 / 4 against the single-context step, dam-break and sloshing (the decomposition changes
+    only who computes what: positions within 2e-6, as tests/test_gpu_slab.py);
   * ndev = 3 with re-balancing against the per-phase slab ABI driven from Python over gloo
     (tests/test_gpu_slab.py's harness, sph_test_amd.slab.SlabRunner): the same kernels on the same data
     in the same order, so every rank's owned particles are BIT-identical, over 60 steps that take the
@@ -25,9 +25,10 @@ def _check(x, v, xs, vs):
     np.testing.assert_allclose(v, vs, rtol=1e-3, atol=2e-3)
 
 
-@pytest.mark.parametrize("ndev", [2, 3])
-def test_group_matches_single(pkg, ndev):
-    sc = _scenario(pkg)
+@pytest.mark.parametrize("ndev,kind", [(2, 0), (3, 0), (4, 0), (3, 1)])
+def test_group_matches_single(pkg, ndev, kind):
+    """kind 0: dam-break; 1: sloshing (the lateral forcing follows every slab's simulated time)."""
+    sc = _scenario(pkg, kind)
     xs, vs = _single(pkg, sc)
     sim = pkg.SPHSim(sc, ndev=ndev, rebalance_every=0)
     try:
