@@ -264,7 +264,7 @@ def main():
     pkg = GE.load_package()
 
     runner = None
-    if (world > 1 or args.slab) and args.transport == "library" and not (world == 1 and args.strong):
+    if (world > 1 or args.slab or args.strong) and args.transport == "library":
         # the decomposed step inside libsphhip.so: one RCCL communicator, no host read per step
         try:
             runner = LibraryRankRunner(pkg, args.config, rank, world, local, profile=not args.no_profile,

@@ -1,0 +1,121 @@
+"""The hit mask's bit stream (wcsph_tiled.hip), restated in Python with the kernels' 64-bit arithmetic:
+pass 1's writer (newest bit enters at bit 63; a word leaves once 32 are pending; the last, partial word is
+masked) and pass 2's reader (64-bit buffer refilled from a queue of words; takes of 0..32 bits; pieces of 16
+for the hit loop). Random candidate streams cut into random windows, in the scan's groups of 4 plus a scalar
+tail, must come back bit for bit, and a reader skipping planes must stay aligned."""
+import numpy as np
+import pytest
+
+HM_WORDS = 8
+M64 = (1 << 64) - 1
+
+
+def write_mask(windows):
+    """windows: list of bool arrays (one per window, visit order). Returns the HM_WORDS words."""
+    mb, mn, mw = 0, 0, 0
+    words = [0] * HM_WORDS
+
+    def bit(h):
+        nonlocal mb
+        mb = ((mb >> 1) | ((1 << 63) if h else 0)) & M64
+
+    def emit():
+        nonlocal mb, mn, mw
+        if mn >= 32:
+            if mw < HM_WORDS:
+                words[mw] = (mb >> (64 - mn)) & 0xFFFFFFFF
+            mw += 1
+            mn -= 32
+
+    for w in windows:
+        t, ln = 0, len(w)
+        while t + 4 <= ln:                      # the 4-wide group
+            for k in range(4):
+                bit(w[t + k])
+            mn += 4
+            emit()
+            t += 4
+        while t < ln:                           # the scalar tail
+            bit(w[t])
+            mn += 1
+            emit()
+            t += 1
+    if mn > 0 and mw < HM_WORDS:
+        words[mw] = (mb >> (64 - mn)) & ((1 << mn) - 1)
+    return words
+
+
+class Reader:
+    def __init__(self, words):
+        self.q = list(words)
+        self.rb = self.q[0] | (self.q[1] << 32)
+        self.rn = 64
+
+    def take(self, ln):
+        assert 0 <= ln <= 32
+        v = self.rb & (0xFFFFFFFF if ln >= 32 else (1 << ln) - 1)
+        self.rb >>= ln
+        self.rn -= ln
+        if self.rn <= 32:
+            self.rb |= self.q[2] << self.rn
+            self.rn += 32
+            self.q[2:] = self.q[3:] + [0]
+        return v
+
+    def hits(self, ln):                          # 16 candidates at a time, as the hit loop
+        out = []
+        off = 0
+        while off < ln:
+            m = self.take(min(16, ln - off))
+            while m:
+                t = (m & -m).bit_length() - 1
+                out.append(off + t)
+                m &= m - 1
+            off += 16
+        return out
+
+    def skip(self, ln):
+        off = 0
+        while off < ln:
+            self.take(min(32, ln - off))
+            off += 32
+
+
+def _windows(rng, total):
+    """random window lengths (0..60) summing to total, as 3 planes of 3 rows"""
+    cuts = np.sort(rng.integers(0, total + 1, 8))
+    lens = np.diff(np.concatenate([[0], cuts, [total]]))
+    return [rng.random(int(n)) < 0.3 for n in lens]
+
+
+@pytest.mark.parametrize("total", [0, 1, 5, 31, 32, 33, 180, 241, 255, 256])
+def test_round_trip(total):
+    rng = np.random.default_rng(total)
+    for _ in range(50):
+        wins = _windows(rng, total)
+        words = write_mask(wins)
+        r = Reader(words)
+        for w in wins:
+            assert r.hits(len(w)) == [int(i) for i in np.flatnonzero(w)]
+
+
+def test_skip_keeps_alignment():
+    """a plane scanned by distance passes over its bits; the next plane's bits are still in place"""
+    rng = np.random.default_rng(7)
+    for _ in range(100):
+        wins = _windows(rng, 240)
+        words = write_mask(wins)
+        r = Reader(words)
+        for p in range(3):
+            plane = wins[3 * p: 3 * p + 3]
+            if p == 1:
+                r.skip(sum(len(w) for w in plane))
+                continue
+            for w in plane:
+                assert r.hits(len(w)) == [int(i) for i in np.flatnonzero(w)]
+
+
+def test_budget_words_beyond_256_are_not_written():
+    wins = [np.ones(300, bool)]
+    words = write_mask(wins)
+    assert words == [0xFFFFFFFF] * HM_WORDS
