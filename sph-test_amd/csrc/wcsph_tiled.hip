@@ -366,25 +366,13 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     auto at = [](const float4* base, uint32_t off) {
         return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + off);
     };
-#ifndef SPH_FLUSH2
-#define SPH_FLUSH2 0
-#endif
     auto flush = [&]() {
-#if SPH_FLUSH2
-        for (int q = 0; __any(q < cnt); q += 2) {   // two independent pairs in flight per lane
-            const uint32_t o0 = lst[q][tid], o1 = lst[min(q + 1, TT_CAP)][tid];
-            const float4 p0 = at(sp, o0), v0 = at(sv, o0), p1 = at(sp, o1), v1 = at(sv, o1);
-            if (q < cnt) pair_force(pk, pi, vi, ri.x, ri.y, p0, v0, acc);
-            if (q + 1 < cnt) pair_force(pk, pi, vi, ri.x, ri.y, p1, v1, acc);
-        }
-#else
         for (int q = 0; __any(q < cnt); ++q) {
             if (q < cnt) {
                 const uint32_t off = lst[q][tid];
                 pair_force(pk, pi, vi, ri.x, ri.y, at(sp, off), at(sv, off), acc);
             }
         }
-#endif
         cnt = 0;
     };
     // hit-mask reader (pass 1's bits of this target, in visit order): rb holds rn bits, LSB next;
