@@ -188,3 +188,27 @@ def test_c2_three_steps_mid_collapse(pkg, oracle):
         np.testing.assert_allclose(sim.density(), rho[order], rtol=1e-4)
     finally:
         sim.close()
+
+
+def test_hit_mask_budget_fallback(pkg, oracle):
+    """A block of fluid compressed to 0.75 dx spacing (~2.4x the candidates per target, past the hit mask's
+    256) beside fluid at rest spacing: pass 2 scans the compressed waves' planes by distance and takes the
+    others from the mask (sph_read_hit_mask_counts: both kinds occur), and the step still meets the
+    tolerances above."""
+    sc = pkg.make_scenario(pkg.SPH_SCENARIO_DAMBREAK, 3, 24, 20, 16, 40, 40, 40, dx=0.01, seed=5)
+    sim = pkg.SPHSim(sc, capacity=40_000)
+    try:
+        def block(x0, n, s, ny, nz):
+            g = np.stack(np.meshgrid(np.arange(n), np.arange(ny), np.arange(nz), indexing="ij"), -1).reshape(-1, 3)
+            return (g * s + s / 2 + np.array([x0, 0.0, 0.0])).astype(np.float32)
+        a = block(0.0, 16, 0.0075, 24, 16)          # compressed: x < 0.12
+        b = block(0.12, 12, 0.01, 18, 12)           # at rest spacing
+        x0 = np.concatenate([a, b])
+        v0 = np.zeros_like(x0)
+        sim.ctx.hit_mask_counts(reset=True)        # arm the counters
+        s, _ = compare_one_step(pkg, oracle, sim, x0, v0, "mask budget")
+        dist_planes, waves = (int(c) for c in sim.ctx.hit_mask_counts(reset=True))
+        print({"distance_wave_planes": dist_planes, "wave_planes": 3 * waves})
+        assert 0 < dist_planes < 3 * waves
+    finally:
+        sim.close()
