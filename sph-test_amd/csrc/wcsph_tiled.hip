@@ -191,20 +191,29 @@ __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restri
     const float4 pi = pos[valid ? i : ilast];
     const BlockRows b = block_rows(g, pos, i0, ilast, pi);
     float s = 0.0f;
-    // hit-mask writer: the newest bit enters at bit 63, so after m bits the oldest unwritten one sits
-    // at 64 − m; a word leaves once 32 are pending
-    uint64_t mb = 0;
+    // hit-mask writer: a 64-bit shift register (mh:ml) takes the newest bit at bit 0 (one v_alignbit per
+    // candidate: ml = ml << 1 | sign(r² − 4h²)); the mn unwritten bits sit at [0, mn). A word leaves once 32
+    // are pending: the oldest 32 (one v_alignbit), bit-reversed so that the oldest lands at bit 0.
+    uint32_t mh = 0, ml = 0;
     int32_t mn = 0, mw = 0;
     const bool rec = valid && hm.w != nullptr;
-    auto bit = [&](float r2) {
-        mb = (mb >> 1) | ((uint64_t)(__float_as_uint(r2 - c.four_h2) & 0x80000000u) << 32);
-    };
+    uint32_t* wp = rec ? hm.w + i : nullptr;
+    auto bit = [&](float r2) { ml = __builtin_amdgcn_alignbit(ml, __float_as_uint(r2 - c.four_h2), 31u); };
     auto emit = [&]() {
         if (mn >= 32) {
-            if (rec && mw < HM_WORDS) hm.w[(size_t)mw * hm.stride + i] = (uint32_t)(mb >> (64 - mn));
-            ++mw;
             mn -= 32;
+            if (rec && mw < HM_WORDS) {
+                *wp = __builtin_bitreverse32(__builtin_amdgcn_alignbit(mh, ml, (uint32_t)mn));
+                wp += hm.stride;
+            }
+            ++mw;
         }
+    };
+    auto one = [&](float r2) {   // a single candidate (scalar tail, global gather)
+        mh = __builtin_amdgcn_alignbit(mh, ml, 31u);
+        bit(r2);
+        ++mn;
+        emit();
     };
     auto scan = [&](int32_t lo, int32_t ln) {
         int32_t t = 0;
@@ -215,6 +224,7 @@ __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restri
             s += spline_w4(c, rb);
             s += spline_w4(c, rc);
             s += spline_w4(c, rd);
+            mh = __builtin_amdgcn_alignbit(mh, ml, 28u);
             bit(ra); bit(rb); bit(rc); bit(rd);
             mn += 4;
             emit();
@@ -223,9 +233,7 @@ __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restri
         for (; t < ln; ++t) {
             const float r2 = dist2(pi, sp[lo + t]);
             s += spline_w4(c, r2);
-            bit(r2);
-            ++mn;
-            emit();
+            one(r2);
         }
     };
 #pragma unroll 1
@@ -259,9 +267,7 @@ __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restri
                 for (int32_t j = r0[r]; j < r1[r]; ++j) {
                     const float r2 = dist2(pi, pos[j]);
                     s += spline_w4(c, r2);
-                    bit(r2);
-                    ++mn;
-                    emit();
+                    one(r2);
                 }
                 continue;
             }
@@ -277,8 +283,8 @@ __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restri
         }
     }
     if (!valid) return;
-    if (rec && mn > 0 && mw < HM_WORDS)   // the last, partial word (its bits above mn are stale)
-        hm.w[(size_t)mw * hm.stride + i] = (uint32_t)(mb >> (64 - mn)) & ((1u << mn) - 1u);
+    if (rec && mn > 0 && mw < HM_WORDS)   // the last, partial word: bits [0, mn), zeros above
+        *wp = __builtin_bitreverse32(ml << (32 - mn));
     const float d = c.mass * (c.sigma * (0.25f * s));
     const float tr = d * c.inv_rho0;
     const float t2 = tr * tr, t4 = t2 * t2;

@@ -1,6 +1,7 @@
-"""The hit mask's bit stream (wcsph_tiled.hip), restated in Python with the kernels' 64-bit arithmetic:
-pass 1's writer (newest bit enters at bit 63; a word leaves once 32 are pending; the last, partial word is
-masked) and pass 2's reader (64-bit buffer refilled from a queue of words; takes of 0..32 bits; pieces of 16
+"""The hit mask's bit stream (wcsph_tiled.hip), restated in Python with the kernels' integer arithmetic:
+pass 1's writer (a 64-bit shift register of two u32 advanced by v_alignbit, newest bit at bit 0; a word
+leaves once 32 are pending, bit-reversed so the oldest candidate lands at bit 0; the last, partial word has
+zeros above its bits) and pass 2's reader (64-bit buffer refilled from a queue of words; takes of 0..32 bits; pieces of 16
 for the hit loop). Random candidate streams cut into random windows, in the scan's groups of 4 plus a scalar
 tail, must come back bit for bit, and a reader skipping planes must stay aligned."""
 import numpy as np
@@ -10,8 +11,57 @@ HM_WORDS = 8
 M64 = (1 << 64) - 1
 
 
+def alignbit(a, b, c):
+    """v_alignbit_b32: ({a, b} >> (c & 31))[31:0]"""
+    return (((a << 32) | b) >> (c & 31)) & 0xFFFFFFFF
+
+
+def bitrev32(x):
+    return int(f"{x:032b}"[::-1], 2)
+
+
 def write_mask(windows):
-    """windows: list of bool arrays (one per window, visit order). Returns the HM_WORDS words."""
+    """The kernel's writer. windows: list of bool arrays (one per window, visit order); the sign bit of
+    r² − 4h² is the hit. Returns the HM_WORDS words."""
+    mh, ml, mn, mw = 0, 0, 0, 0
+    words = [0] * HM_WORDS
+
+    def bit(h):
+        nonlocal ml
+        d = 0x80000000 if h else 0x3F800000          # r² − 4h² < 0 (sign set) or > 0
+        ml = alignbit(ml, d, 31)
+
+    def emit():
+        nonlocal mn, mw
+        if mn >= 32:
+            mn -= 32
+            if mw < HM_WORDS:
+                words[mw] = bitrev32(alignbit(mh, ml, mn))
+            mw += 1
+
+    for w in windows:
+        t, ln = 0, len(w)
+        while t + 4 <= ln:                      # the 4-wide group
+            mh = alignbit(mh, ml, 28)
+            for k in range(4):
+                bit(w[t + k])
+            mn += 4
+            emit()
+            t += 4
+        while t < ln:                           # the scalar tail
+            mh = alignbit(mh, ml, 31)
+            bit(w[t])
+            mn += 1
+            emit()
+            t += 1
+    if mn > 0 and mw < HM_WORDS:
+        words[mw] = bitrev32((ml << (32 - mn)) & 0xFFFFFFFF)
+    return words
+
+
+def write_mask_plain(windows):
+    """The stream's definition (oldest bit first, 32 to a word, zeros past the end) with a 64-bit
+    register that takes the newest bit at bit 63 (the round-2 writer before v_alignbit)."""
     mb, mn, mw = 0, 0, 0
     words = [0] * HM_WORDS
 
@@ -113,6 +163,14 @@ def test_skip_keeps_alignment():
                 continue
             for w in plane:
                 assert r.hits(len(w)) == [int(i) for i in np.flatnonzero(w)]
+
+
+@pytest.mark.parametrize("total", [0, 3, 32, 35, 100, 255, 256, 300])
+def test_alignbit_writer_equals_plain_definition(total):
+    rng = np.random.default_rng(100 + total)
+    for _ in range(50):
+        wins = _windows(rng, total)
+        assert write_mask(wins) == write_mask_plain(wins)
 
 
 def test_budget_words_beyond_256_are_not_written():
