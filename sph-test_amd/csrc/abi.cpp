@@ -785,6 +785,14 @@ int sph_read_hit_mask_counts(sph_ctx* ctx, uint32_t counts[2], int32_t reset) {
     return read_paths(ctx, 4, 2, counts, reset);
 }
 
+// Lane-utilisation counters of a -DSPH_DIAG build (zero otherwise): pass 1 candidates, 4-candidate
+// iterations and tail iterations per wave (summed); pass 2 pairs, flush iterations, flushes, append
+// iterations, mask pieces. Diagnostics only (scripts/pass_util.py); not part of include/sphhip.h.
+int sph_debug_pass_counts(sph_ctx* ctx, uint32_t counts[8], int32_t reset) {
+    if (!ctx || !counts) return SPH_ERR_INVALID;
+    return read_paths(ctx, 8, 8, counts, reset);
+}
+
 int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int32_t key_bits, uint32_t* perm_out,
                          uint32_t* sorted_keys_out) {
     if (!ctx || count < 0 || (count > 0 && !keys) || key_bits < 1 || key_bits > 32) return SPH_ERR_INVALID;

@@ -106,7 +106,8 @@ struct sph_ctx {
     std::vector<sph::Pending> pending;
     std::vector<hipEvent_t> ev_pool;
     int64_t device_bytes = 0;
-    uint32_t* paths = nullptr;   // [8] path counters of the neighbour passes (sph_read_path_counts, _mask_counts)
+    uint32_t* paths = nullptr;   // [16] path counters of the neighbour passes (sph_read_path_counts, _mask_counts;
+                                 // [8, 16): lane-utilisation counters of -DSPH_DIAG builds)
     bool count_paths = false;    // armed by the first counter read: counted launches pay for atomics
     uint32_t* hmask = nullptr;   // Model S: HM_WORDS x capacity hit-mask words (pass 1 -> pass 2)
     // slab decomposition (SPEC_SPH.md §3)

@@ -19,10 +19,13 @@
 //
 // Hit mask (common.h HitMask): pass 1 computes every candidate's r² anyway; it also records
 // r² < 4h² as one bit per candidate, in visit order (the sign bit of r² − 4h²: exact). Pass 2 then
-// takes its hits from the mask (a bit reader and a find-first-set loop that appends only hits) instead
-// of re-reading every candidate from LDS and recomputing its distance. A target with more than
+// takes its hits from the mask instead of re-reading every candidate from LDS and recomputing its
+// distance. On a staged plane whose bits fit 128 per lane (the common case) the pair loop walks the
+// plane's bits directly, one hit per iteration, with no hit list: lanes idle only at the end of the
+// plane instead of at every 16-hit flush (lanes busy 54% -> 66% at C3 from rest, 36% -> 53%
+// mid-collapse). Longer planes append the mask's hits to the lists above; a target with more than
 // HM_WORDS·32 candidates, and the sparse paths, fall back to the distance scan for the plane in
-// question (wave-uniform); both give the same hits, so results do not depend on the path.
+// question (wave-uniform); every path gives the same hits in the same order.
 #include "common.h"
 
 namespace sph {
@@ -99,6 +102,25 @@ __device__ __forceinline__ void count_path(uint32_t* paths, int k) {
 __device__ __forceinline__ void count_wave(uint32_t* paths, int k) {
     if (paths && lane_id() == 0) atomicAdd(paths + k, 1u);
 }
+
+#ifdef SPH_DIAG
+// Diagnostic builds only (-DSPH_DIAG): lane-utilisation counters in paths[8..16) (sph_debug_pass_counts).
+__device__ __forceinline__ int wave_max(int v) {
+    for (int o = 32; o; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+    for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+#define SPH_DIAG_ADD(k, v)                                                                   \
+    do {                                                                                     \
+        const int v_ = (v);                                                                  \
+        if (paths && lane_id() == 0) atomicAdd(paths + (k), (uint32_t)v_);                   \
+    } while (0)
+#else
+#define SPH_DIAG_ADD(k, v) ((void)0)
+#endif
 
 __device__ __forceinline__ float dist2(float4 a, float4 b) {
     const float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
@@ -216,6 +238,9 @@ __global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restri
         emit();
     };
     auto scan = [&](int32_t lo, int32_t ln) {
+        SPH_DIAG_ADD(8, wave_sum(ln));          // candidates
+        SPH_DIAG_ADD(9, wave_max(ln >> 2));     // 4-candidate iterations
+        SPH_DIAG_ADD(10, wave_max(ln & 3));     // tail iterations
         int32_t t = 0;
         for (; t + 4 <= ln; t += 4) {
             const float4 a = sp[lo + t], bb = sp[lo + t + 1], cc = sp[lo + t + 2], d = sp[lo + t + 3];
@@ -359,6 +384,10 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     }
     const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
     if (i0 >= n) return;   // whole workgroup: before any barrier
+    // Targets stay in sorted order here. Lanes ordered by quarters of fx (a dx plane's hit count follows
+    // fx) fill the plane loop better (66% -> 80% of lanes busy at C3) but run slower, 206 -> 246 us: the
+    // lanes of a wave then read scattered LDS slots instead of their column's shared ones
+    // (profiles/r02_direct_plane_ab.log).
     const int32_t i = i0 + tid;
     const bool valid = i < n;
     const int32_t ilast = min(i0 + TT_BLK, n) - 1;
@@ -373,6 +402,9 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + off);
     };
     auto flush = [&]() {
+        SPH_DIAG_ADD(11, wave_sum(cnt));   // pairs
+        SPH_DIAG_ADD(12, wave_max(cnt));   // flush iterations
+        SPH_DIAG_ADD(13, 1);               // flushes
         for (int q = 0; __any(q < cnt); ++q) {
             if (q < cnt) {
                 const uint32_t off = lst[q][tid];
@@ -409,6 +441,8 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     auto hits = [&](int32_t lo, int32_t ln) {
         for (int32_t off = 0; __any(off < ln); off += 16) {
             uint32_t m = take(max(0, min(16, ln - off)));
+            SPH_DIAG_ADD(14, wave_max(((int)__popc(m) + 1) >> 1));   // append iterations
+            SPH_DIAG_ADD(15, 1);                                    // pieces
             if (__any(cnt + (int)__popc(m) > TT_CAP)) flush();
             const uint32_t base = (uint32_t)(lo + off) * 16u;
             while (__any(m != 0u)) {
@@ -445,6 +479,41 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
             if (__any(cnt > TT_CAP - 4)) flush();
         }
     };
+    // A staged plane whose bits (its three row windows back to back, plen <= 128) come from the mask:
+    // the pair loop walks them directly, one hit per iteration, with no hit list and no 16-hit flushes.
+    // Bit b of the plane is candidate b of the concatenated windows; its LDS slot is b plus the offset
+    // of its row. Words are consumed from w0; an emptied w0 takes the next word (an all-zero word in the
+    // middle costs the lane one idle iteration).
+    auto plane_direct = [&](int32_t plen, const int32_t(&c0)[3], const int32_t(&len)[3], const int32_t(&r0)[3],
+                            const int32_t(&r1)[3]) {
+        uint32_t w0 = take(min(max(plen, 0), 32)), w1 = take(min(max(plen - 32, 0), 32));
+        uint32_t w2 = take(min(max(plen - 64, 0), 32)), w3 = take(min(max(plen - 96, 0), 32));
+        int32_t nh = (int32_t)(__popc(w0) + __popc(w1) + __popc(w2) + __popc(w3));
+        const int32_t l0 = r1[0] - r0[0], e2 = l0 + (r1[1] - r0[1]);
+        const int32_t d0 = r0[0] - c0[0];
+        const int32_t d1 = len[0] + (r0[1] - c0[1]) - l0;
+        const int32_t d2 = len[0] + len[1] + (r0[2] - c0[2]) - e2;
+        int32_t base = 0;
+        SPH_DIAG_ADD(11, wave_sum(nh));
+        SPH_DIAG_ADD(12, wave_max(nh));
+        SPH_DIAG_ADD(13, 1);
+        while (__any(nh > 0)) {
+            if (w0 != 0u) {
+                const int32_t b = base + (int32_t)__builtin_ctz(w0);
+                w0 &= w0 - 1u;
+                --nh;
+                const int32_t slot = b + (b < l0 ? d0 : (b < e2 ? d1 : d2));
+                pair_force(pk, pi, vi, ri.x, ri.y, sp[slot], sv[slot], acc);
+            }
+            if (w0 == 0u) {
+                w0 = w1;
+                w1 = w2;
+                w2 = w3;
+                w3 = 0u;
+                base += 32;
+            }
+        }
+    };
     auto put = [&](int32_t t, int32_t src) {
         const float4 p = pos[src], v = vel[src];
         const float2 r = rp[src];
@@ -473,6 +542,10 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
             __syncthreads();
             stage_plane(c0, len, total, put);
             __syncthreads();
+            if (by_mask && !__any(plen > 128)) {
+                plane_direct(plen, c0, len, r0, r1);
+                continue;
+            }
             int32_t o = 0;
 #pragma unroll
             for (int r = 0; r < 3; ++r) {
