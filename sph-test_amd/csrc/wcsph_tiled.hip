@@ -8,39 +8,40 @@
 // walks its own three windows out of LDS, and lanes of one cell read the same address
 // (broadcast). The visit order is the §0 order.
 //
-// Scan: 4 candidates per iteration, branchless (clamped LDS reads, predicated
-// accumulation). Force pass: only ~25% of the trimmed candidates are within 2h. So the scan
-// appends hits (u16 LDS index) to a per-lane LDS list with an unconditional store and a
-// predicated increment. A wave-uniform flush then runs the ~50-op pair body with nearly full
-// lanes, once per plane (or when a list fills).
-// A plane whose intervals exceed TT_GCAP candidates (sparse blocks spanning many rows) is
-// processed offset by offset in chunks, and an offset beyond TT_FALLBACK is gathered directly
-// from global memory.
-//
-// Hit mask (common.h HitMask): pass 1 computes every candidate's r² anyway; it also records
-// r² < 4h² as one bit per candidate, in visit order (the sign bit of r² − 4h²: exact). Pass 2 then
-// takes its hits from the mask instead of re-reading every candidate from LDS and recomputing its
-// distance. On a staged plane whose bits fit 128 per lane (the common case) the pair loop walks the
-// plane's bits directly, one hit per iteration, with no hit list: lanes idle only at the end of the
-// plane instead of at every 16-hit flush (lanes busy 54% -> 66% at C3 from rest, 36% -> 53%
-// mid-collapse). Longer planes append the mask's hits to the lists above; a target with more than
-// HM_WORDS·32 candidates, and the sparse paths, fall back to the distance scan for the plane in
-// question (wave-uniform); every path gives the same hits in the same order.
+// Pass 1 scans 4 candidates per iteration, branchless (clamped LDS reads, predicated
+// accumulation), and records every candidate's r² < 4h² as one bit in visit order (the hit mask,
+// common.h HitMask; the sign bit of r² − 4h²: exact). Only ~30% of the trimmed candidates are within
+// 2h. Pass 2 runs on the same positions and windows, so it takes its hits from the mask instead of
+// re-reading every candidate from LDS and recomputing its distance: per staged plane it walks the
+// plane's bits (its three row windows back to back) in one pair loop, one hit per iteration (find-first-
+// set, LDS slot = bit + its row's offset, pair body). A target with more than HM_WORDS·32 candidates
+// falls back to a distance loop for the plane in question (wave-uniform); both give the same hits
+// in the same order, so results do not depend on the path.
+// A plane whose intervals exceed the LDS budget (sparse blocks spanning many rows) is processed
+// offset by offset in chunks, and an offset beyond the fallback length is gathered directly from
+// global memory.
 #include "common.h"
 
 namespace sph {
 
 constexpr int TT_BLK = 256;     // targets per workgroup (128 / 192 / 512 measured 13-25% slower)
-constexpr int TT_GCAP = 1024;   // candidates staged per plane (LDS), density pass
-constexpr int TT_CAP = 16;      // per-lane hit list (force)
+// Candidates staged per plane (LDS), density pass: 1500 (24.6 KB) keeps six workgroups per CU (74
+// VGPRs) and stages more sparse planes at once than 1024: 143.5 -> 141.4 us from rest, 166 -> 160 us
+// mid-collapse (profiles/r02_density_budget_ab.log).
+#ifndef SPH_TT_GCAP
+#define SPH_TT_GCAP 1500
+#endif
+constexpr int TT_GCAP = SPH_TT_GCAP;
 constexpr int TT_FALLBACK = 4 * TT_GCAP;
-// The force pass stages 32 B per candidate and keeps per-lane hit lists in LDS. With the hit mask
-// (117 VGPRs) four workgroups fit a CU by registers, so the plane budget takes what four leave of the
-// LDS: 1000 candidates (40.8 KB), and most planes (~840 candidates at C3) are staged at once instead of
-// row by row in chunks. Measured against 704 / 832 / 960 (profiles/r02_force_budget_ab.log): force pass
-// 241 -> 232 us from rest, 314 -> 287 us mid-collapse. (Before the mask, 704 with 16-entry lists kept a
-// workgroup under 32 KiB for five per CU: 305 -> 258 us then.)
-constexpr int TF_GCAP = 1000;
+// The force pass stages 32 B per candidate (no hit lists since the mask walk). With 124 VGPRs four
+// workgroups fit a CU, so the plane budget takes what four leave of the LDS: 1270 candidates (40.6 KB);
+// more of the C3 planes (~840 candidates on average) are then staged at once, not row by row in chunks.
+// Interleaved A/B (profiles/r02_nolist_budget_ab.log): 1000 -> 1270 cut the force pass 205 -> 192 us
+// from rest and 233 -> 222 us mid-collapse; five waves per SIMD (96 VGPRs, spills) cost 80 us.
+#ifndef SPH_TF_GCAP
+#define SPH_TF_GCAP 1270
+#endif
+constexpr int TF_GCAP = SPH_TF_GCAP;
 constexpr int TF_FALLBACK = 4 * TF_GCAP;
 
 struct BlockRows {
@@ -376,7 +377,6 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     HitMask hm, uint32_t* __restrict__ paths, DevRange dr) {
     __shared__ float4 sp[TF_GCAP + 4];     // (x, y, z, ρ)
     __shared__ float4 sv[TF_GCAP + 4];     // (u, v, w, P/ρ²)
-    __shared__ uint16_t lst[TT_CAP + 1][TT_BLK];   // + a row for the stores of lanes out of hits
     const int tid = threadIdx.x;
     if (dr.lo) {   // device-resident bounds (slab step); the grid is an upper bound
         ib = (int32_t)*dr.lo;
@@ -396,23 +396,6 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     const float2 ri = rp[ii];
     const BlockRows b = block_rows(g, pos, i0, ilast, pi);
     ForceAcc acc{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int cnt = 0;
-    // hit lists hold LDS byte offsets (slot·16) of the candidate in sp / sv
-    auto at = [](const float4* base, uint32_t off) {
-        return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + off);
-    };
-    auto flush = [&]() {
-        SPH_DIAG_ADD(11, wave_sum(cnt));   // pairs
-        SPH_DIAG_ADD(12, wave_max(cnt));   // flush iterations
-        SPH_DIAG_ADD(13, 1);               // flushes
-        for (int q = 0; __any(q < cnt); ++q) {
-            if (q < cnt) {
-                const uint32_t off = lst[q][tid];
-                pair_force(pk, pi, vi, ri.x, ri.y, at(sp, off), at(sv, off), acc);
-            }
-        }
-        cnt = 0;
-    };
     // hit-mask reader (pass 1's bits of this target, in visit order): rb holds rn bits, LSB next;
     // the remaining words wait in a queue of registers (static indices only). Measured against a
     // one-word prefetch from global memory (with and without 5 waves per SIMD): the queue is 2-3%
@@ -435,82 +418,50 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         }
         return v;
     };
-    // the hits of LDS slots [lo, lo+ln) from the mask, 16 candidates at a time: at most 16 hits, so
-    // one list check per piece; then two hits per iteration with unconditional stores (a lane out of
-    // hits stores to its next free entry, at most row TT_CAP, without advancing)
-    auto hits = [&](int32_t lo, int32_t ln) {
-        for (int32_t off = 0; __any(off < ln); off += 16) {
-            uint32_t m = take(max(0, min(16, ln - off)));
-            SPH_DIAG_ADD(14, wave_max(((int)__popc(m) + 1) >> 1));   // append iterations
-            SPH_DIAG_ADD(15, 1);                                    // pieces
-            if (__any(cnt + (int)__popc(m) > TT_CAP)) flush();
-            const uint32_t base = (uint32_t)(lo + off) * 16u;
-            while (__any(m != 0u)) {
-                lst[cnt][tid] = (uint16_t)(base + 16u * (uint32_t)__builtin_ctz(m | 0x10000u));
-                cnt += m != 0u;
-                m &= m - 1u;
-                lst[cnt][tid] = (uint16_t)(base + 16u * (uint32_t)__builtin_ctz(m | 0x10000u));
-                cnt += m != 0u;
-                m &= m - 1u;
-            }
-        }
-    };
     auto skip = [&](int32_t ln) {
         for (int32_t off = 0; __any(off < ln); off += 32) (void)take(max(0, min(32, ln - off)));
     };
-    // scan LDS slots [lo, lo+ln), appending hits
-    auto scan = [&](int32_t lo, int32_t ln) {
-        for (int t = 0; __any(t < ln); t += 4) {
-            const int32_t j = min(lo + t, TF_GCAP);   // lanes past their range stay in the array
-            const float4 a = sp[j], bb = sp[j + 1], cc = sp[j + 2], d = sp[j + 3];
-            // bitwise &, not &&: every read is unconditional (no exec branches around LDS loads).
-            // The target itself is a hit: its pair adds exactly ±0 (dx = du = 0, q = 0 finite), so
-            // no per-candidate self test is needed.
-            const bool h0 = (t < ln) & (dist2(pi, a) < c.four_h2);
-            const bool h1 = (t + 1 < ln) & (dist2(pi, bb) < c.four_h2);
-            const bool h2 = (t + 2 < ln) & (dist2(pi, cc) < c.four_h2);
-            const bool h3 = (t + 3 < ln) & (dist2(pi, d) < c.four_h2);
-            const uint32_t jb = (uint32_t)j * 16u;
-            lst[cnt][tid] = (uint16_t)jb;         cnt += h0;
-            lst[cnt][tid] = (uint16_t)(jb + 16u); cnt += h1;
-            lst[cnt][tid] = (uint16_t)(jb + 32u); cnt += h2;
-            lst[cnt][tid] = (uint16_t)(jb + 48u); cnt += h3;
-            keep_b128(a, bb, cc, d);
-            if (__any(cnt > TT_CAP - 4)) flush();
+    // The pair loop over the next nb bits of the mask, 128 at a time (four words), one hit per
+    // iteration: bit b is candidate b of up to three windows back to back (lengths l0, e2 − l0 and the
+    // rest), at LDS slot b + d0, d1 or d2. Lanes idle only at the end of a piece (one piece per plane
+    // at C3: 54% -> 66% of lanes busy against the 16-entry hit lists this replaced, 36% -> 53%
+    // mid-collapse). Words are consumed from w0; an emptied w0 takes the next word (an all-zero word
+    // in the middle costs the lane one idle iteration).
+    auto walk = [&](int32_t nb, int32_t l0, int32_t e2, int32_t d0, int32_t d1, int32_t d2) {
+        for (int32_t off = 0; __any(off < nb); off += 128) {
+            const int32_t rem = nb - off;
+            uint32_t w0 = take(min(max(rem, 0), 32)), w1 = take(min(max(rem - 32, 0), 32));
+            uint32_t w2 = take(min(max(rem - 64, 0), 32)), w3 = take(min(max(rem - 96, 0), 32));
+            int32_t nh = (int32_t)(__popc(w0) + __popc(w1) + __popc(w2) + __popc(w3));
+            int32_t base = off;
+            SPH_DIAG_ADD(11, wave_sum(nh));   // pairs
+            SPH_DIAG_ADD(12, wave_max(nh));   // loop iterations
+            SPH_DIAG_ADD(13, 1);              // loops
+            while (__any(nh > 0)) {
+                if (w0 != 0u) {
+                    const int32_t bi = base + (int32_t)__builtin_ctz(w0);
+                    w0 &= w0 - 1u;
+                    --nh;
+                    const int32_t slot = bi + (bi < l0 ? d0 : (bi < e2 ? d1 : d2));
+                    pair_force(pk, pi, vi, ri.x, ri.y, sp[slot], sv[slot], acc);
+                }
+                if (w0 == 0u) {
+                    w0 = w1;
+                    w1 = w2;
+                    w2 = w3;
+                    w3 = 0u;
+                    base += 32;
+                }
+            }
         }
     };
-    // A staged plane whose bits (its three row windows back to back, plen <= 128) come from the mask:
-    // the pair loop walks them directly, one hit per iteration, with no hit list and no 16-hit flushes.
-    // Bit b of the plane is candidate b of the concatenated windows; its LDS slot is b plus the offset
-    // of its row. Words are consumed from w0; an emptied w0 takes the next word (an all-zero word in the
-    // middle costs the lane one idle iteration).
-    auto plane_direct = [&](int32_t plen, const int32_t(&c0)[3], const int32_t(&len)[3], const int32_t(&r0)[3],
-                            const int32_t(&r1)[3]) {
-        uint32_t w0 = take(min(max(plen, 0), 32)), w1 = take(min(max(plen - 32, 0), 32));
-        uint32_t w2 = take(min(max(plen - 64, 0), 32)), w3 = take(min(max(plen - 96, 0), 32));
-        int32_t nh = (int32_t)(__popc(w0) + __popc(w1) + __popc(w2) + __popc(w3));
-        const int32_t l0 = r1[0] - r0[0], e2 = l0 + (r1[1] - r0[1]);
-        const int32_t d0 = r0[0] - c0[0];
-        const int32_t d1 = len[0] + (r0[1] - c0[1]) - l0;
-        const int32_t d2 = len[0] + len[1] + (r0[2] - c0[2]) - e2;
-        int32_t base = 0;
-        SPH_DIAG_ADD(11, wave_sum(nh));
-        SPH_DIAG_ADD(12, wave_max(nh));
-        SPH_DIAG_ADD(13, 1);
-        while (__any(nh > 0)) {
-            if (w0 != 0u) {
-                const int32_t b = base + (int32_t)__builtin_ctz(w0);
-                w0 &= w0 - 1u;
-                --nh;
-                const int32_t slot = b + (b < l0 ? d0 : (b < e2 ? d1 : d2));
-                pair_force(pk, pi, vi, ri.x, ri.y, sp[slot], sv[slot], acc);
-            }
-            if (w0 == 0u) {
-                w0 = w1;
-                w1 = w2;
-                w2 = w3;
-                w3 = 0u;
-                base += 32;
+    // Planes the mask does not cover (a target past its 256 bits): LDS slots [lo, lo+ln) by distance,
+    // in visit order. The target itself is a hit: its pair adds exactly ±0 (dx = du = 0, q = 0 finite).
+    auto dscan = [&](int32_t lo, int32_t ln) {
+        for (int32_t t = 0; __any(t < ln); ++t) {
+            if (t < ln) {
+                const float4 pj = sp[lo + t];
+                if (dist2(pi, pj) < c.four_h2) pair_force(pk, pi, vi, ri.x, ri.y, pj, sv[lo + t], acc);
             }
         }
     };
@@ -542,20 +493,18 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
             __syncthreads();
             stage_plane(c0, len, total, put);
             __syncthreads();
-            if (by_mask && !__any(plen > 128)) {
-                plane_direct(plen, c0, len, r0, r1);
-                continue;
-            }
-            int32_t o = 0;
+            if (by_mask) {
+                const int32_t l0 = r1[0] - r0[0], e2 = l0 + (r1[1] - r0[1]);
+                walk(plen, l0, e2, r0[0] - c0[0], len[0] + (r0[1] - c0[1]) - l0,
+                     len[0] + len[1] + (r0[2] - c0[2]) - e2);
+            } else {
+                int32_t o = 0;
 #pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                if (by_mask)
-                    hits(o + (r0[r] - c0[r]), r1[r] - r0[r]);
-                else
-                    scan(o + (r0[r] - c0[r]), r1[r] - r0[r]);
-                o += len[r];
+                for (int r = 0; r < 3; ++r) {
+                    dscan(o + (r0[r] - c0[r]), r1[r] - r0[r]);
+                    o += len[r];
+                }
             }
-            flush();
             continue;
         }
         // sparse block: offset by offset, in chunks (the chunks of a row take its bits in order), or
@@ -586,10 +535,9 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
                 const int32_t lo = max(r0[r], base) - base;
                 const int32_t wl = max(min(r1[r], base + ln) - base - lo, 0);
                 if (by_mask)
-                    hits(lo, wl);
+                    walk(wl, wl, wl, lo, 0, 0);
                 else
-                    scan(lo, wl);
-                flush();
+                    dscan(lo, wl);
             }
         }
     }
