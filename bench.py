@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event pass")
+    ap.add_argument("--profile-every", type=int, default=4,
+                    help="time the kernels of one step in this many (events in the dispatch packets still cost a "
+                         "C3 step ~15 us, so the timed region samples them)")
     ap.add_argument("--slab", action="store_true", help="run the multi-GPU slab step even at N=1 (rehearsal)")
     ap.add_argument("--rebalance", type=int, default=50, help="slab cut re-balancing interval in steps (0: off)")
     ap.add_argument("--transport", choices=("library", "python"), default="library",
@@ -237,8 +240,15 @@ def rate_table(budget_s: float, gpu_steps: int = 50):
             "gpu_steps": gpu_steps, "rows": rows}
 
 
+def per_step_ms(kstats: dict, steps: int) -> dict:
+    """Mean time per step of each timed scope: mean duration of the sampled launches × launches per step."""
+    return {k: round(v["total_ms"] / v["timed"] * v["launches"] / max(1, steps), 4)
+            for k, v in kstats.items() if v.get("timed", 0) > 0 and v["total_ms"] > 0}
+
+
 def main():
     args = parse()
+    prof = 0 if args.no_profile else max(1, args.profile_every)
     import torch
     if args.table:
         torch.cuda.set_device(0)
@@ -267,7 +277,7 @@ def main():
     if (world > 1 or args.slab or args.strong) and args.transport == "library":
         # the decomposed step inside libsphhip.so: one RCCL communicator, no host read per step
         try:
-            runner = LibraryRankRunner(pkg, args.config, rank, world, local, profile=not args.no_profile,
+            runner = LibraryRankRunner(pkg, args.config, rank, world, local, profile=prof,
                                        rebalance_every=args.rebalance, strong=args.strong)
         except Exception as e:   # noqa: BLE001 - reported, then the torch.distributed slab path (also RCCL)
             print(json.dumps({"rank": rank, "library_transport_failed": str(e)}), file=sys.stderr, flush=True)
@@ -289,11 +299,11 @@ def main():
             runner = None
     if runner is None and (world > 1 or args.slab or args.strong):
         from sph_test_amd import slab
-        runner = slab.SlabRunner(args.config, rank, world, device=local, profile=not args.no_profile,
+        runner = slab.SlabRunner(args.config, rank, world, device=local, profile=bool(prof),
                                  rebalance_every=args.rebalance,
                                  scenario=pkg.config_scenario(args.config) if args.strong else None)
     elif runner is None:
-        runner = SingleRunner(pkg, args.config, local, profile=not args.no_profile)
+        runner = SingleRunner(pkg, args.config, local, profile=prof)
 
     # one explicit HIP stream shared by torch (events, RCCL ordering) and libsphhip
     stream = torch.cuda.Stream()
@@ -328,8 +338,8 @@ def main():
 
     roofline = None
     fi = kstats.get("force_integrate")
-    if fi and fi["launches"] > 0 and fi["total_ms"] > 0:
-        avg_s = fi["total_ms"] / fi["launches"] / 1e3
+    if fi and fi.get("timed", 0) > 0 and fi["total_ms"] > 0:
+        avg_s = fi["total_ms"] / fi["timed"] / 1e3
         bytes_per_launch = FORCE_BYTES_PER_PARTICLE * runner.local_particles()
         achieved = bytes_per_launch / avg_s / 1e9
         pmc = load_pmc(args.config) if world == 1 else {}
@@ -378,8 +388,7 @@ def main():
         mid = {"ms_per_step_mid_collapse": round(mwall * 1e3 / args.mid_steps, 4),
                "value_mid_collapse": round(runner.total_particles() * args.mid_steps / mwall, 1),
                "mid_collapse_state": runner.mid_state(max(done, args.mid_at), args.mid_steps),
-               "kernels_ms_per_step_mid_collapse": {k: round(v["total_ms"] / max(1, args.mid_steps), 4)
-                                                    for k, v in mks.items() if v["total_ms"] > 0}}
+               "kernels_ms_per_step_mid_collapse": per_step_ms(mks, args.mid_steps)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -406,8 +415,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
-            "kernels_ms_per_step": {k: round(v["total_ms"] / max(1, args.steps), 4) for k, v in kstats.items()
-                                    if v["total_ms"] > 0},
+            "kernels_ms_per_step": per_step_ms(kstats, args.steps),
         }
         if mid:
             line.update(mid)
@@ -438,7 +446,9 @@ class LibraryRankRunner:
         if world > 1:
             dist.broadcast(buf, 0)
         torch.cuda.synchronize()
-        self.ctx = pkg.Context(pkg.SPH_MODEL_WCSPH, self.scenario.dim, 1024, device=device, profile=profile)
+        self.ctx = pkg.Context(pkg.SPH_MODEL_WCSPH, self.scenario.dim, 1024, device=device, profile=bool(profile))
+        if profile:
+            self.ctx.set_profile_every(profile)
         self.ctx.comm_init(bytes(buf.cpu().numpy().tobytes()), world, rank)
         self.ctx.set_params(self.params)
         self.ctx.set_rebalance(rebalance_every)
@@ -479,7 +489,9 @@ class SingleRunner:
     def __init__(self, pkg, config, device, profile):
         self.pkg = pkg
         self.config = config
-        self.sim = pkg.SPHSim.from_config(config, device=device, profile=profile)
+        self.sim = pkg.SPHSim.from_config(config, device=device, profile=bool(profile))
+        if profile:
+            self.sim.ctx.set_profile_every(profile)
 
     def bind_stream(self, handle):
         self.sim.ctx.set_stream(handle)

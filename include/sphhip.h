@@ -116,6 +116,7 @@ typedef struct sph_kernel_stat {
     int64_t launches;
     double total_ms;            /* Σ HIP-event durations (SPH_FLAG_PROFILE only) */
     double bytes_per_launch;    /* algorithmic HBM bytes of the last launch */
+    int64_t timed;              /* launches that carried events: total_ms / timed is the mean duration */
 } sph_kernel_stat;
 
 /* ---- lifetime: replaces InitializeBuffers / ReleaseBuffers (controller:373-482) ---- */
@@ -232,6 +233,9 @@ int sph_write_draw_args(sph_ctx* ctx, void* dev_args);
 int sph_get_stats(sph_ctx* ctx, sph_stats* out);
 int sph_get_kernel_stat(sph_ctx* ctx, int32_t index, sph_kernel_stat* out);
 int sph_reset_kernel_stats(sph_ctx* ctx);
+/* SPH_FLAG_PROFILE: time the launches of one step in `every` (default 1; the events cost the step
+ * ~15 us at C3, so a bench samples); the other steps launch without events */
+int sph_set_profile_every(sph_ctx* ctx, int32_t every);
 /* sorted-slot views of the last step (slot order = cell order) */
 int sph_read_sorted_ids(sph_ctx* ctx, int32_t* ids, int32_t count);
 int sph_read_cell_start(sph_ctx* ctx, uint32_t* cell_start, int32_t count);

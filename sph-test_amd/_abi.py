@@ -103,7 +103,7 @@ class SphStats(C.Structure):
 
 class SphKernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("total_ms", C.c_double),
-                ("bytes_per_launch", C.c_double)]
+                ("bytes_per_launch", C.c_double), ("timed", C.c_int64)]
 
 
 class SphSlab(C.Structure):
@@ -168,6 +168,7 @@ SIGNATURES = {
     "sph_get_stats": ([_P, C.POINTER(SphStats)], C.c_int),
     "sph_get_kernel_stat": ([_P, _I, C.POINTER(SphKernelStat)], C.c_int),
     "sph_reset_kernel_stats": ([_P], C.c_int),
+    "sph_set_profile_every": ([_P, _I], C.c_int),
     "sph_read_sorted_ids": ([_P, _P, _I], C.c_int),
     "sph_read_cell_start": ([_P, _P, _I], C.c_int),
     "sph_read_torque_int": ([_P, _P, _I], C.c_int),

@@ -262,12 +262,16 @@ class Context:
             if self._L.sph_get_kernel_stat(self._h, i, C.byref(k)) != A.SPH_OK:
                 break
             out[k.name.decode()] = {"launches": k.launches, "total_ms": k.total_ms,
-                                    "bytes_per_launch": k.bytes_per_launch}
+                                    "bytes_per_launch": k.bytes_per_launch, "timed": k.timed}
             i += 1
         return out
 
     def reset_kernel_stats(self) -> None:
         self._chk("sph_reset_kernel_stats", self._L.sph_reset_kernel_stats(self._h))
+
+    def set_profile_every(self, every: int) -> None:
+        """SPH_FLAG_PROFILE: time the launches of one step in `every` (sph_set_profile_every)."""
+        self._chk("sph_set_profile_every", self._L.sph_set_profile_every(self._h, int(every)))
 
 
 def scenario_params(sc: A.SphScenario):

@@ -703,6 +703,7 @@ static void merge_kid_stats(sph_ctx* ctx) {
             const int i = kstat_index(ctx, s.name.c_str());
             ctx->kstats[i].launches += s.launches;
             ctx->kstats[i].total_ms += s.total_ms;
+            ctx->kstats[i].timed += s.timed;
             ctx->kstats[i].bytes = s.bytes;
         }
     }
@@ -719,6 +720,14 @@ int sph_get_kernel_stat(sph_ctx* ctx, int32_t index, sph_kernel_stat* out) {
     out->launches = k.launches;
     out->total_ms = k.total_ms;
     out->bytes_per_launch = k.bytes;
+    out->timed = k.timed;
+    return SPH_OK;
+}
+
+int sph_set_profile_every(sph_ctx* ctx, int32_t every) {
+    if (!ctx || every < 1) return SPH_ERR_INVALID;
+    ctx->prof_every = every;
+    for (sph_ctx* k : multi_kids(ctx)) k->prof_every = every;
     return SPH_OK;
 }
 
@@ -726,7 +735,11 @@ int sph_reset_kernel_stats(sph_ctx* ctx) {
     if (!ctx) return SPH_ERR_INVALID;
     for (sph_ctx* k : multi_kids(ctx)) sph_reset_kernel_stats(k);
     if (!ctx->pending.empty()) resolve_pending(ctx);
-    for (auto& k : ctx->kstats) { k.launches = 0; k.total_ms = 0.0; }
+    for (auto& k : ctx->kstats) {
+        k.launches = 0;
+        k.timed = 0;
+        k.total_ms = 0.0;
+    }
     return SPH_OK;
 }
 

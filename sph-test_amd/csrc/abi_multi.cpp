@@ -542,7 +542,7 @@ int phase_assemble(RankState& R, bool exact) {
             launch_slab_rec(src, n_ub, ctx->grid, key_base, ctx->vals, ctx->keys2, mv, s, &sizes);  // grid: nl_ub + nr_ub
         }
         CKPT(R, "sizes + slab_rec");
-        KTimer t(ctx, "resort", (double)R.n_ub * (2 * 4 + 2 * 36));
+        KTimer t(ctx, "resort", (double)R.n_ub * (2 * 4 + 2 * 36), true);
         if (ctx->has_left || ctx->has_right)   // without neighbours the own block keeps its cell starts
             launch_slab_cs_old(ctx->cs, ctx->grid.ncells, gyz(ctx), (uint32_t)ctx->grid.gx, ctx->has_left,
                                ctx->has_right, 0, ctx->keys2, 0, 0, 0, s, R.dz);
@@ -594,7 +594,7 @@ int phase_assemble(RankState& R, bool exact) {
     }
     {   // the owned slots of the new order: the column starts the re-sort picked (k_slab_lag copies the
         // ranges for the host at the end of the step)
-        KTimer t(ctx, "density", 24.0 * (double)R.n_ub);
+        KTimer t(ctx, "density", 24.0 * (double)R.n_ub, true);
         launch_density_tiled(ctx->pos, ctx->cs, 0, (int32_t)R.n_ub, ctx->grid, ctx->sc, ctx->rp, hit_mask(ctx), path_ctr(ctx), s,
                              DevRange{&R.dz->pick[1], &R.dz->pick[4]});
     }
@@ -633,7 +633,7 @@ int phase_rho_out(RankState& R, Multi& M) {
 // ---------------------------------------------------------------- phase C: force passes, finish
 void force_dev(sph_ctx* ctx, const uint32_t* lo, const uint32_t* hi, int64_t grid_ub, float dt) {
     if (grid_ub <= 0) return;
-    KTimer t(ctx, "force_integrate", 76.0 * (double)grid_ub);
+    KTimer t(ctx, "force_integrate", 76.0 * (double)grid_ub, true);
     MoverSink mv = mover_sink(ctx);
     mv.err = &ctx->dz->flags;
     launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, (int32_t)grid_ub, ctx->grid, ctx->sc, dt, forcing(ctx),

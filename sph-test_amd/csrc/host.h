@@ -36,6 +36,7 @@ struct KStat {
     int64_t launches = 0;
     double total_ms = 0.0;
     double bytes = 0.0;
+    int64_t timed = 0;   // launches whose events were resolved into total_ms
 };
 
 struct Pending {
@@ -102,6 +103,7 @@ struct sph_ctx {
     sph_drag_input drag{-1, {0.f, 0.f, 0.f}, 0.f};
     std::string err;
     bool profiling = false;
+    int32_t prof_every = 1;   // profiling: time the launches of one step in prof_every (sph_set_profile_every)
     std::vector<sph::KStat> kstats;
     std::vector<sph::Pending> pending;
     std::vector<hipEvent_t> ev_pool;
@@ -192,25 +194,48 @@ int kstat_index(sph_ctx* c, const char* name);
 hipEvent_t take_event(sph_ctx* c);
 void resolve_pending(sph_ctx* c);
 
+// Times a scope of launches on the context's stream when profiling. ext: the scope's kernels launch
+// through SPH_LAUNCH, and the events ride in their dispatch packets (common.h LaunchEvents); otherwise
+// the events are recorded around the scope.
 struct KTimer {
     sph_ctx* c;
     int k;
+    bool ext, on;
     hipEvent_t a = nullptr;
-    KTimer(sph_ctx* ctx, const char* name, double bytes) : c(ctx), k(kstat_index(ctx, name)) {
+    LaunchEvents le;
+    LaunchEvents* prev = nullptr;
+    KTimer(sph_ctx* ctx, const char* name, double bytes, bool ext_events = false)
+        : c(ctx), k(kstat_index(ctx, name)), ext(ext_events),
+          on(ctx->profiling && (ctx->prof_every <= 1 || ctx->steps % ctx->prof_every == 0)) {
         c->kstats[k].launches++;
         c->kstats[k].bytes = bytes;
-        if (c->profiling) {
-            a = take_event(c);
+        if (!on) return;
+        a = take_event(c);
+        if (ext) {
+            le.start = a;
+            le.stop = take_event(c);
+            prev = g_launch_events;
+            g_launch_events = &le;
+        } else {
             (void)hipEventRecord(a, c->stream);
         }
     }
     ~KTimer() {
-        if (c->profiling) {
+        if (!on) return;
+        if (ext) {
+            g_launch_events = prev;
+            if (le.launches == 0) {   // nothing launched: no time
+                c->ev_pool.push_back(le.start);
+                c->ev_pool.push_back(le.stop);
+                return;
+            }
+            c->pending.push_back({k, le.start, le.stop});
+        } else {
             hipEvent_t b = take_event(c);
             (void)hipEventRecord(b, c->stream);
             c->pending.push_back({k, a, b});
-            if (c->pending.size() > 8192) resolve_pending(c);
         }
+        if (c->pending.size() > 8192) resolve_pending(c);
     }
 };
 

@@ -153,6 +153,8 @@ int kstat_index(sph_ctx* c, const char* name) {
     return (int)c->kstats.size() - 1;
 }
 
+thread_local LaunchEvents* g_launch_events = nullptr;
+
 hipEvent_t take_event(sph_ctx* c) {
     if (!c->ev_pool.empty()) {
         hipEvent_t e = c->ev_pool.back();
@@ -168,7 +170,10 @@ void resolve_pending(sph_ctx* c) {
     for (auto& p : c->pending) {
         (void)hipEventSynchronize(p.b);
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) c->kstats[p.k].total_ms += ms;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            c->kstats[p.k].total_ms += ms;
+            c->kstats[p.k].timed++;
+        }
         c->ev_pool.push_back(p.a);
         c->ev_pool.push_back(p.b);
     }

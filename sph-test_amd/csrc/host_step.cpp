@@ -98,7 +98,7 @@ int sort_wcsph(sph_ctx* ctx) {
     const bool many = ctx->resort_mode == 1 && *(volatile uint32_t*)ctx->mv_host > resort_limit(n);
     if (ctx->resort_mode != 0 && !many && ctx->keys_valid && ctx->keys_active == 0 && ctx->sk_valid) {
         {
-            KTimer t(ctx, "resort", (double)n * (2 * 4 + 2 * 36));
+            KTimer t(ctx, "resort", (double)n * (2 * 4 + 2 * 36), true);
             const int used = ctx->mv_par;
             launch_resort(asm_plain(ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->keys, n), ctx->cs,
                           ctx->grid.ncells, n, ctx->mv_count + used, ctx->mv_count + (1 - used), resort_scratch(ctx),
@@ -124,12 +124,12 @@ int step_wcsph(sph_ctx* ctx, float dt) {
     int r = sort_wcsph(ctx);
     if (r != SPH_OK) return r;
     {
-        KTimer t(ctx, "density", 24.0 * n);
+        KTimer t(ctx, "density", 24.0 * n, true);
         density_range(ctx, 0, n);
     }
     const MoverSink mv = mover_sink(ctx);
     {
-        KTimer t(ctx, "force_integrate", 76.0 * n);
+        KTimer t(ctx, "force_integrate", 76.0 * n, true);
         force_range(ctx, 0, n, dt, forcing(ctx), mv);
     }
     // this step's mover count, for the next steps' sort choice (no host wait); every 8th step, as the

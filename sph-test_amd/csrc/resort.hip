@@ -393,11 +393,11 @@ void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const u
                    uint32_t* sk_o, hipStream_t s, CsPick pick, ResortExtra ex) {
     if (n <= 0) return;
     const int32_t nb = (n + MV_BLK - 1) / MV_BLK;
-    k_mv_rank<<<MV_RANK_GRID, MV_BLK, 0, s>>>(count, count_other, cs, w);
-    k_mv_place<<<std::min(nb, 1024), MV_BLK, 0, s>>>(count, cs, w, src, pos_o, vel_o, id_o, sk_o, ex);
+    SPH_LAUNCH(k_mv_rank, MV_RANK_GRID, MV_BLK, 0, s, count, count_other, cs, w);
+    SPH_LAUNCH(k_mv_place, std::min(nb, 1024), MV_BLK, 0, s, count, cs, w, src, pos_o, vel_o, id_o, sk_o, ex);
     // + the cell-start update, after every reader of cs_old (k_mv_rank, k_mv_place)
     const int32_t ncs = (int32_t)((ncells + MV_CS_CELLS) / MV_CS_CELLS);
-    k_mv_merge<<<nb + ncs, MV_BLK, 0, s>>>(src, n, count, w, pos_o, vel_o, id_o, sk_o, nb, cs, ncells, pick, ex);
+    SPH_LAUNCH(k_mv_merge, nb + ncs, MV_BLK, 0, s, src, n, count, w, pos_o, vel_o, id_o, sk_o, nb, cs, ncells, pick, ex);
 }
 
 }  // namespace sph

@@ -374,7 +374,7 @@ __global__ void k_slab_sizes(SlabSizes* __restrict__ dz, SizesIn in) {
 
 void launch_slab_sizes(SlabSizes* dz, const float4* msg_l, const float4* msg_r, int32_t cap_l, int32_t cap_r,
                        int32_t capacity, hipStream_t s) {
-    k_slab_sizes<<<1, 64, 0, s>>>(dz, SizesIn{msg_l, msg_r, cap_l, cap_r, capacity});
+    SPH_LAUNCH(k_slab_sizes, 1, 64, 0, s, dz, SizesIn{msg_l, msg_r, cap_l, cap_r, capacity});
 }
 
 // ρ messages: a 32-byte header (count, capacity) = 4 float2, then the entries
@@ -467,8 +467,8 @@ void launch_slab_cs_old(uint32_t* cs, uint32_t ncells, uint32_t gyz, uint32_t gx
                         int32_t shift, const uint32_t* sk, int32_t nl, int32_t no, int32_t nr, hipStream_t s,
                         const SlabSizes* dz) {
     const uint32_t m = ncells + 2u;
-    k_slab_cs_old<<<(m + SL_BLK - 1) / SL_BLK, SL_BLK, 0, s>>>(cs, ncells, gyz, gx, has_left ? 1 : 0,
-                                                               has_right ? 1 : 0, shift, sk, nl, no, nr, dz);
+    SPH_LAUNCH(k_slab_cs_old, (m + SL_BLK - 1) / SL_BLK, SL_BLK, 0, s, cs, ncells, gyz, gx, has_left ? 1 : 0,
+               has_right ? 1 : 0, shift, sk, nl, no, nr, dz);
 }
 
 void launch_slab_select_columns(const float4* pos, const float4* vel, const int32_t* id, int32_t n, GridDesc g,

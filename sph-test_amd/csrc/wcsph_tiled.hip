@@ -564,15 +564,15 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
                           float2* rp, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr) {
     if (ie > ib)
-        k_density_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, cs, ib, ie, g, c, rp, dr, hm, paths);
+        SPH_LAUNCH(k_density_tiled, (ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s, pos, cs, ib, ie, g, c, rp, dr, hm, paths);
 }
 
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,
                         int32_t ie, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o,
                         uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr) {
     if (ie > ib)
-        k_force_tiled<<<(ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s>>>(pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt, fext_x,
-                                                                         pos_o, vel_o, keys_o, mv, hm, paths, dr);
+        SPH_LAUNCH(k_force_tiled, (ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c,
+                   pair_constants(c), dt, fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr);
 }
 
 }  // namespace sph
