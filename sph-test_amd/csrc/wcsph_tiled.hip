@@ -385,9 +385,9 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
     if (i0 >= n) return;   // whole workgroup: before any barrier
     // Targets stay in sorted order here. Lanes ordered by quarters of fx (a dx plane's hit count follows
-    // fx) fill the plane loop better (66% -> 80% of lanes busy at C3) but run slower, 206 -> 246 us: the
-    // lanes of a wave then read scattered LDS slots instead of their column's shared ones
-    // (profiles/r02_direct_plane_ab.log).
+    // fx) fill the plane loop better (66% -> 80% of lanes busy at C3) but run slower, 206 -> 246 us, and
+    // by halves of fx (83%) 190 -> 229 us: the lanes of a wave then come from more z layers and read
+    // scattered LDS slots (profiles/r02_direct_plane_ab.log, r02_fx2_noself_ab.log).
     const int32_t i = i0 + tid;
     const bool valid = i < n;
     const int32_t ilast = min(i0 + TT_BLK, n) - 1;
