@@ -25,11 +25,15 @@
 namespace sph {
 
 constexpr int TT_BLK = 256;     // targets per workgroup (128 / 192 / 512 measured 13-25% slower)
-// Candidates staged per plane (LDS), density pass: 1500 (24.6 KB) keeps six workgroups per CU (74
-// VGPRs) and stages more sparse planes at once than 1024: 143.5 -> 141.4 us from rest, 166 -> 160 us
-// mid-collapse (profiles/r02_density_budget_ab.log).
+// Candidates staged per plane (LDS), density pass: 1350 (21.7 KB) with the kernel held to 72 VGPRs
+// (amdgpu_waves_per_eu(7)) gives seven workgroups per CU. Against six at 1500 (74 VGPRs): -0.5 us from rest,
+// -2 us mid-collapse; eight at 1200 (64 VGPRs, spills) +19 us (profiles/r02_density_waves_ab.log). 1500
+// against 1024 at six per CU: 143.5 -> 141.4 us from rest (profiles/r02_density_budget_ab.log).
 #ifndef SPH_TT_GCAP
-#define SPH_TT_GCAP 1500
+#define SPH_TT_GCAP 1350
+#endif
+#ifndef SPH_DWAVES
+#define SPH_DWAVES 7
 #endif
 constexpr int TT_GCAP = SPH_TT_GCAP;
 constexpr int TT_FALLBACK = 4 * TT_GCAP;
@@ -195,10 +199,9 @@ __device__ __forceinline__ int32_t quadrant_target(const GridDesc& g, const floa
     return perm[threadIdx.x];
 }
 
-__global__ __launch_bounds__(TT_BLK) void k_density_tiled(const float4* __restrict__ pos,
-                                                          const uint32_t* __restrict__ cs, int32_t ib, int32_t n,
-                                                          GridDesc g, SphConst c, float2* __restrict__ rp,
-                                                          DevRange dr, HitMask hm, uint32_t* __restrict__ paths) {
+__global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAVES))) void k_density_tiled(
+    const float4* __restrict__ pos, const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c,
+    float2* __restrict__ rp, DevRange dr, HitMask hm, uint32_t* __restrict__ paths) {
     __shared__ float4 sp[TT_GCAP + 4];
     __shared__ int32_t perm[TT_BLK];
     __shared__ uint32_t qcnt[TT_BLK / 64][5];

@@ -17,7 +17,7 @@ from __future__ import annotations
 import numpy as np
 
 # wcsph_tiled.hip budgets: targets per workgroup, LDS candidates per plane (density, force)
-TT_BLK, TT_GCAP, TF_GCAP = 256, 1500, 1270   # wcsph_tiled.hip (the plane budgets)
+TT_BLK, TT_GCAP, TF_GCAP = 256, 1350, 1270   # wcsph_tiled.hip (the plane budgets)
 
 
 def wall_state(O, op, nx, ny, nz, dx, dt, seed=11):
