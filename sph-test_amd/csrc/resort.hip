@@ -198,10 +198,12 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_place(const uint32_t* __restrict_
 // workgroup. A workgroup whose counts agree at its start and that holds no mover key leaves its cells.
 // Runs as extra workgroups of k_mv_merge (it needs only k_mv_place's tables), beside the scatter.
 constexpr int MV_CS_CELLS = 4 * MV_BLK;
+// movers staged in LDS for the merge's binary searches (a workgroup's cells or slots rarely hold more)
+constexpr uint32_t MV_LDS = 1024;
 
 // Picks falling in this workgroup's cells are read back once its cells are final.
 static __device__ void mv_cell_start(uint32_t* __restrict__ cs, uint32_t ncells, uint32_t m, const ResortScratch& w,
-                                     uint32_t blk, uint32_t* b, const CsPick& pick) {
+                                     uint32_t blk, uint32_t* b, const CsPick& pick, uint64_t* lms, uint32_t* lmo) {
     const uint32_t k0 = blk * MV_CS_CELLS, k1 = k0 + MV_CS_CELLS;
     const int wv = threadIdx.x >> 6;
     const uint32_t p = wv < 2 ? wave_lower_bound(w.ms, m, comp(wv == 0 ? k0 : k1, 0u))
@@ -210,12 +212,20 @@ static __device__ void mv_cell_start(uint32_t* __restrict__ cs, uint32_t ncells,
     __syncthreads();
     const uint32_t nlo = b[0], nhi = b[1], olo = b[2], ohi = b[3];
     if (!(nlo == olo && nhi == nlo && ohi == olo)) {
+        // the movers' new and old keys in this workgroup's cell range, staged in LDS (block-uniform test)
+        const uint32_t nn = nhi - nlo, no = ohi - olo;
+        const bool staged = nn <= MV_LDS && no <= MV_LDS;
+        if (staged) {
+            for (uint32_t t = threadIdx.x; t < nn; t += MV_BLK) lms[t] = w.ms[nlo + t];
+            for (uint32_t t = threadIdx.x; t < no; t += MV_BLK) lmo[t] = w.mos[olo + t];
+            __syncthreads();
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t k = k0 + j * MV_BLK + threadIdx.x;
             if (k > ncells) break;
-            const uint32_t cn = nlo + lower_bound(w.ms + nlo, nhi - nlo, comp(k, 0u));
-            const uint32_t co = olo + lower_bound(w.mos + olo, ohi - olo, k);
+            const uint32_t cn = nlo + (staged ? lower_bound(lms, nn, comp(k, 0u)) : lower_bound(w.ms + nlo, nn, comp(k, 0u)));
+            const uint32_t co = olo + (staged ? lower_bound(lmo, no, k) : lower_bound(w.mos + olo, no, k));
             cs[k] += cn - co;
         }
     }
@@ -240,8 +250,10 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
                                                      uint32_t ncells, CsPick pick, ResortExtra ex) {
     __shared__ uint32_t wc[MV_BLK / 64];
     __shared__ uint32_t b[4];
+    __shared__ uint64_t lms[MV_LDS];
+    __shared__ uint32_t lmo[MV_LDS];
     if ((int32_t)blockIdx.x >= nb) {   // the cell-start workgroups
-        mv_cell_start(cs, ncells, *mtotal, w, blockIdx.x - nb, b, pick);
+        mv_cell_start(cs, ncells, *mtotal, w, blockIdx.x - nb, b, pick, lms, lmo);
         return;
     }
     resolve_sizes(src, w, n);          // device-sized slab step: nb is an upper bound
@@ -265,9 +277,15 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
     const bool stay = i < n && asm_key(src, i) == ko;
     __syncthreads();
     const uint32_t a = movers_before(i < n && !stay, b[0], wc);
-    if (!stay) return;
     const uint32_t lo = b[1], hi = b[2];
-    const uint32_t below = lo + lower_bound(w.ms + lo, hi - lo, comp(ko, (uint32_t)i));
+    const bool staged = hi - lo <= MV_LDS;   // block-uniform
+    if (staged) {
+        for (uint32_t t = threadIdx.x; t < hi - lo; t += MV_BLK) lms[t] = w.ms[lo + t];
+        __syncthreads();
+    }
+    if (!stay) return;
+    const uint64_t kv = comp(ko, (uint32_t)i);
+    const uint32_t below = lo + (staged ? lower_bound(lms, hi - lo, kv) : lower_bound(w.ms + lo, hi - lo, kv));
     const uint32_t dst = ((uint32_t)i - a) + below;
     if (dst >= w.cap) {
         if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
