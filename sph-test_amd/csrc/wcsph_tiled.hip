@@ -162,6 +162,27 @@ __device__ __forceinline__ void stage_plane(const int32_t (&c0)[3], const int32_
     }
 }
 
+// A plane whose three intervals exceed the LDS budget: consecutive rows that fit together are staged as
+// one group (rows 0+1 or 1+2), the others one by one; a row past the budget goes to big_row (chunks or
+// global memory). Groups run in visit order, so the hit mask's bits are taken in order. At C3 ~10% of
+// the block-planes from rest exceed the budgets: a block in a column of 2 x 2 lattice lines spans ~64
+// layers, and its side rows in columns of 3 lattice lines hold ~1.5x its own count each.
+template <typename G, typename B>
+__device__ __forceinline__ void plane_groups(const int32_t (&len)[3], int32_t cap, G&& group, B&& big_row) {
+    const bool f0 = len[0] <= cap, f1 = len[1] <= cap, f2 = len[2] <= cap;
+    if (f0 && f1 && len[0] + len[1] <= cap) {
+        group(3u);
+        if (f2) group(4u); else big_row(2);
+    } else if (f1 && f2 && len[1] + len[2] <= cap) {
+        if (f0) group(1u); else big_row(0);
+        group(6u);
+    } else {
+        if (f0) group(1u); else big_row(0);
+        if (f1) group(2u); else big_row(1);
+        if (f2) group(4u); else big_row(2);
+    }
+}
+
 // Lanes of one wave take targets of one in-cell quadrant (fx < ½, fy < ½). A side row's trimmed z
 // window and a plane's hit count grow with the target's distance to the neighbour column, so lanes
 // with alike windows idle less in the wave-wide scan and flush loops. Stable within a quadrant;
@@ -277,22 +298,26 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
             lane_window(g, cs, b, valid, 3 * p + r, r0[r], r1[r]);
         }
         const int32_t total = len[0] + len[1] + len[2];
-        if (total <= TT_GCAP) {
+        // rows of mask gm staged back to back (they fit the budget together), each window scanned
+        auto group = [&](uint32_t gm) {
+            int32_t lg[3], tot = 0;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                lg[r] = (gm >> r & 1u) ? len[r] : 0;
+                tot += lg[r];
+            }
             __syncthreads();
-            stage_plane(c0, len, total, [&](int32_t t, int32_t src) { sp[t] = pos[src]; });
+            stage_plane(c0, lg, tot, [&](int32_t t, int32_t src) { sp[t] = pos[src]; });
             __syncthreads();
             int32_t o = 0;
 #pragma unroll
             for (int r = 0; r < 3; ++r) {
-                scan(o + (r0[r] - c0[r]), r1[r] - r0[r]);
-                o += len[r];
+                if (gm >> r & 1u) scan(o + (r0[r] - c0[r]), r1[r] - r0[r]);
+                o += lg[r];
             }
-            continue;
-        }
-        // sparse block: offset by offset, in chunks, or straight from global memory
-        count_path(paths, 0);
-#pragma unroll 1
-        for (int r = 0; r < 3; ++r) {
+        };
+        // a row past the budget: in chunks, or straight from global memory
+        auto big_row = [&](int r) {
             if (len[r] > TT_FALLBACK) {
                 count_path(paths, 1);
                 for (int32_t j = r0[r]; j < r1[r]; ++j) {
@@ -300,7 +325,7 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
                     s += spline_w4(c, r2);
                     one(r2);
                 }
-                continue;
+                return;
             }
 #pragma unroll 1
             for (int32_t base = c0[r]; base < c1[r]; base += TT_GCAP) {
@@ -311,7 +336,13 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
                 const int32_t lo = max(r0[r], base) - base;
                 scan(lo, max(min(r1[r], base + ln) - base - lo, 0));
             }
+        };
+        if (total <= TT_GCAP) {
+            group(7u);
+            continue;
         }
+        count_path(paths, 0);
+        plane_groups(len, TT_GCAP, group, big_row);
     }
     if (!valid) return;
     if (rec && mn > 0 && mw < HM_WORDS)   // the last, partial word: bits [0, mn), zeros above
@@ -494,29 +525,35 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
             count_wave(paths, 4);
             skip(plen);
         }
-        if (total <= TF_GCAP) {
+        // rows of mask gm staged back to back (they fit the budget together); the mask walk takes their
+        // windows' bits in visit order (rows outside gm count zero bits)
+        auto group = [&](uint32_t gm) {
+            int32_t lg[3], wg[3], tot = 0;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                lg[r] = (gm >> r & 1u) ? len[r] : 0;
+                wg[r] = (gm >> r & 1u) ? r1[r] - r0[r] : 0;
+                tot += lg[r];
+            }
             __syncthreads();
-            stage_plane(c0, len, total, put);
+            stage_plane(c0, lg, tot, put);
             __syncthreads();
             if (by_mask) {
-                const int32_t l0 = r1[0] - r0[0], e2 = l0 + (r1[1] - r0[1]);
-                walk(plen, l0, e2, r0[0] - c0[0], len[0] + (r0[1] - c0[1]) - l0,
-                     len[0] + len[1] + (r0[2] - c0[2]) - e2);
+                const int32_t l0 = wg[0], e2 = l0 + wg[1];
+                walk(e2 + wg[2], l0, e2, r0[0] - c0[0], lg[0] + (r0[1] - c0[1]) - l0,
+                     lg[0] + lg[1] + (r0[2] - c0[2]) - e2);
             } else {
                 int32_t o = 0;
 #pragma unroll
                 for (int r = 0; r < 3; ++r) {
-                    dscan(o + (r0[r] - c0[r]), r1[r] - r0[r]);
-                    o += len[r];
+                    if (gm >> r & 1u) dscan(o + (r0[r] - c0[r]), wg[r]);
+                    o += lg[r];
                 }
             }
-            continue;
-        }
-        // sparse block: offset by offset, in chunks (the chunks of a row take its bits in order), or
-        // straight from global memory
-        count_path(paths, 2);
-#pragma unroll 1
-        for (int r = 0; r < 3; ++r) {
+        };
+        // a row past the budget: in chunks (the chunks take the row's bits in order), or straight from
+        // global memory
+        auto big_row = [&](int r) {
             if (len[r] > TF_FALLBACK) {
                 count_path(paths, 3);
                 if (by_mask) skip(r1[r] - r0[r]);
@@ -529,7 +566,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
                                    make_float4(vj.x, vj.y, vj.z, rj.y), acc);
                     }
                 }
-                continue;
+                return;
             }
 #pragma unroll 1
             for (int32_t base = c0[r]; base < c1[r]; base += TF_GCAP) {
@@ -544,7 +581,13 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
                 else
                     dscan(lo, wl);
             }
+        };
+        if (total <= TF_GCAP) {
+            group(7u);
+            continue;
         }
+        count_path(paths, 2);
+        plane_groups(len, TF_GCAP, group, big_row);
     }
     count_wave(paths, 5);   // waves (3 planes each)
     if (!valid) return;
