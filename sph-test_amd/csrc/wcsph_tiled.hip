@@ -27,7 +27,8 @@ namespace sph {
 constexpr int TT_BLK = 256;     // targets per workgroup (128 / 192 / 512 measured 13-25% slower)
 // Candidates staged per plane (LDS), density pass: 1350 (21.7 KB) with the kernel held to 72 VGPRs
 // (amdgpu_waves_per_eu(7)) gives seven workgroups per CU. Against six at 1500 (74 VGPRs): -0.5 us from rest,
-// -2 us mid-collapse; eight at 1200 (64 VGPRs, spills) +19 us (profiles/r02_density_waves_ab.log). 1500
+// -2 us mid-collapse; eight at 1200 (64 VGPRs, spills) +1 to +19 us, five +8 us, four +17 us
+// (profiles/r02_density_waves_ab.log). 1500
 // against 1024 at six per CU: 143.5 -> 141.4 us from rest (profiles/r02_density_budget_ab.log).
 #ifndef SPH_TT_GCAP
 #define SPH_TT_GCAP 1350
@@ -107,6 +108,25 @@ __device__ __forceinline__ void count_path(uint32_t* paths, int k) {
 __device__ __forceinline__ void count_wave(uint32_t* paths, int k) {
     if (paths && lane_id() == 0) atomicAdd(paths + k, 1u);
 }
+
+#ifdef SPH_BTIME
+// Diagnostic builds only (-DSPH_BTIME): each workgroup's start and end (s_memrealtime, 100 MHz) of the last
+// launch of each pass, read by sph_debug_block_times (scripts/block_times.py).
+constexpr int BT_MAX = 16384;
+__device__ uint64_t g_btime[2][BT_MAX][2];
+#define SPH_BT_START const uint64_t bt0_ = __builtin_amdgcn_s_memrealtime()
+#define SPH_BT_END(kid)                                                                                      \
+    do {                                                                                                     \
+        __syncthreads();                                                                                     \
+        if (threadIdx.x == 0 && blockIdx.x < BT_MAX) {                                                       \
+            g_btime[kid][blockIdx.x][0] = bt0_;                                                              \
+            g_btime[kid][blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();                                  \
+        }                                                                                                    \
+    } while (0)
+#else
+#define SPH_BT_START ((void)0)
+#define SPH_BT_END(kid) ((void)0)
+#endif
 
 #ifdef SPH_DIAG
 // Diagnostic builds only (-DSPH_DIAG): lane-utilisation counters in paths[8..16) (sph_debug_pass_counts).
@@ -232,6 +252,7 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
     }
     const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
     if (i0 >= n) return;   // whole workgroup: before any barrier
+    SPH_BT_START;
     // quadrant order, measured against plain sorted order (138 -> 154 us) and halves by fx or by fy
     // (+1 to +2 us) at C3 (profiles/r02_pass1_lane_order_ab.log)
     const int32_t i = quadrant_target(g, pos, i0, n, perm, qcnt);
@@ -344,6 +365,7 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
         count_path(paths, 0);
         plane_groups(len, TT_GCAP, group, big_row);
     }
+    SPH_BT_END(0);
     if (!valid) return;
     if (rec && mn > 0 && mw < HM_WORDS)   // the last, partial word: bits [0, mn), zeros above
         *wp = __builtin_bitreverse32(ml << (32 - mn));
@@ -420,6 +442,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     }
     const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
     if (i0 >= n) return;   // whole workgroup: before any barrier
+    SPH_BT_START;
     // Targets stay in sorted order here. Lanes ordered by quarters of fx (a dx plane's hit count follows
     // fx) fill the plane loop better (66% -> 80% of lanes busy at C3) but run slower, 206 -> 246 us, and
     // by halves of fx (83%) 190 -> 229 us: the lanes of a wave then come from more z layers and read
@@ -590,6 +613,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         plane_groups(len, TF_GCAP, group, big_row);
     }
     count_wave(paths, 5);   // waves (3 planes each)
+    SPH_BT_END(1);
     if (!valid) return;
     float nv[3] = {vi.x + (acc.ax + c.gx + fext_x) * dt, vi.y + (acc.ay + c.gy) * dt, vi.z + (acc.az + c.gz) * dt};
     float np[3] = {pi.x + (nv[0] + acc.sx) * dt, pi.y + (nv[1] + acc.sy) * dt, pi.z + (nv[2] + acc.sz) * dt};
@@ -622,5 +646,12 @@ void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, 
         SPH_LAUNCH(k_force_tiled, (ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c,
                    pair_constants(c), dt, fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr);
 }
+
+#ifdef SPH_BTIME
+extern "C" int sph_debug_block_times(uint64_t* out, int32_t count) {   // count <= 2 * BT_MAX * 2
+    if (!out || count < 0 || count > 2 * BT_MAX * 2) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_btime), (size_t)count * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // namespace sph
