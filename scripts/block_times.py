@@ -23,6 +23,7 @@ def report(label):
     buf = np.zeros(2 * BT_MAX * 2, np.uint64)
     assert L.sph_debug_block_times(buf.ctypes.data_as(C.c_void_p), len(buf)) == 0
     t = buf.reshape(2, BT_MAX, 2)[:, :nb, :].astype(np.float64) * 10.0 / 1e3   # 100 MHz ticks -> us
+    np.save(Path(__file__).resolve().parent.parent / "gpurun_out" / f"block_times_{label}.npy", t)
     for k, name in enumerate(("density", "force")):
         st, en = t[k, :, 0], t[k, :, 1]
         t0 = st.min()
