@@ -47,6 +47,9 @@ constexpr int TT_FALLBACK = 4 * TT_GCAP;
 #define SPH_TF_GCAP 1270
 #endif
 constexpr int TF_GCAP = SPH_TF_GCAP;
+#ifndef SPH_WALK_UNROLL
+#define SPH_WALK_UNROLL 4
+#endif
 constexpr int TF_FALLBACK = 4 * TF_GCAP;
 
 struct BlockRows {
@@ -496,20 +499,27 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
             SPH_DIAG_ADD(11, wave_sum(nh));   // pairs
             SPH_DIAG_ADD(12, wave_max(nh));   // loop iterations
             SPH_DIAG_ADD(13, 1);              // loops
+            // SPH_WALK_UNROLL hits per loop trip: fewer loop and exec-mask instructions per hit, and the next
+            // hit's slot and LDS reads can issue before the current pair body ends. Force pass 189 -> 181 us
+            // from rest, 214 -> 203 us mid-collapse at 4 (2: 184, 3: 182 us; the word shift as selects instead
+            // of a branch: no change; profiles/r02_walk_unroll_ab.log).
             while (__any(nh > 0)) {
-                if (w0 != 0u) {
-                    const int32_t bi = base + (int32_t)__builtin_ctz(w0);
-                    w0 &= w0 - 1u;
-                    --nh;
-                    const int32_t slot = bi + (bi < l0 ? d0 : (bi < e2 ? d1 : d2));
-                    pair_force(pk, pi, vi, ri.x, ri.y, sp[slot], sv[slot], acc);
-                }
-                if (w0 == 0u) {
-                    w0 = w1;
-                    w1 = w2;
-                    w2 = w3;
-                    w3 = 0u;
-                    base += 32;
+#pragma unroll
+                for (int u = 0; u < SPH_WALK_UNROLL; ++u) {
+                    if (w0 != 0u) {
+                        const int32_t bi = base + (int32_t)__builtin_ctz(w0);
+                        w0 &= w0 - 1u;
+                        --nh;
+                        const int32_t slot = bi + (bi < l0 ? d0 : (bi < e2 ? d1 : d2));
+                        pair_force(pk, pi, vi, ri.x, ri.y, sp[slot], sv[slot], acc);
+                    }
+                    if (w0 == 0u) {
+                        w0 = w1;
+                        w1 = w2;
+                        w2 = w3;
+                        w3 = 0u;
+                        base += 32;
+                    }
                 }
             }
         }
