@@ -22,6 +22,8 @@ import sys
 import time
 from pathlib import Path
 
+import numpy as np
+
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
@@ -29,9 +31,18 @@ import __graft_entry__ as GE  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 # SURVEY.md §8d, algorithmic bytes per particle-step of the force+visc+XSPH+KDK pass: read x,v,ρ,P 32 B
-# + write x,v 24 B (SoA fp32, neighbour reads counted once) + this design's hit mask, 8 words read 32 B
-# (pass 1 writes it)
-FORCE_BYTES_PER_PARTICLE = 88.0
+# + write x,v 24 B (SoA fp32, neighbour reads counted once). roofline.frac prices the kernel on these.
+FORCE_BYTES_PER_PARTICLE = 56.0
+# this design's own traffic on top: pass 2 reads pass 1's hit mask, 8 words = 32 B per
+# target (pass 1 writes the same 32 B). Reported apart, as roofline.frac_design, never as frac.
+HIT_MASK_BYTES_PER_PARTICLE = 32.0
+
+
+def step_bytes_per_particle(key_bits: int, ncells: int, n: int) -> float:
+    """algorithmic bytes of one whole step per particle, B = 152 + 20·P + 8·C/N (hash 20,
+    sort 20 per 8-bit pass, reorder 52, cell start 4 + 8·C/N, density 20, force 56)."""
+    passes = (int(key_bits) + 7) // 8
+    return 152.0 + 20.0 * passes + 8.0 * float(ncells) / max(1, int(n))
 
 
 def parse():
@@ -58,6 +69,13 @@ def parse():
                     help="N=1: also time this many steps from a mid-collapse state (0: skip)")
     ap.add_argument("--mid-at", type=int, default=5000,
                     help="step count (from the lattice) at which the mid-collapse timing starts")
+    ap.add_argument("--no-check", action="store_true",
+                    help="N > 1: skip the decomposed step's correctness check against one context")
+    ap.add_argument("--no-strong-extra", action="store_true",
+                    help="N = 4 / 8: skip the extra strong-scaling line of BASELINE's C4 / C5")
+    ap.add_argument("--watchdog", type=float, default=900.0,
+                    help="seconds after which a rank stuck in a phase (a peer failed inside a collective) "
+                         "prints the failure and exits 3")
     ap.add_argument("--table", action="store_true",
                     help="print the GPU / 1-thread / all-thread CPU rate table (SURVEY §8d) instead of the bench line")
     return ap.parse_args()
@@ -75,16 +93,17 @@ def force_kernel_name() -> str:
     return "k_force_tiled"
 
 
-def load_clock():
+def load_clock(code_hash: str):
     """Effective shader clocks from the committed rocprofv3 GRBM passes (profiles/clock_*.json,
-    scripts/gpu_clock.sh): the force pass on its longest dispatches (C5) and the VALU microbenchmark."""
+    scripts/gpu_clock.sh): the force pass on its longest dispatches (C5) and the VALU microbenchmark.
+    The force-pass clock is used only from a file stamped with the code objects that are running."""
     out = {}
     for f in sorted((ROOT / "profiles").glob("clock_*.json")):
         try:
             d = json.loads(f.read_text())
         except Exception:
             continue
-        if "k_force_tiled" in d.get("C5", {}):
+        if "k_force_tiled" in d.get("C5", {}) and d.get("device_code_hash") == code_hash:
             out["force_ghz"] = d["C5"]["k_force_tiled"]["clock_ghz_median"]
             out["force_src"] = f"{f.name}: C5 k_force_tiled, {d['C5']['k_force_tiled']['mean_us']:.0f} us dispatches"
         if "k_fma" in d.get("valu", {}):
@@ -93,11 +112,14 @@ def load_clock():
     return out
 
 
-def load_pmc(config: str):
+def load_pmc(config: str, code_hash: str):
     """Per-launch counters of the dominant kernel from the committed rocprofv3 PMC passes
     (profiles/pmc_*.json): HBM bytes = FETCH_SIZE×2 + WRITE_SIZE (MI355X_MICROARCH.md §HBM) and
-    SQ_INSTS_VALU (wave-level VALU instructions)."""
-    out = {}
+    SQ_INSTS_VALU (wave-level VALU instructions). Only a file stamped with the device-code hash of the
+    library that is running counts (scripts/pmc_summary.py writes it): counters of other kernels are
+    refused, and `note` says why the line then carries no traffic."""
+    out = {"note": f"no profiles/pmc_*.json for {config} stamped with device_code_hash {code_hash} "
+                   f"(re-take them with scripts/gpu_pmc.sh + scripts/pmc_summary.py)"}
     for f in sorted((ROOT / "profiles").glob("pmc_*.json")):
         try:
             d = json.loads(f.read_text())
@@ -105,6 +127,9 @@ def load_pmc(config: str):
             continue
         if d.get("config") != config:
             continue
+        if d.get("device_code_hash") != code_hash:
+            continue
+        out = {"file": f.name}
         if d.get("kernel_bytes", {}).get("force_integrate"):
             out["traffic"] = d["kernel_bytes"]["force_integrate"]
         for ks in d.get("kernels", {}).values():
@@ -273,36 +298,45 @@ def main():
         torch.cuda.set_device(0)
     pkg = GE.load_package()
 
-    runner = None
-    if (world > 1 or args.slab or args.strong) and args.transport == "library":
-        # the decomposed step inside libsphhip.so: one RCCL communicator, no host read per step
-        try:
-            runner = LibraryRankRunner(pkg, args.config, rank, world, local, profile=prof,
-                                       rebalance_every=args.rebalance, strong=args.strong)
-        except Exception as e:   # noqa: BLE001 - reported, then the torch.distributed slab path (also RCCL)
-            print(json.dumps({"rank": rank, "library_transport_failed": str(e)}), file=sys.stderr, flush=True)
-            runner = None
-    if runner is not None and world > 1:
-        # every rank checks one step of the in-library path; if any rank failed, all take the
-        # torch.distributed slab path instead (the same kernels, RCCL through torch)
-        ok = 1
-        try:
-            runner.step(1)
-            torch.cuda.synchronize()
-        except Exception as e:   # noqa: BLE001 - reported
-            ok = 0
-            print(json.dumps({"rank": rank, "library_step_failed": str(e)}), file=sys.stderr, flush=True)
-        flag = torch.tensor([ok], dtype=torch.int32, device="cuda" if backend == "nccl" else "cpu")
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if int(flag.item()) == 0:
-            runner.close()
-            runner = None
-    if runner is None and (world > 1 or args.slab or args.strong):
+    dev_kind = "cuda" if backend == "nccl" else "cpu"
+    multi = world > 1 or args.slab or args.strong
+    watchdog = Watchdog(rank, world, args.watchdog)
+
+    def fail_line(key: str, err: str, extra=None):
+        """A multi-rank failure: one JSON line (rank 0) with the failure instead of a number, exit 3."""
+        if rank == 0:
+            line = {"metric": METRIC, "value": None, "unit": "particle-steps/s", "n_gpus": world, key: err}
+            line.update(extra or {})
+            print(json.dumps(line), flush=True)
+        print(json.dumps({"rank": rank, key: err}), file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(3)
+
+    check = None
+    if multi and world > 1 and not args.no_check:
+        # correctness of the decomposed step through the SAME transport before anything is timed
+        watchdog.arm("slab_check", 300)
+        check = slab_check(pkg, args.transport, rank, world, local, dist, dev_kind)
+        watchdog.disarm()
+        if not check["ok"]:
+            fail_line("slab_check_failed", check.get("error", "mismatch"), {"slab_check": check})
+
+    if multi and args.transport == "library":
+        # the decomposed step inside libsphhip.so: one RCCL communicator, no host read per step. No
+        # fallback: a failure on any rank ends the run with the failure in the line.
+        watchdog.arm("library transport setup", 300)
+        scenario = pkg.config_scenario(args.config) if args.strong else None
+        runner, err = make_library_runner(pkg, args.config, scenario, rank, world, local, prof, args.rebalance,
+                                          dist, dev_kind)
+        if err:
+            fail_line("library_transport_failed", err)
+        watchdog.disarm()
+    elif multi:
         from sph_test_amd import slab
         runner = slab.SlabRunner(args.config, rank, world, device=local, profile=bool(prof),
                                  rebalance_every=args.rebalance,
                                  scenario=pkg.config_scenario(args.config) if args.strong else None)
-    elif runner is None:
+    else:
         runner = SingleRunner(pkg, args.config, local, profile=prof)
 
     # one explicit HIP stream shared by torch (events, RCCL ordering) and libsphhip
@@ -316,37 +350,75 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    runner.step(args.warmup)
-    barrier()
-    runner.reset_stats()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    runner.step(args.steps)
-    ev1.record(stream)
-    barrier()
-    wall = time.perf_counter() - t0
-    gpu_ms = ev0.elapsed_time(ev1)
-    el = torch.tensor([wall], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    wall = float(el.item())
+    def timed(r, warmup, steps):
+        """W untimed steps, then K steps between barrier + synchronize pairs; max wall over ranks."""
+        watchdog.arm("timed steps", args.watchdog)
+        try:
+            r.step(warmup)
+            barrier()
+            r.reset_stats()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            barrier()
+            t = time.perf_counter()
+            e0.record(stream)
+            r.step(steps)
+            e1.record(stream)
+            barrier()
+            w = time.perf_counter() - t
+        except Exception as e:   # noqa: BLE001 - reported; the other ranks end by the watchdog
+            fail_line("step_failed", f"rank {rank}: {e}")
+        watchdog.disarm()
+        el = torch.tensor([w], dtype=torch.float64, device=dev_kind)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el.item()), e0.elapsed_time(e1)
+
+    wall, gpu_ms = timed(runner, args.warmup, args.steps)
     n_total = runner.total_particles()
     value = n_total * args.steps / wall
     kstats = runner.kernel_stats()
 
     roofline = None
     fi = kstats.get("force_integrate")
+    code_hash = pkg._abi.device_code_hash()
     if fi and fi.get("timed", 0) > 0 and fi["total_ms"] > 0:
         avg_s = fi["total_ms"] / fi["timed"] / 1e3
-        bytes_per_launch = FORCE_BYTES_PER_PARTICLE * runner.local_particles()
+        n_local = runner.local_particles()
+        bytes_per_launch = FORCE_BYTES_PER_PARTICLE * n_local
         achieved = bytes_per_launch / avg_s / 1e9
-        pmc = load_pmc(args.config) if world == 1 else {}
+        design = (FORCE_BYTES_PER_PARTICLE + HIT_MASK_BYTES_PER_PARTICLE) * n_local / avg_s / 1e9
+        if world == 1:
+            pmc = load_pmc(args.config, code_hash)
+        else:
+            pmc = {"note": "PMC counters are taken on one GPU (profiles/pmc_*.json); none at N > 1"}
+        traffic = pmc.get("traffic")
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": pmc.get("traffic"),
+                    "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
                     "kernel": force_kernel_name(), "kernel_avg_us": round(avg_s * 1e6, 2),
-                    "bytes_per_launch": bytes_per_launch}
+                    "bytes_per_launch": bytes_per_launch,
+                    "algorithmic_bytes_per_particle": FORCE_BYTES_PER_PARTICLE,
+                    "bytes_source": "SURVEY.md §8d: force+visc+XSPH+KDK reads x,v,rho,P 32 B, writes x,v 24 B",
+                    "frac_design": round(design / PEAK_HBM_GBS, 5),
+                    "design_bytes_per_particle": FORCE_BYTES_PER_PARTICLE + HIT_MASK_BYTES_PER_PARTICLE,
+                    "design_bytes_note": "+32 B hit-mask read (pass 1 writes it; DESIGN.md §4)",
+                    "device_code_hash": code_hash}
+        if traffic:
+            roofline["traffic_over_algorithmic"] = round(traffic / bytes_per_launch, 3)
+            roofline["traffic_source"] = pmc.get("file")
+        else:
+            roofline["traffic_note"] = pmc.get("note")
+        try:
+            st = runner.grid_stats()
+            b = step_bytes_per_particle(st["key_bits"], st["ncells"], n_local)
+            ms = wall * 1e3 / args.steps
+            roofline["step"] = {"bytes_per_particle": round(b, 2), "achieved": round(b * n_local / (ms * 1e-3) / 1e9, 2),
+                                "frac": round(b * n_local / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 5),
+                                "ms_per_step": round(ms, 4),
+                                "source": "SURVEY.md §8d: B = 152 + 20*P + 8*C/N over the whole step, against "
+                                          f"ms_per_step (P = {(st['key_bits'] + 7) // 8} 8-bit sort passes, "
+                                          f"C = {st['ncells']} cells, N = {n_local})"}
+        except Exception as e:   # noqa: BLE001 - reported in the line
+            roofline["step"] = {"error": str(e)}
         if "valu_instr" in pmc:
             # what bounds the neighbour pass in practice (DESIGN.md §4): VALU issue, from the same
             # kernel's committed PMC pass and this run's kernel time, priced two ways: against the
@@ -357,7 +429,7 @@ def main():
                                 "unit": "G wave-instr/s", "frac": round(va / PEAK_VALU_WAVE_INSTR_PER_S, 4),
                                 "source": "rocprofv3 SQ_INSTS_VALU per launch (profiles/pmc_C3.json); peak measured by "
                                           "scripts/valu_peak.hip, long dispatches (profiles/r02_valu_peak_long.log)"}
-            clk = load_clock()
+            clk = load_clock(code_hash)
             if "force_ghz" in clk:
                 spec = 256 * 4 * 0.5 * clk["force_ghz"] * 1e9
                 roofline["valu"].update({
@@ -394,9 +466,33 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.config, args.cpu_seconds)
 
+    workload = runner.workload("strong" if args.strong else "weak")
+    local_n = runner.local_particles()
+    transport = getattr(runner, "transport", "single" if world == 1 else "python")
+    runner.close()
+
+    strong = None
+    if world in STRONG_CONFIGS and not args.strong and args.transport == "library" and not args.no_strong_extra:
+        # BASELINE.json's own multi-GPU configurations in the same invocation: C4 (sloshing) decomposed
+        # over 4 GPUs, C5 over 8 (strong scaling), beside the C3xN weak line above
+        cfg = STRONG_CONFIGS[world]
+        watchdog.arm(f"strong {cfg} setup", 300)
+        r2, err = make_library_runner(pkg, cfg, pkg.config_scenario(cfg), rank, world, local, 0, args.rebalance,
+                                      dist, dev_kind)
+        if err:
+            fail_line("library_transport_failed", f"strong {cfg}: {err}")
+        watchdog.disarm()
+        r2.bind_stream(stream.cuda_stream)
+        w2, g2 = timed(r2, args.warmup, args.steps)
+        strong = {"config": cfg, "workload": r2.workload("strong"), "particles": r2.total_particles(),
+                  "value": round(r2.total_particles() * args.steps / w2, 1), "unit": "particle-steps/s",
+                  "ms_per_step": round(w2 * 1e3 / args.steps, 4), "gpu_event_ms_per_step": round(g2 / args.steps, 4),
+                  "scaling": "strong", "steps": args.steps, "warmup": args.warmup}
+        r2.close()
+
     if rank == 0:
         line = {
-            "metric": "particle-steps/sec + ms/step at 1M particles; 1/2/4/8 MI355X scaling",
+            "metric": METRIC,
             "value": round(value, 1),
             "unit": "particle-steps/s",
             "n_gpus": world,
@@ -408,10 +504,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (dam-break lattice, seed 1234)",
-            "config": {"workload": runner.workload("strong" if args.strong else "weak"), "particles": n_total,
-                       "particles_per_gpu": runner.local_particles(), "h_over_dx": 1.2,
+            "config": {"workload": workload, "particles": n_total,
+                       "particles_per_gpu": local_n, "h_over_dx": 1.2,
                        "parallelism": f"slab{world}" if world > 1 else "single",
-                       "transport": getattr(runner, "transport", "single" if world == 1 else "python")},
+                       "transport": transport},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
@@ -419,42 +515,198 @@ def main():
         }
         if mid:
             line.update(mid)
+        if check is not None:
+            line["slab_check"] = check
+            line["slab_check_max_dx"] = check.get("max_dx")
+        if strong is not None:
+            line["strong_baseline_config"] = strong
         print(json.dumps(line), flush=True)
-    runner.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+METRIC = "particle-steps/sec + ms/step at 1M particles; 1/2/4/8 MI355X scaling"
+# BASELINE.json configs[3] / configs[4]: the strong lines a 4- and an 8-GPU run add to the weak C3xN line
+STRONG_CONFIGS = {4: "C4", 8: "C5"}
+
+
+class Watchdog:
+    """Ends a rank whose phase does not finish in time (a collective whose peer failed never returns):
+    prints the failure (rank 0: as the JSON line) and exits 3, instead of hanging until an outer limit."""
+
+    def __init__(self, rank, world, default_s):
+        self.rank, self.world, self.default = rank, world, default_s
+        self.t = None
+
+    def arm(self, what, seconds=None):
+        import threading
+        self.disarm()
+        secs = seconds or self.default
+
+        def fire():
+            err = f"rank {self.rank}: '{what}' did not finish in {secs} s (a rank failed or hung)"
+            if self.rank == 0:
+                print(json.dumps({"metric": METRIC, "value": None, "unit": "particle-steps/s", "n_gpus": self.world,
+                                  "watchdog": err}), flush=True)
+            print(json.dumps({"rank": self.rank, "watchdog": err}), file=sys.stderr, flush=True)
+            os._exit(3)
+        self.t = threading.Timer(secs, fire)
+        self.t.daemon = True
+        self.t.start()
+
+    def disarm(self):
+        if self.t is not None:
+            self.t.cancel()
+            self.t = None
+
+
+def agree(ok: bool, dist, dev_kind) -> bool:
+    """True on every rank iff every rank's ok is True (an all-reduce MIN)."""
+    import torch
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev_kind)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return int(flag.item()) == 1
+
+
+def make_library_runner(pkg, config, scenario, rank, world, device, profile, rebalance_every, dist, dev_kind):
+    """LibraryRankRunner in phases, each followed by an agreement over all ranks, so a rank that fails
+    before a collective (ncclCommInitRank, the first step's exchanges) never leaves the others waiting
+    in it: (runner, None) on every rank, or (None, error) on every rank."""
+    runner, err = None, None
+    try:
+        runner = LibraryRankRunner(pkg, config, scenario, rank, world, device, profile, rebalance_every, dist, dev_kind)
+    except Exception as e:   # noqa: BLE001 - agreed on below
+        err = f"rank {rank} create: {e}"
+    for phase in ("join", "init"):
+        if world > 1 and not agree(err is None, dist, dev_kind):
+            if runner is not None:
+                runner.ctx.close()
+            return None, err or f"another rank failed before '{phase}'"
+        try:
+            getattr(runner, phase)()
+        except Exception as e:   # noqa: BLE001 - agreed on below
+            err = f"rank {rank} {phase}: {e}"
+    if world > 1 and not agree(err is None, dist, dev_kind):
+        if runner is not None:
+            runner.ctx.close()
+        return None, err or "another rank failed in init"
+    if err:
+        return None, err
+    return runner, None
+
+
+def check_scenario(pkg, world):
+    """The multi-rank check's workload: a dam-break whose fluid column and tank grow with the ranks
+    (24 lattice columns and 60 dx of tank per rank: ~10 grid columns per slab at h = 1.2 dx)."""
+    return pkg.make_scenario(pkg.SPH_SCENARIO_DAMBREAK, 3, 24 * world, 32, 32, 60 * world, 48, 32, dx=0.01, seed=99)
+
+
+CHECK_STEPS, CHECK_REBALANCE = 60, 20
+# owned positions against one context on rank 0 after CHECK_STEPS: the decomposition changes only the
+# order of key ties in the neighbour sums (fp32 rounding); tests/test_gpu_multi.py measures the
+# difference of the same check on local groups of 2 to 8 slabs
+CHECK_MAX_DX = 2e-5
+
+
+def slab_check(pkg, transport, rank, world, device, dist, dev_kind):
+    """Before timing N > 1: run the decomposed step through the same transport on a small dam-break for
+    CHECK_STEPS steps with re-balancing every CHECK_REBALANCE, gather every rank's owned particles on
+    rank 0 and compare them with a single context there. Returns a dict (the same on every rank)."""
+    sc = check_scenario(pkg, world)
+    out = {"ok": True, "steps": CHECK_STEPS, "rebalance_every": CHECK_REBALANCE, "transport": transport,
+           "scenario": f"dam-break column {sc.nx}x{sc.ny}x{sc.nz}, tank {sc.tx}x{sc.ty}x{sc.tz} dx"}
+    if transport == "library":
+        r, err = make_library_runner(pkg, "check", sc, rank, world, device, 0, CHECK_REBALANCE, dist, dev_kind)
+        if err:
+            return {**out, "ok": False, "error": f"library transport: {err}"}
+    else:
+        from sph_test_amd import slab
+        r = slab.SlabRunner("check", rank, world, device=device, scenario=sc, rebalance_every=CHECK_REBALANCE)
+    err = None
+    try:
+        r.step(CHECK_STEPS)
+        rec = r.owned()
+    except Exception as e:   # noqa: BLE001 - agreed on below
+        err, rec = f"rank {rank}: {e}", np.zeros((0, 8), np.float32)
+    r.close()
+    if not agree(err is None, dist, dev_kind):
+        return {**out, "ok": False, "error": err or "another rank's step failed"}
+    allrec = [None] * world
+    dist.all_gather_object(allrec, rec)
+    res = None
+    if rank == 0:
+        rec = np.concatenate(allrec)
+        ids = rec[:, 6].view(np.int32)
+        sim = pkg.SPHSim(sc, device=device)
+        sim.step(CHECK_STEPS)
+        xs, vs = sim.positions(), sim.velocities()
+        sim.close()
+        res = {"particles": len(xs), "owned_total": int(len(rec))}
+        if len(rec) != len(xs) or not np.array_equal(np.sort(ids), np.arange(len(xs))):
+            res.update(ok=False, error="the ranks do not own every particle exactly once")
+        else:
+            order = np.argsort(ids)
+            dx = float(np.abs(rec[order, 0:3] - xs).max())
+            dv = float(np.abs(rec[order, 3:6] - vs).max())
+            res.update(max_dx=dx, max_dv=dv, max_dx_limit=CHECK_MAX_DX, bitwise=bool(dx == 0.0 and dv == 0.0))
+            if not np.isfinite(rec[:, :6]).all() or not dx <= CHECK_MAX_DX:
+                res.update(ok=False, error=f"max |dx| {dx:.3g} > {CHECK_MAX_DX:g} against one context")
+    box = [res]
+    dist.broadcast_object_list(box, 0)
+    out.update(box[0])
+    return out
 
 
 class LibraryRankRunner:
     """One rank of the in-library decomposed step (sphhip.h sph_comm_init): rank 0 makes the RCCL
     unique id, torch.distributed hands its 128 bytes to every rank, and from then on sph_step runs the
     whole decomposed step (halos, re-sort, density, ρ halo overlapped with the interior force pass,
-    re-balancing) with no host read per step."""
+    re-balancing) with no host read per step. Built in three phases (make_library_runner agrees on
+    each one's outcome over all ranks before the next, collective one starts)."""
     transport = "library-rccl"
 
-    def __init__(self, pkg, config, rank, world, device, profile, rebalance_every, strong):
+    def __init__(self, pkg, config, scenario, rank, world, device, profile, rebalance_every, dist, dev_kind):
         import torch
-        import torch.distributed as dist
         from sph_test_amd import slab
         from sph_test_amd.context import comm_unique_id
-        self.pkg, self.config, self.world = pkg, config, world
-        self.scenario = pkg.config_scenario(config) if strong else slab.weak_scenario(config, world)
+        self.pkg, self.config, self.world, self.rank = pkg, config, world, rank
+        self.scenario = scenario if scenario is not None else slab.weak_scenario(config, world)
         self.params, self.dt = pkg.scenario_params(self.scenario)
-        buf = torch.zeros(128, dtype=torch.uint8, device=torch.device("cuda", device))
+        self.rebalance_every, self.profile = rebalance_every, profile
+        buf = torch.zeros(128, dtype=torch.uint8, device=torch.device(dev_kind, device) if dev_kind == "cuda" else "cpu")
         if rank == 0:
             buf.copy_(torch.frombuffer(bytearray(comm_unique_id()), dtype=torch.uint8))
         if world > 1:
             dist.broadcast(buf, 0)
-        torch.cuda.synchronize()
+        self.uid = bytes(buf.cpu().numpy().tobytes())
         self.ctx = pkg.Context(pkg.SPH_MODEL_WCSPH, self.scenario.dim, 1024, device=device, profile=bool(profile))
         if profile:
             self.ctx.set_profile_every(profile)
-        self.ctx.comm_init(bytes(buf.cpu().numpy().tobytes()), world, rank)
+
+    def join(self):
+        """ncclCommInitRank: collective over all ranks."""
+        self.ctx.comm_init(self.uid, self.world, self.rank)
+
+    def init(self):
         self.ctx.set_params(self.params)
-        self.ctx.set_rebalance(rebalance_every)
+        self.ctx.set_rebalance(self.rebalance_every)
         self.ctx.init_scenario(self.scenario)
         d = self.ctx.decomposition()
         self.n_total, self.cut = d.total, (d.cut.cx_lo, d.cut.cx_hi)
+
+    def grid_stats(self):
+        st = self.ctx.stats()
+        return {"key_bits": st.key_bits, "ncells": st.grid[0] * st.grid[1] * st.grid[2]}
+
+    def owned(self):
+        """This rank's owned particles as 8-float records (x, y, z, u, v, w, id-bits, ρ)."""
+        import ctypes as C
+        A = self.pkg._abi
+        rec = np.empty((max(self.ctx.stats().capacity, 1), 8), np.float32)
+        n = C.c_int32()
+        A.check("sph_slab_read_owned", self.ctx._L.sph_slab_read_owned(self.ctx.handle, A.ptr(rec), len(rec), C.byref(n)),
+                self.ctx.handle)
+        return rec[: n.value]
 
     def bind_stream(self, handle):
         self.ctx.set_stream(handle)
@@ -517,6 +769,10 @@ class SingleRunner:
         T = start * self.sim.dt * (2 * 9.81 / L) ** 0.5
         return (f"{self.config} steps {start}-{start + steps} from the lattice: t = {start * self.sim.dt:.3f} s, "
                 f"T = t*sqrt(2g/L) = {T:.2f} (surge front running along the floor)")
+
+    def grid_stats(self):
+        st = self.sim.ctx.stats()
+        return {"key_bits": st.key_bits, "ncells": st.grid[0] * st.grid[1] * st.grid[2]}
 
     def workload(self, scaling: str = "weak"):
         sc = self.sim.scenario

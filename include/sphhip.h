@@ -181,6 +181,10 @@ int sph_set_particles_aos84(sph_ctx* ctx, int32_t first, int32_t count, const vo
  *      (controller:265-331: torque clear, ClearGrid, BuildHashGrid, ApplySPHForces,
  *       ApplyDragForce, UpdateMotion, UpdateRotation) ---- */
 int sph_step(sph_ctx* ctx, float dt, int32_t nsteps);
+/* the simulated time t (Σ dt; Time.time in the reference's frame loop) the next step starts at: the
+ * sloshing forcing f_ext(t) reads it. Uploads and scenario inits reset it to 0; this sets it after an
+ * upload, e.g. to resume a saved state. Not for ndev > 1 groups. */
+int sph_set_sim_time(sph_ctx* ctx, double t);
 /* replaces HandleMouseDrag → dragInputBuffer.SetData (controller:975-1034) */
 int sph_set_drag(sph_ctx* ctx, const sph_drag_input* drag);
 /* replaces: adhesionConnectionBuffer.SetData + the ApplyAdhesionConstraints /

@@ -9,6 +9,10 @@ import json
 import os
 import sys
 from collections import defaultdict
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import __graft_entry__ as GE  # noqa: E402
 
 
 def one(d):
@@ -43,7 +47,8 @@ def one(d):
 
 
 def main():
-    res = {"method": "GRBM_GUI_ACTIVE / 8 / kernel duration, rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT"}
+    res = {"method": "GRBM_GUI_ACTIVE / 8 / kernel duration, rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT",
+           "device_code_hash": GE.load_package()._abi.device_code_hash()}
     for arg in sys.argv[2:]:
         label, d = arg.split("=", 1)
         res[label] = one(d)

@@ -9,6 +9,10 @@ import json
 import os
 import sys
 from collections import defaultdict
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import __graft_entry__ as GE  # noqa: E402
 
 
 def main(root, out, config):
@@ -27,7 +31,10 @@ def main(root, out, config):
         if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
             m["hbm_bytes_per_launch"] = (2 * m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024
         summary.setdefault(var, {})[k] = m
-    doc = {"config": config, "source": "rocprofv3 --kernel-trace --pmc, one counter group per run", "kernels": summary}
+    A = GE.load_package()._abi
+    # the kernels these counters belong to: bench.py uses the file only for the same code objects
+    doc = {"config": config, "source": "rocprofv3 --kernel-trace --pmc, one counter group per run",
+           "device_code_hash": A.device_code_hash(), "lib": str(A.lib_path().name), "kernels": summary}
     force = {}
     for var, ks in summary.items():
         for k in ("k_force_tiled", "k_force_integrate"):

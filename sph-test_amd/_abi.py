@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 from pathlib import Path
+from typing import Optional
 
 import numpy as np
 
@@ -149,6 +150,7 @@ SIGNATURES = {
     "sph_get_particles_aos84": ([_P, _I, _I, _P], C.c_int),
     "sph_set_particles_aos84": ([_P, _I, _I, _P], C.c_int),
     "sph_step": ([_P, C.c_float, _I], C.c_int),
+    "sph_set_sim_time": ([_P, C.c_double], C.c_int),
     "sph_set_drag": ([_P, C.POINTER(SphDragInput)], C.c_int),
     "sph_set_adhesion": ([_P, _P, _I], C.c_int),
     "sph_read_adhesion_terms": ([_P, _P, _I], C.c_int),
@@ -219,7 +221,7 @@ def lib() -> C.CDLL:
             import torch  # noqa: F401
         except ImportError:
             pass
-        path = Path(os.environ.get("SPHHIP_LIB", str(LIB_PATH)))
+        path = lib_path()
         if not path.exists():
             raise RuntimeError(f"libsphhip.so not built at {path}: run __graft_entry__.build()")
         L = C.CDLL(str(path))
@@ -229,6 +231,32 @@ def lib() -> C.CDLL:
             fn.restype = res
         _lib = L
     return _lib
+
+
+def lib_path() -> Path:
+    """The library lib() loads (SPHHIP_LIB overrides the in-tree build, for variant A/Bs)."""
+    return Path(os.environ.get("SPHHIP_LIB", str(LIB_PATH)))
+
+
+def device_code_hash(path: Optional[Path] = None) -> str:
+    """sha256 (16 hex digits) of the library's gfx950 code objects: the ELF section `.hip_fatbin` of
+    libsphhip.so. It identifies the kernels that ran, independent of host-only changes, and stamps the
+    committed counter files (profiles/pmc_*.json, clock_*.json) so that bench.py uses counters only
+    of the kernels it is timing."""
+    import hashlib
+    import struct
+    data = Path(path or lib_path()).read_bytes()
+    if data[:4] != b"\x7fELF" or data[4] != 2:
+        raise RuntimeError(f"{path}: not a 64-bit ELF")
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize) for i in range(shnum)]
+    stro = secs[shstrndx][4]
+    for name, _typ, _flags, _addr, off, size in secs:
+        end = data.index(b"\0", stro + name)
+        if data[stro + name:end] == b".hip_fatbin":
+            return hashlib.sha256(data[off:off + size]).hexdigest()[:16]
+    raise RuntimeError(f"{path}: no .hip_fatbin section")
 
 
 def ptr(a) -> C.c_void_p:

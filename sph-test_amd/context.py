@@ -136,6 +136,10 @@ class Context:
     def step(self, dt: float, nsteps: int = 1) -> None:
         self._chk("sph_step", self._L.sph_step(self._h, dt, nsteps))
 
+    def set_sim_time(self, t: float) -> None:
+        """The simulated time the next step starts at (the sloshing forcing reads it)."""
+        self._chk("sph_set_sim_time", self._L.sph_set_sim_time(self._h, float(t)))
+
     def set_drag(self, selected_id: int, target, strength: float) -> None:
         d = A.SphDragInput(selected_id, (C.c_float * 3)(*target), strength)
         self._chk("sph_set_drag", self._L.sph_set_drag(self._h, C.byref(d)))

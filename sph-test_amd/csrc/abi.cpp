@@ -411,6 +411,13 @@ int sph_step(sph_ctx* ctx, float dt, int32_t nsteps) {
     return SPH_OK;
 }
 
+int sph_set_sim_time(sph_ctx* ctx, double t) {
+    if (!ctx || !(t >= 0.0)) return SPH_ERR_INVALID;
+    if (is_group(ctx)) return fail(ctx, SPH_ERR_STATE, "sph_set_sim_time: one-GPU contexts and RCCL ranks only");
+    ctx->sim_time = t;
+    return SPH_OK;
+}
+
 int sph_set_drag(sph_ctx* ctx, const sph_drag_input* drag) {
     if (!ctx || !drag) return SPH_ERR_INVALID;
     ctx->drag = *drag;

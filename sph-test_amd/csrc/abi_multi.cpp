@@ -46,7 +46,8 @@ struct RankState {
     float2* rho_in[2] = {nullptr, nullptr};
     int32_t rcap_out[2] = {0, 0}, rcap_in[2] = {0, 0};
     int32_t c1o[2] = {0, 0}, c1i[2] = {0, 0}, c2o[2] = {0, 0}, c2i[2] = {0, 0};   // this step's capacities
-    uint32_t* cnt_dev = nullptr;   // [4] received counts (exact-size steps over RCCL)
+    uint32_t* cnt_dev = nullptr;   // [4] received counts (exact-size steps over RCCL); [2]: every rank's
+                                   // SZ_* flags, max-reduced over the communicator each step (RCCL, world > 1)
     uint32_t* lag = nullptr;       // pinned, mapped: LAG_SLOTS x LAG_WORDS (launch_slab_lag)
     hipEvent_t lag_ev[LAG_SLOTS] = {};
     int64_t cin_hist[LAG_SLOTS] = {};   // Σ records received per step (slot bound bookkeeping)
@@ -83,7 +84,30 @@ namespace {
 int32_t cap_of(uint32_t cnt) {
     // the count two steps ago + 25% + 512 (a one-column halo changes by far less in two steps), whole 256s
     const int64_t c = (int64_t)cnt + cnt / 4 + 512;
+    // SPH_DEBUG_MSG_CAP (tests only): cap every lag-sized message, to force the overflow path
+    if (const char* e = std::getenv("SPH_DEBUG_MSG_CAP"))
+        if (std::atoll(e) > 0) return (int32_t)std::atoll(e);
     return (int32_t)std::min<int64_t>((c + 255) / 256 * 256, INT32_MAX / 4);
+}
+
+// Neighbouring slabs of a local group on different GPUs copy halos device to device: enable peer
+// access both ways so the copies go GPU to GPU over xGMI (a copy without it may be staged through host
+// memory). A pair that cannot reach each other is an error, not a silent slow path.
+int enable_peers(sph_ctx* ctx, int da, int db) {
+    if (da == db) return SPH_OK;
+    for (int k = 0; k < 2; ++k) {
+        const int from = k ? db : da, to = k ? da : db;
+        int can = 0;
+        HIPCHK(hipDeviceCanAccessPeer(&can, from, to));
+        if (!can) return fail(ctx, SPH_ERR_HIP, "device %d cannot access device %d (no peer path for the slab halo)", from, to);
+        HIPCHK(hipSetDevice(from));
+        const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+            return fail(ctx, SPH_ERR_HIP, "hipDeviceEnablePeerAccess(%d -> %d): %s", from, to, hipGetErrorString(e));
+        (void)hipGetLastError();   // clear an "already enabled"
+    }
+    HIPCHK(hipSetDevice(ctx->device));
+    return SPH_OK;
 }
 
 int global_columns(const sph_params& p) {
@@ -192,6 +216,7 @@ int rank_init(RankState& R) {
     HIPCHK(hipMemset(R.dz, 0, sizeof(SlabSizes)));
     R.c->dz = R.dz;
     HIPCHK(hipMalloc((void**)&R.cnt_dev, 4 * sizeof(uint32_t)));
+    HIPCHK(hipMemset(R.cnt_dev, 0, 4 * sizeof(uint32_t)));
     HIPCHK(hipMemset(R.c->sdev + SDEV_TOTALS, 0, 2 * sizeof(uint32_t)));
     HIPCHK(hipHostMalloc((void**)&R.lag, LAG_SLOTS * LAG_WORDS * sizeof(uint32_t), hipHostMallocMapped));
     std::memset(R.lag, 0, LAG_SLOTS * LAG_WORDS * sizeof(uint32_t));
@@ -510,6 +535,10 @@ int exchange2_start(Multi& M) {
         NCCLCHK(ncclRecv(R.rho_in[s], (size_t)(RHO_HDR + R.c2i[s]) * sizeof(float2), ncclUint8, peer, M.comm, R.comm));
     }
     NCCLCHK(ncclGroupEnd());
+    // every rank's sticky SZ_* flags as of its density pass, max-reduced (any nonzero = a rank flagged):
+    // the step's lag record carries this value, so all ranks stop at the same later step. One word on
+    // the comm stream, in flight with the interior force pass like the ρ halo.
+    NCCLCHK(ncclAllReduce(&R.dz->flags, R.cnt_dev + 2, 1, ncclUint32, ncclMax, M.comm, R.comm));
     HIPCHK(hipEventRecord(R.ev_rho_recv, R.comm));
     return SPH_OK;
 }
@@ -517,6 +546,7 @@ int exchange2_start(Multi& M) {
 // ---------------------------------------------------------------- phase B: assemble, density, ρ out
 int phase_assemble(RankState& R, bool exact) {
     sph_ctx* ctx = R.c;
+    ctx->hm_valid = false;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     // the layout [left | own | right] from the message headers: in k_slab_rec on device-sized steps
@@ -576,8 +606,9 @@ int phase_assemble(RankState& R, bool exact) {
         HIPCHK(hipStreamSynchronize(s));
         SlabSizes h;
         HIPCHK(hipMemcpy(&h, R.dz, sizeof h, hipMemcpyDeviceToHost));
-        if (h.flags & (SZ_OVF_MSG | SZ_OVF_CAP))
-            return fail(ctx, SPH_ERR_CAPACITY, "slab step: halo message overflow or slots over capacity (rank %d)", R.rank);
+        // an overflow here is not returned on this rank alone (its neighbours would wait in the next
+        // exchange): the sizes are clamped (nl = nr = 0 past the capacity), the step completes, and the
+        // sticky flag stops every rank together two steps on (multi_one_step)
         ctx->dz_ahead = false;
         ctx->o0 = (int32_t)h.o0;
         ctx->o1 = (int32_t)h.o1;
@@ -595,7 +626,7 @@ int phase_assemble(RankState& R, bool exact) {
     {   // the owned slots of the new order: the column starts the re-sort picked (k_slab_lag copies the
         // ranges for the host at the end of the step)
         KTimer t(ctx, "density", 24.0 * (double)R.n_ub, true);
-        launch_density_tiled(ctx->pos, ctx->cs, 0, (int32_t)R.n_ub, ctx->grid, ctx->sc, ctx->rp, hit_mask(ctx), path_ctr(ctx), s,
+        launch_density_tiled(ctx->pos, ctx->cs, 0, (int32_t)R.n_ub, ctx->grid, ctx->sc, ctx->rp, hit_mask_write(ctx), path_ctr(ctx), s,
                              DevRange{&R.dz->pick[1], &R.dz->pick[4]});
     }
     CKPT(R, "density");
@@ -637,7 +668,7 @@ void force_dev(sph_ctx* ctx, const uint32_t* lo, const uint32_t* hi, int64_t gri
     MoverSink mv = mover_sink(ctx);
     mv.err = &ctx->dz->flags;
     launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, (int32_t)grid_ub, ctx->grid, ctx->sc, dt, forcing(ctx),
-                       ctx->pos2, ctx->vel2, ctx->keys, mv, hit_mask(ctx), path_ctr(ctx), ctx->stream, DevRange{lo, hi});
+                       ctx->pos2, ctx->vel2, ctx->keys, mv, hit_mask_read(ctx), path_ctr(ctx), ctx->stream, DevRange{lo, hi});
 }
 
 int phase_interior(RankState& R, float dt) {
@@ -651,7 +682,7 @@ int phase_interior(RankState& R, float dt) {
     return SPH_OK;
 }
 
-int phase_finish(RankState& R, float dt, int64_t step) {
+int phase_finish(RankState& R, float dt, int64_t step, bool global_flags) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
@@ -676,7 +707,8 @@ int phase_finish(RankState& R, float dt, int64_t step) {
     const int k = (int)(step % LAG_SLOTS);
     launch_slab_lag(R.dz, ctx->has_left ? 1 : 0, ctx->has_right ? 1 : 0, ctx->sdev + SDEV_TOTALS,
                     R.left >= 0 ? R.msg_in[0] : nullptr, R.right >= 0 ? R.msg_in[1] : nullptr,
-                    R.left >= 0 ? R.rho_in[0] : nullptr, R.right >= 0 ? R.rho_in[1] : nullptr, R.lag + k * LAG_WORDS, s);
+                    R.left >= 0 ? R.rho_in[0] : nullptr, R.right >= 0 ? R.rho_in[1] : nullptr,
+                    global_flags ? R.cnt_dev + 2 : nullptr, R.lag + k * LAG_WORDS, s);
     if (R.left >= 0 || R.right >= 0) HIPCHK(hipEventRecord(R.lag_ev[k], s));   // read two steps on
     R.cin_hist[k] = R.c1i[0] + R.c1i[1];
     R.n_prev_ub = R.n_ub;
@@ -690,27 +722,41 @@ int phase_finish(RankState& R, float dt, int64_t step) {
 int rebalance(Multi& M, sph_ctx* pctx) {
     sph_ctx* ctx = pctx;
     const int G = global_columns(M.ranks[0].c->prm);
-    std::vector<int64_t> hist(G, 0), part(G);
+    // hist[G]: ranks that failed to read their counts (a flagged step): over RCCL every rank still joins
+    // the all-reduce, so all of them learn of the failure together and none waits in a collective alone
+    std::vector<int64_t> hist(G + 1, 0), part(G);
+    int local_rc = SPH_OK;
+    std::string local_err;
     for (auto& R : M.ranks) {
         int r = sync_dz(R);
-        if (r != SPH_OK) return r;
-        r = sph_slab_column_counts(R.c, part.data(), G);
-        if (r != SPH_OK) return r;
+        if (r == SPH_OK) r = sph_slab_column_counts(R.c, part.data(), G);
+        if (r != SPH_OK) {
+            if (M.mode != 2) return fail(ctx, r, "%s", R.c->err.c_str());
+            local_rc = r;
+            local_err = R.c->err;
+            hist[G] += 1;
+            break;
+        }
         for (int c = 0; c < G; ++c) hist[c] += part[c];
     }
     if (M.mode == 2 && M.world > 1) {
         sph_ctx* rc = M.ranks[0].c;
         HIPCHK(hipSetDevice(rc->device));
-        if (M.hist_cap < G) {
+        if (M.hist_cap < G + 1) {
             dfree(M.hist_dev);
-            HIPCHK(hipMalloc((void**)&M.hist_dev, (size_t)G * sizeof(int64_t)));
-            M.hist_cap = G;
+            HIPCHK(hipMalloc((void**)&M.hist_dev, (size_t)(G + 1) * sizeof(int64_t)));
+            M.hist_cap = G + 1;
         }
-        HIPCHK(hipMemcpyAsync(M.hist_dev, hist.data(), (size_t)G * 8, hipMemcpyHostToDevice, rc->stream));
-        NCCLCHK(ncclAllReduce(M.hist_dev, M.hist_dev, (size_t)G, ncclInt64, ncclSum, M.comm, rc->stream));
-        HIPCHK(hipMemcpyAsync(hist.data(), M.hist_dev, (size_t)G * 8, hipMemcpyDeviceToHost, rc->stream));
+        HIPCHK(hipMemcpyAsync(M.hist_dev, hist.data(), (size_t)(G + 1) * 8, hipMemcpyHostToDevice, rc->stream));
+        NCCLCHK(ncclAllReduce(M.hist_dev, M.hist_dev, (size_t)(G + 1), ncclInt64, ncclSum, M.comm, rc->stream));
+        HIPCHK(hipMemcpyAsync(hist.data(), M.hist_dev, (size_t)(G + 1) * 8, hipMemcpyDeviceToHost, rc->stream));
         HIPCHK(hipStreamSynchronize(rc->stream));
     }
+    if (local_rc != SPH_OK) return fail(ctx, local_rc, "%s", local_err.c_str());
+    if (hist[G] > 0)
+        return fail(ctx, SPH_ERR_CAPACITY, "re-balancing at step %lld: %lld rank(s) reported a flagged slab step",
+                    (long long)M.steps, (long long)hist[G]);
+    hist.resize(G);
     const std::vector<sph_slab> nc = rebalance_cuts(M.cuts, hist);
     bool changed = false;
     for (int r = 0; r < M.world; ++r) changed |= nc[r].cx_lo != M.cuts[r].cx_lo || nc[r].cx_hi != M.cuts[r].cx_hi;
@@ -774,12 +820,27 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
     if (exact) {
         if ((r = exchange_counts(M, pctx)) != SPH_OK) return r;
     } else {
+        // an overflow flagged two steps ago (or earlier; flags are sticky) stops every rank at this same
+        // step, before any exchange: over RCCL the lag record holds the flags max-reduced over all ranks
+        // (exchange2_start), in a local group the host ORs its ranks' own
+        uint32_t flags = 0;
+        for (auto& R : M.ranks) {
+            if (R.left < 0 && R.right < 0) continue;
+            const uint32_t* L = lag_slot(R, M.steps - 2, R.c, &r);
+            if (r != SPH_OK) return r;
+            flags |= L[9];
+        }
+        if (flags)
+            return fail(pctx, SPH_ERR_CAPACITY, "slab step %lld: a rank flagged%s%s%s%s (flags %#x, seen two steps on)",
+                        (long long)M.steps, (flags & SZ_OVF_MSG) ? " a halo message overflow" : "",
+                        (flags & SZ_OVF_CAP) ? " slots over capacity" : "",
+                        (flags & SZ_RHO_MISMATCH) ? " a ghost density count mismatch" : "",
+                        (flags & SZ_OVF_MOVERS) ? " a mover list / re-sort destination out of range" : "", flags);
         for (auto& R : M.ranks) {
             if (R.left < 0 && R.right < 0) continue;   // no messages: nothing to size
             // the counts of two steps before: both neighbours read the same numbers
             const uint32_t* L = lag_slot(R, M.steps - 2, R.c, &r);
             if (r != SPH_OK) return r;
-            if (L[9]) return sync_dz(R);   // an overflow flagged two steps ago: report it
             R.c1o[0] = R.left >= 0 ? cap_of(L[0]) : 0;
             R.c1o[1] = R.right >= 0 ? cap_of(L[1]) : 0;
             R.c1i[0] = R.left >= 0 ? cap_of(L[2]) : 0;
@@ -805,7 +866,7 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
     for (auto& R : M.ranks)
         if ((r = phase_interior(R, dt)) != SPH_OK) return r;
     for (auto& R : M.ranks)
-        if ((r = phase_finish(R, dt, M.steps)) != SPH_OK) return r;
+        if ((r = phase_finish(R, dt, M.steps, M.mode == 2 && M.world > 1)) != SPH_OK) return r;
     M.steps++;
     return SPH_OK;
 }
@@ -881,6 +942,10 @@ int multi_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
             int rc = sph_create(&kc, (ctx->device + r) % nvis, &k);
             if (rc != SPH_OK) return fail(ctx, rc, "slab context %d on device %d", r, (ctx->device + r) % nvis);
             M.kids.push_back(k);
+        }
+        for (int r = 0; r + 1 < M.world; ++r) {   // halo neighbours r, r + 1
+            const int rc = enable_peers(ctx, M.kids[r]->device, M.kids[r + 1]->device);
+            if (rc != SPH_OK) return rc;
         }
         M.ranks.resize(M.world);
         for (int r = 0; r < M.world; ++r) {

@@ -248,6 +248,7 @@ int sph_slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void
 // full-sort steps). force_full: take the full radix sort even when the incremental one is possible.
 int sph::slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void* dev_right, int32_t nr,
                        bool force_full) {
+    ctx->hm_valid = false;   // a new slot order
     const int32_t no = ctx->o1 - ctx->o0;
     const int64_t n = (int64_t)nl + no + nr;
     if (n > ctx->capacity) return fail(ctx, SPH_ERR_CAPACITY, "slab needs %lld slots > capacity %d", (long long)n, ctx->capacity);
@@ -349,7 +350,7 @@ int sph_slab_density(sph_ctx* ctx) {
     if (ctx->rng_pending) {   // owned range [sdev[1], sdev[4]) on the device; grid sized for all slots
         KTimer t(ctx, "density", 24.0 * ctx->n);
         const DevRange dr{ctx->sdev + 1, ctx->sdev + 4};
-        launch_density_tiled(ctx->pos, ctx->cs, 0, ctx->n, ctx->grid, ctx->sc, ctx->rp, hit_mask(ctx), path_ctr(ctx), ctx->stream, dr);
+        launch_density_tiled(ctx->pos, ctx->cs, 0, ctx->n, ctx->grid, ctx->sc, ctx->rp, hit_mask_write(ctx), path_ctr(ctx), ctx->stream, dr);
         HIPCHK(hipGetLastError());
         return SPH_OK;
     }

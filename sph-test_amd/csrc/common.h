@@ -205,7 +205,7 @@ __device__ __forceinline__ void slab_sizes_store(SlabSizes* dz, uint32_t nl, uin
     dz->nr = nr;
     dz->no = no;
     dz->n = nl + no + nr;
-    dz->flags = f;
+    atomicOr(&dz->flags, f);   // other workgroups of k_slab_rec may be setting SZ_OVF_MOVERS meanwhile
 }
 #endif
 
@@ -439,10 +439,10 @@ void launch_slab_pack_rho(const float2* rp, SlabSizes* dz, int32_t side, float2*
 void launch_slab_unpack_rho(float2* rp, SlabSizes* dz, int32_t side, const float2* msg, int32_t cap, hipStream_t s);
 // per-step counts for the host's lagged capacity choice, written to mapped pinned memory:
 // out[0..1] sent records (left, right), out[2..3] received headers, out[4..5] ρ sent, out[6..7] ρ received,
-// out[8] assembled slots, out[9] flags
+// out[8] assembled slots, out[9] flags (gflags non-null: that word instead, every rank's flags reduced)
 void launch_slab_lag(SlabSizes* dz, int32_t has_left, int32_t has_right, const uint32_t* totals,
                      const float4* msg_in_l, const float4* msg_in_r, const float2* rho_in_l, const float2* rho_in_r,
-                     uint32_t* out, hipStream_t s);
+                     const uint32_t* gflags, uint32_t* out, hipStream_t s);
 
 // owned slots [o0, o0+n) -> records of 8 floats (x,y,z,u,v,w,id-bits,ρ)
 void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, const float2* rp,

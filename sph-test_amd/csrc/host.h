@@ -112,6 +112,7 @@ struct sph_ctx {
                                  // [8, 16): lane-utilisation counters of -DSPH_DIAG builds)
     bool count_paths = false;    // armed by the first counter read: counted launches pay for atomics
     uint32_t* hmask = nullptr;   // Model S: HM_WORDS x capacity hit-mask words (pass 1 -> pass 2)
+    bool hm_valid = false;       // hmask describes the current slot order (a density pass ran since the last sort)
     // slab decomposition (SPEC_SPH.md §3)
     bool slab = false;
     sph_slab sl{};
@@ -242,7 +243,11 @@ struct KTimer {
 // per-step launch sequences (host_step.cpp)
 void swap_sv(sph_ctx* c);
 int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id, const uint32_t** sorted_keys = nullptr);
-HitMask hit_mask(const sph_ctx* ctx);   // Model S pass 1 -> pass 2 (common.h)
+// Model S pass 1 -> pass 2 (common.h): the density pass writes the mask (and marks it valid for the
+// current slot order); the force pass reads it only while valid, else scans by distance. Every change
+// of the slot order (sorts, uploads, assembles, re-cuts) invalidates it.
+HitMask hit_mask_write(sph_ctx* ctx);
+HitMask hit_mask_read(const sph_ctx* ctx);
 inline uint32_t* path_ctr(const sph_ctx* ctx) { return ctx->count_paths ? ctx->paths : nullptr; }
 void density_range(sph_ctx* ctx, int32_t b, int32_t e);
 void force_range(sph_ctx* ctx, int32_t b, int32_t e, float dt, float fext, MoverSink mv = MoverSink{});

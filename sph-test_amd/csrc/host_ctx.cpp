@@ -141,6 +141,7 @@ int derive(sph_ctx* ctx) {
 void invalidate_sort(sph_ctx* c) {
     c->keys_valid = false;
     c->sk_valid = false;
+    c->hm_valid = false;
 }
 
 // ---------------------------------------------------------------- profiling

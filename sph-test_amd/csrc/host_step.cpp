@@ -51,17 +51,22 @@ int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id, const uint32_t** sorted_
     return SPH_OK;
 }
 
-HitMask hit_mask(const sph_ctx* ctx) {
+HitMask hit_mask_write(sph_ctx* ctx) {
+    ctx->hm_valid = ctx->hmask != nullptr;
     return HitMask{ctx->hmask, (uint32_t)std::max(ctx->capacity, 1)};
 }
 
+HitMask hit_mask_read(const sph_ctx* ctx) {
+    return ctx->hm_valid ? HitMask{ctx->hmask, (uint32_t)std::max(ctx->capacity, 1)} : HitMask{};
+}
+
 void density_range(sph_ctx* ctx, int32_t b, int32_t e) {
-    launch_density_tiled(ctx->pos, ctx->cs, b, e, ctx->grid, ctx->sc, ctx->rp, hit_mask(ctx), path_ctr(ctx), ctx->stream);
+    launch_density_tiled(ctx->pos, ctx->cs, b, e, ctx->grid, ctx->sc, ctx->rp, hit_mask_write(ctx), path_ctr(ctx), ctx->stream);
 }
 
 void force_range(sph_ctx* ctx, int32_t b, int32_t e, float dt, float fext, MoverSink mv) {
     launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, b, e, ctx->grid, ctx->sc, dt, fext, ctx->pos2, ctx->vel2,
-                       ctx->keys, mv, hit_mask(ctx), path_ctr(ctx), ctx->stream);
+                       ctx->keys, mv, hit_mask_read(ctx), path_ctr(ctx), ctx->stream);
 }
 
 // f_ext(t) of SPEC_SPH.md §2 at the context's simulated time (sloshing; 0 otherwise)
@@ -93,6 +98,7 @@ uint32_t resort_limit(int32_t n) {
 
 int sort_wcsph(sph_ctx* ctx) {
     const int32_t n = ctx->n;
+    ctx->hm_valid = false;
     // adaptive mode: the latest mover count the host has seen (a step or more behind the device;
     // both paths give the same permutation, so the choice only affects time)
     const bool many = ctx->resort_mode == 1 && *(volatile uint32_t*)ctx->mv_host > resort_limit(n);

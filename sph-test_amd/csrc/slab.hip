@@ -417,7 +417,8 @@ void launch_slab_unpack_rho(float2* rp, SlabSizes* dz, int32_t side, const float
 __global__ void k_slab_lag(SlabSizes* __restrict__ dz, int32_t has_left, int32_t has_right,
                            const uint32_t* __restrict__ totals, const float4* __restrict__ msg_in_l,
                            const float4* __restrict__ msg_in_r, const float2* __restrict__ rho_in_l,
-                           const float2* __restrict__ rho_in_r, uint32_t* __restrict__ out) {
+                           const float2* __restrict__ rho_in_r, const uint32_t* __restrict__ gflags,
+                           uint32_t* __restrict__ out) {
     if (threadIdx.x != 0) return;
     const uint32_t* v = dz->pick;
     const uint32_t rg[10] = {v[0], v[1], v[1], v[4], v[4], v[5], v[1], v[2], v[3], v[4]};
@@ -450,13 +451,13 @@ __global__ void k_slab_lag(SlabSizes* __restrict__ dz, int32_t has_left, int32_t
     out[6] = rho_in_l ? __float_as_uint(rho_in_l[0].x) : 0u;
     out[7] = rho_in_r ? __float_as_uint(rho_in_r[0].x) : 0u;
     out[8] = v[5];
-    out[9] = f;
+    out[9] = gflags ? *gflags : f;   // RCCL: every rank's flags, max-reduced (the same on all ranks)
 }
 
 void launch_slab_lag(SlabSizes* dz, int32_t has_left, int32_t has_right, const uint32_t* totals,
                      const float4* msg_in_l, const float4* msg_in_r, const float2* rho_in_l, const float2* rho_in_r,
-                     uint32_t* out, hipStream_t s) {
-    k_slab_lag<<<1, 64, 0, s>>>(dz, has_left, has_right, totals, msg_in_l, msg_in_r, rho_in_l, rho_in_r, out);
+                     const uint32_t* gflags, uint32_t* out, hipStream_t s) {
+    k_slab_lag<<<1, 64, 0, s>>>(dz, has_left, has_right, totals, msg_in_l, msg_in_r, rho_in_l, rho_in_r, gflags, out);
 }
 
 void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, int32_t* id, hipStream_t s) {

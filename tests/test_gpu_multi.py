@@ -110,3 +110,87 @@ def test_rccl_world1_bitwise(pkg):
         assert np.array_equal(rec[order, 3:6], vs)
     finally:
         ctx.close()
+
+
+def test_group_overflow_stops_the_group(pkg, monkeypatch):
+    """A forced tiny halo-message capacity (SPH_DEBUG_MSG_CAP: every lag-sized message holds 256
+    records, far fewer than a ghost column) overflows on the receiving side. The overflow is flagged
+    on the device, the step still completes on clamped sizes (no rank returns alone), and sph_step
+    fails with SPH_ERR_CAPACITY for the whole group at the step the flag is read: the first lag-sized
+    step is 3 (three exact-size steps after the initial cut), its flags are read two steps on."""
+    sc = _scenario(pkg)
+    sim = pkg.SPHSim(sc, ndev=3, rebalance_every=0)
+    try:
+        monkeypatch.setenv("SPH_DEBUG_MSG_CAP", "256")
+        with pytest.raises(pkg.SphError) as ei:
+            sim.step(20)
+        msg = str(ei.value)
+        assert ei.value.status == -3, msg
+        assert "slab step 5:" in msg and "halo message overflow" in msg, msg
+    finally:
+        monkeypatch.delenv("SPH_DEBUG_MSG_CAP", raising=False)
+        sim.close()
+
+
+def test_force_without_density_scans_by_distance(pkg):
+    """The per-phase ABI lets a caller run the force pass after a new assemble without a density pass
+    in between: the hit mask then describes the previous slot order, so the force pass must not read
+    it (every wave-plane scans by distance; sph_read_hit_mask_counts), while after a density pass it
+    takes its hits from the mask."""
+    import ctypes as C
+    from sph_test_amd import _abi as A
+    from sph_test_amd import slab
+    sc = _scenario(pkg)
+    p, dt = pkg.scenario_params(sc)
+    n = sc.nx * sc.ny * sc.nz
+    ctx = pkg.Context(pkg.SPH_MODEL_WCSPH, 3, n + 4096)
+    L, h = ctx._L, ctx.handle
+    try:
+        ctx.set_params(p)
+        A.check("sph_slab_set", L.sph_slab_set(h, C.byref(A.SphSlab(0, slab.global_columns(p)))), h)
+        A.check("sph_slab_init_scenario", L.sph_slab_init_scenario(h, C.byref(sc)), h)
+        cnt = (C.c_int32 * 2)()
+        rng = (C.c_int32 * 10)()
+
+        def step(density: bool):
+            A.check("sph_slab_count_sends", L.sph_slab_count_sends(h, cnt), h)
+            A.check("sph_slab_assemble", L.sph_slab_assemble(h, None, 0, None, 0), h)
+            if density:
+                A.check("sph_slab_density", L.sph_slab_density(h), h)
+            A.check("sph_slab_ranges", L.sph_slab_ranges(h, rng), h)
+            A.check("sph_slab_force", L.sph_slab_force(h, dt, 0), h)
+            A.check("sph_slab_finish_step", L.sph_slab_finish_step(h, dt), h)
+            ctx.synchronize()
+
+        ctx.hit_mask_counts(reset=True)     # arm the counters
+        for _ in range(3):
+            step(True)
+        dist_planes, waves = (int(c) for c in ctx.hit_mask_counts(reset=True))
+        assert waves > 0 and dist_planes < 3 * waves      # the mask was used
+        step(False)
+        dist_planes, waves = (int(c) for c in ctx.hit_mask_counts(reset=True))
+        assert waves > 0 and dist_planes == 3 * waves     # stale mask: never read
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("ndev", [2, 4, 8])
+def test_bench_check_tolerance_on_groups(pkg, ndev):
+    """bench.py's N > 1 correctness check (slab_check: CHECK_STEPS steps of check_scenario with
+    re-balancing every CHECK_REBALANCE, owned positions against one context, |dx| <= CHECK_MAX_DX) run
+    on local groups of the same slab counts: the driver's 2/4/8-GPU bench must not fail its own check
+    on a correct decomposition. The measured difference is printed."""
+    import bench
+    sc = bench.check_scenario(pkg, ndev)
+    xs, vs = _single(pkg, sc, bench.CHECK_STEPS)
+    sim = pkg.SPHSim(sc, ndev=ndev, rebalance_every=bench.CHECK_REBALANCE)
+    try:
+        sim.step(bench.CHECK_STEPS)
+        x, v = sim.positions(), sim.velocities()
+        dx = float(np.abs(x - xs).max())
+        print({"ndev": ndev, "max_dx": dx, "max_dv": float(np.abs(v - vs).max()),
+               "rebalances": sim.ctx.decomposition().rebalances, "limit": bench.CHECK_MAX_DX})
+        assert dx <= bench.CHECK_MAX_DX
+        assert sim.ctx.decomposition().rebalances > 0
+    finally:
+        sim.close()

@@ -74,11 +74,15 @@ def _check(label, dt, e, L, x0, xg, vg, xr, vr, S, extra, n):
 
 
 def compare_one_step(pkg, O, sim, x0, v0, label, t=0.0):
-    """Upload (x0, v0) to the GPU context, step once; run the oracle on the same input; assert the
-    tolerances above. Returns (summary, sparse-path counts of the GPU step)."""
+    """Upload (x0, v0) to the GPU context at simulated time t (the sloshing forcing reads it), step
+    once; run the oracle on the same input at the same t; assert the tolerances above. Returns
+    (summary, sparse-path counts of the GPU step)."""
     op = oracle_sph_params(O, sim.params, sim.scenario.dim)
     n = len(x0)
     sim.ctx.upload_state(x0, v0)
+    t = float(np.float32(t))
+    if t != 0.0:
+        sim.ctx.set_sim_time(t)
     sim.ctx.path_counts(reset=True)
     sim.step(1)
     paths = sim.ctx.path_counts(reset=True)
@@ -117,6 +121,39 @@ def test_c3_one_step_from_rest(pkg, oracle):
         x0 = sim.positions()
         assert len(x0) == 1_048_576
         compare_one_step(pkg, oracle, sim, x0, np.zeros_like(x0), "C3 rest")
+    finally:
+        sim.close()
+
+
+def test_c4_one_step_sloshing_forced(pkg, oracle):
+    """Full C4 (4,194,304 particles, BASELINE configs[3], sloshing): 400 GPU steps so that the lateral
+    forcing f_ext(t) = A·sin(2πf₁t) is well away from zero, then one step on both sides from the
+    same uploaded state at the same t (sph_set_sim_time)."""
+    sim = pkg.SPHSim.from_config("C4")
+    try:
+        assert sim.n == 4_194_304
+        sim.step(400)
+        t = float(np.float32(sim.ctx.stats().sim_time))
+        p = sim.params
+        fext = float(p.forcing_amp) * np.sin(2 * np.pi * float(p.forcing_freq) * t)
+        assert abs(fext) > 0.05 * abs(float(p.forcing_amp)) > 0, (fext, p.forcing_amp, t)
+        x0, v0 = sim.positions(), sim.velocities()
+        assert np.isfinite(x0).all() and np.isfinite(v0).all()
+        assert np.abs(v0[:, 0]).max() > 0           # the forcing has set the layer moving
+        compare_one_step(pkg, oracle, sim, x0, v0, "C4 sloshing", t=t)
+    finally:
+        sim.close()
+
+
+def test_c5_one_step_from_rest(pkg, oracle):
+    """Full C5 (16,777,216 particles, BASELINE configs[4]) on ONE context, one step from the lattice:
+    the 8-GPU configuration's whole domain against the oracle (the decomposed step is checked
+    against the single context in test_gpu_multi.py)."""
+    sim = pkg.SPHSim.from_config("C5")
+    try:
+        x0 = sim.positions()
+        assert len(x0) == 16_777_216
+        compare_one_step(pkg, oracle, sim, x0, np.zeros_like(x0), "C5 rest")
     finally:
         sim.close()
 
