@@ -384,9 +384,13 @@ def main():
     if fi and fi.get("timed", 0) > 0 and fi["total_ms"] > 0:
         avg_s = fi["total_ms"] / fi["timed"] / 1e3
         n_local = runner.local_particles()
-        bytes_per_launch = FORCE_BYTES_PER_PARTICLE * n_local
+        # the force pass may run as several x-plane chunks per step (host_step.cpp, SPH_CHUNKS): a launch
+        # then covers its share of the particles
+        per_step = max(1.0, fi["launches"] / max(1, args.steps))
+        n_launch = n_local / per_step
+        bytes_per_launch = FORCE_BYTES_PER_PARTICLE * n_launch
         achieved = bytes_per_launch / avg_s / 1e9
-        design = (FORCE_BYTES_PER_PARTICLE + HIT_MASK_BYTES_PER_PARTICLE) * n_local / avg_s / 1e9
+        design = (FORCE_BYTES_PER_PARTICLE + HIT_MASK_BYTES_PER_PARTICLE) * n_launch / avg_s / 1e9
         if world == 1:
             pmc = load_pmc(args.config, code_hash)
         else:
@@ -395,7 +399,7 @@ def main():
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
                     "kernel": force_kernel_name(), "kernel_avg_us": round(avg_s * 1e6, 2),
-                    "bytes_per_launch": bytes_per_launch,
+                    "bytes_per_launch": bytes_per_launch, "launches_per_step": per_step,
                     "algorithmic_bytes_per_particle": FORCE_BYTES_PER_PARTICLE,
                     "bytes_source": "SURVEY.md §8d: force+visc+XSPH+KDK reads x,v,rho,P 32 B, writes x,v 24 B",
                     "frac_design": round(design / PEAK_HBM_GBS, 5),
