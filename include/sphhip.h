@@ -252,7 +252,8 @@ int sph_read_torque_int(sph_ctx* ctx, int32_t* xyz, int32_t count);  /* Model R,
 int sph_read_path_counts(sph_ctx* ctx, uint32_t counts[4], int32_t reset);
 /* Model S pass 2 takes its hits from pass 1's hit mask (8 words = 256 candidates per target):
  * [0] wave-planes (one wave, one dx plane) that scanned by distance instead, because a lane's
- * candidates passed the mask or the plane took a sparse path, [1] waves run (3 planes each).
+ * candidates passed the mask, or no valid mask exists (a force pass without a density pass since the
+ * last change of the slot order), [1] waves run (3 planes each).
  * reset != 0 zeroes them after the read. */
 int sph_read_hit_mask_counts(sph_ctx* ctx, uint32_t counts[2], int32_t reset);
 /* stable LSD radix sort of (key, index) on the device: the sort of the step, exposed for

@@ -29,7 +29,6 @@ int sph_create(const sph_config* cfg, int32_t device, sph_ctx** out) {
     ctx->profiling = (cfg->flags & SPH_FLAG_PROFILE) != 0;
     if (const char* v = std::getenv("SPH_RESORT")) ctx->resort_mode = std::atoi(v);
     if (const char* v = std::getenv("SPH_CT_TEAM")) ctx->ct_team = std::atoi(v);
-    if (const char* v = std::getenv("SPH_CHUNKS")) ctx->chunks = std::max(1, std::min(SPH_MAX_CHUNKS, std::atoi(v)));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&ctx->mv_host, sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -85,7 +84,6 @@ void sph_destroy(sph_ctx* ctx) {
     if (ctx->rb_ready) (void)hipEventDestroy(ctx->rb_ready);
     if (ctx->rb_stream) (void)hipStreamDestroy(ctx->rb_stream);
     if (ctx->mv_host) (void)hipHostFree(ctx->mv_host);
-    free_chunks(ctx);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

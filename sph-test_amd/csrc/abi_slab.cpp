@@ -54,7 +54,6 @@ int sph::slab_local_grid(sph_ctx* ctx) {
     g.gx_all = G.gx;
     g.ncells = (uint32_t)g.gx * (uint32_t)g.gy * (uint32_t)g.gz;
     ctx->grid = g;
-    ctx->chunk_cx.clear();
     ctx->key_bits = bit_width(g.ncells);
     invalidate_sort(ctx);
     return ensure_cells(ctx);

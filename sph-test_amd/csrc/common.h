@@ -392,8 +392,6 @@ struct HitMask {
 };
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g,
                           SphConst c, float2* rp, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr = DevRange{});
-// out[c] = cs[c·gyz] for the planes c = 0 .. gx (plane starts in slots), into host-visible memory
-void launch_plane_starts(const uint32_t* cs, uint32_t gyz, int32_t gx, uint32_t* out, hipStream_t s);
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs,
                         int32_t ib, int32_t ie, GridDesc g, SphConst c, float dt, float fext_x,
                         float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths,

@@ -46,9 +46,6 @@ struct Pending {
 
 }  // namespace sph
 
-constexpr int SPH_MAX_CHUNKS = 8;
-constexpr int32_t CHUNK_MIN_PARTICLES = 131072;
-
 struct sph_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -101,19 +98,6 @@ struct sph_ctx {
     int resort_mode = 1;
     int ct_team = 0;                // env SPH_CT_TEAM: Model R lanes per target (0 = by size; tests)
     uint32_t* mv_host = nullptr;    // pinned: the mover count of the latest step copied back
-    // chunked Model S neighbour passes (host_step.cpp step_wcsph): x-plane chunks, the density pass on
-    // the context stream and the force pass on a second stream, so that one pass's tail overlaps the
-    // other's workgroups. env SPH_CHUNKS (1: one launch per pass, one stream)
-    int chunks = 4;
-    hipStream_t stream2 = nullptr;
-    hipEvent_t ev_chunk[SPH_MAX_CHUNKS + 1] = {};   // density chunk k done; [SPH_MAX_CHUNKS]: force done
-    std::vector<int32_t> chunk_cx;  // plane cuts 0 = cx_0 < ... < cx_S = gx (empty: not chosen yet)
-    uint32_t* plane_host = nullptr; // pinned: cs at every plane start (gx + 1 values), for the cuts
-    int32_t plane_host_cap = 0;
-    hipEvent_t plane_ev = nullptr;  // recorded after their copy
-    bool plane_pending = false;     // a copy is in flight
-    int64_t plane_step = -1;        // step of the last copy
-    std::vector<int32_t> chunk_est; // particles per chunk at the last copy (grid sizes)
     int64_t steps = 0;
     double sim_time = 0.0;
     sph_drag_input drag{-1, {0.f, 0.f, 0.f}, 0.f};
@@ -266,7 +250,6 @@ HitMask hit_mask_write(sph_ctx* ctx);
 HitMask hit_mask_read(const sph_ctx* ctx);
 inline uint32_t* path_ctr(const sph_ctx* ctx) { return ctx->count_paths ? ctx->paths : nullptr; }
 void density_range(sph_ctx* ctx, int32_t b, int32_t e);
-void free_chunks(sph_ctx* ctx);
 void force_range(sph_ctx* ctx, int32_t b, int32_t e, float dt, float fext, MoverSink mv = MoverSink{});
 ResortScratch resort_scratch(sph_ctx* ctx);
 MoverSink mover_sink(sph_ctx* ctx);

@@ -133,7 +133,6 @@ int derive(sph_ctx* ctx) {
     g.gx_all = g.gx;
     g.ncells = (uint32_t)g.gx * (uint32_t)g.gy * (uint32_t)g.gz;
     ctx->grid = g;
-    ctx->chunk_cx.clear();   // the chunk cuts are planes of this grid
     ctx->key_bits = bit_width(g.ncells);   // the sentinel key == ncells must sort last
     invalidate_sort(ctx);
     return ensure_cells(ctx);
@@ -143,7 +142,6 @@ void invalidate_sort(sph_ctx* c) {
     c->keys_valid = false;
     c->sk_valid = false;
     c->hm_valid = false;
-    c->plane_step = INT64_MIN / 2;   // re-balance the pass chunks on the next step (host_step.cpp)
 }
 
 // ---------------------------------------------------------------- profiling

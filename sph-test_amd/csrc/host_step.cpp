@@ -125,135 +125,10 @@ int sort_wcsph(sph_ctx* ctx) {
     return SPH_OK;
 }
 
-// ---------------------------------------------------------------- chunked neighbour passes
-// The density pass ends in a tail of partly filled CUs (its last round of workgroups), and so does
-// the force pass: at C3 ~20% and ~14% of their spans. Cut at x-planes into S chunks of
-// about equal particle counts, the density chunks run in order on the context stream and the force
-// chunks on a second stream, force chunk k after density chunk k + 1: its targets' neighbours lie
-// within one plane, and chunk k + 1 holds at least one plane. Each pass's tail then overlaps the
-// other pass's workgroups. Every target is computed exactly as in one launch (same windows, same
-// order), so results are bit-identical for any S.
-void free_chunks(sph_ctx* c) {
-    if (c->stream2) {
-        (void)hipStreamSynchronize(c->stream2);
-        (void)hipStreamDestroy(c->stream2);
-        c->stream2 = nullptr;
-    }
-    for (auto& e : c->ev_chunk)
-        if (e) { (void)hipEventDestroy(e); e = nullptr; }
-    if (c->plane_ev) { (void)hipEventDestroy(c->plane_ev); c->plane_ev = nullptr; }
-    if (c->plane_host) { (void)hipHostFree(c->plane_host); c->plane_host = nullptr; }
-    c->plane_host_cap = 0;
-    c->plane_pending = false;
-}
-
-static int ensure_chunks(sph_ctx* ctx) {
-    if (ctx->stream2) return SPH_OK;
-    HIPCHK(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
-    for (auto& e : ctx->ev_chunk) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&ctx->plane_ev, hipEventDisableTiming));
-    return SPH_OK;
-}
-
-// the current plane starts (cs at every x-plane) into pinned memory, on the context stream
-static int plane_copy(sph_ctx* ctx) {
-    const int32_t gx = ctx->grid.gx;
-    if (ctx->plane_host_cap < gx + 1) {
-        if (ctx->plane_host) HIPCHK(hipHostFree(ctx->plane_host));
-        ctx->plane_host = nullptr;
-        HIPCHK(hipHostMalloc((void**)&ctx->plane_host, (size_t)(gx + 1) * sizeof(uint32_t), hipHostMallocMapped));
-        ctx->plane_host_cap = gx + 1;
-    }
-    launch_plane_starts(ctx->cs, (uint32_t)ctx->grid.gy * (uint32_t)ctx->grid.gz, gx, ctx->plane_host, ctx->stream);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(ctx->plane_ev, ctx->stream));
-    ctx->plane_pending = true;
-    ctx->plane_step = ctx->steps;
-    return SPH_OK;
-}
-
-// S cuts at planes, about equal particle counts, strictly increasing (every chunk holds a plane)
-static void choose_cuts(sph_ctx* ctx, int S, std::vector<int32_t>& est) {
-    const int32_t gx = ctx->grid.gx;
-    const uint32_t* ps = ctx->plane_host;
-    const double total = (double)ps[gx];
-    std::vector<int32_t>& cut = ctx->chunk_cx;
-    cut.assign((size_t)S + 1, 0);
-    for (int k = 1; k < S; ++k) {
-        const double target = total * k / S;
-        int32_t c = (int32_t)(std::lower_bound(ps, ps + gx + 1, (uint32_t)target) - ps);
-        c = std::max(c, cut[(size_t)k - 1] + 1);
-        c = std::min(c, gx - (S - k));
-        cut[(size_t)k] = c;
-    }
-    cut[(size_t)S] = gx;
-    est.assign((size_t)S, 0);
-    for (int k = 0; k < S; ++k) est[(size_t)k] = (int32_t)(ps[cut[(size_t)k + 1]] - ps[cut[(size_t)k]]);
-}
-
-static int step_wcsph_chunked(sph_ctx* ctx, float dt, int S) {
-    int r = ensure_chunks(ctx);
-    if (r != SPH_OK) return r;
-    // the cuts: from plane starts copied asynchronously (every 32 steps; particles cross planes slowly),
-    // or, when none are known for this grid, copied and waited for now. The counts only balance the
-    // chunks and size their grids: the kernels read their bounds from cs and loop over extra tiles.
-    if (ctx->plane_pending && hipEventQuery(ctx->plane_ev) == hipSuccess) {
-        choose_cuts(ctx, S, ctx->chunk_est);
-        ctx->plane_pending = false;
-    }
-    if ((int)ctx->chunk_cx.size() != S + 1) {
-        if ((r = plane_copy(ctx)) != SPH_OK) return r;
-        HIPCHK(hipEventSynchronize(ctx->plane_ev));
-        choose_cuts(ctx, S, ctx->chunk_est);
-        ctx->plane_pending = false;
-    } else if (!ctx->plane_pending && ctx->steps - ctx->plane_step >= 32) {
-        if ((r = plane_copy(ctx)) != SPH_OK) return r;
-    }
-    const uint32_t gyz = (uint32_t)ctx->grid.gy * (uint32_t)ctx->grid.gz;
-    hipStream_t s1 = ctx->stream, s2 = ctx->stream2;
-    auto range = [&](int k) {
-        return DevRange{ctx->cs + (size_t)ctx->chunk_cx[(size_t)k] * gyz, ctx->cs + (size_t)ctx->chunk_cx[(size_t)k + 1] * gyz};
-    };
-    auto est = [&](int k) {   // grid size: the count seen a few steps ago, +1/16 (tiles past it loop)
-        const int32_t e = ctx->chunk_est[(size_t)k];
-        return std::max<int32_t>(e + e / 16 + 256, 1);
-    };
-    const HitMask hw = hit_mask_write(ctx);
-    for (int k = 0; k < S; ++k) {
-        {
-            KTimer t(ctx, "density", 24.0 * est(k), true);
-            launch_density_tiled(ctx->pos, ctx->cs, 0, est(k), ctx->grid, ctx->sc, ctx->rp, hw, path_ctr(ctx), s1,
-                                 range(k));
-        }
-        HIPCHK(hipEventRecord(ctx->ev_chunk[k], s1));
-    }
-    const MoverSink mv = mover_sink(ctx);
-    const HitMask hr = hit_mask_read(ctx);
-    const float fext = forcing(ctx);
-    for (int k = 0; k < S; ++k) {
-        HIPCHK(hipStreamWaitEvent(s2, ctx->ev_chunk[std::min(k + 1, S - 1)], 0));
-        KTimer t(ctx, "force_integrate", 76.0 * est(k), true);
-        launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, est(k), ctx->grid, ctx->sc, dt, fext, ctx->pos2,
-                           ctx->vel2, ctx->keys, mv, hr, path_ctr(ctx), s2, range(k));
-    }
-    HIPCHK(hipEventRecord(ctx->ev_chunk[SPH_MAX_CHUNKS], s2));
-    HIPCHK(hipStreamWaitEvent(s1, ctx->ev_chunk[SPH_MAX_CHUNKS], 0));   // the step ends on the context stream
-    HIPCHK(hipGetLastError());
-    if (mv.sk && (ctx->steps & 7) == 0)
-        HIPCHK(hipMemcpyAsync(ctx->mv_host, mv.count, sizeof(uint32_t), hipMemcpyDeviceToHost, s1));
-    swap_sv(ctx);
-    ctx->keys_valid = true;
-    ctx->keys_active = 0;
-    return SPH_OK;
-}
-
 int step_wcsph(sph_ctx* ctx, float dt) {
     const int32_t n = ctx->n;
     int r = sort_wcsph(ctx);
     if (r != SPH_OK) return r;
-    // chunked passes from C2's size up (smaller steps are launch-bound: more launches cost more)
-    const int S = std::min(ctx->chunks, ctx->grid.gx);
-    if (S > 1 && n >= CHUNK_MIN_PARTICLES) return step_wcsph_chunked(ctx, dt, S);
     {
         KTimer t(ctx, "density", 24.0 * n, true);
         density_range(ctx, 0, n);

@@ -253,13 +253,8 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
         ib = (int32_t)*dr.lo;
         n = (int32_t)*dr.hi;
     }
-    // tiles of TT_BLK targets: one per workgroup when the grid covers [ib, n) (the host's bound), more
-    // when the bounds come from the device (dr) and exceed the grid (a chunk larger than estimated)
-#pragma unroll 1
-    for (int32_t tb = blockIdx.x;; tb += gridDim.x) {
-    if (tb != (int32_t)blockIdx.x) __syncthreads();   // the previous tile's LDS reads are done
-    const int32_t i0 = ib + (tb < (int32_t)gridDim.x ? xcd_block(tb, gridDim.x) : tb) * TT_BLK;
-    if (i0 >= n) break;   // whole workgroup: before any barrier
+    const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
+    if (i0 >= n) return;   // whole workgroup: before any barrier
     SPH_BT_START;
     // quadrant order, measured against plain sorted order (138 -> 154 us) and halves by fx or by fy
     // (+1 to +2 us) at C3 (profiles/r02_pass1_lane_order_ab.log)
@@ -374,16 +369,14 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
         plane_groups(len, TT_GCAP, group, big_row);
     }
     SPH_BT_END(0);
-    if (valid) {
-        if (rec && mn > 0 && mw < HM_WORDS)   // the last, partial word: bits [0, mn), zeros above
-            *wp = __builtin_bitreverse32(ml << (32 - mn));
-        const float d = c.mass * (c.sigma * (0.25f * s));
-        const float tr = d * c.inv_rho0;
-        const float t2 = tr * tr, t4 = t2 * t2;
-        const float P = c.B * (t4 * t2 * tr - 1.0f);
-        rp[i] = make_float2(d, P / (d * d));
-    }
-    }   // tiles
+    if (!valid) return;
+    if (rec && mn > 0 && mw < HM_WORDS)   // the last, partial word: bits [0, mn), zeros above
+        *wp = __builtin_bitreverse32(ml << (32 - mn));
+    const float d = c.mass * (c.sigma * (0.25f * s));
+    const float tr = d * c.inv_rho0;
+    const float t2 = tr * tr, t4 = t2 * t2;
+    const float P = c.B * (t4 * t2 * tr - 1.0f);
+    rp[i] = make_float2(d, P / (d * d));
 }
 
 struct ForceAcc {
@@ -450,11 +443,8 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         ib = (int32_t)*dr.lo;
         n = (int32_t)*dr.hi;
     }
-#pragma unroll 1
-    for (int32_t tb = blockIdx.x;; tb += gridDim.x) {   // tiles (see k_density_tiled)
-    if (tb != (int32_t)blockIdx.x) __syncthreads();
-    const int32_t i0 = ib + (tb < (int32_t)gridDim.x ? xcd_block(tb, gridDim.x) : tb) * TT_BLK;
-    if (i0 >= n) break;   // whole workgroup: before any barrier
+    const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
+    if (i0 >= n) return;   // whole workgroup: before any barrier
     SPH_BT_START;
     // Targets stay in sorted order here. Lanes ordered by quarters of fx (a dx plane's hit count follows
     // fx) fill the plane loop better (66% -> 80% of lanes busy at C3) but run slower, 206 -> 246 us, and
@@ -564,9 +554,9 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         // the mask covers this plane for every lane of the wave (wave-uniform)
         const bool by_mask = hm.w != nullptr && !__any(kb + plen > HM_WORDS * 32);
         kb += plen;
-        if (hm.w != nullptr && !by_mask) {   // this plane scans by distance: its bits are passed over
+        if (!by_mask) {   // this plane scans by distance (its bits, if any, are passed over)
             count_wave(paths, 4);
-            skip(plen);
+            if (hm.w != nullptr) skip(plen);
         }
         // rows of mask gm staged back to back (they fit the budget together); the mask walk takes their
         // windows' bits in visit order (rows outside gm count zero bits)
@@ -634,7 +624,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     }
     count_wave(paths, 5);   // waves (3 planes each)
     SPH_BT_END(1);
-    if (!valid) continue;
+    if (!valid) return;
     float nv[3] = {vi.x + (acc.ax + c.gx + fext_x) * dt, vi.y + (acc.ay + c.gy) * dt, vi.z + (acc.az + c.gz) * dt};
     float np[3] = {pi.x + (nv[0] + acc.sx) * dt, pi.y + (nv[1] + acc.sy) * dt, pi.z + (nv[2] + acc.sz) * dt};
     const float L[3] = {c.Lx, c.Ly, c.Lz};
@@ -650,7 +640,6 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     // the mover list takes the window key: in a slab, a particle that left the held columns sorts
     // last (window_key = cell_key in a single domain); it changed iff the clamped key changed
     append_mover(mv, i, window_key(g, np[0], np[1], np[2]));
-    }   // tiles
 }
 
 // dr set: [ib, ie) only sizes the grid (an upper bound); the kernels read their bounds from dr
@@ -666,15 +655,6 @@ void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, 
     if (ie > ib)
         SPH_LAUNCH(k_force_tiled, (ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c,
                    pair_constants(c), dt, fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr);
-}
-
-__global__ void k_plane_starts(const uint32_t* __restrict__ cs, uint32_t gyz, int32_t gx, uint32_t* __restrict__ out) {
-    const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c <= gx) out[c] = cs[(uint32_t)c * gyz];
-}
-
-void launch_plane_starts(const uint32_t* cs, uint32_t gyz, int32_t gx, uint32_t* out, hipStream_t s) {
-    k_plane_starts<<<(gx + 1 + 255) / 256, 256, 0, s>>>(cs, gyz, gx, out);
 }
 
 #ifdef SPH_BTIME

@@ -168,52 +168,3 @@ def test_resort_bitwise_contact(pkg, monkeypatch, case):
     inc = _contact_run(pkg, monkeypatch, "2", parts, 20, conns, act)
     for a, b, what in zip(full[:4], inc[:4], ("particles", "torque", "sorted ids", "cell starts")):
         assert a == b, what
-
-
-@pytest.mark.parametrize("config,chunks,steps", [("C2", "3", 40), ("C3", "8", 12)])
-def test_chunked_passes_bitwise(pkg, monkeypatch, config, chunks, steps):
-    """The neighbour passes cut into x-plane chunks on two streams (host_step.cpp step_wcsph_chunked,
-    SPH_CHUNKS) against one launch per pass: every target is computed the same way, so whole runs are
-    bit-identical; the chunk cuts are re-chosen from the plane counts every 32 steps on the way."""
-    def make(flag):
-        monkeypatch.setenv("SPH_CHUNKS", flag)
-        s = pkg.SPHSim.from_config(config, profile=True)
-        monkeypatch.delenv("SPH_CHUNKS")
-        return s
-    one, cut = make("1"), make(chunks)
-    try:
-        for k in (1, steps):
-            one.step(k)
-            cut.step(k)
-            _assert_same(one.ctx, cut.ctx, f"{config}, {chunks} chunks")
-        ks1, ksc = one.ctx.kernel_stats(), cut.ctx.kernel_stats()
-        assert ks1["force_integrate"]["launches"] == 1 + steps
-        assert ksc["force_integrate"]["launches"] == int(chunks) * (1 + steps)
-    finally:
-        one.close()
-        cut.close()
-
-
-def test_chunked_passes_bitwise_splash(pkg, monkeypatch):
-    """Chunks whose particle counts differ wildly from the estimate (a state uploaded after the cuts
-    were chosen): the kernels loop over the tiles past their grids, results stay bit-identical."""
-    sc = pkg.make_scenario(pkg.SPH_SCENARIO_DAMBREAK, 3, 64, 64, 64, 128, 128, 128, dx=0.01, seed=5)
-
-    def make(flag):
-        monkeypatch.setenv("SPH_CHUNKS", flag)
-        s = pkg.SPHSim(sc)
-        monkeypatch.delenv("SPH_CHUNKS")
-        s.step(2)                                  # cuts chosen for the column at low x
-        x = s.positions()
-        x[:, 0] = np.float32(1.27) - x[:, 0]       # mirror in x: the fluid now sits at high x
-        s.ctx.upload_state(x, np.zeros_like(x))
-        return s
-    one, cut = make("1"), make("4")
-    try:
-        for k in (1, 3):
-            one.step(k)
-            cut.step(k)
-            _assert_same(one.ctx, cut.ctx, "mirrored state")
-    finally:
-        one.close()
-        cut.close()
