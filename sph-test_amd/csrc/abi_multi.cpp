@@ -653,8 +653,9 @@ int phase_rho_out(RankState& R, Multi& M) {
         r = ensure_buf(M, ctx, &R.rho_in[s], &R.rcap_in[s], RHO_HDR + R.c2i[s]);
         if (r != SPH_OK) return r;
         if (M.mode == 1) HIPCHK(hipStreamWaitEvent(ctx->stream, M.ranks[peer - M.ranks[0].rank].ev_rho_recv, 0));
-        launch_slab_pack_rho(ctx->rp, R.dz, s, R.rho_out[s], R.c2o[s], ctx->stream);
     }
+    launch_slab_pack_rho2(ctx->rp, R.dz, R.left >= 0 ? R.rho_out[0] : nullptr, R.c2o[0],
+                          R.right >= 0 ? R.rho_out[1] : nullptr, R.c2o[1], ctx->stream);
     HIPCHK(hipGetLastError());
     if (R.left >= 0 || R.right >= 0) HIPCHK(hipEventRecord(R.ev_rho_packed, ctx->stream));
     CKPT(R, "rho pack");
@@ -688,8 +689,8 @@ int phase_finish(RankState& R, float dt, int64_t step, bool global_flags) {
     hipStream_t s = ctx->stream;
     if (R.left >= 0 || R.right >= 0) HIPCHK(hipStreamWaitEvent(s, R.ev_rho_recv, 0));
     CKPT(R, "exchange 2");
-    for (int side = 0; side < 2; ++side)
-        if ((side == 0 ? R.left : R.right) >= 0) launch_slab_unpack_rho(ctx->rp, R.dz, side, R.rho_in[side], R.c2i[side], s);
+    launch_slab_unpack_rho2(ctx->rp, R.dz, R.left >= 0 ? R.rho_in[0] : nullptr, R.c2i[0],
+                            R.right >= 0 ? R.rho_in[1] : nullptr, R.c2i[1], s);
     CKPT(R, "rho unpack");
     const bool one_col = ctx->sl.cx_hi - ctx->sl.cx_lo == 1;
     const uint32_t* pk = R.dz->pick;

@@ -434,9 +434,12 @@ void launch_slab_sizes(SlabSizes* dz, const float4* msg_l, const float4* msg_r, 
                        int32_t capacity, hipStream_t s);
 // after the re-sort: dz->pick -> the ranges (rg, fr, o0/o1 of the new order, n and dropped)
 // ρ, P/ρ² of boundary column `side` ([pick[1+2side], pick[2+2side])) -> message (header + cap entries)
-void launch_slab_pack_rho(const float2* rp, SlabSizes* dz, int32_t side, float2* msg, int32_t cap, hipStream_t s);
+// both sides' ρ messages in one launch each way (a null message: no neighbour on that side)
+void launch_slab_pack_rho2(const float2* rp, SlabSizes* dz, float2* msg_l, int32_t cap_l, float2* msg_r, int32_t cap_r,
+                           hipStream_t s);
 // received densities -> the ghost column of `side` ([pick[4side], pick[4side+1])); mismatch -> SZ_RHO_MISMATCH
-void launch_slab_unpack_rho(float2* rp, SlabSizes* dz, int32_t side, const float2* msg, int32_t cap, hipStream_t s);
+void launch_slab_unpack_rho2(float2* rp, SlabSizes* dz, const float2* msg_l, int32_t cap_l, const float2* msg_r,
+                             int32_t cap_r, hipStream_t s);
 // per-step counts for the host's lagged capacity choice, written to mapped pinned memory:
 // out[0..1] sent records (left, right), out[2..3] received headers, out[4..5] ρ sent, out[6..7] ρ received,
 // out[8] assembled slots, out[9] flags (gflags non-null: that word instead, every rank's flags reduced)

@@ -141,9 +141,13 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_pack(const uint32_t* __restrict
                                                       int32_t col_le, int32_t col_ge,
                                                       const uint32_t* __restrict__ blk, int32_t nblk,
                                                       float4* __restrict__ out, const SlabSizes* __restrict__ dz,
-                                                      uint32_t cap) {
+                                                      uint32_t cap, float4* __restrict__ hdr,
+                                                      const uint32_t* __restrict__ total) {
     __shared__ uint32_t wc[SL_PER][SL_WAVES];
     const int w = threadIdx.x >> 6;
+    // the message header (device-sized steps): the count k_slab_scan left, written by one lane here
+    // instead of by a launch of its own
+    if (hdr && blockIdx.x == 0 && threadIdx.x == 0) write_header(hdr, *total, cap);
     if (dz) {   // device-sized step (see k_slab_count)
         b = (int32_t)dz->o0;
         e = (int32_t)dz->o1;
@@ -201,14 +205,26 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_unpack(const float4* __restrict
 // The cell-start table of the assembled old keys [left | own | right] (sk), for the incremental
 // re-sort, made from the previous step's table in place. Owned columns: the own block kept its
 // order, so cs[k] shifts by nl − o0 (o0: the previous owned start). Halo columns: lower bounds in
-// the left / right blocks. cs[ncells] = cs[ncells + 1] = n.
+// the left / right blocks. cs[ncells] = cs[ncells + 1] = n. Four cells per lane: the owned cells,
+// nearly all of the table, move as one 16-byte load and store (the table is ~15 MB at C3).
+__device__ __forceinline__ uint32_t cs_old_halo(const uint32_t* __restrict__ sk, uint32_t k, uint32_t lo, uint32_t len,
+                                                uint32_t off) {
+    uint32_t a = 0u, b = len;   // lower bound of k in sk[lo, lo + len)
+    while (a < b) {
+        const uint32_t mid = (a + b) >> 1;
+        if (sk[lo + mid] < k) a = mid + 1u;
+        else b = mid;
+    }
+    return off + a;
+}
+
 __global__ __launch_bounds__(SL_BLK) void k_slab_cs_old(uint32_t* __restrict__ cs, uint32_t ncells, uint32_t gyz,
                                                         uint32_t gx, int32_t has_left, int32_t has_right,
                                                         int32_t shift, const uint32_t* __restrict__ sk,
                                                         int32_t nl, int32_t no, int32_t nr,
                                                         const SlabSizes* __restrict__ dz) {
-    const uint32_t k = blockIdx.x * SL_BLK + threadIdx.x;
-    if (k > ncells + 1u) return;
+    const uint32_t k0 = 4u * (blockIdx.x * SL_BLK + threadIdx.x);
+    if (k0 > ncells + 1u) return;
     if (dz) {
         nl = (int32_t)dz->nl;
         no = (int32_t)dz->no;
@@ -216,27 +232,30 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_cs_old(uint32_t* __restrict__ c
         shift = nl - (int32_t)dz->o0;
     }
     const uint32_t n = (uint32_t)(nl + no + nr);
-    if (k >= ncells) {
-        cs[k] = n;
+    // the owned cells: [owned_lo, owned_hi) (halo columns are the first / last column when present)
+    const uint32_t owned_lo = has_left ? gyz : 0u, owned_hi = has_right ? (gx - 1u) * gyz : ncells;
+    if (k0 + 3u < owned_hi && k0 >= owned_lo) {   // four owned cells (cs is 16-byte aligned)
+        if (shift != 0) {
+            uint4 v = reinterpret_cast<uint4*>(cs)[k0 >> 2];
+            v.x = (uint32_t)((int32_t)v.x + shift);
+            v.y = (uint32_t)((int32_t)v.y + shift);
+            v.z = (uint32_t)((int32_t)v.z + shift);
+            v.w = (uint32_t)((int32_t)v.w + shift);
+            reinterpret_cast<uint4*>(cs)[k0 >> 2] = v;
+        }
         return;
     }
-    const uint32_t col = k / gyz;
-    uint32_t lo, len, off;
-    if (has_left && col == 0u) {
-        lo = 0u; len = (uint32_t)nl; off = 0u;
-    } else if (has_right && col == gx - 1u) {
-        lo = (uint32_t)(nl + no); len = (uint32_t)nr; off = lo;
-    } else {
-        if (shift != 0) cs[k] = (uint32_t)((int32_t)cs[k] + shift);
-        return;
+    for (uint32_t k = k0; k < k0 + 4u && k <= ncells + 1u; ++k) {
+        if (k >= ncells) {
+            cs[k] = n;
+        } else if (k < owned_lo) {
+            cs[k] = cs_old_halo(sk, k, 0u, (uint32_t)nl, 0u);
+        } else if (k >= owned_hi) {
+            cs[k] = cs_old_halo(sk, k, (uint32_t)(nl + no), (uint32_t)nr, (uint32_t)(nl + no));
+        } else if (shift != 0) {
+            cs[k] = (uint32_t)((int32_t)cs[k] + shift);
+        }
     }
-    uint32_t a = 0u, b = len;   // lower bound of k in sk[lo, lo + len)
-    while (a < b) {
-        const uint32_t mid = (a + b) >> 1;
-        if (sk[lo + mid] < k) a = mid + 1u;
-        else b = mid;
-    }
-    cs[k] = off + a;
 }
 
 // ---- init-time selection of owned columns (global grid in `g`)
@@ -341,7 +360,7 @@ void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel
     const int32_t nb = slab_send_blocks(b, e);
     if (e > b)
         k_slab_pack<<<nb, SL_BLK, 0, s>>>(keys, pos, vel, id, sk, key_base, b, e, gyz, side, col_le, col_ge, blk, nb,
-                                          out, nullptr, 0xffffffffu);
+                                          out, nullptr, 0xffffffffu, nullptr, nullptr);
 }
 
 void launch_slab_count_dev(const uint32_t* keys, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz, int32_t col_le,
@@ -350,17 +369,12 @@ void launch_slab_count_dev(const uint32_t* keys, const SlabSizes* dz, int32_t nb
     k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb_ub, totals, nullptr, nullptr, nullptr, 0, 0);
 }
 
-__global__ void k_msg_header(float4* __restrict__ msg, const uint32_t* __restrict__ total, int32_t cap) {
-    if (threadIdx.x == 0) write_header(msg, *total, (uint32_t)cap);
-}
-
 void launch_slab_pack_dev(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
                           const uint32_t* sk, uint32_t key_base, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz,
                           int32_t side, int32_t col_le, int32_t col_ge, const uint32_t* blk, float4* msg, int32_t cap,
                           const uint32_t* total, hipStream_t s) {
-    k_msg_header<<<1, 64, 0, s>>>(msg, total, cap);
     k_slab_pack<<<nb_ub, SL_BLK, 0, s>>>(keys, pos, vel, id, sk, key_base, 0, 0, gyz, side, col_le, col_ge, blk,
-                                         nb_ub, msg + MSG_HDR_F4, dz, (uint32_t)cap);
+                                         nb_ub, msg + MSG_HDR_F4, dz, (uint32_t)cap, msg, total);
 }
 
 // The assembled layout from the message headers and the owned range of the previous order (a
@@ -380,9 +394,15 @@ void launch_slab_sizes(SlabSizes* dz, const float4* msg_l, const float4* msg_r, 
 // ρ messages: a 32-byte header (count, capacity) = 4 float2, then the entries
 constexpr int RHO_HDR = 4;
 
-__global__ __launch_bounds__(SL_BLK) void k_slab_pack_rho(const float2* __restrict__ rp, const SlabSizes* __restrict__ dz,
-                                                          int32_t side, float2* __restrict__ msg, int32_t cap) {
-    const uint32_t b = dz->pick[1 + 2 * side], e = dz->pick[2 + 2 * side];   // boundary column of `side`
+// both sides in one launch (blockIdx.y = side; a side without a message has no workgroups' work)
+__global__ __launch_bounds__(SL_BLK) void k_slab_pack_rho2(const float2* __restrict__ rp, const SlabSizes* __restrict__ dz,
+                                                           float2* __restrict__ msg_l, int32_t cap_l,
+                                                           float2* __restrict__ msg_r, int32_t cap_r) {
+    const int32_t side = (int32_t)blockIdx.y;
+    float2* msg = side == 0 ? msg_l : msg_r;
+    const int32_t cap = side == 0 ? cap_l : cap_r;
+    if (!msg || (int32_t)(blockIdx.x * SL_BLK) > cap) return;
+    const uint32_t b = dz->pick[1 + 2 * side], e = dz->pick[2 + 2 * side];
     const uint32_t cnt = e - b;
     const uint32_t t = blockIdx.x * SL_BLK + threadIdx.x;
     if (t == 0) {
@@ -392,9 +412,14 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_pack_rho(const float2* __restri
     if (t < cnt && t < (uint32_t)cap) msg[RHO_HDR + t] = rp[b + t];
 }
 
-__global__ __launch_bounds__(SL_BLK) void k_slab_unpack_rho(float2* __restrict__ rp, SlabSizes* __restrict__ dz,
-                                                            int32_t side, const float2* __restrict__ msg, int32_t cap) {
-    const uint32_t b = dz->pick[4 * side], e = dz->pick[4 * side + 1];   // ghost column of `side`
+__global__ __launch_bounds__(SL_BLK) void k_slab_unpack_rho2(float2* __restrict__ rp, SlabSizes* __restrict__ dz,
+                                                             const float2* __restrict__ msg_l, int32_t cap_l,
+                                                             const float2* __restrict__ msg_r, int32_t cap_r) {
+    const int32_t side = (int32_t)blockIdx.y;
+    const float2* msg = side == 0 ? msg_l : msg_r;
+    const int32_t cap = side == 0 ? cap_l : cap_r;
+    if (!msg || (int32_t)(blockIdx.x * SL_BLK) > cap) return;
+    const uint32_t b = dz->pick[4 * side], e = dz->pick[4 * side + 1];
     const uint32_t cnt = __float_as_uint(msg[0].x);
     const uint32_t m = min(min(cnt, (uint32_t)cap), e - b);
     const uint32_t t = blockIdx.x * SL_BLK + threadIdx.x;
@@ -402,12 +427,18 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_unpack_rho(float2* __restrict__
     if (t < m) rp[b + t] = msg[RHO_HDR + t];
 }
 
-void launch_slab_pack_rho(const float2* rp, SlabSizes* dz, int32_t side, float2* msg, int32_t cap, hipStream_t s) {
-    k_slab_pack_rho<<<cap / SL_BLK + 1, SL_BLK, 0, s>>>(rp, dz, side, msg, cap);
+void launch_slab_pack_rho2(const float2* rp, SlabSizes* dz, float2* msg_l, int32_t cap_l, float2* msg_r, int32_t cap_r,
+                           hipStream_t s) {
+    if (!msg_l && !msg_r) return;
+    const int32_t cl = msg_l ? cap_l : 0, cr = msg_r ? cap_r : 0, cap = cl > cr ? cl : cr;
+    k_slab_pack_rho2<<<dim3(cap / SL_BLK + 1, 2), SL_BLK, 0, s>>>(rp, dz, msg_l, cap_l, msg_r, cap_r);
 }
 
-void launch_slab_unpack_rho(float2* rp, SlabSizes* dz, int32_t side, const float2* msg, int32_t cap, hipStream_t s) {
-    k_slab_unpack_rho<<<cap / SL_BLK + 1, SL_BLK, 0, s>>>(rp, dz, side, msg, cap);
+void launch_slab_unpack_rho2(float2* rp, SlabSizes* dz, const float2* msg_l, int32_t cap_l, const float2* msg_r,
+                             int32_t cap_r, hipStream_t s) {
+    if (!msg_l && !msg_r) return;
+    const int32_t cl = msg_l ? cap_l : 0, cr = msg_r ? cap_r : 0, cap = cl > cr ? cl : cr;
+    k_slab_unpack_rho2<<<dim3(cap / SL_BLK + 1, 2), SL_BLK, 0, s>>>(rp, dz, msg_l, cap_l, msg_r, cap_r);
 }
 
 // End of a device-sized step: the slot ranges of the new order from the picked column starts (the
@@ -467,7 +498,7 @@ void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, 
 void launch_slab_cs_old(uint32_t* cs, uint32_t ncells, uint32_t gyz, uint32_t gx, bool has_left, bool has_right,
                         int32_t shift, const uint32_t* sk, int32_t nl, int32_t no, int32_t nr, hipStream_t s,
                         const SlabSizes* dz) {
-    const uint32_t m = ncells + 2u;
+    const uint32_t m = (ncells + 2u + 3u) / 4u;   // four cells per lane
     SPH_LAUNCH(k_slab_cs_old, (m + SL_BLK - 1) / SL_BLK, SL_BLK, 0, s, cs, ncells, gyz, gx, has_left ? 1 : 0,
                has_right ? 1 : 0, shift, sk, nl, no, nr, dz);
 }

@@ -406,6 +406,11 @@ class SlabRunner:
     def owned(self) -> np.ndarray:
         return self.be.read_owned()
 
+    def grid_stats(self) -> dict:
+        """This rank's slab grid (bench.py's whole-step roofline: key bits and cells)."""
+        st = self.be.ctx.stats()
+        return {"key_bits": st.key_bits, "ncells": st.grid[0] * st.grid[1] * st.grid[2]}
+
     def reset_stats(self) -> None:
         self.be.reset_stats()
 
