@@ -1,0 +1,86 @@
+"""bench.py's multi-rank safety logic on CPU (gloo, world 2): the phase agreement of the library-transport
+setup (a rank that fails before a collective makes every rank give up together, none waits in it), and the
+watchdog that turns a rank stuck in a collective into a failure line and exit status 3."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _agree_worker(rank, world, port, fail_phase, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    import torch.distributed as dist
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class FakeRunner:
+        """Stands in for LibraryRankRunner: rank 1 fails in `fail_phase`; join and init count their calls."""
+        calls = []
+
+        def __init__(self, *a, **k):
+            if rank == 1 and fail_phase == "create":
+                raise RuntimeError("create failed")
+            self.ctx = type("C", (), {"close": lambda self: None})()
+
+        def join(self):
+            FakeRunner.calls.append("join")
+            if rank == 1 and fail_phase == "join":
+                raise RuntimeError("join failed")
+
+        def init(self):
+            FakeRunner.calls.append("init")
+            if rank == 1 and fail_phase == "init":
+                raise RuntimeError("init failed")
+
+    bench.LibraryRankRunner = FakeRunner
+    runner, err = bench.make_library_runner(None, "C3", None, rank, world, 0, 0, 50, dist, "cpu")
+    with open(os.path.join(out, f"r{rank}.json"), "w") as f:
+        json.dump({"ok": runner is not None, "err": err, "calls": FakeRunner.calls}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_phase", ["none", "create", "join", "init"])
+def test_library_setup_agreement(tmp_path, fail_phase):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, 2, port, fail_phase, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res = [json.load(open(tmp_path / f"r{r}.json")) for r in range(2)]
+    if fail_phase == "none":
+        assert all(r["ok"] and r["err"] is None and r["calls"] == ["join", "init"] for r in res)
+        return
+    # every rank gives up, and no rank entered a phase after the one that failed on rank 1
+    assert not any(r["ok"] for r in res) and all(r["err"] for r in res)
+    stop = {"create": [], "join": ["join"], "init": ["join", "init"]}[fail_phase]
+    assert res[0]["calls"] == stop and res[1]["calls"] == stop
+    assert f"{fail_phase} failed" in res[1]["err"]
+
+
+def test_watchdog_fires_with_a_failure_line():
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "w = bench.Watchdog(0, 2, 1.0); w.arm('a stuck collective', 1.0); time.sleep(30)") % str(ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 3
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["value"] is None and "a stuck collective" in line["watchdog"] and line["n_gpus"] == 2
