@@ -243,24 +243,10 @@ __device__ __forceinline__ int32_t quadrant_target(const GridDesc& g, const floa
     return perm[threadIdx.x];
 }
 
-// A/B (SPH_P1_SWZ): pass 1's staged slot s at LDS index s ^ ((s >> 4) & 3). Its lanes read window
-// starts that differ by multiples of a lattice layer (4 particles in a 2 x 2-line column), so at most
-// four 16-B bank groups of a ds_read_b128 lane group are busy; the XOR spreads them (bank model:
-// scripts/lds_bank_model.py, conflict share 0.46 -> 0.38), at one bit-field extract and XOR per read.
-#ifdef SPH_P1_SWZ
-__device__ __forceinline__ int32_t p1_slot(int32_t s) { return s ^ ((s >> 4) & 3); }
-#else
-__device__ __forceinline__ int32_t p1_slot(int32_t s) { return s; }
-#endif
-
 __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAVES))) void k_density_tiled(
     const float4* __restrict__ pos, const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c,
     float2* __restrict__ rp, DevRange dr, HitMask hm, uint32_t* __restrict__ paths) {
-#ifdef SPH_P1_SWZ
-    __shared__ float4 sp[(TT_GCAP + 4 + 15) / 16 * 16];   // the XOR stays inside a 16-slot group
-#else
     __shared__ float4 sp[TT_GCAP + 4];
-#endif
     __shared__ int32_t perm[TT_BLK];
     __shared__ uint32_t qcnt[TT_BLK / 64][5];
     if (dr.lo) {   // device-resident bounds (slab mode); the grid is an upper bound
@@ -308,8 +294,7 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
         SPH_DIAG_ADD(10, wave_max(ln & 3));     // tail iterations
         int32_t t = 0;
         for (; t + 4 <= ln; t += 4) {
-            const float4 a = sp[p1_slot(lo + t)], bb = sp[p1_slot(lo + t + 1)], cc = sp[p1_slot(lo + t + 2)],
-                         d = sp[p1_slot(lo + t + 3)];
+            const float4 a = sp[lo + t], bb = sp[lo + t + 1], cc = sp[lo + t + 2], d = sp[lo + t + 3];
             const float ra = dist2(pi, a), rb = dist2(pi, bb), rc = dist2(pi, cc), rd = dist2(pi, d);
             s += spline_w4(c, ra);
             s += spline_w4(c, rb);
@@ -322,7 +307,7 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
             keep_b128(a, bb, cc, d);
         }
         for (; t < ln; ++t) {
-            const float r2 = dist2(pi, sp[p1_slot(lo + t)]);
+            const float r2 = dist2(pi, sp[lo + t]);
             s += spline_w4(c, r2);
             one(r2);
         }
@@ -346,7 +331,7 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
                 tot += lg[r];
             }
             __syncthreads();
-            stage_plane(c0, lg, tot, [&](int32_t t, int32_t src) { sp[p1_slot(t)] = pos[src]; });
+            stage_plane(c0, lg, tot, [&](int32_t t, int32_t src) { sp[t] = pos[src]; });
             __syncthreads();
             int32_t o = 0;
 #pragma unroll
@@ -370,7 +355,7 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
             for (int32_t base = c0[r]; base < c1[r]; base += TT_GCAP) {
                 const int32_t ln = min(TT_GCAP, c1[r] - base);
                 __syncthreads();
-                for (int32_t t = threadIdx.x; t < ln; t += TT_BLK) sp[p1_slot(t)] = pos[base + t];
+                for (int32_t t = threadIdx.x; t < ln; t += TT_BLK) sp[t] = pos[base + t];
                 __syncthreads();
                 const int32_t lo = max(r0[r], base) - base;
                 scan(lo, max(min(r1[r], base + ln) - base - lo, 0));
