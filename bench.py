@@ -54,9 +54,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event pass")
-    ap.add_argument("--profile-every", type=int, default=4,
-                    help="time the kernels of one step in this many (events in the dispatch packets still cost a "
-                         "C3 step ~15 us, so the timed region samples them)")
+    ap.add_argument("--profile-every", type=int, default=0,
+                    help="time the kernels of one step in this many (events in the dispatch packets cost the step "
+                         "they ride on; C3: every 4th step +1.0%%, every 16th +0.4%%, profiles/r03_profile_cost_ab.log). "
+                         "0 (default): 16, or 4 when fewer than 160 steps are timed")
     ap.add_argument("--slab", action="store_true", help="run the multi-GPU slab step even at N=1 (rehearsal)")
     ap.add_argument("--rebalance", type=int, default=50, help="slab cut re-balancing interval in steps (0: off)")
     ap.add_argument("--transport", choices=("library", "python"), default="library",
@@ -273,7 +274,8 @@ def per_step_ms(kstats: dict, steps: int) -> dict:
 
 def main():
     args = parse()
-    prof = 0 if args.no_profile else max(1, args.profile_every)
+    every = args.profile_every if args.profile_every > 0 else (16 if args.steps >= 160 else 4)
+    prof = 0 if args.no_profile else max(1, every)
     import torch
     if args.table:
         torch.cuda.set_device(0)
