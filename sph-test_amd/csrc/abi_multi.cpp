@@ -30,7 +30,7 @@ namespace sph {
 
 constexpr int LAG_SLOTS = 4;
 constexpr int LAG_WORDS = 16;
-constexpr int SDEV_TOTALS = 10;   // sdev[10..11]: this step's send counts (sdev[0..5] picks, [8..9] gap counters)
+constexpr int SDEV_TOTALS = 10;   // sdev[10..11]: this step's send counts (sdev[0..7] picks, [8..9] gap counters)
 
 struct RankState {
     sph_ctx* c = nullptr;
@@ -397,7 +397,7 @@ int phase_count(RankState& R) {
     R.nb_send = slab_send_blocks(0, (int32_t)std::max<int64_t>(R.n_prev_ub, 1));
     KTimer t(ctx, "slab_count", 4.0 * R.n_prev_ub);
     launch_slab_count_dev(ctx->keys, R.dz, R.nb_send, gyz(ctx), col_le(ctx), col_ge(ctx), ctx->sblk,
-                          ctx->sdev + SDEV_TOTALS, ctx->stream);
+                          ctx->sdev + SDEV_TOTALS, ctx->stream, R.since_cut >= 3);
     CKPT(R, "count");
     return SPH_OK;
 }
@@ -418,7 +418,8 @@ int phase_pack(RankState& R, Multi& M) {
         launch_slab_pack_dev(ctx->keys, ctx->pos, ctx->vel, ctx->id, ctx->sk_valid ? ctx->sk_cur : nullptr,
                              (uint32_t)ctx->grid.cx0 * gyz(ctx), R.dz,
                              R.nb_send, gyz(ctx), s, col_le(ctx),
-                             col_ge(ctx), ctx->sblk, R.msg_out[s], R.c1o[s], ctx->sdev + SDEV_TOTALS + s, ctx->stream);
+                             col_ge(ctx), ctx->sblk, R.msg_out[s], R.c1o[s], ctx->sdev + SDEV_TOTALS + s, ctx->stream,
+                             R.since_cut >= 3);
     }
     HIPCHK(hipGetLastError());
     // the peer copies of a local group wait for it (RCCL orders its sends on this stream itself); a
@@ -583,8 +584,9 @@ int phase_assemble(RankState& R, bool exact) {
         }
         const int32_t lc_lo = ctx->sl.cx_lo - ctx->grid.cx0, lc_hi = ctx->sl.cx_hi - ctx->grid.cx0;
         CsPick pick{{col_start(ctx, 0), col_start(ctx, lc_lo), col_start(ctx, lc_lo + 1), col_start(ctx, lc_hi - 1),
-                     col_start(ctx, lc_hi), col_start(ctx, ctx->grid.gx)},
-                    6, R.dz->pick, nullptr};
+                     col_start(ctx, lc_hi), col_start(ctx, ctx->grid.gx), col_start(ctx, std::min(lc_lo + 2, lc_hi)),
+                     col_start(ctx, std::max(lc_hi - 2, lc_lo))},
+                    8, R.dz->pick, nullptr};
         ResortScratch w = resort_scratch(ctx);
         w.dz = R.dz;
         w.err = &R.dz->flags;
@@ -616,8 +618,8 @@ int phase_assemble(RankState& R, bool exact) {
                               R.right >= 0 ? (const void*)(R.msg_in[1] + MSG_HDR_F4) : nullptr, (int32_t)h.nr, true);
         if (r != SPH_OK) return r;
         ctx->rng_pending = false;
-        // the picked column starts (sdev[0..5]) and the slot count into the device sizes
-        HIPCHK(hipMemcpyAsync(R.dz->pick, ctx->sdev, 6 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+        // the picked column starts (sdev[0..7]) and the slot count into the device sizes
+        HIPCHK(hipMemcpyAsync(R.dz->pick, ctx->sdev, 8 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
         const uint32_t nn = (uint32_t)ctx->n;
         HIPCHK(hipMemcpyAsync(&R.dz->n, &nn, sizeof nn, hipMemcpyHostToDevice, s));
         HIPCHK(hipStreamSynchronize(s));   // nn lives on this stack frame
@@ -668,6 +670,7 @@ void force_dev(sph_ctx* ctx, const uint32_t* lo, const uint32_t* hi, int64_t gri
     KTimer t(ctx, "force_integrate", 76.0 * (double)grid_ub, true);
     MoverSink mv = mover_sink(ctx);
     mv.err = &ctx->dz->flags;
+    mv.jump = &ctx->dz->jump;
     launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, (int32_t)grid_ub, ctx->grid, ctx->sc, dt, forcing(ctx),
                        ctx->pos2, ctx->vel2, ctx->keys, mv, hit_mask_read(ctx), path_ctr(ctx), ctx->stream, DevRange{lo, hi});
 }
@@ -832,11 +835,12 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
             flags |= L[9];
         }
         if (flags)
-            return fail(pctx, SPH_ERR_CAPACITY, "slab step %lld: a rank flagged%s%s%s%s (flags %#x, seen two steps on)",
+            return fail(pctx, SPH_ERR_CAPACITY, "slab step %lld: a rank flagged%s%s%s%s%s (flags %#x, seen two steps on)",
                         (long long)M.steps, (flags & SZ_OVF_MSG) ? " a halo message overflow" : "",
                         (flags & SZ_OVF_CAP) ? " slots over capacity" : "",
                         (flags & SZ_RHO_MISMATCH) ? " a ghost density count mismatch" : "",
-                        (flags & SZ_OVF_MOVERS) ? " a mover list / re-sort destination out of range" : "", flags);
+                        (flags & SZ_OVF_MOVERS) ? " a mover list / re-sort destination out of range" : "",
+                        (flags & SZ_JUMP) ? " a particle that left the held columns in one step" : "", flags);
         for (auto& R : M.ranks) {
             if (R.left < 0 && R.right < 0) continue;   // no messages: nothing to size
             // the counts of two steps before: both neighbours read the same numbers

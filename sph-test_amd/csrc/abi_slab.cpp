@@ -14,10 +14,11 @@ int sph::slab_sync_ranges(sph_ctx* ctx) {
         SlabSizes h;
         HIPCHK(hipMemcpy(&h, ctx->dz, sizeof h, hipMemcpyDeviceToHost));
         if (h.flags)
-            return fail(ctx, SPH_ERR_CAPACITY, "slab step:%s%s%s%s", (h.flags & SZ_OVF_MSG) ? " halo message overflow" : "",
+            return fail(ctx, SPH_ERR_CAPACITY, "slab step:%s%s%s%s%s", (h.flags & SZ_OVF_MSG) ? " halo message overflow" : "",
                         (h.flags & SZ_OVF_CAP) ? " slots over capacity" : "",
                         (h.flags & SZ_RHO_MISMATCH) ? " ghost density count mismatch" : "",
-                        (h.flags & SZ_OVF_MOVERS) ? " mover list / re-sort destination out of range" : "");
+                        (h.flags & SZ_OVF_MOVERS) ? " mover list / re-sort destination out of range" : "",
+                        (h.flags & SZ_JUMP) ? " a particle left the held columns in one step" : "");
         for (int k = 0; k < 10; ++k) ctx->rng[k] = (int32_t)h.rg[k];
         ctx->o0 = (int32_t)h.o0;
         ctx->o1 = (int32_t)h.o1;
@@ -259,8 +260,9 @@ int sph::slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const voi
     // ranges from the cell table at column starts: picked on the device (density reads them there)
     // and written to mapped pinned memory; slab_sync_ranges waits for the event after the sort
     const int32_t lc_lo = ctx->sl.cx_lo - ctx->grid.cx0, lc_hi = ctx->sl.cx_hi - ctx->grid.cx0;
-    const int32_t idx[6] = {col_start(ctx, 0), col_start(ctx, lc_lo), col_start(ctx, lc_lo + 1),
-                            col_start(ctx, lc_hi - 1), col_start(ctx, lc_hi), col_start(ctx, ctx->grid.gx)};
+    const int32_t idx[8] = {col_start(ctx, 0), col_start(ctx, lc_lo), col_start(ctx, lc_lo + 1),
+                            col_start(ctx, lc_hi - 1), col_start(ctx, lc_hi), col_start(ctx, ctx->grid.gx),
+                            col_start(ctx, std::min(lc_lo + 2, lc_hi)), col_start(ctx, std::max(lc_hi - 2, lc_lo))};
     if (ctx->resort_mode != 0 && !many && !force_full && ctx->sk_valid && n > 0) {
         // incremental: the re-sort reads [left records | own slots | right records] in place. The force
         // pass already appended the own movers (window keys); the records' keys and movers join here.
@@ -276,8 +278,8 @@ int sph::slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const voi
         KTimer t(ctx, "resort", (double)n * (2 * 4 + 2 * 36));
         launch_slab_cs_old(ctx->cs, ctx->grid.ncells, gyz, (uint32_t)ctx->grid.gx, ctx->has_left, ctx->has_right,
                            nl - ctx->o0, ctx->keys2, nl, no, nr, s);
-        CsPick pick{{0}, 6, ctx->sdev, ctx->rng_host};   // the ranges, read as the cell table completes
-        for (int k = 0; k < 6; ++k) pick.idx[k] = idx[k];
+        CsPick pick{{0}, 8, ctx->sdev, ctx->rng_host};   // the ranges, read as the cell table completes
+        for (int k = 0; k < 8; ++k) pick.idx[k] = idx[k];
         ResortScratch w = resort_scratch(ctx);
         w.mi_off = nl - ctx->o0;   // own movers were appended by slot in the previous order
         launch_resort(src, ctx->cs, ctx->grid.ncells, (int32_t)n, ctx->mv_count + used, ctx->mv_count + (1 - used), w,
@@ -323,7 +325,7 @@ int sph::slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const voi
         if (ctx->resort_mode != 0 && n > 0)
             HIPCHK(hipMemcpyAsync(ctx->sk_cur, sk, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
         HIPCHK(hipMemsetAsync(ctx->mv_count, 0, 2 * sizeof(uint32_t), s));
-        launch_pick(ctx->cs, idx, 6, ctx->sdev, s, ctx->rng_host);
+        launch_pick(ctx->cs, idx, 8, ctx->sdev, s, ctx->rng_host);
     }
     HIPCHK(hipEventRecord(ctx->rng_ev, s));
     ctx->rng_pending = true;

@@ -164,16 +164,20 @@ struct SlabSizes {
     uint32_t nl, nr;          // records taken from the left / right message (clamped to capacity)
     uint32_t o0, o1;          // owned slots of the previous sorted order
     uint32_t no, n;           // o1 - o0; assembled slots nl + no + nr
-    uint32_t pick[6];         // column starts of the new order (launch_resort's CsPick)
+    uint32_t pick[8];         // column starts of the new order (launch_resort's CsPick): columns 0, lo, lo+1,
+                              // hi-1, hi, gx (local), then lo+2 and hi-2 (clamped into [lo, hi]): the send candidates
     uint32_t rg[10];          // ghost-left [0,1), owned [2,3), ghost-right [4,5), boundary columns [6,7), [8,9)
     uint32_t fr[6];           // force pass: interior [0,1), boundary [2,3) and [4,5)
     uint32_t dropped;         // own particles the assemble dropped (left the held window)
     uint32_t flags;           // sticky: SZ_* bits
+    uint32_t jump;            // this step's force pass moved an own particle by more than one column (the next
+                              // step's sends then scan every own slot; cleared when the sizes are derived)
 };
 constexpr uint32_t SZ_OVF_MSG = 1u;     // a halo message held more records than its capacity
 constexpr uint32_t SZ_OVF_CAP = 2u;     // the assembled slots exceed the context's capacity
 constexpr uint32_t SZ_RHO_MISMATCH = 4u;  // a ghost column and the densities received differ in count
 constexpr uint32_t SZ_OVF_MOVERS = 8u;    // a mover list or a re-sort destination past the slot capacity
+constexpr uint32_t SZ_JUMP = 16u;         // an own particle left the held window in one step (two columns or more)
 // Halo messages: one 32-byte header record, then the records. Header: (count, capacity, 0, 0 | 0...)
 constexpr int MSG_HDR_F4 = 2;
 // What the assembled layout is computed from: the two message headers (null: no neighbour), the
@@ -205,6 +209,7 @@ __device__ __forceinline__ void slab_sizes_store(SlabSizes* dz, uint32_t nl, uin
     dz->nr = nr;
     dz->no = no;
     dz->n = nl + no + nr;
+    dz->jump = 0u;             // read by this step's sends (before); set again by its force pass (after)
     atomicOr(&dz->flags, f);   // other workgroups of k_slab_rec may be setting SZ_OVF_MOVERS meanwhile
 }
 #endif
@@ -220,6 +225,7 @@ struct MoverSink {
     uint32_t* rank;       // 3 x cap rank accumulators, zeroed here
     uint32_t cap;
     uint32_t* err = nullptr;   // SZ_OVF_MOVERS is or-ed here if the list would pass cap (entries dropped)
+    uint32_t* jump = nullptr;  // slab step: SlabSizes.jump (a column jump > 1), SZ_JUMP into err (window exit)
 };
 
 #if defined(__HIPCC__)
@@ -421,13 +427,14 @@ void launch_pick(const uint32_t* cs, const int32_t* idx, int32_t m, uint32_t* ou
 // count + pack over the owned slots [dz->o0, dz->o1): the same order-preserving compaction as above,
 // into messages of a header and `cap[side]` records (header = true count; records past cap dropped and
 // flagged by the receiver). nb_ub: count-block upper bound (slab_send_blocks of the slot bound).
+// cand: steady state, scan only the columns a send can come from (slab.hip send_ranges)
 void launch_slab_count_dev(const uint32_t* keys, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz, int32_t col_le,
-                           int32_t col_ge, uint32_t* blk, uint32_t* totals, hipStream_t s);
+                           int32_t col_ge, uint32_t* blk, uint32_t* totals, hipStream_t s, bool cand);
 // total: the side's count from launch_slab_count_dev, written into the message header
 void launch_slab_pack_dev(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
                           const uint32_t* sk, uint32_t key_base, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz,
                           int32_t side, int32_t col_le, int32_t col_ge, const uint32_t* blk, float4* msg, int32_t cap,
-                          const uint32_t* total, hipStream_t s);
+                          const uint32_t* total, hipStream_t s, bool cand);
 int32_t slab_send_blocks(int32_t b, int32_t e);
 // the received messages' counts -> dz (nl, nr clamped to the capacities, no, n, overflow flags)
 void launch_slab_sizes(SlabSizes* dz, const float4* msg_l, const float4* msg_r, int32_t cap_l, int32_t cap_r,

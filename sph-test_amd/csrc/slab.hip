@@ -43,23 +43,46 @@ constexpr int SL_SEND = SL_BLK * SL_PER;
 
 int32_t slab_send_blocks(int32_t b, int32_t e) { return e > b ? (e - b + SL_SEND - 1) / SL_SEND : 1; }
 
+// The own slots each side's sends are taken from (previous order). Device-sized steps: all own slots
+// [o0, o1), or, in steady state (cand: the cut is older than the previous step, so its column starts are
+// the picks), only the columns a send can come from: a particle moves less than a column per step, so one
+// that is now in column <= lo was in lo or lo + 1 (left), >= hi - 1 in hi - 2 or hi - 1 (right). A force
+// pass that moved an own particle further sets dz->jump, and the next sends scan every own slot again.
+__device__ __forceinline__ void send_ranges(const SlabSizes* __restrict__ dz, int32_t cand, int32_t& bl, int32_t& el,
+                                            int32_t& br, int32_t& er) {
+    bl = br = (int32_t)dz->o0;
+    el = er = (int32_t)dz->o1;
+    if (cand && dz->jump == 0u) {
+        el = max(bl, min(el, (int32_t)dz->pick[6]));
+        br = min(er, max(br, (int32_t)dz->pick[7]));
+    }
+}
+
 __global__ __launch_bounds__(SL_BLK) void k_slab_count(const uint32_t* __restrict__ keys, int32_t b, int32_t e,
                                                        uint32_t gyz, int32_t col_le, int32_t col_ge,
                                                        uint32_t* __restrict__ blk, int32_t nblk,
-                                                       const SlabSizes* __restrict__ dz) {
+                                                       const SlabSizes* __restrict__ dz, int32_t cand) {
     __shared__ uint32_t wl[SL_WAVES], wr[SL_WAVES];
-    if (dz) {   // device-sized step: the owned slots of the previous order; nblk is an upper bound
-        b = (int32_t)dz->o0;
-        e = (int32_t)dz->o1;
-    }
+    int32_t bl = b, el = e, br = b, er = e;
+    if (dz) send_ranges(dz, cand, bl, el, br, er);   // device-sized step; nblk is an upper bound
     uint32_t cl = 0, cr = 0;
-    const int32_t i0 = b + blockIdx.x * SL_SEND + threadIdx.x;
+    if (bl == br && el == er) {   // one range for both sides
+        const int32_t i0 = bl + blockIdx.x * SL_SEND + threadIdx.x;
 #pragma unroll
-    for (int j = 0; j < SL_PER && e > b; ++j) {   // clamped index: every load issues before any is used
-        const int32_t i = i0 + j * SL_BLK;
-        const int32_t col = (int32_t)(keys[min(i, e - 1)] / gyz);
-        cl += i < e && col <= col_le;
-        cr += i < e && col >= col_ge;
+        for (int j = 0; j < SL_PER && el > bl; ++j) {   // clamped index: every load issues before any is used
+            const int32_t i = i0 + j * SL_BLK;
+            const int32_t col = (int32_t)(keys[min(i, el - 1)] / gyz);
+            cl += i < el && col <= col_le;
+            cr += i < el && col >= col_ge;
+        }
+    } else {
+        const int32_t l0 = bl + blockIdx.x * SL_SEND + threadIdx.x, r0 = br + blockIdx.x * SL_SEND + threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < SL_PER; ++j) {
+            const int32_t il = l0 + j * SL_BLK, ir = r0 + j * SL_BLK;
+            if (il < el) cl += (int32_t)(keys[il] / gyz) <= col_le;
+            if (ir < er) cr += (int32_t)(keys[ir] / gyz) >= col_ge;
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -142,15 +165,17 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_pack(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ blk, int32_t nblk,
                                                       float4* __restrict__ out, const SlabSizes* __restrict__ dz,
                                                       uint32_t cap, float4* __restrict__ hdr,
-                                                      const uint32_t* __restrict__ total) {
+                                                      const uint32_t* __restrict__ total, int32_t cand) {
     __shared__ uint32_t wc[SL_PER][SL_WAVES];
     const int w = threadIdx.x >> 6;
     // the message header (device-sized steps): the count k_slab_scan left, written by one lane here
     // instead of by a launch of its own
     if (hdr && blockIdx.x == 0 && threadIdx.x == 0) write_header(hdr, *total, cap);
-    if (dz) {   // device-sized step (see k_slab_count)
-        b = (int32_t)dz->o0;
-        e = (int32_t)dz->o1;
+    if (dz) {   // device-sized step: this side's range, as k_slab_count took it
+        int32_t bl, el, br, er;
+        send_ranges(dz, cand, bl, el, br, er);
+        b = side == 0 ? bl : br;
+        e = side == 0 ? el : er;
     }
     if (b + (int32_t)blockIdx.x * SL_SEND >= e) return;   // whole workgroup, before the barrier
     const int32_t i0 = b + blockIdx.x * SL_SEND + threadIdx.x;
@@ -350,7 +375,7 @@ void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, 
 void launch_slab_count(const uint32_t* keys, int32_t b, int32_t e, uint32_t gyz, int32_t col_le, int32_t col_ge,
                        uint32_t* blk, uint32_t* totals, hipStream_t s, int64_t* totals64) {
     const int32_t nb = slab_send_blocks(b, e);
-    k_slab_count<<<nb, SL_BLK, 0, s>>>(keys, b, e, gyz, col_le, col_ge, blk, nb, nullptr);
+    k_slab_count<<<nb, SL_BLK, 0, s>>>(keys, b, e, gyz, col_le, col_ge, blk, nb, nullptr, 0);
     k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb, totals, totals64, nullptr, nullptr, 0, 0);
 }
 
@@ -360,21 +385,21 @@ void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel
     const int32_t nb = slab_send_blocks(b, e);
     if (e > b)
         k_slab_pack<<<nb, SL_BLK, 0, s>>>(keys, pos, vel, id, sk, key_base, b, e, gyz, side, col_le, col_ge, blk, nb,
-                                          out, nullptr, 0xffffffffu, nullptr, nullptr);
+                                          out, nullptr, 0xffffffffu, nullptr, nullptr, 0);
 }
 
 void launch_slab_count_dev(const uint32_t* keys, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz, int32_t col_le,
-                           int32_t col_ge, uint32_t* blk, uint32_t* totals, hipStream_t s) {
-    k_slab_count<<<nb_ub, SL_BLK, 0, s>>>(keys, 0, 0, gyz, col_le, col_ge, blk, nb_ub, dz);
+                           int32_t col_ge, uint32_t* blk, uint32_t* totals, hipStream_t s, bool cand) {
+    k_slab_count<<<nb_ub, SL_BLK, 0, s>>>(keys, 0, 0, gyz, col_le, col_ge, blk, nb_ub, dz, cand ? 1 : 0);
     k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb_ub, totals, nullptr, nullptr, nullptr, 0, 0);
 }
 
 void launch_slab_pack_dev(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
                           const uint32_t* sk, uint32_t key_base, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz,
                           int32_t side, int32_t col_le, int32_t col_ge, const uint32_t* blk, float4* msg, int32_t cap,
-                          const uint32_t* total, hipStream_t s) {
+                          const uint32_t* total, hipStream_t s, bool cand) {
     k_slab_pack<<<nb_ub, SL_BLK, 0, s>>>(keys, pos, vel, id, sk, key_base, 0, 0, gyz, side, col_le, col_ge, blk,
-                                         nb_ub, msg + MSG_HDR_F4, dz, (uint32_t)cap, msg, total);
+                                         nb_ub, msg + MSG_HDR_F4, dz, (uint32_t)cap, msg, total, cand ? 1 : 0);
 }
 
 // The assembled layout from the message headers and the owned range of the previous order (a

@@ -639,7 +639,17 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     keys_o[i] = key;
     // the mover list takes the window key: in a slab, a particle that left the held columns sorts
     // last (window_key = cell_key in a single domain); it changed iff the clamped key changed
-    append_mover(mv, i, window_key(g, np[0], np[1], np[2]));
+    const uint32_t wk = window_key(g, np[0], np[1], np[2]);
+    if (mv.jump && mv.sk) {   // slab step: the next sends assume moves of at most one column (slab.hip send_ranges)
+        const uint32_t gyz = (uint32_t)g.gy * (uint32_t)g.gz;
+        const int32_t d = (int32_t)(wk / gyz) - (int32_t)(mv.sk[i] / gyz);
+        if (wk >= g.ncells) {
+            if (mv.err) atomicOr(mv.err, SZ_JUMP);   // left the held window: it reaches no neighbour
+        } else if (d > 1 || d < -1) {
+            *mv.jump = 1u;
+        }
+    }
+    append_mover(mv, i, wk);
 }
 
 // dr set: [ib, ie) only sizes the grid (an upper bound); the kernels read their bounds from dr
