@@ -84,3 +84,39 @@ def test_watchdog_fires_with_a_failure_line():
     assert r.returncode == 3
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["value"] is None and "a stuck collective" in line["watchdog"] and line["n_gpus"] == 2
+
+
+def test_device_code_hash_identifies_the_code_objects(pkg):
+    """The counter files are stamped with this hash and bench.py refuses counters of other code: it is the
+    sha256 of libsphhip.so's .hip_fatbin section, stable across loads, and differs for other bytes."""
+    import hashlib
+    A = pkg._abi
+    h = A.device_code_hash()
+    assert len(h) == 16 and int(h, 16) >= 0
+    assert A.device_code_hash() == h
+    data = A.lib_path().read_bytes()
+    assert hashlib.sha256(data).hexdigest()[:16] != h        # the section, not the whole file
+
+
+def test_load_pmc_refuses_other_code(tmp_path, monkeypatch):
+    """A counter file stamped with another hash yields no traffic and a note saying why."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "pmc_C3.json").write_text(json.dumps({"config": "C3", "device_code_hash": "0000000000000000",
+                                                  "kernel_bytes": {"force_integrate": 123.0}, "kernels": {}}))
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    out = bench.load_pmc("C3", "1111111111111111")
+    assert "traffic" not in out and "1111111111111111" in out["note"]
+    out = bench.load_pmc("C3", "0000000000000000")
+    assert out["traffic"] == 123.0
+
+
+def test_step_bytes_follow_survey_8d():
+    """B = 152 + 20·P + 8·C/N (P = ceil(key bits / 8) sort passes)."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    assert bench.step_bytes_per_particle(22, 0, 1) == 152 + 20 * 3
+    assert abs(bench.step_bytes_per_particle(22, 3663680, 1048576) - (212 + 8 * 3663680 / 1048576)) < 1e-9
+    assert bench.FORCE_BYTES_PER_PARTICLE == 56.0
