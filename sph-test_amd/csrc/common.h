@@ -33,6 +33,7 @@ struct SphConst {
     float gx, gy, gz;
     float Lx, Ly, Lz;
     float wall_e;
+    float inv_h2;   // 1/h², the neighbour passes' q = sqrt(r²/h²)
 };
 
 // Model R uniforms (SimulateParticles.compute:89-100) + DragInput (:70-74).

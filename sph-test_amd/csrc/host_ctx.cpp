@@ -128,6 +128,7 @@ int derive(sph_ctx* ctx) {
         s.gx = p.gravity[0]; s.gy = p.gravity[1]; s.gz = p.gravity[2];
         s.Lx = p.box[0]; s.Ly = p.box[1]; s.Lz = ctx->cfg.dim == 3 ? p.box[2] : 0.f;
         s.wall_e = p.wall_restitution;
+        s.inv_h2 = s.inv_h * s.inv_h;
     }
     g.cx0 = 0;
     g.gx_all = g.gx;

@@ -9,8 +9,8 @@
 // (broadcast). The visit order is the §0 order.
 //
 // Pass 1 scans 4 candidates per iteration, branchless (clamped LDS reads, predicated
-// accumulation), and records every candidate's r² < 4h² as one bit in visit order (the hit mask,
-// common.h HitMask; the sign bit of r² − 4h²: exact). Only ~30% of the trimmed candidates are within
+// accumulation), and records every candidate's q = r/h ≤ 2 as one bit in visit order (the hit mask,
+// common.h HitMask; the sign bit of 2 − q, see spline_w4). Only ~30% of the trimmed candidates are within
 // 2h. Pass 2 runs on the same positions and windows, so it takes its hits from the mask instead of
 // re-reading every candidate from LDS and recomputing its distance: per staged plane it walks the
 // plane's bits (its three row windows back to back) in one pair loop, one hit per iteration (find-first-
@@ -51,6 +51,14 @@ constexpr int TF_GCAP = SPH_TF_GCAP;
 #define SPH_WALK_UNROLL 4
 #endif
 constexpr int TF_FALLBACK = 4 * TF_GCAP;
+// Slots each thread stages per round (loads in flight together): pass 1 up to 1,350 slots in 256 threads
+// takes all of a plane in one or two rounds; pass 2 holds 40 B per slot in registers.
+constexpr int TT_STAGE_U = 3;
+constexpr int TF_STAGE_U = 2;
+struct Staged {
+    float4 p, v;
+    float2 r;
+};
 
 struct BlockRows {
     int64_t kf, kl;           // key range of the block's targets
@@ -155,17 +163,28 @@ __device__ __forceinline__ float dist2(float4 a, float4 b) {
     return dx * dx + dy * dy + dz * dz;
 }
 
-// 4·w(q) of the unnormalised cubic spline (W = σ·w) for r² < 4h², else 0. Branchless: both arms
+// 4·w(q) of the unnormalised cubic spline (W = σ·w) for q ≤ 2, else 0. Branchless: both arms
 // are computed and selected (a ?: over expressions compiles to an exec branch per candidate).
 // Scaling by 4 (and the final 0.25) is exact in binary floating point: no rounding is added.
 // 4w = (2−q)₊³ − 4(1−q)₊³: the outer arm (2−q)₊³ lies below the inner polynomial exactly where
 // q ≥ 1 (their difference is 4(1−q)³), and (2−q)₊ is 0 past the support, where the polynomial is ≥ 4.
 // So one min replaces both selects (18 VALU slots per candidate instead of 20; C3 pass 1 −5%).
-// A candidate at r² ≥ 4h² whose q rounds just below 2 adds (2−q)³ < 1e-20 instead of 0.
-__device__ __forceinline__ float spline_w4(const SphConst& c, float r2) {
-    const float q = __builtin_amdgcn_sqrtf(r2) * c.inv_h;
-    const float t = fmaxf(2.0f - q, 0.0f);
-    return fminf(fmaf(q * q, fmaf(3.0f, q, -6.0f), 4.0f), t * t * t);
+// q = sqrt(r²/h²) (q² is then r²/h², no square), and v = 2 − q comes back: its sign bit is set exactly
+// for the candidates that are NOT neighbours (q > 2), so the hit test costs no instruction of its own
+// (pass 1 records the complement and inverts each word once). A neighbour is q ≤ 2 with q rounded as
+// here; r = 2h exactly adds 0 in both passes. Against sqrt(r²)·(1/h), q·q and r² − 4h² for the bit: two
+// VALU fewer per candidate.
+__device__ __forceinline__ float spline_w4(const SphConst& c, float r2, float& v) {
+    const float r2h = r2 * c.inv_h2;
+    const float q = __builtin_amdgcn_sqrtf(r2h);
+    v = 2.0f - q;
+    const float t = __builtin_amdgcn_fmed3f(v, 0.0f, 4.0f);   // max(v, 0) (v ≤ 2); fmaxf adds a canonicalize here
+    return fminf(fmaf(r2h, fmaf(3.0f, q, -6.0f), 4.0f), t * t * t);
+}
+
+// The neighbour test of both passes, for paths without the hit mask: the bit pass 1 records.
+__device__ __forceinline__ bool is_hit(const SphConst& c, float r2) {
+    return (__float_as_uint(2.0f - __builtin_amdgcn_sqrtf(r2 * c.inv_h2)) >> 31) == 0u;
 }
 
 // The scans use x, y, z only, and the compiler then narrows the float4 LDS read to
@@ -175,14 +194,35 @@ __device__ __forceinline__ void keep_b128(float4 a, float4 b, float4 c, float4 d
     asm volatile("" ::"v"(a.w), "v"(b.w), "v"(c.w), "v"(d.w));
 }
 
-// Stage the plane's three intervals back to back: slot t of interval r sits at off[r] + t.
-template <typename F>
-__device__ __forceinline__ void stage_plane(const int32_t (&c0)[3], const int32_t (&len)[3], int32_t total, F&& put) {
-    for (int32_t t = threadIdx.x; t < total; t += TT_BLK) {
-        const int r = t < len[0] ? 0 : (t < len[0] + len[1] ? 1 : 2);
-        const int32_t o = r == 0 ? 0 : (r == 1 ? len[0] : len[0] + len[1]);
-        put(t, (r == 0 ? c0[0] : (r == 1 ? c0[1] : c0[2])) + (t - o));
+// Stage the plane's three intervals back to back: slot t of interval r sits at off[r] + t, from sorted
+// slot c0[r] + (t − off[r]). U slots per thread per round, all U loads issued before the LDS writes, so
+// they are in flight together; the source interval is picked by selects (indexing c0[] by a computed r
+// put the array in scratch memory: one scratch load and one global load, serialised, per staged slot).
+template <int U, typename L, typename W>
+__device__ __forceinline__ void stage_plane(const int32_t (&c0)[3], const int32_t (&len)[3], int32_t total, L&& load,
+                                            W&& write) {
+    const int32_t e0 = len[0], e1 = len[0] + len[1];
+    const int32_t d0 = c0[0], d1 = c0[1] - e0, d2 = c0[2] - e1;
+    for (int32_t base = threadIdx.x; base < total; base += U * TT_BLK) {
+        decltype(load(0)) v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t t = base + u * TT_BLK;
+            if (t < total) v[u] = load(t + (t < e0 ? d0 : (t < e1 ? d1 : d2)));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t t = base + u * TT_BLK;
+            if (t < total) write(t, v[u]);
+        }
     }
+}
+
+// One contiguous run [src0, src0 + ln) into slots [0, ln) (the chunked rows), the same way.
+template <int U, typename L, typename W>
+__device__ __forceinline__ void stage_run(int32_t src0, int32_t ln, L&& load, W&& write) {
+    const int32_t c0[3] = {src0, 0, 0}, len[3] = {ln, 0, 0};
+    stage_plane<U>(c0, len, ln, load, write);
 }
 
 // A plane whose three intervals exceed the LDS budget: consecutive rows that fit together are staged as
@@ -264,53 +304,66 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
     const float4 pi = pos[valid ? i : ilast];
     const BlockRows b = block_rows(g, pos, i0, ilast, pi);
     float s = 0.0f;
+    auto load_p = [&](int32_t src) { return pos[src]; };
+    auto write_p = [&](int32_t t, float4 e) { sp[t] = e; };
     // hit-mask writer: a 64-bit shift register (mh:ml) takes the newest bit at bit 0 (one v_alignbit per
     // candidate: ml = ml << 1 | sign(r² − 4h²)); the mn unwritten bits sit at [0, mn). A word leaves once 32
     // are pending: the oldest 32 (one v_alignbit), bit-reversed so that the oldest lands at bit 0.
+    // The mask's words are stored while wp < wend (HM_WORDS of them; none without a mask).
     uint32_t mh = 0, ml = 0;
-    int32_t mn = 0, mw = 0;
+    int32_t mn = 0;
     const bool rec = valid && hm.w != nullptr;
     uint32_t* wp = rec ? hm.w + i : nullptr;
-    auto bit = [&](float r2) { ml = __builtin_amdgcn_alignbit(ml, __float_as_uint(r2 - c.four_h2), 31u); };
-    auto emit = [&]() {
-        if (mn >= 32) {
-            mn -= 32;
-            if (rec && mw < HM_WORDS) {
-                *wp = __builtin_bitreverse32(__builtin_amdgcn_alignbit(mh, ml, (uint32_t)mn));
-                wp += hm.stride;
-            }
-            ++mw;
+    uint32_t* const wend = rec ? hm.w + i + (size_t)HM_WORDS * hm.stride : nullptr;
+    // the register pair takes sign(2 − q): 1 for a candidate that is NOT a neighbour; words are inverted
+    auto bit = [&](float v) { ml = __builtin_amdgcn_alignbit(ml, __float_as_uint(v), 31u); };
+    auto store = [&](uint32_t sh) {   // the oldest 32 pending bits, sh newer ones above them
+        if (wp < wend) {
+            *wp = __builtin_bitreverse32(~__builtin_amdgcn_alignbit(mh, ml, sh));
+            wp += hm.stride;
         }
     };
     auto one = [&](float r2) {   // a single candidate (scalar tail, global gather)
+        float v;
+        s += spline_w4(c, r2, v);
         mh = __builtin_amdgcn_alignbit(mh, ml, 31u);
-        bit(r2);
-        ++mn;
-        emit();
+        bit(v);
+        if (++mn >= 32) {
+            mn -= 32;
+            store((uint32_t)mn);
+        }
     };
+    // Four candidates per iteration, through an LDS pointer. mn advances by 4, so the iterations that
+    // complete a word are known before the loop: the first at k0 = (31 − mn)/4, then every eighth, each
+    // with mn mod 4 newer bits above the word. One compare per iteration (pointer against the next
+    // word's iteration) replaces the counter update and compare, and the loop bound is the pointer too.
     auto scan = [&](int32_t lo, int32_t ln) {
         SPH_DIAG_ADD(8, wave_sum(ln));          // candidates
         SPH_DIAG_ADD(9, wave_max(ln >> 2));     // 4-candidate iterations
         SPH_DIAG_ADD(10, wave_max(ln & 3));     // tail iterations
-        int32_t t = 0;
-        for (; t + 4 <= ln; t += 4) {
-            const float4 a = sp[lo + t], bb = sp[lo + t + 1], cc = sp[lo + t + 2], d = sp[lo + t + 3];
+        const int32_t n4 = ln >> 2;
+        const float4* p = sp + lo;
+        const float4* const pe = p + 4 * n4;
+        const float4* pw = p + 4 * ((31 - mn) >> 2);
+        const uint32_t sh = (uint32_t)mn & 3u;
+        for (; p < pe; p += 4) {
+            const float4 a = p[0], bb = p[1], cc = p[2], d = p[3];
             const float ra = dist2(pi, a), rb = dist2(pi, bb), rc = dist2(pi, cc), rd = dist2(pi, d);
-            s += spline_w4(c, ra);
-            s += spline_w4(c, rb);
-            s += spline_w4(c, rc);
-            s += spline_w4(c, rd);
+            float ua, ub, uc, ud;
+            s += spline_w4(c, ra, ua);
+            s += spline_w4(c, rb, ub);
+            s += spline_w4(c, rc, uc);
+            s += spline_w4(c, rd, ud);
             mh = __builtin_amdgcn_alignbit(mh, ml, 28u);
-            bit(ra); bit(rb); bit(rc); bit(rd);
-            mn += 4;
-            emit();
+            bit(ua); bit(ub); bit(uc); bit(ud);
+            if (p == pw) {
+                store(sh);
+                pw += 32;
+            }
             keep_b128(a, bb, cc, d);
         }
-        for (; t < ln; ++t) {
-            const float r2 = dist2(pi, sp[lo + t]);
-            s += spline_w4(c, r2);
-            one(r2);
-        }
+        mn = (mn + 4 * n4) & 31;
+        for (int32_t t = 4 * n4; t < ln; ++t) one(dist2(pi, sp[lo + t]));
     };
 #pragma unroll 1
     for (int p = 0; p < 3; ++p) {
@@ -331,7 +384,7 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
                 tot += lg[r];
             }
             __syncthreads();
-            stage_plane(c0, lg, tot, [&](int32_t t, int32_t src) { sp[t] = pos[src]; });
+            stage_plane<TT_STAGE_U>(c0, lg, tot, load_p, write_p);
             __syncthreads();
             int32_t o = 0;
 #pragma unroll
@@ -344,18 +397,14 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
         auto big_row = [&](int r) {
             if (len[r] > TT_FALLBACK) {
                 count_path(paths, 1);
-                for (int32_t j = r0[r]; j < r1[r]; ++j) {
-                    const float r2 = dist2(pi, pos[j]);
-                    s += spline_w4(c, r2);
-                    one(r2);
-                }
+                for (int32_t j = r0[r]; j < r1[r]; ++j) one(dist2(pi, pos[j]));
                 return;
             }
 #pragma unroll 1
             for (int32_t base = c0[r]; base < c1[r]; base += TT_GCAP) {
                 const int32_t ln = min(TT_GCAP, c1[r] - base);
                 __syncthreads();
-                for (int32_t t = threadIdx.x; t < ln; t += TT_BLK) sp[t] = pos[base + t];
+                stage_run<TT_STAGE_U>(base, ln, load_p, write_p);
                 __syncthreads();
                 const int32_t lo = max(r0[r], base) - base;
                 scan(lo, max(min(r1[r], base + ln) - base - lo, 0));
@@ -370,8 +419,8 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
     }
     SPH_BT_END(0);
     if (!valid) return;
-    if (rec && mn > 0 && mw < HM_WORDS)   // the last, partial word: bits [0, mn), zeros above
-        *wp = __builtin_bitreverse32(ml << (32 - mn));
+    if (mn > 0 && wp < wend)   // the last, partial word: bits [0, mn), zeros above
+        *wp = __builtin_bitreverse32(~ml << (32 - mn));
     const float d = c.mass * (c.sigma * (0.25f * s));
     const float tr = d * c.inv_rho0;
     const float t2 = tr * tr, t4 = t2 * t2;
@@ -530,15 +579,14 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         for (int32_t t = 0; __any(t < ln); ++t) {
             if (t < ln) {
                 const float4 pj = sp[lo + t];
-                if (dist2(pi, pj) < c.four_h2) pair_force(pk, pi, vi, ri.x, ri.y, pj, sv[lo + t], acc);
+                if (is_hit(c, dist2(pi, pj))) pair_force(pk, pi, vi, ri.x, ri.y, pj, sv[lo + t], acc);
             }
         }
     };
-    auto put = [&](int32_t t, int32_t src) {
-        const float4 p = pos[src], v = vel[src];
-        const float2 r = rp[src];
-        sp[t] = make_float4(p.x, p.y, p.z, r.x);
-        sv[t] = make_float4(v.x, v.y, v.z, r.y);
+    auto load_f = [&](int32_t src) { return Staged{pos[src], vel[src], rp[src]}; };
+    auto write_f = [&](int32_t t, const Staged& e) {
+        sp[t] = make_float4(e.p.x, e.p.y, e.p.z, e.r.x);
+        sv[t] = make_float4(e.v.x, e.v.y, e.v.z, e.r.y);
     };
 #pragma unroll 1
     for (int p = 0; p < 3; ++p) {
@@ -569,7 +617,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
                 tot += lg[r];
             }
             __syncthreads();
-            stage_plane(c0, lg, tot, put);
+            stage_plane<TF_STAGE_U>(c0, lg, tot, load_f, write_f);
             __syncthreads();
             if (by_mask) {
                 const int32_t l0 = wg[0], e2 = l0 + wg[1];
@@ -592,7 +640,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
                 if (by_mask) skip(r1[r] - r0[r]);
                 for (int32_t j = r0[r]; j < r1[r]; ++j) {
                     const float4 pj = pos[j];
-                    if (j != i && dist2(pi, pj) < c.four_h2) {
+                    if (j != i && is_hit(c, dist2(pi, pj))) {
                         const float4 vj = vel[j];
                         const float2 rj = rp[j];
                         pair_force(pk, pi, vi, ri.x, ri.y, make_float4(pj.x, pj.y, pj.z, rj.x),
@@ -605,7 +653,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
             for (int32_t base = c0[r]; base < c1[r]; base += TF_GCAP) {
                 const int32_t ln = min(TF_GCAP, c1[r] - base);
                 __syncthreads();
-                for (int32_t t = tid; t < ln; t += TT_BLK) put(t, base + t);
+                stage_run<TF_STAGE_U>(base, ln, load_f, write_f);
                 __syncthreads();
                 const int32_t lo = max(r0[r], base) - base;
                 const int32_t wl = max(min(r1[r], base + ln) - base - lo, 0);
