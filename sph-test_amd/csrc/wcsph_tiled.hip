@@ -53,8 +53,14 @@ constexpr int TF_GCAP = SPH_TF_GCAP;
 constexpr int TF_FALLBACK = 4 * TF_GCAP;
 // Slots each thread stages per round (loads in flight together): pass 1 up to 1,350 slots in 256 threads
 // takes all of a plane in one or two rounds; pass 2 holds 40 B per slot in registers.
-constexpr int TT_STAGE_U = 3;
-constexpr int TF_STAGE_U = 2;
+#ifndef SPH_TT_STAGE_U
+#define SPH_TT_STAGE_U 3
+#endif
+#ifndef SPH_TF_STAGE_U
+#define SPH_TF_STAGE_U 2
+#endif
+constexpr int TT_STAGE_U = SPH_TT_STAGE_U;
+constexpr int TF_STAGE_U = SPH_TF_STAGE_U;
 struct Staged {
     float4 p, v;
     float2 r;
@@ -432,27 +438,33 @@ struct ForceAcc {
     float ax, ay, az, sx, sy, sz;
 };
 
-// Per-launch constants of the pair body, folded on the host from SphConst (SPEC_SPH.md §2):
+// Per-launch constants of the pair body, folded on the host from SphConst (SPEC_SPH.md §2), q = r/h:
 //   W = σ·w4/4 with w4 = 4 + q²(3q − 6) (q < 1) or (2 − q)³;  G = −m·F (the kernel-gradient factor)
-//   G = kin_a·q + kin_b (q < 1) or kout·(2 − q)²/r;  Π_ij·ρ̄ = 2·α·c0·h·min(v·r, 0)/(r² + η²)
+//   = 3mσ/h²·(1 − 0.75q) (q < 1) or 0.75mσ/h·(2 − q)²/r = kf·g with kf = 0.75mσ/h² and g = 4 − 3q or
+//   (2 − q)²·h/r;  Π_ij·ρ̄ = 2·α·c0·h·min(v·r, 0)/(r² + η²);  XSPH ε·m·W/ρ̄ = kx·w4/(ρi + ρj).
+// The pair body adds g- and w4-weighted terms; kf and kx scale the target's sums once, at the end, and
+// g_in = −2 − (3q − 6) reuses w4's 3q − 6: two VALU fewer per pair than kin_a·q + kin_b (two SGPR operands:
+// one move) and kx·(1/ρ̄)·w4. q itself is r²·rsq(r²)·(1/h), the oracle's sqrt(r²)·(1/h) to an ulp: near the
+// support edge 2 − q cancels, and a q rounded another way (sqrt(r²/h²), measured) moves single-neighbour
+// splash particles past the parity bound (tests/test_gpu_parity_headline.py).
 struct PairK {
-    float inv_h, kin_a, kin_b, kout, kvisc, eta2, kx;
+    float inv_h, h, kvisc, eta2, kf, kx;
 };
 
 static PairK pair_constants(const SphConst& c) {
     PairK k;
     k.inv_h = c.inv_h;
-    k.kin_a = -2.25f * c.mass * c.sigma_h2;
-    k.kin_b = 3.0f * c.mass * c.sigma_h2;
-    k.kout = 0.75f * c.mass * c.sigma_h;
+    k.h = c.h;
     k.kvisc = -2.0f * c.ac0 * c.h;            // inv_rbar = 2/(ρi + ρj)
     k.eta2 = c.eta2;
-    k.kx = 0.5f * c.eps * c.mass * c.sigma;   // ε·m·W/ρ̄ = kx·w4/(ρi + ρj)
+    k.kf = 0.75f * c.mass * c.sigma_h2;
+    k.kx = 0.5f * c.eps * c.mass * c.sigma;
     return k;
 }
 
 // Pair body (SPEC_SPH.md §2). pj = (x, y, z, ρ_j), vj = (u, v, w, P_j/ρ_j²). Branchless, for
-// pairs with r < 2h: one rsq gives r and 1/r; r = 0 (coincident, distinct particles) gives q = 0.
+// pairs with q ≤ 2: one rsq gives r and 1/r; r = 0 (the target itself, or coincident distinct
+// particles) gives q = 0 and adds ±0 along dx = 0.
 __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi, float rhoi, float prhoi, float4 pj,
                                            float4 vj, ForceAcc& a) {
     const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
@@ -463,8 +475,9 @@ __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi,
     const float t2 = t * t;
     const bool inner = q < 1.0f;
     // both arms first, then a plain select (a ?: over expressions compiles to an exec branch)
-    const float w_in = fmaf(q * q, fmaf(3.0f, q, -6.0f), 4.0f), w_out = t2 * t;
-    const float g_in = fmaf(k.kin_a, q, k.kin_b), g_out = k.kout * t2 * rs;
+    const float c36 = fmaf(3.0f, q, -6.0f);
+    const float w_in = fmaf(q * q, c36, 4.0f), w_out = t2 * t;
+    const float g_in = -2.0f - c36, g_out = t2 * rs * k.h;
     const float w4 = inner ? w_in : w_out;
     const float G = inner ? g_in : g_out;
     const float du = vi.x - vj.x, dv = vi.y - vj.y, dw = vi.z - vj.z;
@@ -476,7 +489,7 @@ __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi,
     const float pij = fminf(vr, 0.0f) * k.kvisc * inv_es;
     const float cf = (prhoi + vj.w + pij) * G;
     a.ax += cf * dx; a.ay += cf * dy; a.az += cf * dz;
-    const float cx = k.kx * inv_s * w4;
+    const float cx = inv_s * w4;
     a.sx -= cx * du; a.sy -= cx * dv; a.sz -= cx * dw;
 }
 
@@ -673,6 +686,8 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     count_wave(paths, 5);   // waves (3 planes each)
     SPH_BT_END(1);
     if (!valid) return;
+    acc.ax *= pk.kf; acc.ay *= pk.kf; acc.az *= pk.kf;
+    acc.sx *= pk.kx; acc.sy *= pk.kx; acc.sz *= pk.kx;
     float nv[3] = {vi.x + (acc.ax + c.gx + fext_x) * dt, vi.y + (acc.ay + c.gy) * dt, vi.z + (acc.az + c.gz) * dt};
     float np[3] = {pi.x + (nv[0] + acc.sx) * dt, pi.y + (nv[1] + acc.sy) * dt, pi.z + (nv[2] + acc.sz) * dt};
     const float L[3] = {c.Lx, c.Ly, c.Lz};
