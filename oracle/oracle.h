@@ -27,6 +27,8 @@ typedef struct {
     float inv_cell_z;   /* z sub-cells: cell / zsub */
     int32_t G[3];       /* G[2] counts z sub-cells */
     int32_t zwin;       /* neighbour z window in sub-cells (zsub + 1) */
+    int32_t xsub;       /* x sub-columns per column: keys count sub-columns (SPEC_SPH.md §0) */
+    float inv_cxs;      /* xsub / cell (exact) */
 } or_grid;
 
 uint32_t or_cell_key(const or_grid* g, float x, float y, float z);

@@ -41,7 +41,7 @@ assert ADHESION84.itemsize == 84
 
 class OrGrid(C.Structure):
     _fields_ = [("origin", C.c_float * 3), ("inv_cell", C.c_float), ("inv_cell_z", C.c_float),
-                ("G", C.c_int32 * 3), ("zwin", C.c_int32)]
+                ("G", C.c_int32 * 3), ("zwin", C.c_int32), ("xsub", C.c_int32), ("inv_cxs", C.c_float)]
 
 
 class OrSphParams(C.Structure):
@@ -128,7 +128,7 @@ def sph_params(dim, dx, h, rho0, c0, alpha, eps_xsph, g, L, wall_e, f_amp=0.0, f
 
 
 def ncells(p: OrSphParams) -> int:
-    return int(p.grid.G[0]) * int(p.grid.G[1]) * int(p.grid.G[2])
+    return int(p.grid.G[0]) * int(p.grid.xsub) * int(p.grid.G[1]) * int(p.grid.G[2])
 
 
 def sph_step(p: OrSphParams, pos, vel, ids, dt, t=0.0, nthreads=0):

@@ -14,6 +14,9 @@
 #include <omp.h>
 #endif
 
+/* x sub-columns per column when SPH_XSUB is unset: the library's SPH_XSUB_DEFAULT (host.h) */
+#define OR_XSUB_DEFAULT 1
+
 static inline int32_t or_coord(float x, float origin, float inv_cell, int32_t G) {
     /* compute:103-104 — (uint)((p + R)/cell) with ftou (neg/NaN -> 0), clamp to [0,G-1] */
     float g = (x - origin) * inv_cell;
@@ -22,8 +25,9 @@ static inline int32_t or_coord(float x, float origin, float inv_cell, int32_t G)
     return (int32_t)g;
 }
 
+/* x counts sub-columns: xsub per column of G[0] (SPEC_SPH.md §0; xsub = 1 is the plain 2h grid) */
 uint32_t or_cell_key(const or_grid* g, float x, float y, float z) {
-    int32_t cx = or_coord(x, g->origin[0], g->inv_cell, g->G[0]);
+    int32_t cx = or_coord(x, g->origin[0], g->inv_cxs, g->G[0] * g->xsub);
     int32_t cy = or_coord(y, g->origin[1], g->inv_cell, g->G[1]);
     int32_t cz = or_coord(z, g->origin[2], g->inv_cell_z, g->G[2]);
     return ((uint32_t)cx * (uint32_t)g->G[1] + (uint32_t)cy) * (uint32_t)g->G[2] + (uint32_t)cz;
@@ -66,6 +70,12 @@ void or_sph_derive(or_sph_params* p) {
     p->grid.inv_cell = 1.0f / cell;
     p->grid.inv_cell_z = 1.0f / cz;
     p->grid.zwin = zsub + 1;
+    /* x sub-columns: SPH_XSUB (1 or 2) as the library reads it (sph-test_amd/csrc/host.h) */
+    int32_t xsub = OR_XSUB_DEFAULT;
+    const char* xe = getenv("SPH_XSUB");
+    if (xe && (atoi(xe) == 1 || atoi(xe) == 2)) xsub = atoi(xe);
+    p->grid.xsub = p->dim == 3 ? xsub : 1;
+    p->grid.inv_cxs = p->grid.inv_cell * (float)p->grid.xsub;
     for (int a = 0; a < 3; ++a) {
         p->grid.origin[a] = 0.0f;
         int32_t G = (int32_t)floorf(p->L[a] / (a == 2 ? cz : cell)) + 1;
@@ -115,9 +125,11 @@ static inline void kernel_wf(const or_sph_params* p, float r2, float* W, float* 
 
 typedef struct { int n; int lo, hi; } row_range;
 
-/* the 9 contiguous neighbour rows of SPEC_SPH.md §0, in visit order, each over the z
- * sub-cell window [cz - zwin, cz + zwin] (a superset of every row's trimmed window) */
-static int neighbour_rows(const or_grid* g, const uint32_t* cs, uint32_t key, uint32_t ranges[9][2]) {
+/* the (2 xsub + 1) x 3 contiguous neighbour rows of SPEC_SPH.md §0 (9 for xsub = 1), in visit order:
+ * sub-column offset outer, y offset inner, each over the z sub-cell window [cz - zwin, cz + zwin]
+ * (a superset of every row's trimmed window) */
+#define OR_MAX_ROWS 15
+static int neighbour_rows(const or_grid* g, const uint32_t* cs, uint32_t key, uint32_t ranges[OR_MAX_ROWS][2]) {
     int32_t GY = g->G[1], GZ = g->G[2];
     int32_t cz = (int32_t)(key % (uint32_t)GZ);
     int32_t cy = (int32_t)((key / (uint32_t)GZ) % (uint32_t)GY);
@@ -126,9 +138,9 @@ static int neighbour_rows(const or_grid* g, const uint32_t* cs, uint32_t key, ui
     if (z0 < 0) z0 = 0;
     if (z1 > GZ - 1) z1 = GZ - 1;
     int nr = 0;
-    for (int ddx = -1; ddx <= 1; ++ddx) {
+    for (int ddx = -g->xsub; ddx <= g->xsub; ++ddx) {
         int32_t x = cx + ddx;
-        if (x < 0 || x >= g->G[0]) continue;
+        if (x < 0 || x >= g->G[0] * g->xsub) continue;
         for (int ddy = -1; ddy <= 1; ++ddy) {
             int32_t y = cy + ddy;
             if (y < 0 || y >= GY) continue;
@@ -153,7 +165,7 @@ void or_sph_density_range(const or_sph_params* p, const float* p2, const uint32_
 #endif
 #pragma omp parallel for schedule(dynamic, 1024)
     for (int i = i0; i < i1; ++i) {
-        uint32_t rg[9][2];
+        uint32_t rg[OR_MAX_ROWS][2];
         int nr = neighbour_rows(g, cs, sk[i], rg);
         float xi = p2[3 * i], yi = p2[3 * i + 1], zi = p2[3 * i + 2];
         float s = 0.0f;
@@ -197,7 +209,7 @@ static void force_range_impl(const or_sph_params* p, const float* p2, const floa
 #endif
 #pragma omp parallel for schedule(dynamic, 1024)
     for (int i = i0; i < i1; ++i) {
-        uint32_t rg[9][2];
+        uint32_t rg[OR_MAX_ROWS][2];
         int nr = neighbour_rows(g, cs, sk[i], rg);
         float xi = p2[3 * i], yi = p2[3 * i + 1], zi = p2[3 * i + 2];
         float ui = v2[3 * i], vi = v2[3 * i + 1], wi = v2[3 * i + 2];
@@ -272,7 +284,7 @@ int or_sph_step(const or_sph_params* p, int n, float* pos, float* vel, int32_t* 
 int or_sph_step_diag(const or_sph_params* p, int n, float* pos, float* vel, int32_t* id, float dt, float t,
                      float* rho_out, float* prho_out, uint32_t* cs_out, float* acc3, float* mag3, int nthreads) {
     const or_grid* g = &p->grid;
-    uint32_t nk = (uint32_t)g->G[0] * (uint32_t)g->G[1] * (uint32_t)g->G[2];
+    uint32_t nk = (uint32_t)g->G[0] * (uint32_t)g->xsub * (uint32_t)g->G[1] * (uint32_t)g->G[2];
     size_t nn = (size_t)(n > 0 ? n : 1);
     uint32_t* keys = (uint32_t*)malloc(sizeof(uint32_t) * nn);
     uint32_t* perm = (uint32_t*)malloc(sizeof(uint32_t) * nn);

@@ -3,6 +3,7 @@
 GRBM_COUNT`: clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel duration (MI355X_MICROARCH.md, DVFS give-back;
 the quotient reads high on dispatches shorter than ~0.3 ms, so long dispatches are the measurement).
 Usage: clock_summary.py <out.json> <label>=<rocprof dir> ..."""
+import re
 import csv
 import glob
 import json
@@ -29,7 +30,7 @@ def one(d):
     crow = list(csv.DictReader(open(cc[0])))
     for r in crow:
         key = r.get("Dispatch_Id") or r.get("Correlation_Id")
-        k = r["Kernel_Name"].split("(")[0].replace("sph::", "")
+        k = re.sub(r"<[^>]*>$", "", r["Kernel_Name"].split("(")[0].replace("void ", "").replace("sph::", ""))
         per[k][r["Counter_Name"]].append((key, float(r["Counter_Value"])))
     out = {"columns_counter": list(crow[0].keys()) if crow else [], "columns_trace": list(rows[0].keys()) if rows else []}
     for k, cs in per.items():

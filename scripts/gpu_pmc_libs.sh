@@ -13,7 +13,7 @@ for lib in "$@"; do
   echo "lib $i = $lib"
 done
 python3 - "$@" <<'PY'
-import csv, glob, os, sys
+import csv, glob, os, re, sys
 from collections import defaultdict
 for i, lib in enumerate(sys.argv[1:], 1):
     acc = defaultdict(lambda: defaultdict(list))
@@ -22,7 +22,7 @@ for i, lib in enumerate(sys.argv[1:], 1):
         if not os.path.exists(f):
             continue
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].replace("sph::", "")
+            k = re.sub(r"<[^>]*>$", "", r["Kernel_Name"].split("(")[0].replace("void ", "").replace("sph::", ""))
             if k in ("k_force_tiled", "k_density_tiled"):
                 acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, cs in acc.items():

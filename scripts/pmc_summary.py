@@ -3,6 +3,7 @@
 into per-kernel mean counter values per launch, and HBM traffic per launch as
 FETCH_SIZE*2 + WRITE_SIZE (KB -> bytes; MI355X_MICROARCH.md §HBM: FETCH_SIZE reads half the
 bytes of wide coalesced streams)."""
+import re
 import csv
 import glob
 import json
@@ -23,7 +24,7 @@ def main(root, out, config):
             continue
         var = os.path.basename(d).split("_")[0]
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].replace("sph::", "")
+            k = re.sub(r"<[^>]*>$", "", r["Kernel_Name"].split("(")[0].replace("void ", "").replace("sph::", ""))
             res[(var, k)][r["Counter_Name"]].append(float(r["Counter_Value"]))
     summary = {}
     for (var, k), cs in sorted(res.items()):

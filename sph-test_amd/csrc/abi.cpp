@@ -679,7 +679,7 @@ int sph_get_stats(sph_ctx* ctx, sph_stats* out) {
     out->sim_time = ctx->sim_time;
     out->active = ctx->n;
     out->capacity = ctx->capacity;
-    out->grid[0] = ctx->grid.gx; out->grid[1] = ctx->grid.gy; out->grid[2] = ctx->grid.gz;
+    out->grid[0] = ctx->grid.gx * ctx->grid.xsub; out->grid[1] = ctx->grid.gy; out->grid[2] = ctx->grid.gz;
     out->key_bits = ctx->key_bits;
     out->device_bytes = ctx->device_bytes;
     const std::vector<sph_ctx*> kids = multi_kids(ctx);
@@ -693,7 +693,7 @@ int sph_get_stats(sph_ctx* ctx, sph_stats* out) {
             out->capacity += k->capacity;
             out->device_bytes += k->device_bytes;
         }
-        out->grid[0] = kids[0]->gglobal.gx; out->grid[1] = kids[0]->gglobal.gy; out->grid[2] = kids[0]->gglobal.gz;
+        out->grid[0] = kids[0]->gglobal.gx * kids[0]->gglobal.xsub; out->grid[1] = kids[0]->gglobal.gy; out->grid[2] = kids[0]->gglobal.gz;
         out->key_bits = kids[0]->key_bits;
     }
     return SPH_OK;

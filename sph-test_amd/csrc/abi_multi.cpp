@@ -269,7 +269,7 @@ int put_dz(RankState& R) {
 
 int col_le(const sph_ctx* c) { return c->has_left ? c->sl.cx_lo - c->grid.cx0 : -1; }
 int col_ge(const sph_ctx* c) { return c->has_right ? c->sl.cx_hi - 1 - c->grid.cx0 : 0x7fffffff; }
-uint32_t gyz(const sph_ctx* c) { return (uint32_t)c->grid.gy * (uint32_t)c->grid.gz; }
+uint32_t gyz(const sph_ctx* c) { return col_keys(c->grid); }
 
 const uint32_t* lag_slot(RankState& R, int64_t step, sph_ctx* ctx, int* rc) {
     const int k = (int)(step % LAG_SLOTS);

@@ -53,7 +53,7 @@ int sph::slab_local_grid(sph_ctx* ctx) {
     g.cx0 = ctx->sl.cx_lo - (ctx->has_left ? 1 : 0);
     g.gx = ctx->sl.cx_hi + (ctx->has_right ? 1 : 0) - g.cx0;
     g.gx_all = G.gx;
-    g.ncells = (uint32_t)g.gx * (uint32_t)g.gy * (uint32_t)g.gz;
+    g.ncells = (uint32_t)g.gx * col_keys(g);
     ctx->grid = g;
     ctx->key_bits = bit_width(g.ncells);
     invalidate_sort(ctx);
@@ -61,7 +61,7 @@ int sph::slab_local_grid(sph_ctx* ctx) {
 }
 
 int32_t sph::col_start(const sph_ctx* c, int32_t local_col) {
-    return local_col * c->grid.gy * c->grid.gz;
+    return local_col * (int32_t)col_keys(c->grid);
 }
 
 extern "C" {
@@ -108,7 +108,7 @@ int sph_slab_column_counts(sph_ctx* ctx, int64_t* counts, int32_t ncols) {
     for (int32_t c = 0; c < ncols; ++c) counts[c] = 0;
     const int32_t m = ctx->sl.cx_hi - ctx->sl.cx_lo + 1;
     std::vector<uint32_t> st(m);
-    const uint32_t gyz = (uint32_t)ctx->grid.gy * (uint32_t)ctx->grid.gz;
+    const uint32_t gyz = col_keys(ctx->grid);
     launch_column_starts(ctx->cs, gyz, ctx->sl.cx_lo - ctx->grid.cx0, m, (uint32_t*)ctx->staging, ctx->stream);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(st.data(), ctx->staging, (size_t)m * 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -168,7 +168,7 @@ static int slab_count(sph_ctx* ctx, int64_t* dev_counts) {
         launch_keys(ctx->pos + ctx->o0, no, nullptr, 0, ctx->grid, ctx->keys + ctx->o0, ctx->stream);
         ctx->keys_valid = true;
     }
-    const uint32_t gyz = (uint32_t)ctx->grid.gy * (uint32_t)ctx->grid.gz;
+    const uint32_t gyz = col_keys(ctx->grid);
     const int32_t col_le = ctx->has_left ? ctx->sl.cx_lo - ctx->grid.cx0 : -1;
     const int32_t col_ge = ctx->has_right ? ctx->sl.cx_hi - 1 - ctx->grid.cx0 : 0x7fffffff;
     KTimer t(ctx, "slab_count", 4.0 * no);
@@ -216,7 +216,7 @@ int sph_slab_pack_send(sph_ctx* ctx, int32_t side, void* dev_records, int32_t ca
     if (!dev_records || capacity < need)
         return fail(ctx, SPH_ERR_CAPACITY, "send buffer %d < %d records", capacity, need);
     HIPCHK(hipSetDevice(ctx->device));
-    const uint32_t gyz = (uint32_t)ctx->grid.gy * (uint32_t)ctx->grid.gz;
+    const uint32_t gyz = col_keys(ctx->grid);
     const int32_t col_le = ctx->has_left ? ctx->sl.cx_lo - ctx->grid.cx0 : -1;
     const int32_t col_ge = ctx->has_right ? ctx->sl.cx_hi - 1 - ctx->grid.cx0 : 0x7fffffff;
     KTimer t(ctx, "slab_pack", 36.0 * ctx->send_counts[side]);
@@ -254,7 +254,7 @@ int sph::slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const voi
     const int64_t n = (int64_t)nl + no + nr;
     if (n > ctx->capacity) return fail(ctx, SPH_ERR_CAPACITY, "slab needs %lld slots > capacity %d", (long long)n, ctx->capacity);
     hipStream_t s = ctx->stream;
-    const uint32_t gyz = (uint32_t)ctx->grid.gy * (uint32_t)ctx->grid.gz;
+    const uint32_t gyz = col_keys(ctx->grid);
     const uint32_t key_base = (uint32_t)ctx->grid.cx0 * gyz;
     const bool many = ctx->resort_mode == 1 && *(volatile uint32_t*)ctx->mv_host > resort_limit((int32_t)n);
     // ranges from the cell table at column starts: picked on the device (density reads them there)

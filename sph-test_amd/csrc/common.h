@@ -13,18 +13,31 @@ namespace sph {
 // decomposition, SPEC_SPH.md §3). The column is computed globally then shifted, so all
 // ranks agree bit for bit on which column a particle is in.
 // Model S splits z into zsub sub-cells (cells 2h × 2h × 2h/zsub, SPEC_SPH.md §0): each of the
-// 9 neighbour rows is then walked over a z window trimmed to the row's xy distance.
+// neighbour rows is then walked over a z window trimmed to the row's xy distance. It may also split
+// each column into xsub x sub-columns (cells cell/xsub wide in x): keys then count sub-columns,
+// key = ((cxs*gy + cy)*gz + cz with cxs = xsub*cx + the sub-column, so a column is still one
+// contiguous run of xsub*gy*gz keys (col_keys) and the slab decomposition keeps whole columns.
 struct GridDesc {
     float ox, oy, oz;
     float inv_cell;      // 1 / cell (x, y)
     float inv_cz;        // 1 / (cell / zsub) (z)
-    int32_t gx, gy, gz;  // gz counts z sub-cells
-    uint32_t ncells;     // gx*gy*gz (keys == ncells mark inactive particles)
+    int32_t gx, gy, gz;  // gx counts columns (cell wide), gz z sub-cells
+    uint32_t ncells;     // gx*xsub*gy*gz (keys == ncells mark inactive particles)
     int32_t cx0;         // first global column held (0 without decomposition)
     int32_t gx_all;      // global column count (== gx without decomposition)
     int32_t zsub;        // z sub-cells per cell (Model S 3D 6, Model R and 2D 1)
     int32_t zwin;        // max |Δ z sub-cell| of a neighbour (zsub + 1; Model R 1)
+    int32_t xsub;        // x sub-columns per column (Model S 3D: SPH_XSUB; Model R and 2D 1)
+    float inv_cxs;       // xsub / cell (x sub-column coordinate; == inv_cell when xsub = 1)
 };
+#if defined(__HIPCC__)
+#define SPH_HD __host__ __device__
+#else
+#define SPH_HD
+#endif
+// keys per column (the slab decomposition's column of keys)
+template <int XS = 0>
+SPH_HD inline uint32_t col_keys(const GridDesc& g) { return (uint32_t)(XS ? XS : g.xsub) * (uint32_t)g.gy * (uint32_t)g.gz; }
 
 // Model S constants (SPEC_SPH.md §2), derived on the host from sph_params.
 struct SphConst {
@@ -59,25 +72,48 @@ __device__ __forceinline__ int32_t cell_cx(const GridDesc& g, float x) {
     return c < 0 ? 0 : (c >= g.gx ? g.gx - 1 : c);
 }
 
+// local x sub-column of a position (xsub per column). inv_cxs = xsub · inv_cell exactly, so the global
+// sub-column is xsub · (global column) + [0, xsub) for every x, clamping included: keys / col_keys
+// give the column of cell_cx. XS: xsub as a compile-time constant (0: read it from the grid).
+template <int XS = 0>
+__device__ __forceinline__ int32_t cell_cxs(const GridDesc& g, float x) {
+    const int32_t xs = XS ? XS : g.xsub;
+    const float inv = XS == 1 ? g.inv_cell : g.inv_cxs;
+    const int32_t c = cell_coord(x, g.ox, inv, g.gx_all * xs) - g.cx0 * xs;
+    const int32_t m = g.gx * xs;
+    return c < 0 ? 0 : (c >= m ? m - 1 : c);
+}
+
+template <int XS = 0>
 __device__ __forceinline__ uint32_t cell_key(const GridDesc& g, float x, float y, float z) {
-    int32_t cx = cell_cx(g, x);
+    int32_t cx = cell_cxs<XS>(g, x);
     int32_t cy = cell_coord(y, g.oy, g.inv_cell, g.gy);
     int32_t cz = cell_coord(z, g.oz, g.inv_cz, g.gz);
     return ((uint32_t)cx * (uint32_t)g.gy + (uint32_t)cy) * (uint32_t)g.gz + (uint32_t)cz;
 }
 
 // slab: a particle outside the held columns (already sent away) gets key ncells: it sorts last
+template <int XS = 0>
 __device__ __forceinline__ uint32_t window_key(const GridDesc& g, float x, float y, float z) {
     const int32_t c = cell_coord(x, g.ox, g.inv_cell, g.gx_all) - g.cx0;
-    return (c < 0 || c >= g.gx) ? g.ncells : cell_key(g, x, y, z);
+    return (c < 0 || c >= g.gx) ? g.ncells : cell_key<XS>(g, x, y, z);
 }
 
-// One of the 9 neighbour rows of a Model S particle (SPEC_SPH.md §0): the z sub-cell window
-// [zlo, zhi] of row (cx+dx, cy+dy) that can hold a particle within 2h, or false when the
-// row's column is ≥ 2h away in xy. fx, fy: the particle's position inside its cell, in [0,1].
+// One of the (2·xsub+1)·3 neighbour rows of a Model S particle (SPEC_SPH.md §0): the z sub-cell window
+// [zlo, zhi] of row (cxs+dx, cy+dy) (dx in sub-columns, |dx| <= xsub) that can hold a particle within
+// 2h, or false when the row's column is ≥ 2h away in xy. fx: the particle's position inside its
+// sub-column, fy inside its cell, in [0,1]. The x gap is counted in sub-columns and scaled by 1/xsub
+// (exact; with xsub = 1 the arithmetic is the 3 x 3 rows' of SPEC_SPH.md §0 to the bit).
+// XS: the grid's xsub as a compile-time constant (the neighbour passes are instantiated per xsub).
+template <int XS>
 __device__ __forceinline__ bool row_window(const GridDesc& g, float fx, float fy, float gzf, int dx, int dy,
                                            int32_t& zlo, int32_t& zhi) {
-    const float gxg = dx < 0 ? fx : (dx > 0 ? 1.0f - fx : 0.0f);
+    float gxg;
+    if constexpr (XS == 1) {
+        gxg = dx < 0 ? fx : (dx > 0 ? 1.0f - fx : 0.0f);
+    } else {
+        gxg = (dx < 0 ? fx + (float)(-dx - 1) : (dx > 0 ? (1.0f - fx) + (float)(dx - 1) : 0.0f)) * (1.0f / XS);
+    }
     const float gyg = dy < 0 ? fy : (dy > 0 ? 1.0f - fy : 0.0f);
     const float d2 = gxg * gxg + gyg * gyg;
     if (!(d2 < 1.0f)) return false;
@@ -89,10 +125,13 @@ __device__ __forceinline__ bool row_window(const GridDesc& g, float fx, float fy
     return true;
 }
 
-// The particle's in-cell fractions (x, y) and z sub-cell coordinate for row_window.
-__device__ __forceinline__ void cell_fracs(const GridDesc& g, float x, float y, float z, int32_t cx, int32_t cy,
+// The particle's in-cell fractions (x in its sub-column cxs, y) and z sub-cell coordinate for row_window.
+template <int XS = 0>
+__device__ __forceinline__ void cell_fracs(const GridDesc& g, float x, float y, float z, int32_t cxs, int32_t cy,
                                            float& fx, float& fy, float& gzf) {
-    fx = fminf(fmaxf((x - g.ox) * g.inv_cell - (float)(cx + g.cx0), 0.0f), 1.0f);
+    const int32_t xs = XS ? XS : g.xsub;
+    const float inv = XS == 1 ? g.inv_cell : g.inv_cxs;
+    fx = fminf(fmaxf((x - g.ox) * inv - (float)(cxs + g.cx0 * xs), 0.0f), 1.0f);
     fy = fminf(fmaxf((y - g.oy) * g.inv_cell - (float)cy, 0.0f), 1.0f);
     gzf = (z - g.oz) * g.inv_cz;
 }

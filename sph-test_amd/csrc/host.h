@@ -30,6 +30,13 @@ struct Multi;   // the multi-GPU step's state (abi_multi.cpp)
 // −8 us each) while the sub-cell crossings it adds cost the re-sort 2 us; 8 costs it 14 us
 // (profiles/r01_zsub_ab.log).
 static const int32_t SPH_ZSUB = 6;
+// x sub-columns per 2h column for Model S 3D (SPEC_SPH.md §0; 1 or 2). With 2 the neighbour rows are h wide
+// in x: 19% fewer candidates per target and pass 2's plane walks better balanced, but measured slower (five
+// staging phases, 15 row windows, twice the cells: 0.338 -> 0.404 ms/step from rest, 0.382 -> 0.403
+// mid-collapse; DESIGN.md §9, profiles/r03_xsub_ab.log). The environment variable SPH_XSUB (1 or 2) selects
+// it per context; the oracle reads the same variable with the same default (tests/test_abi_cpu.py).
+#define SPH_XSUB_DEFAULT 1
+int32_t model_s_xsub();
 
 struct KStat {
     std::string name;

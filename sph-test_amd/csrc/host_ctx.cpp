@@ -1,4 +1,5 @@
 // host_ctx.cpp — context memory, grid derivation and per-kernel profiling (see host.h).
+#include <cstdlib>
 #include "host.h"
 
 namespace sph {
@@ -79,6 +80,14 @@ int ensure_cells(sph_ctx* ctx) {
     return SPH_OK;
 }
 
+int32_t model_s_xsub() {
+    if (const char* v = std::getenv("SPH_XSUB")) {
+        const int x = std::atoi(v);
+        if (x == 1 || x == 2) return x;
+    }
+    return SPH_XSUB_DEFAULT;
+}
+
 // Grid + constants from params (SPEC_SPH.md §0/§2; same float arithmetic as the oracle).
 int derive(sph_ctx* ctx) {
     const sph_params& p = ctx->prm;
@@ -91,6 +100,8 @@ int derive(sph_ctx* ctx) {
         g.gx = g.gy = g.gz = 32;
         g.zsub = 1;
         g.zwin = 1;
+        g.xsub = 1;
+        g.inv_cxs = g.inv_cell;
     } else {
         if (!(p.h > 0.f) || !(p.dx > 0.f) || !(p.rho0 > 0.f))
             return fail(ctx, SPH_ERR_INVALID, "Model S needs dx, h, rho0 > 0");
@@ -102,6 +113,8 @@ int derive(sph_ctx* ctx) {
         g.inv_cz = 1.0f / cz;
         g.zsub = zsub;
         g.zwin = zsub + 1;
+        g.xsub = ctx->cfg.dim == 3 ? model_s_xsub() : 1;
+        g.inv_cxs = g.inv_cell * (float)g.xsub;   // exact (xsub is 1 or 2)
         int32_t G[3];
         for (int a = 0; a < 3; ++a) {
             G[a] = (int32_t)floorf(p.box[a] / (a == 2 ? cz : cell)) + 1;
@@ -109,7 +122,7 @@ int derive(sph_ctx* ctx) {
         }
         if (ctx->cfg.dim == 2) G[2] = 1;
         g.gx = G[0]; g.gy = G[1]; g.gz = G[2];
-        const double nc = (double)G[0] * G[1] * G[2];
+        const double nc = (double)G[0] * g.xsub * G[1] * G[2];
         if (nc > 2.0e9) return fail(ctx, SPH_ERR_INVALID, "grid too large (%g cells)", nc);
         const float PI = 3.14159265358979f, d = p.dx, h = p.h;
         SphConst& s = ctx->sc;
@@ -132,7 +145,7 @@ int derive(sph_ctx* ctx) {
     }
     g.cx0 = 0;
     g.gx_all = g.gx;
-    g.ncells = (uint32_t)g.gx * (uint32_t)g.gy * (uint32_t)g.gz;
+    g.ncells = (uint32_t)g.gx * col_keys(g);
     ctx->grid = g;
     ctx->key_bits = bit_width(g.ncells);   // the sentinel key == ncells must sort last
     invalidate_sort(ctx);

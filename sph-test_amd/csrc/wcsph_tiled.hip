@@ -68,26 +68,30 @@ struct Staged {
 
 struct BlockRows {
     int64_t kf, kl;           // key range of the block's targets
-    int32_t cx, cy;           // this lane's cell (x, y)
-    float fx, fy, gzf;        // in-cell fractions and z sub-cell coordinate (row_window)
+    int32_t cx, cy;           // this lane's sub-column (x, GridDesc::xsub per column) and cell (y)
+    float fx, fy, gzf;        // in-sub-column / in-cell fractions and z sub-cell coordinate (row_window)
 };
 
+template <int XS>
 __device__ __forceinline__ BlockRows block_rows(const GridDesc& g, const float4* __restrict__ pos, int32_t i0,
                                                 int32_t ilast, float4 pi) {
     BlockRows b;
     const float4 pf = pos[i0], pl = pos[ilast];
-    b.kf = cell_key(g, pf.x, pf.y, pf.z);
-    b.kl = cell_key(g, pl.x, pl.y, pl.z);
-    b.cx = cell_cx(g, pi.x);
+    b.kf = cell_key<XS>(g, pf.x, pf.y, pf.z);
+    b.kl = cell_key<XS>(g, pl.x, pl.y, pl.z);
+    b.cx = cell_cxs<XS>(g, pi.x);
     b.cy = cell_coord(pi.y, g.oy, g.inv_cell, g.gy);
-    cell_fracs(g, pi.x, pi.y, pi.z, b.cx, b.cy, b.fx, b.fy, b.gzf);
+    cell_fracs<XS>(g, pi.x, pi.y, pi.z, b.cx, b.cy, b.fx, b.fy, b.gzf);
     return b;
 }
 
+// Row k = 3·plane + r: sub-column offset plane − XS, y offset r − 1 (planes 0..2·XS; XS = the grid's
+// xsub, a template parameter of both passes so that the default grid compiles to the plain 3 x 3 rows).
 // Block interval of row offset k ([c0,c1) sorted slots; uniform over the block).
+template <int XS>
 __device__ __forceinline__ void block_interval(const GridDesc& g, const uint32_t* __restrict__ cs, const BlockRows& b,
                                                int k, int32_t& c0, int32_t& c1) {
-    const int32_t dxk = k / 3 - 1, dyk = k % 3 - 1;
+    const int32_t dxk = k / 3 - XS, dyk = k % 3 - 1;
     const int64_t off = ((int64_t)dxk * g.gy + dyk) * g.gz;
     int64_t ka = b.kf + off - g.zwin, kb = b.kl + off + g.zwin;
     const int64_t last = (int64_t)g.ncells - 1;
@@ -102,14 +106,15 @@ __device__ __forceinline__ void block_interval(const GridDesc& g, const uint32_t
 }
 
 // This lane's trimmed window of row offset k ([r0,r1) sorted slots, empty if out of range).
+template <int XS>
 __device__ __forceinline__ void lane_window(const GridDesc& g, const uint32_t* __restrict__ cs, const BlockRows& b,
                                             bool valid, int k, int32_t& r0, int32_t& r1) {
-    const int32_t dxk = k / 3 - 1, dyk = k % 3 - 1;
+    const int32_t dxk = k / 3 - XS, dyk = k % 3 - 1;
     const int32_t xx = b.cx + dxk, yy = b.cy + dyk;
     r0 = r1 = 0;
     int32_t zlo, zhi;
-    if (valid && xx >= 0 && xx < g.gx && yy >= 0 && yy < g.gy &&
-        row_window(g, b.fx, b.fy, b.gzf, dxk, dyk, zlo, zhi)) {
+    if (valid && xx >= 0 && xx < g.gx * XS && yy >= 0 && yy < g.gy &&
+        row_window<XS>(g, b.fx, b.fy, b.gzf, dxk, dyk, zlo, zhi)) {
         const uint32_t rowk = ((uint32_t)xx * (uint32_t)g.gy + (uint32_t)yy) * (uint32_t)g.gz;
         r0 = (int32_t)cs[rowk + (uint32_t)zlo];
         r1 = (int32_t)cs[rowk + (uint32_t)zhi + 1u];
@@ -257,6 +262,7 @@ __device__ __forceinline__ void plane_groups(const int32_t (&len)[3], int32_t ca
 // with alike windows idle less in the wave-wide scan and flush loops. Stable within a quadrant;
 // every target keeps its own visit order, so results are bit-identical. Returns the lane's slot
 // (>= n for the padding lanes of the last block, which sort last).
+template <int XS>
 __device__ __forceinline__ int32_t quadrant_target(const GridDesc& g, const float4* __restrict__ pos, int32_t i0,
                                                    int32_t n, int32_t* perm, uint32_t (*cnt)[5]) {
     static_assert(TT_BLK % 64 == 0, "whole waves");
@@ -264,9 +270,9 @@ __device__ __forceinline__ int32_t quadrant_target(const GridDesc& g, const floa
     int bin = 4;
     if (i < n) {
         const float4 p = pos[i];
-        const int32_t cx = cell_cx(g, p.x), cy = cell_coord(p.y, g.oy, g.inv_cell, g.gy);
+        const int32_t cx = cell_cxs<XS>(g, p.x), cy = cell_coord(p.y, g.oy, g.inv_cell, g.gy);
         float fx, fy, gzf;
-        cell_fracs(g, p.x, p.y, p.z, cx, cy, fx, fy, gzf);
+        cell_fracs<XS>(g, p.x, p.y, p.z, cx, cy, fx, fy, gzf);
         bin = (fx >= 0.5f ? 1 : 0) + (fy >= 0.5f ? 2 : 0);
     }
     const int w = threadIdx.x >> 6;
@@ -289,6 +295,7 @@ __device__ __forceinline__ int32_t quadrant_target(const GridDesc& g, const floa
     return perm[threadIdx.x];
 }
 
+template <int XS>
 __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAVES))) void k_density_tiled(
     const float4* __restrict__ pos, const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c,
     float2* __restrict__ rp, DevRange dr, HitMask hm, uint32_t* __restrict__ paths) {
@@ -304,11 +311,11 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
     SPH_BT_START;
     // quadrant order, measured against plain sorted order (138 -> 154 us) and halves by fx or by fy
     // (+1 to +2 us) at C3 (profiles/r02_pass1_lane_order_ab.log)
-    const int32_t i = quadrant_target(g, pos, i0, n, perm, qcnt);
+    const int32_t i = quadrant_target<XS>(g, pos, i0, n, perm, qcnt);
     const bool valid = i < n;
     const int32_t ilast = min(i0 + TT_BLK, n) - 1;
     const float4 pi = pos[valid ? i : ilast];
-    const BlockRows b = block_rows(g, pos, i0, ilast, pi);
+    const BlockRows b = block_rows<XS>(g, pos, i0, ilast, pi);
     float s = 0.0f;
     auto load_p = [&](int32_t src) { return pos[src]; };
     auto write_p = [&](int32_t t, float4 e) { sp[t] = e; };
@@ -371,14 +378,15 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
         mn = (mn + 4 * n4) & 31;
         for (int32_t t = 4 * n4; t < ln; ++t) one(dist2(pi, sp[lo + t]));
     };
+    constexpr int nplanes = 2 * XS + 1;
 #pragma unroll 1
-    for (int p = 0; p < 3; ++p) {
+    for (int p = 0; p < nplanes; ++p) {
         int32_t c0[3], c1[3], len[3], r0[3], r1[3];
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
-            block_interval(g, cs, b, 3 * p + r, c0[r], c1[r]);
+            block_interval<XS>(g, cs, b, 3 * p + r, c0[r], c1[r]);
             len[r] = c1[r] - c0[r];
-            lane_window(g, cs, b, valid, 3 * p + r, r0[r], r1[r]);
+            lane_window<XS>(g, cs, b, valid, 3 * p + r, r0[r], r1[r]);
         }
         const int32_t total = len[0] + len[1] + len[2];
         // rows of mask gm staged back to back (they fit the budget together), each window scanned
@@ -493,6 +501,7 @@ __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi,
     a.sx -= cx * du; a.sy -= cx * dv; a.sz -= cx * dw;
 }
 
+template <int XS>
 __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
     const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, PairK pk, float dt,
@@ -518,7 +527,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     const int32_t ii = valid ? i : ilast;
     const float4 pi = pos[ii], vi = vel[ii];
     const float2 ri = rp[ii];
-    const BlockRows b = block_rows(g, pos, i0, ilast, pi);
+    const BlockRows b = block_rows<XS>(g, pos, i0, ilast, pi);
     ForceAcc acc{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     // hit-mask reader (pass 1's bits of this target, in visit order): rb holds rn bits, LSB next;
     // the remaining words wait in a queue of registers (static indices only). Measured against a
@@ -601,14 +610,15 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         sp[t] = make_float4(e.p.x, e.p.y, e.p.z, e.r.x);
         sv[t] = make_float4(e.v.x, e.v.y, e.v.z, e.r.y);
     };
+    constexpr int nplanes = 2 * XS + 1;
 #pragma unroll 1
-    for (int p = 0; p < 3; ++p) {
+    for (int p = 0; p < nplanes; ++p) {
         int32_t c0[3], c1[3], len[3], r0[3], r1[3];
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
-            block_interval(g, cs, b, 3 * p + r, c0[r], c1[r]);
+            block_interval<XS>(g, cs, b, 3 * p + r, c0[r], c1[r]);
             len[r] = c1[r] - c0[r];
-            lane_window(g, cs, b, valid, 3 * p + r, r0[r], r1[r]);
+            lane_window<XS>(g, cs, b, valid, 3 * p + r, r0[r], r1[r]);
         }
         const int32_t total = len[0] + len[1] + len[2];
         const int32_t plen = (r1[0] - r0[0]) + (r1[1] - r0[1]) + (r1[2] - r0[2]);
@@ -698,13 +708,13 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     }
     pos_o[i] = make_float4(np[0], np[1], np[2], 0.f);
     vel_o[i] = make_float4(nv[0], nv[1], nv[2], 0.f);
-    const uint32_t key = cell_key(g, np[0], np[1], np[2]);
+    const uint32_t key = cell_key<XS>(g, np[0], np[1], np[2]);
     keys_o[i] = key;
     // the mover list takes the window key: in a slab, a particle that left the held columns sorts
     // last (window_key = cell_key in a single domain); it changed iff the clamped key changed
-    const uint32_t wk = window_key(g, np[0], np[1], np[2]);
+    const uint32_t wk = window_key<XS>(g, np[0], np[1], np[2]);
     if (mv.jump && mv.sk) {   // slab step: the next sends assume moves of at most one column (slab.hip send_ranges)
-        const uint32_t gyz = (uint32_t)g.gy * (uint32_t)g.gz;
+        const uint32_t gyz = col_keys<XS>(g);
         const int32_t d = (int32_t)(wk / gyz) - (int32_t)(mv.sk[i] / gyz);
         if (wk >= g.ncells) {
             if (mv.err) atomicOr(mv.err, SZ_JUMP);   // left the held window: it reaches no neighbour
@@ -718,15 +728,22 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
 // dr set: [ib, ie) only sizes the grid (an upper bound); the kernels read their bounds from dr
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
                           float2* rp, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr) {
-    if (ie > ib)
-        SPH_LAUNCH(k_density_tiled, (ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s, pos, cs, ib, ie, g, c, rp, dr, hm, paths);
+    if (ie <= ib) return;
+    if (g.xsub == 2)
+        SPH_LAUNCH(k_density_tiled<2>, (ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s, pos, cs, ib, ie, g, c, rp, dr, hm, paths);
+    else
+        SPH_LAUNCH(k_density_tiled<1>, (ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s, pos, cs, ib, ie, g, c, rp, dr, hm, paths);
 }
 
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,
                         int32_t ie, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o,
                         uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr) {
-    if (ie > ib)
-        SPH_LAUNCH(k_force_tiled, (ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c,
+    if (ie <= ib) return;
+    if (g.xsub == 2)
+        SPH_LAUNCH(k_force_tiled<2>, (ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c,
+                   pair_constants(c), dt, fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr);
+    else
+        SPH_LAUNCH(k_force_tiled<1>, (ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c,
                    pair_constants(c), dt, fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr);
 }
 

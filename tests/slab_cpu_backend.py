@@ -18,7 +18,7 @@ class CpuSlabBackend:
         self.cx_lo, self.cx_hi = cut
         G = op.grid.G
         self.G = (int(G[0]), int(G[1]), int(G[2]))
-        self.gyz = self.G[1] * self.G[2]
+        self.gyz = int(op.grid.xsub) * self.G[1] * self.G[2]   # keys per column (x sub-columns)
         self.nk = self.G[0] * self.gyz
         self.has_left = self.cx_lo > 0
         self.has_right = self.cx_hi < self.G[0]

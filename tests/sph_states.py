@@ -56,14 +56,16 @@ def splash_state(nx_cols, ny, nz, cell, dense_per_col, sparse_per_col, box, seed
 
 
 def grid_dims(op):
-    return int(op.grid.G[0]), int(op.grid.G[1]), int(op.grid.G[2]), int(op.grid.zwin)
+    """(sub-columns, gy, gz, zwin, xsub): keys count x sub-columns (SPEC_SPH.md §0)."""
+    xs = int(op.grid.xsub)
+    return int(op.grid.G[0]) * xs, int(op.grid.G[1]), int(op.grid.G[2]), int(op.grid.zwin), xs
 
 
 def block_paths(O, op, x):
     """How the tiled passes will process state x: [density planes chunked, density rows global,
     force planes chunked, force rows global], summed over workgroups (the kernels' counters count
     the same events, sph_read_path_counts)."""
-    gx, gy, gz, zwin = grid_dims(op)
+    gx, gy, gz, zwin, xs = grid_dims(op)
     nc = gx * gy * gz
     keys = O.grid_keys(op, x).astype(np.int64)
     sk = np.sort(keys, kind="stable")
@@ -72,10 +74,10 @@ def block_paths(O, op, x):
     out = np.zeros(4, np.int64)
     for i0 in range(0, n, TT_BLK):
         kf, kl = sk[i0], sk[min(i0 + TT_BLK, n) - 1]
-        for p in range(3):
+        for p in range(2 * xs + 1):
             lens = []
             for r in range(3):
-                dxk, dyk = p - 1, r - 1
+                dxk, dyk = p - xs, r - 1
                 off = (dxk * gy + dyk) * gz
                 ka, kb = kf + off - zwin, kl + off + zwin
                 if kb < 0 or ka > nc - 1:

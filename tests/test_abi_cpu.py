@@ -101,3 +101,14 @@ def test_null_arguments_rejected(pkg):
     assert L.sph_step(None, 0.01, 1) == -1
     assert L.sph_create(None, 0, None) == -1
     assert L.sph_last_error(None) == b"null context"
+
+
+def test_xsub_defaults_agree():
+    """The library and the oracle read SPH_XSUB with the same default (x sub-columns, SPEC_SPH.md §0):
+    otherwise the GPU-vs-oracle parity tests would compare two different grids."""
+    import re
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    lib = re.search(r"#define SPH_XSUB_DEFAULT (\d+)", (root / "sph-test_amd/csrc/host.h").read_text())
+    orc = re.search(r"#define OR_XSUB_DEFAULT (\d+)", (root / "oracle/sph_oracle.c").read_text())
+    assert lib and orc and lib.group(1) == orc.group(1)

@@ -162,14 +162,16 @@ def test_force_without_density_scans_by_distance(pkg):
             A.check("sph_slab_finish_step", L.sph_slab_finish_step(h, dt), h)
             ctx.synchronize()
 
+        xsub = ctx.stats().grid[0] // slab.global_columns(p)   # x sub-columns: 2 * xsub + 1 planes per wave
+        npl = 2 * xsub + 1
         ctx.hit_mask_counts(reset=True)     # arm the counters
         for _ in range(3):
             step(True)
         dist_planes, waves = (int(c) for c in ctx.hit_mask_counts(reset=True))
-        assert waves > 0 and dist_planes < 3 * waves      # the mask was used
+        assert waves > 0 and dist_planes < npl * waves      # the mask was used
         step(False)
         dist_planes, waves = (int(c) for c in ctx.hit_mask_counts(reset=True))
-        assert waves > 0 and dist_planes == 3 * waves     # stale mask: never read
+        assert waves > 0 and dist_planes == npl * waves     # stale mask: never read
     finally:
         ctx.close()
 

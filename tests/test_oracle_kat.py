@@ -217,7 +217,8 @@ def test_grid_keys_clamp(oracle):
     pos = np.array([[-1, -1, -1], [0.0, 0.0, 0.0], [0.0241, 0.0, 0.0], [5, 5, 5], [np.nan, 0, 0],
                     [0.0, 0.0, 0.0061]], np.float32)
     k = O.grid_keys(p, pos)
-    assert k.tolist() == [0, 0, 1 * 11 * 60, 10 * 11 * 60 + 10 * 60 + 59, 0, 1]
+    xs = int(p.grid.xsub)                        # x sub-columns per column (SPH_XSUB): keys count them
+    assert k.tolist() == [0, 0, xs * 11 * 60, (11 * xs - 1) * 11 * 60 + 10 * 60 + 59, 0, 1]
 
 
 def test_lattice_deterministic_and_bounded(oracle):
