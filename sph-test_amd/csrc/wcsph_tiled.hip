@@ -573,8 +573,11 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
             // SPH_WALK_UNROLL hits per loop trip: fewer loop and exec-mask instructions per hit, and the next
             // hit's slot and LDS reads can issue before the current pair body ends. Force pass 189 -> 181 us
             // from rest, 214 -> 203 us mid-collapse at 4 (2: 184, 3: 182 us; the word shift as selects instead
-            // of a branch: no change; profiles/r02_walk_unroll_ab.log).
-            while (__any(nh > 0)) {
+            // of a branch: no change; profiles/r02_walk_unroll_ab.log). The trip test sits at the bottom
+            // (do-while): with it at the top the compiler copied the six accumulators twice per trip (12 moves
+            // for 4 hits); force pass 171.3 -> 167.6 us from rest, 193.2 -> 189.1 mid-collapse
+            // (profiles/r03_walk_dowhile_ab.log).
+            if (__any(nh > 0)) do {
 #pragma unroll
                 for (int u = 0; u < SPH_WALK_UNROLL; ++u) {
                     if (w0 != 0u) {
@@ -592,7 +595,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
                         base += 32;
                     }
                 }
-            }
+            } while (__any(nh > 0));
         }
     };
     // Planes the mask does not cover (a target past its 256 bits): LDS slots [lo, lo+ln) by distance,
