@@ -376,7 +376,34 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
             keep_b128(a, bb, cc, d);
         }
         mn = (mn + 4 * n4) & 31;
-        for (int32_t t = 4 * n4; t < ln; ++t) one(dist2(pi, sp[lo + t]));
+        // the 0–3 remaining candidates as one group of three (wave-uniform branch): the reads past the window
+        // stay inside sp (the window ends at most at the staged data's end, and sp has 4 slots to spare) and
+        // those candidates add a selected +0 and no bit; the k = ln mod 4 bits join the register pair in one
+        // 64-bit shift. Sums and bits are those of k single steps (one), in the same order.
+        const int32_t k = ln & 3;
+        if (__any(k > 0)) {
+            const float4* q = sp + lo + 4 * n4;
+            const float4 a = q[0], bb = q[1], cc = q[2];
+            float ua, ub, uc;
+            const float wa = spline_w4(c, dist2(pi, a), ua);
+            const float wb = spline_w4(c, dist2(pi, bb), ub);
+            const float wc = spline_w4(c, dist2(pi, cc), uc);
+            s += k > 0 ? wa : 0.0f;
+            s += k > 1 ? wb : 0.0f;
+            s += k > 2 ? wc : 0.0f;
+            // sign bits (1: not a neighbour), oldest highest, then the k oldest kept
+            const uint32_t f = ((__float_as_uint(ua) >> 31) << 2 | (__float_as_uint(ub) >> 31) << 1 |
+                                (__float_as_uint(uc) >> 31)) >> (3 - k);
+            const uint64_t m = ((uint64_t)mh << 32 | ml) << k | f;
+            mh = (uint32_t)(m >> 32);
+            ml = (uint32_t)m;
+            mn += k;
+            if (mn >= 32) {
+                mn -= 32;
+                store((uint32_t)mn);
+            }
+            keep_b128(a, bb, cc, cc);
+        }
     };
     constexpr int nplanes = 2 * XS + 1;
 #pragma unroll 1
