@@ -355,10 +355,9 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
         SPH_DIAG_ADD(9, wave_max(ln >> 2));     // 4-candidate iterations
         SPH_DIAG_ADD(10, wave_max(ln & 3));     // tail iterations
         const int32_t n4 = ln >> 2;
-        const float4* p = sp + lo;
+        const float4* const p0 = sp + lo;
+        const float4* p = p0;
         const float4* const pe = p + 4 * n4;
-        const float4* pw = p + 4 * ((31 - mn) >> 2);
-        const uint32_t sh = (uint32_t)mn & 3u;
         for (; p < pe; p += 4) {
             const float4 a = p[0], bb = p[1], cc = p[2], d = p[3];
             const float ra = dist2(pi, a), rb = dist2(pi, bb), rc = dist2(pi, cc), rd = dist2(pi, d);
@@ -369,13 +368,14 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
             s += spline_w4(c, rd, ud);
             mh = __builtin_amdgcn_alignbit(mh, ml, 28u);
             bit(ua); bit(ub); bit(uc); bit(ud);
-            if (p == pw) {
-                store(sh);
-                pw += 32;
-            }
+            // every eighth iteration the lanes still running (all of them at the same iteration, so the test is
+            // wave-uniform) hold mn + 32 bits: store the oldest 32
+            if ((__builtin_amdgcn_readfirstlane((uint32_t)(p - p0)) & 31u) == 28u) store((uint32_t)mn);
             keep_b128(a, bb, cc, d);
         }
-        mn = (mn + 4 * n4) & 31;
+        const int32_t pend = mn + 4 * (n4 & 7);   // the bits since the last store
+        if (pend >= 32) store((uint32_t)(pend - 32));
+        mn = pend & 31;
         // the 0–3 remaining candidates as one group of three (wave-uniform branch): the reads past the window
         // stay inside sp (the window ends at most at the staged data's end, and sp has 4 slots to spare) and
         // those candidates add a selected +0 and no bit; the k = ln mod 4 bits join the register pair in one

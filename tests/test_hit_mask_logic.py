@@ -59,6 +59,52 @@ def write_mask(windows):
     return words
 
 
+def write_mask_uniform(windows):
+    """The kernel's writer since round 3: a window's 4-wide groups store a word after every eighth group
+    (the test is wave-uniform: all lanes still scanning are at the same group) with the mn bits pending
+    before the scan above it, the bits since the last such store are settled once after the groups, and
+    the 0-3 remaining candidates enter as one group (k bits in one 64-bit shift)."""
+    mh, ml, mn, mw = 0, 0, 0, 0
+    words = [0] * HM_WORDS
+
+    def store(sh):
+        nonlocal mw
+        if mw < HM_WORDS:
+            words[mw] = bitrev32(alignbit(mh, ml, sh))
+        mw += 1
+
+    def sign(h):
+        return 1 if h else 0
+
+    for w in windows:
+        ln = len(w)
+        n4 = ln // 4
+        for it in range(n4):
+            mh = alignbit(mh, ml, 28)
+            for k in range(4):
+                ml = alignbit(ml, 0x80000000 if w[4 * it + k] else 0x3F800000, 31)
+            if it % 8 == 7:
+                store(mn)
+        pend = mn + 4 * (n4 % 8)
+        if pend >= 32:
+            store(pend - 32)
+        mn = pend & 31
+        k = ln % 4
+        if k:
+            t = 4 * n4
+            bits = [sign(w[t + j]) if j < k else 0 for j in range(3)]
+            f = (bits[0] << 2 | bits[1] << 1 | bits[2]) >> (3 - k)
+            m = (((mh << 32) | ml) << k | f) & M64
+            mh, ml = m >> 32, m & 0xFFFFFFFF
+            mn += k
+            if mn >= 32:
+                mn -= 32
+                store(mn)
+    if mn > 0 and mw < HM_WORDS:
+        words[mw] = bitrev32((ml << (32 - mn)) & 0xFFFFFFFF)
+    return words
+
+
 def write_mask_plain(windows):
     """The stream's definition (oldest bit first, 32 to a word, zeros past the end) with a 64-bit
     register that takes the newest bit at bit 63 (the round-2 writer before v_alignbit)."""
@@ -177,3 +223,14 @@ def test_budget_words_beyond_256_are_not_written():
     wins = [np.ones(300, bool)]
     words = write_mask(wins)
     assert words == [0xFFFFFFFF] * HM_WORDS
+
+
+@pytest.mark.parametrize("total", [0, 3, 32, 35, 100, 255, 256, 300])
+def test_uniform_store_writer_equals_plain_definition(total):
+    """the round-3 schedule (wave-uniform stores every eighth group, grouped tail) writes the same words"""
+    rng = np.random.default_rng(200 + total)
+    for _ in range(50):
+        wins = _windows(rng, total)
+        assert write_mask_uniform(wins) == write_mask_plain(wins)
+    long = [rng.random(n) < 0.3 for n in (37, 70, 5, 0, 64, 33)]   # windows of more than eight groups
+    assert write_mask_uniform(long) == write_mask_plain(long)
