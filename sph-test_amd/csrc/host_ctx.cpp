@@ -48,7 +48,7 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
         AL(mode, n); AL(mode2, n); AL(torque, 3 * n); AL(slot_of, n);
     } else {
         AL(rp, n);
-        AL(hmask, (size_t)HM_WORDS * n);
+        AL(hmask, (size_t)(HM_WORDS + 1) * n);   // + the writer's overflow row (wcsph_tiled.hip)
     }
     // incremental re-sort (both models)
     AL(sk_cur, n); AL(sk_next, n);

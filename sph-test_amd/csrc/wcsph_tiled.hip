@@ -330,10 +330,13 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
     uint32_t* const wend = rec ? hm.w + i + (size_t)HM_WORDS * hm.stride : nullptr;
     // the register pair takes sign(2 − q): 1 for a candidate that is NOT a neighbour; words are inverted
     auto bit = [&](float v) { ml = __builtin_amdgcn_alignbit(ml, __float_as_uint(v), 31u); };
-    auto store = [&](uint32_t sh) {   // the oldest 32 pending bits, sh newer ones above them
-        if (wp < wend) {
+    // the oldest 32 pending bits, sh newer ones above them. Words past the HM_WORDS budget all go to the extra
+    // row at wend (allocated, never read), so the budget test sits inside the store and not in every group.
+    // Only lanes with a target scan candidates, so wp is set wherever a store runs; hm.w is uniform.
+    auto store = [&](uint32_t sh) {
+        if (hm.w != nullptr) {
             *wp = __builtin_bitreverse32(~__builtin_amdgcn_alignbit(mh, ml, sh));
-            wp += hm.stride;
+            if (wp < wend) wp += hm.stride;
         }
     };
     auto one = [&](float r2) {   // a single candidate (scalar tail, global gather)
@@ -355,10 +358,10 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
         SPH_DIAG_ADD(9, wave_max(ln >> 2));     // 4-candidate iterations
         SPH_DIAG_ADD(10, wave_max(ln & 3));     // tail iterations
         const int32_t n4 = ln >> 2;
-        const float4* const p0 = sp + lo;
-        const float4* p = p0;
+        const float4* p = sp + lo;
         const float4* const pe = p + 4 * n4;
-        for (; p < pe; p += 4) {
+        int32_t it = 0;   // the group index: the same in every lane still scanning (uniform, a scalar register)
+        for (; p < pe; p += 4, ++it) {
             const float4 a = p[0], bb = p[1], cc = p[2], d = p[3];
             const float ra = dist2(pi, a), rb = dist2(pi, bb), rc = dist2(pi, cc), rd = dist2(pi, d);
             float ua, ub, uc, ud;
@@ -370,7 +373,7 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
             bit(ua); bit(ub); bit(uc); bit(ud);
             // every eighth iteration the lanes still running (all of them at the same iteration, so the test is
             // wave-uniform) hold mn + 32 bits: store the oldest 32
-            if ((__builtin_amdgcn_readfirstlane((uint32_t)(p - p0)) & 31u) == 28u) store((uint32_t)mn);
+            if ((it & 7) == 7) store((uint32_t)mn);
             keep_b128(a, bb, cc, d);
         }
         const int32_t pend = mn + 4 * (n4 & 7);   // the bits since the last store
