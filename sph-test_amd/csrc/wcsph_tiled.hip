@@ -617,13 +617,15 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
                         const int32_t slot = bi + (bi < l0 ? d0 : (bi < e2 ? d1 : d2));
                         pair_force(pk, pi, vi, ri.x, ri.y, sp[slot], sv[slot], acc);
                     }
-                    if (w0 == 0u) {
-                        w0 = w1;
-                        w1 = w2;
-                        w2 = w3;
-                        w3 = 0u;
-                        base += 32;
-                    }
+                    // the next word moves up, as selects: as a branch the compiler copied each queue word into a
+                    // new register every step (3 moves + 4 masked moves per step; force pass 189.2 -> 187.7 us
+                    // mid-collapse, profiles/r03_walk_select_shift_ab.log)
+                    const bool z = w0 == 0u;
+                    w0 = z ? w1 : w0;
+                    w1 = z ? w2 : w1;
+                    w2 = z ? w3 : w2;
+                    w3 = z ? 0u : w3;
+                    base += z ? 32 : 0;
                 }
             } while (__any(nh > 0));
         }
