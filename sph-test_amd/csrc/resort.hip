@@ -20,7 +20,8 @@
 // for bit with the full sort.
 //
 // Kernels:
-//   k_mv_rank        all-pairs counts per mover: (key, index) rank, index rank, A(q)
+//   k_mv_rank        counts per mover against every 64-mover tile (sorted in LDS, binary searches):
+//                    (key, index) rank, index rank, A(q)
 //   k_mv_place       movers: scatter of (pos, vel, id, key); tables by (key, index) and by index
 //   k_mv_merge       stayers: scatter of (pos, vel, id, key); extra workgroups update the cell
 //                    starts in place: cs[k] += #{movers: new key < k} − #{movers: old key < k}
@@ -120,24 +121,68 @@ static __device__ __forceinline__ uint32_t movers_before(bool mv, uint32_t block
     return off + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
 }
 
+// #entries below v in a sorted 64-entry LDS array (branchless; pads sort last and are never below v)
+template <typename T>
+static __device__ __forceinline__ uint32_t lb64(const T* __restrict__ a, T v) {
+    uint32_t p = 0;
+#pragma unroll
+    for (uint32_t s = 32; s > 0; s >>= 1) p += a[p + s - 1] < v ? s : 0u;
+    return p + (a[p] < v ? 1u : 0u);
+}
+
 // Per mover x (append order): rank[x] = #{y : (k_y, i_y) < (k_x, i_x)}, rank[cap + x] =
 // #{y : i_y < i_x}, rank[2cap + x] = A(q_x) = #{y : i_y < q_x}. Work items = (MV_BLK movers) x
 // (MV_TILE-mover tile); partial counts are added atomically (integers: order-independent).
+// The tile is sorted twice in LDS (by (key, index) and by index: each entry's rank among the 64, counted a
+// quarter per wave), and each mover counts by three 7-probe binary searches instead of 3 x 64 compares
+// (~6.5 VALU per mover pair before, O(m^2) in the movers).
 // Also zeroes the next step's mover counter.
 __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__ mtotal,
                                                     uint32_t* __restrict__ next_count,
                                                     const uint32_t* __restrict__ cs_old, ResortScratch w) {
-    __shared__ uint64_t tile[MV_TILE];
+    constexpr int NPART = MV_BLK / MV_TILE;                  // waves counting one quarter of the tile each
+    __shared__ uint64_t tile[MV_TILE];                       // (key, index) in append order; pads ~0
+    __shared__ uint64_t sc[MV_TILE];                         // sorted by (key, index)
+    __shared__ uint32_t si[MV_TILE];                         // indices, sorted
+    __shared__ uint32_t part_c[NPART][MV_TILE], part_i[NPART][MV_TILE];
     if (w.dz) w.mi_off = (int32_t)w.dz->nl - (int32_t)w.dz->o0;
     if (blockIdx.x == 0 && threadIdx.x == 0) *next_count = 0u;
     const uint32_t m = *mtotal;
     const uint64_t nr = (m + MV_BLK - 1) / MV_BLK, nt = (m + MV_TILE - 1) / MV_TILE;
+    const int e = threadIdx.x % MV_TILE, part = threadIdx.x / MV_TILE;
     for (uint64_t item = blockIdx.x; item < nr * nt; item += gridDim.x) {
         const uint32_t ir = (uint32_t)(item % nr), it = (uint32_t)(item / nr);
         __syncthreads();
-        for (int t = threadIdx.x; t < MV_TILE; t += MV_BLK) {
-            const uint32_t y = it * MV_TILE + t;
-            tile[t] = y < m ? comp(w.mk[y], mv_slot(w, w.mi[y])) : ~0ull;
+        if (threadIdx.x < MV_TILE) {
+            const uint32_t y = it * MV_TILE + threadIdx.x;
+            tile[threadIdx.x] = y < m ? comp(w.mk[y], mv_slot(w, w.mi[y])) : ~0ull;
+        }
+        __syncthreads();
+        {   // entry e's rank among the tile, over this wave's quarter (ties, i.e. pads, by position)
+            const uint64_t c = tile[e];
+            const uint32_t i = (uint32_t)c;
+            uint32_t rc = 0, ri = 0;
+#pragma unroll 4
+            for (int u = part * (MV_TILE / NPART); u < (part + 1) * (MV_TILE / NPART); ++u) {
+                const uint64_t cu = tile[u];
+                const uint32_t iu = (uint32_t)cu;
+                rc += (cu < c || (cu == c && u < e)) ? 1u : 0u;
+                ri += (iu < i || (iu == i && u < e)) ? 1u : 0u;
+            }
+            part_c[part][e] = rc;
+            part_i[part][e] = ri;
+        }
+        __syncthreads();
+        if (threadIdx.x < MV_TILE) {
+            uint32_t rc = 0, ri = 0;
+#pragma unroll
+            for (int k = 0; k < NPART; ++k) {
+                rc += part_c[k][threadIdx.x];
+                ri += part_i[k][threadIdx.x];
+            }
+            const uint64_t c = tile[threadIdx.x];
+            sc[rc] = c;
+            si[ri] = (uint32_t)c;
         }
         __syncthreads();
         const uint32_t x = ir * MV_BLK + threadIdx.x;
@@ -146,15 +191,7 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
             const uint64_t cx = comp(k, ix);
             const uint32_t c0 = cs_old[k], c1 = cs_old[k + 1];
             const uint32_t q = ix < c0 ? c0 : (ix > c1 ? c1 : ix);
-            uint32_t nk = 0, ni = 0, nq = 0;
-#pragma unroll 4
-            for (int t = 0; t < MV_TILE; ++t) {
-                const uint64_t c = tile[t];
-                const uint32_t iy = (uint32_t)c;   // padding: 0xffffffff, never below
-                nk += c < cx;
-                ni += iy < ix;
-                nq += iy < q;
-            }
+            const uint32_t nk = lb64(sc, cx), ni = lb64(si, ix), nq = lb64(si, q);
             if (nk) atomicAdd(&w.rank[x], nk);
             if (ni) atomicAdd(&w.rank[w.cap + x], ni);
             if (nq) atomicAdd(&w.rank[2 * w.cap + x], nq);
