@@ -115,7 +115,7 @@ __device__ __forceinline__ bool row_window(const GridDesc& g, float fx, float fy
         gxg = (dx < 0 ? fx + (float)(-dx - 1) : (dx > 0 ? (1.0f - fx) + (float)(dx - 1) : 0.0f)) * (1.0f / XS);
     }
     const float gyg = dy < 0 ? fy : (dy > 0 ? 1.0f - fy : 0.0f);
-    const float d2 = gxg * gxg + gyg * gyg;
+    const float d2 = fmaf(gyg, gyg, gxg * gxg);   // explicit: both passes must trim every window identically
     if (!(d2 < 1.0f)) return false;
     const float hz = __builtin_amdgcn_sqrtf(1.0f - d2) * (float)g.zsub + 1e-3f;
     const float a = gzf - hz, b = gzf + hz;

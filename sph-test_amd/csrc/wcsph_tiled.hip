@@ -51,6 +51,10 @@ constexpr int TF_GCAP = SPH_TF_GCAP;
 #define SPH_WALK_UNROLL 4
 #endif
 constexpr int TF_FALLBACK = 4 * TF_GCAP;
+#ifndef SPH_TF_BLK
+#define SPH_TF_BLK 256
+#endif
+constexpr int TF_BLK = SPH_TF_BLK;
 // Slots each thread stages per round (loads in flight together): pass 1 up to 1,350 slots in 256 threads
 // takes all of a plane in one or two rounds; pass 2 holds 40 B per slot in registers.
 #ifndef SPH_TT_STAGE_U
@@ -169,9 +173,13 @@ __device__ __forceinline__ int wave_sum(int v) {
 #define SPH_DIAG_ADD(k, v) ((void)0)
 #endif
 
+// Sums of products are written as explicit fmaf chains: left to the compiler's contraction, dx·dx + dy·dy
+// + dz·dz became fma(dx, dx, dy·dy) in the LDS scans but fma(dy, dy, dx·dx) in the global-gather path, so a
+// candidate at q = 2 to the last ulp could be a hit on one path and not on the other, and results depended
+// on which path a block took (on the plane budget and block size; tests/test_gpu_slab.py decompositions).
 __device__ __forceinline__ float dist2(float4 a, float4 b) {
     const float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
-    return dx * dx + dy * dy + dz * dz;
+    return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
 }
 
 // 4·w(q) of the unnormalised cubic spline (W = σ·w) for q ≤ 2, else 0. Branchless: both arms
@@ -209,31 +217,31 @@ __device__ __forceinline__ void keep_b128(float4 a, float4 b, float4 c, float4 d
 // slot c0[r] + (t − off[r]). U slots per thread per round, all U loads issued before the LDS writes, so
 // they are in flight together; the source interval is picked by selects (indexing c0[] by a computed r
 // put the array in scratch memory: one scratch load and one global load, serialised, per staged slot).
-template <int U, typename L, typename W>
+template <int U, int BLK = TT_BLK, typename L, typename W>
 __device__ __forceinline__ void stage_plane(const int32_t (&c0)[3], const int32_t (&len)[3], int32_t total, L&& load,
                                             W&& write) {
     const int32_t e0 = len[0], e1 = len[0] + len[1];
     const int32_t d0 = c0[0], d1 = c0[1] - e0, d2 = c0[2] - e1;
-    for (int32_t base = threadIdx.x; base < total; base += U * TT_BLK) {
+    for (int32_t base = threadIdx.x; base < total; base += U * BLK) {
         decltype(load(0)) v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int32_t t = base + u * TT_BLK;
+            const int32_t t = base + u * BLK;
             if (t < total) v[u] = load(t + (t < e0 ? d0 : (t < e1 ? d1 : d2)));
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int32_t t = base + u * TT_BLK;
+            const int32_t t = base + u * BLK;
             if (t < total) write(t, v[u]);
         }
     }
 }
 
 // One contiguous run [src0, src0 + ln) into slots [0, ln) (the chunked rows), the same way.
-template <int U, typename L, typename W>
+template <int U, int BLK = TT_BLK, typename L, typename W>
 __device__ __forceinline__ void stage_run(int32_t src0, int32_t ln, L&& load, W&& write) {
     const int32_t c0[3] = {src0, 0, 0}, len[3] = {ln, 0, 0};
-    stage_plane<U>(c0, len, ln, load, write);
+    stage_plane<U, BLK>(c0, len, ln, load, write);
 }
 
 // A plane whose three intervals exceed the LDS budget: consecutive rows that fit together are staged as
@@ -506,7 +514,7 @@ static PairK pair_constants(const SphConst& c) {
 __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi, float rhoi, float prhoi, float4 pj,
                                            float4 vj, ForceAcc& a) {
     const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
-    const float r2 = dx * dx + dy * dy + dz * dz;
+    const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));   // explicit chains: the same rounding on every path
     const float rs = __builtin_amdgcn_rsqf(fmaxf(r2, 1e-30f));
     const float q = r2 * rs * k.inv_h;
     const float t = 2.0f - q;
@@ -519,7 +527,7 @@ __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi,
     const float w4 = inner ? w_in : w_out;
     const float G = inner ? g_in : g_out;
     const float du = vi.x - vj.x, dv = vi.y - vj.y, dw = vi.z - vj.z;
-    const float vr = du * dx + dv * dy + dw * dz;
+    const float vr = fmaf(dw, dz, fmaf(dv, dy, du * dx));
     // one reciprocal for both 1/(ρi + ρj) and 1/((r² + η²)(ρi + ρj))
     const float e = r2 + k.eta2;
     const float inv_es = __builtin_amdgcn_rcpf(e * (rhoi + pj.w));
@@ -532,7 +540,7 @@ __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi,
 }
 
 template <int XS>
-__global__ __launch_bounds__(TT_BLK) void k_force_tiled(
+__global__ __launch_bounds__(TF_BLK) __attribute__((amdgpu_waves_per_eu(4))) void k_force_tiled(
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
     const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, PairK pk, float dt,
     float fext_x, float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o, MoverSink mv,
@@ -544,7 +552,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
         ib = (int32_t)*dr.lo;
         n = (int32_t)*dr.hi;
     }
-    const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
+    const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TF_BLK;
     if (i0 >= n) return;   // whole workgroup: before any barrier
     SPH_BT_START;
     // Targets stay in sorted order here. Lanes ordered by quarters of fx (a dx plane's hit count follows
@@ -553,7 +561,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
     // scattered LDS slots (profiles/r02_direct_plane_ab.log, r02_fx2_noself_ab.log).
     const int32_t i = i0 + tid;
     const bool valid = i < n;
-    const int32_t ilast = min(i0 + TT_BLK, n) - 1;
+    const int32_t ilast = min(i0 + TF_BLK, n) - 1;
     const int32_t ii = valid ? i : ilast;
     const float4 pi = pos[ii], vi = vel[ii];
     const float2 ri = rp[ii];
@@ -675,7 +683,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
                 tot += lg[r];
             }
             __syncthreads();
-            stage_plane<TF_STAGE_U>(c0, lg, tot, load_f, write_f);
+            stage_plane<TF_STAGE_U, TF_BLK>(c0, lg, tot, load_f, write_f);
             __syncthreads();
             if (by_mask) {
                 const int32_t l0 = wg[0], e2 = l0 + wg[1];
@@ -711,7 +719,7 @@ __global__ __launch_bounds__(TT_BLK) void k_force_tiled(
             for (int32_t base = c0[r]; base < c1[r]; base += TF_GCAP) {
                 const int32_t ln = min(TF_GCAP, c1[r] - base);
                 __syncthreads();
-                stage_run<TF_STAGE_U>(base, ln, load_f, write_f);
+                stage_run<TF_STAGE_U, TF_BLK>(base, ln, load_f, write_f);
                 __syncthreads();
                 const int32_t lo = max(r0[r], base) - base;
                 const int32_t wl = max(min(r1[r], base + ln) - base - lo, 0);
@@ -775,10 +783,10 @@ void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, 
                         uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr) {
     if (ie <= ib) return;
     if (g.xsub == 2)
-        SPH_LAUNCH(k_force_tiled<2>, (ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c,
+        SPH_LAUNCH(k_force_tiled<2>, (ie - ib + TF_BLK - 1) / TF_BLK, TF_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c,
                    pair_constants(c), dt, fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr);
     else
-        SPH_LAUNCH(k_force_tiled<1>, (ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c,
+        SPH_LAUNCH(k_force_tiled<1>, (ie - ib + TF_BLK - 1) / TF_BLK, TF_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c,
                    pair_constants(c), dt, fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr);
 }
 
