@@ -95,21 +95,31 @@ def force_kernel_name() -> str:
 
 
 def load_clock(code_hash: str):
-    """Effective shader clocks from the committed rocprofv3 GRBM passes (profiles/clock_*.json,
-    scripts/gpu_clock.sh): the force pass on its longest dispatches (C5) and the VALU microbenchmark.
-    The force-pass clock is used only from a file stamped with the code objects that are running."""
+    """Effective shader clocks and the measured VALU issue peak from ONE committed clock file
+    (profiles/clock_*.json, scripts/gpu_clock.sh): the force pass on its longest dispatches (C5), the VALU
+    microbenchmark's GRBM clock and its issue rate, all taken in the same run on the same box. Only a file
+    stamped with the code objects that are running is used (the newest such file)."""
     out = {}
     for f in sorted((ROOT / "profiles").glob("clock_*.json")):
         try:
             d = json.loads(f.read_text())
         except Exception:
             continue
-        if "k_force_tiled" in d.get("C5", {}) and d.get("device_code_hash") == code_hash:
-            out["force_ghz"] = d["C5"]["k_force_tiled"]["clock_ghz_median"]
-            out["force_src"] = f"{f.name}: C5 k_force_tiled, {d['C5']['k_force_tiled']['mean_us']:.0f} us dispatches"
-        if "k_fma" in d.get("valu", {}):
-            out["micro_ghz"] = d["valu"]["k_fma"]["clock_ghz_median"]
-        out["file"] = f.name
+        if d.get("device_code_hash") != code_hash:
+            continue
+        cur = {"file": f.name}
+        fk = d.get("C5", {}).get("k_force_tiled", {})
+        if "clock_ghz_median" in fk:
+            cur["force_ghz"] = fk["clock_ghz_median"]
+            cur["force_src"] = f"{f.name}: C5 k_force_tiled, {fk['mean_us']:.0f} us dispatches"
+        mk = d.get("valu", {}).get("k_fma", {})
+        if "clock_ghz_median" in mk:
+            cur["micro_ghz"] = mk["clock_ghz_median"]
+        vp = d.get("valu_peak", {})
+        if "G_wave_instr_per_s" in vp:
+            cur["peak"] = vp["G_wave_instr_per_s"] * 1e9
+            cur["peak_src"] = f"{f.name}: scripts/valu_peak.hip, 8 waves/SIMD, {vp.get('us', 0):.0f} us dispatches"
+        out = cur
     return out
 
 
@@ -428,14 +438,17 @@ def main():
         if "valu_instr" in pmc:
             # what bounds the neighbour pass in practice: VALU issue, from the same
             # kernel's committed PMC pass and this run's kernel time, priced two ways: against the
-            # microbenchmark's measured issue rate, and against the spec issue rate (256 CUs × 4 SIMDs
-            # × ½ wave64-instruction per cycle) at the clock the chip held during the force pass
+            # microbenchmark's issue rate and against the spec issue rate (256 CUs × 4 SIMDs × ½
+            # wave64-instruction per cycle) at the clock the chip held during the force pass. The peak, both
+            # clocks and the counters come from files stamped with this library's device-code hash; the peak
+            # and its clock were measured in one run on one box (scripts/gpu_clock.sh).
             va = pmc["valu_instr"] / avg_s
-            roofline["valu"] = {"achieved": round(va / 1e9, 2), "peak": round(PEAK_VALU_WAVE_INSTR_PER_S / 1e9, 1),
-                                "unit": "G wave-instr/s", "frac": round(va / PEAK_VALU_WAVE_INSTR_PER_S, 4),
-                                "source": "rocprofv3 SQ_INSTS_VALU per launch (profiles/pmc_C3.json); peak measured by "
-                                          "scripts/valu_peak.hip, long dispatches (profiles/r02_valu_peak_long.log)"}
             clk = load_clock(code_hash)
+            peak = clk.get("peak", PEAK_VALU_WAVE_INSTR_PER_S)
+            roofline["valu"] = {"achieved": round(va / 1e9, 2), "peak": round(peak / 1e9, 1),
+                                "unit": "G wave-instr/s", "frac": round(va / peak, 4),
+                                "source": "rocprofv3 SQ_INSTS_VALU per launch (" + str(pmc.get("file")) + "); peak: " +
+                                          clk.get("peak_src", "scripts/valu_peak.hip (profiles/r02_valu_peak_long.log)")}
             if "force_ghz" in clk:
                 spec = 256 * 4 * 0.5 * clk["force_ghz"] * 1e9
                 roofline["valu"].update({
@@ -443,10 +456,18 @@ def main():
                     "spec_peak_at_force_clock": round(spec / 1e9, 1),
                     "frac_of_spec_at_clock": round(va / spec, 4),
                     "clock_source": clk["force_src"]})
-            if "micro_ghz" in clk:
-                roofline["valu"]["microbench_clock_ghz"] = round(clk["micro_ghz"], 3)
-                roofline["valu"]["microbench_frac_of_spec_at_its_clock"] = round(
-                    PEAK_VALU_WAVE_INSTR_PER_S / (256 * 4 * 0.5 * clk["micro_ghz"] * 1e9), 4)
+            if "micro_ghz" in clk and "peak" in clk:
+                mf = clk["peak"] / (256 * 4 * 0.5 * clk["micro_ghz"] * 1e9)
+                if mf <= 1.0:
+                    roofline["valu"]["microbench_clock_ghz"] = round(clk["micro_ghz"], 3)
+                    roofline["valu"]["microbench_frac_of_spec_at_its_clock"] = round(mf, 4)
+                else:   # a rate above the spec at its clock: the clock reading is wrong, report neither
+                    roofline["valu"]["microbench_clock_note"] = (
+                        f"refused: measured peak over spec at the GRBM clock {clk['micro_ghz']:.3f} GHz ({mf:.3f} > 1)")
+            for k in ("frac", "frac_of_spec_at_clock"):
+                if roofline["valu"].get(k, 0) > 1.0:
+                    roofline["valu"][k + "_note"] = "above 1: inconsistent denominators, not a measurement"
+                    roofline["valu"].pop(k)
 
     mid = None
     if isinstance(runner, SingleRunner) and args.mid_steps > 0:

@@ -260,6 +260,10 @@ int sph_read_hit_mask_counts(sph_ctx* ctx, uint32_t counts[2], int32_t reset);
  * bit-exact parity tests. perm[i] = source index of sorted slot i. */
 int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int32_t key_bits,
                          uint32_t* perm_out, uint32_t* sorted_keys_out);
+/* Test hook, Model S: add dv to the velocity of particle `id` between steps, in every context of a
+ * group that holds it (tests/test_gpu_multi.py: a particle made to cross several slab columns in one
+ * step, the decomposition's column-jump fallback and its window-exit stop). Not a Unity call. */
+int sph_debug_kick(sph_ctx* ctx, int32_t id, const float dv[3]);
 
 /* ---- slab decomposition (multi-GPU; SPEC_SPH.md §3). New capability: the reference is one
  *      GPU. One context per rank owns global cell columns [cx_lo, cx_hi)

@@ -2,7 +2,11 @@
 """Effective shader clock per kernel from rocprofv3 passes with `--kernel-trace --pmc GRBM_GUI_ACTIVE
 GRBM_COUNT`: clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel duration (MI355X_MICROARCH.md, DVFS give-back;
 the quotient reads high on dispatches shorter than ~0.3 ms, so long dispatches are the measurement).
-Usage: clock_summary.py <out.json> <label>=<rocprof dir> ..."""
+Dispatches shorter than MIN_US are dropped: the GRBM count of a short dispatch includes its launch ramp and
+reads 3-17 GHz (profiles/clock_r03.json), which no clock reaches. A `valu_peak=<log>` argument adds the VALU
+microbenchmark's issue rate measured in the same run on the same box (scripts/valu_peak.hip JSON lines; the
+8-waves-per-SIMD plain-f32 line), so the rate and its clock come from one box.
+Usage: clock_summary.py <out.json> <label>=<rocprof dir> ... [valu_peak=<log>]"""
 import re
 import csv
 import glob
@@ -14,6 +18,9 @@ from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 import __graft_entry__ as GE  # noqa: E402
+
+
+MIN_US = 50.0
 
 
 def one(d):
@@ -40,6 +47,12 @@ def one(d):
             if key in dur and dur[key] > 0:
                 clocks.append(v / 8.0 / dur[key] / 1e9)
                 durs.append(dur[key] * 1e6)
+        keep = [(c, u) for c, u in zip(clocks, durs) if u >= MIN_US]
+        if clocks and not keep:
+            out[k] = {"dispatches": len(clocks), "mean_us": sum(durs) / len(durs),
+                      "dropped": f"every dispatch shorter than {MIN_US:g} us: no clock reading"}
+            continue
+        clocks, durs = [c for c, _ in keep], [u for _, u in keep]
         if clocks:
             clocks.sort()
             out[k] = {"dispatches": len(clocks), "mean_us": sum(durs) / len(durs),
@@ -52,6 +65,11 @@ def main():
            "device_code_hash": GE.load_package()._abi.device_code_hash()}
     for arg in sys.argv[2:]:
         label, d = arg.split("=", 1)
+        if label == "valu_peak":
+            rows = [json.loads(l) for l in open(d) if l.startswith("{")]
+            best = [r for r in rows if r.get("waves_per_simd") == 8 and r.get("packed") == 0]
+            res[label] = {"file": os.path.basename(d), **(best[0] if best else {"error": "no 8-wave plain line"})}
+            continue
         res[label] = one(d)
     json.dump(res, open(sys.argv[1], "w"), indent=1)
     print(json.dumps(res, indent=1))

@@ -11,5 +11,5 @@ for c in C3 C5; do
   timeout -s KILL 180 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT -d "$GRAFT_REPO_ROOT/gpurun_out/clock/$c" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/scripts/run_steps.py" --config $c --steps 20 --warmup 3 > gpurun_out/clock/$c.log 2>&1; rc=$?
   echo "$c pmc rc=$rc"; [ $rc -ne 0 ] && { tail -5 gpurun_out/clock/$c.log; exit $rc; }
 done
-python3 scripts/clock_summary.py gpurun_out/clock/clock.json valu=gpurun_out/clock/valu C3=gpurun_out/clock/C3 C5=gpurun_out/clock/C5 > gpurun_out/clock/summary.log 2>&1
+python3 scripts/clock_summary.py gpurun_out/clock/clock.json valu=gpurun_out/clock/valu C3=gpurun_out/clock/C3 C5=gpurun_out/clock/C5 valu_peak=gpurun_out/clock/valu_peak_long.log > gpurun_out/clock/summary.log 2>&1
 echo "summary rc=$?"; grep -A6 '"k_force_tiled"\|"k_fma"\|"k_density_tiled"' gpurun_out/clock/summary.log | head -60

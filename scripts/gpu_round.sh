@@ -22,7 +22,7 @@ python3 scripts/pmc_summary.py gpurun_out/pmc gpurun_out/pmc_C3.json C3 > gpurun
 echo "pmc_summary rc=$?"
 bash scripts/gpu_clock.sh > gpurun_out/clock.log 2>&1; echo "clock rc=$?"; tail -3 gpurun_out/clock.log
 # the driver's default bench line, after the counter files exist (its roofline reads them)
-cp gpurun_out/pmc_C3.json profiles/pmc_C3.json; cp gpurun_out/clock/clock.json profiles/clock_r03.json 2>/dev/null
+cp gpurun_out/pmc_C3.json profiles/pmc_C3.json; cp gpurun_out/clock/clock.json profiles/clock_${ROUND:-r04}.json 2>/dev/null
 timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1; rc=$?
 echo "bench rc=$rc"; tail -1 gpurun_out/bench.log | cut -c 1-600
 exit 0

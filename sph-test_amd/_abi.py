@@ -177,6 +177,7 @@ SIGNATURES = {
     "sph_read_path_counts": ([_P, _P, _I], C.c_int),
     "sph_read_hit_mask_counts": ([_P, _P, _I], C.c_int),
     "sph_debug_radix_sort": ([_P, _P, _I, _I, _P, _P], C.c_int),
+    "sph_debug_kick": ([_P, _I, _P], C.c_int),
     "sph_slab_set": ([_P, C.POINTER(SphSlab)], C.c_int),
     "sph_slab_init_scenario": ([_P, C.POINTER(SphScenario)], C.c_int),
     "sph_slab_count_sends": ([_P, C.POINTER(C.c_int32)], C.c_int),

@@ -237,6 +237,11 @@ class Context:
         self._chk("sph_read_path_counts", self._L.sph_read_path_counts(self._h, A.ptr(out), 1 if reset else 0))
         return out
 
+    def debug_kick(self, pid: int, dv) -> None:
+        """Test hook (sph_debug_kick): add dv to particle pid's velocity, in every slab that holds it."""
+        d = np.ascontiguousarray(dv, dtype=np.float32)
+        self._chk("sph_debug_kick", self._L.sph_debug_kick(self._h, int(pid), A.ptr(d)))
+
     def hit_mask_counts(self, reset: bool = True) -> np.ndarray:
         """(wave-planes of the force pass scanned by distance instead of the hit mask, waves run)
         (sph_read_hit_mask_counts)."""

@@ -842,6 +842,19 @@ int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int3
     return SPH_OK;
 }
 
+int sph_debug_kick(sph_ctx* ctx, int32_t id, const float dv[3]) {
+    if (!ctx || !dv) return SPH_ERR_INVALID;
+    if (is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "sph_debug_kick is Model S only");
+    std::vector<sph_ctx*> cs = is_group(ctx) ? multi_kids(ctx) : std::vector<sph_ctx*>{ctx};
+    for (sph_ctx* k : cs) {   // every slot up to the capacity: ghosts and stale slots are overwritten before use
+        HIPCHK(hipSetDevice(k->device));
+        launch_kick(k->id, k->vel, k->capacity, id, dv, k->stream);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(k->stream));
+    }
+    return SPH_OK;
+}
+
 int sph_resize(sph_ctx* ctx, int32_t capacity) {
     if (!ctx || capacity < 0) return SPH_ERR_INVALID;
     NOT_GROUP(ctx);

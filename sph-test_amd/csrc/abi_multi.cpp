@@ -52,6 +52,8 @@ struct RankState {
     hipEvent_t lag_ev[LAG_SLOTS] = {};
     int64_t cin_hist[LAG_SLOTS] = {};   // Σ records received per step (slot bound bookkeeping)
     int64_t since_cut = 0;              // steps since the initial cut or the last re-cut
+    bool jump_guard = false;            // the last force pass ran the column-jump guard (it needs the sorted old
+                                        // keys: incremental re-sort on); without it the sends scan every own slot
     int64_t n_prev_ub = 0;              // upper bound of the previous step's assembled slots
     int64_t n_ub = 0;                   // this step's
     int32_t nb_send = 1;                // count / pack blocks of this step
@@ -380,6 +382,12 @@ int validate_movers(RankState& R, int used) {
 }
 
 // ---------------------------------------------------------------- phase A: counts and messages
+// Sends from the four boundary columns only (slab.hip send_ranges): the cut is older than three steps and the
+// last force pass checked that no own particle moved more than one column (SlabSizes.jump). That check reads
+// the previous slot order's keys (MoverSink.sk), which exist only with the incremental re-sort; after a
+// full-sort step (SPH_RESORT=0, or a step past the mover limit) every own slot is scanned.
+bool steady_sends(const RankState& R) { return R.since_cut >= 3 && R.jump_guard; }
+
 int phase_count(RankState& R) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
@@ -397,7 +405,7 @@ int phase_count(RankState& R) {
     R.nb_send = slab_send_blocks(0, (int32_t)std::max<int64_t>(R.n_prev_ub, 1));
     KTimer t(ctx, "slab_count", 4.0 * R.n_prev_ub);
     launch_slab_count_dev(ctx->keys, R.dz, R.nb_send, gyz(ctx), col_le(ctx), col_ge(ctx), ctx->sblk,
-                          ctx->sdev + SDEV_TOTALS, ctx->stream, R.since_cut >= 3);
+                          ctx->sdev + SDEV_TOTALS, ctx->stream, steady_sends(R));
     CKPT(R, "count");
     return SPH_OK;
 }
@@ -419,7 +427,7 @@ int phase_pack(RankState& R, Multi& M) {
                              (uint32_t)ctx->grid.cx0 * gyz(ctx), R.dz,
                              R.nb_send, gyz(ctx), s, col_le(ctx),
                              col_ge(ctx), ctx->sblk, R.msg_out[s], R.c1o[s], ctx->sdev + SDEV_TOTALS + s, ctx->stream,
-                             R.since_cut >= 3);
+                             steady_sends(R));
     }
     HIPCHK(hipGetLastError());
     // the peer copies of a local group wait for it (RCCL orders its sends on this stream itself); a
@@ -665,14 +673,16 @@ int phase_rho_out(RankState& R, Multi& M) {
 }
 
 // ---------------------------------------------------------------- phase C: force passes, finish
-void force_dev(sph_ctx* ctx, const uint32_t* lo, const uint32_t* hi, int64_t grid_ub, float dt) {
-    if (grid_ub <= 0) return;
-    KTimer t(ctx, "force_integrate", 76.0 * (double)grid_ub, true);
+// Returns whether the pass ran the column-jump guard (steady_sends).
+bool force_dev(sph_ctx* ctx, const uint32_t* lo, const uint32_t* hi, int64_t grid_ub, float dt) {
     MoverSink mv = mover_sink(ctx);
+    if (grid_ub <= 0) return mv.sk != nullptr;
+    KTimer t(ctx, "force_integrate", 76.0 * (double)grid_ub, true);
     mv.err = &ctx->dz->flags;
     mv.jump = &ctx->dz->jump;
     launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, (int32_t)grid_ub, ctx->grid, ctx->sc, dt, forcing(ctx),
                        ctx->pos2, ctx->vel2, ctx->keys, mv, hit_mask_read(ctx), path_ctr(ctx), ctx->stream, DevRange{lo, hi});
+    return mv.sk != nullptr;
 }
 
 int phase_interior(RankState& R, float dt) {
@@ -681,7 +691,7 @@ int phase_interior(RankState& R, float dt) {
     // interior columns: [pick[2] or pick[1], pick[3] or pick[4]) (empty when a one-column slab has both
     // neighbours: then the bound is below the start and every workgroup exits)
     const uint32_t* pk = R.dz->pick;
-    force_dev(ctx, ctx->has_left ? &pk[2] : &pk[1], ctx->has_right ? &pk[3] : &pk[4], R.n_ub, dt);
+    R.jump_guard = force_dev(ctx, ctx->has_left ? &pk[2] : &pk[1], ctx->has_right ? &pk[3] : &pk[4], R.n_ub, dt);
     CKPT(R, "interior force");
     return SPH_OK;
 }

@@ -416,6 +416,7 @@ void launch_aos84_to_soa(const void* aos, int32_t n, float4* pos, float4* vel, f
 void launch_soa_to_aos84(const float4* pos, const float4* vel, const float4* omg, const float4* rot,
                          const float4* aux, const int32_t* mode, const int32_t* id, int32_t n,
                          void* aos, hipStream_t s);
+void launch_kick(const int32_t* id, float4* vel, int32_t n, int32_t target, const float dv[3], hipStream_t s);
 void launch_pack_sv(const float* pos3, const float* vel3, int32_t n, float4* pos, float4* vel,
                     int32_t* id, hipStream_t s);
 void launch_lattice(int32_t dim, int32_t nx, int32_t ny, int32_t nz, float dx, float x0, float y0,

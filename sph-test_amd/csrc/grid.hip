@@ -258,6 +258,18 @@ void launch_soa_to_aos84(const float4* pos, const float4* vel, const float4* omg
     if (n > 0)
         k_soa_to_aos84<<<nblk(n), BLK, 0, s>>>(pos, vel, omg, rot, aux, mode, id, n, (uint32_t*)aos);
 }
+// Test hook (sph_debug_kick): every slot in [0, n) that holds particle `target` gets dv added to its velocity.
+__global__ void k_kick(const int32_t* __restrict__ id, float4* __restrict__ vel, int32_t n, int32_t target, float dvx,
+                       float dvy, float dvz) {
+    const int32_t i = blockIdx.x * BLK + threadIdx.x;
+    if (i < n && id[i] == target) {
+        const float4 v = vel[i];
+        vel[i] = make_float4(v.x + dvx, v.y + dvy, v.z + dvz, v.w);
+    }
+}
+void launch_kick(const int32_t* id, float4* vel, int32_t n, int32_t target, const float dv[3], hipStream_t s) {
+    if (n > 0) k_kick<<<nblk(n), BLK, 0, s>>>(id, vel, n, target, dv[0], dv[1], dv[2]);
+}
 void launch_pack_sv(const float* pos3, const float* vel3, int32_t n, float4* pos, float4* vel, int32_t* id,
                     hipStream_t s) {
     if (n > 0) k_pack_sv<<<nblk(n), BLK, 0, s>>>(pos3, vel3, n, pos, vel, id);

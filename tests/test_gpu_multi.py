@@ -197,3 +197,78 @@ def test_bench_check_tolerance_on_groups(pkg, ndev):
         assert sim.ctx.decomposition().rebalances > 0
     finally:
         sim.close()
+
+
+def _top_of_column(x, colw, col, up):
+    """The highest particle of global column `col` (a free-surface particle: few neighbours to brake it)."""
+    sel = np.where(np.floor(x[:, 0] / colw).astype(np.int64) == col)[0]
+    assert len(sel) > 0, col
+    return int(sel[np.argmax(x[sel, up])])
+
+
+@pytest.mark.parametrize("resort", ["1", "0"])
+def test_group_column_jump_falls_back_to_full_sends(pkg, monkeypatch, resort):
+    """A particle of rank 0 kicked from column c1 − 3 across two columns in one step, into its last own
+    column or the halo column c1 (rank 0 owns [0, c1)): it must be sent to rank 1, although the steady-
+    state sends scan only the old columns c1 − 2 and c1 − 1. With the incremental re-sort (SPH_RESORT=1)
+    the force pass's column-jump guard flags the move and the next sends scan every own slot; with the
+    full sort (SPH_RESORT=0) the guard cannot run (it reads the previous order's keys) and the sends scan
+    every own slot on every step (abi_multi.cpp steady_sends). Either way the group stays bit-identical
+    to one context. The kick is taken back after the jump, so the run goes on in the steady state."""
+    monkeypatch.setenv("SPH_RESORT", resort)
+    sc = _scenario(pkg)
+    p, dt = pkg.scenario_params(sc)
+    colw = float(np.float32(2.0) * np.float32(p.h))
+    up = int(np.argmax(np.abs(np.array(p.gravity))))
+    single = pkg.SPHSim(sc)
+    group = pkg.SPHSim(sc, ndev=3, rebalance_every=0)
+    try:
+        for s in (single, group):
+            s.step(10)
+        c1 = int(group.ctx.decomposition().cut.cx_hi)
+        x = single.positions()
+        pid = _top_of_column(x, colw, c1 - 3, up)
+        f = float(x[pid, 0]) / colw - (c1 - 3)
+        kick = np.array([(3.0 - f) * colw / float(dt), 0.0, 0.0], np.float32)   # XSPH / viscosity take some back
+        for s in (single, group):
+            s.ctx.debug_kick(pid, kick)
+            s.step(1)
+        x1 = single.positions()
+        col1 = int(np.floor(float(x1[pid, 0]) / colw))
+        print({"resort": resort, "c1": c1, "pid": pid, "f": f, "landed_column": col1,
+               "moved_columns": float(x1[pid, 0] - x[pid, 0]) / colw})
+        assert col1 in (c1 - 1, c1), (col1, c1)             # moved two or three columns, still in the window
+        assert np.array_equal(group.positions(), x1) and np.array_equal(group.velocities(), single.velocities())
+        v1 = single.velocities()[pid]
+        for s in (single, group):
+            s.ctx.debug_kick(pid, -v1)                       # stop it: the run continues in the steady state
+            s.step(6)
+        assert np.array_equal(group.positions(), single.positions())
+        assert np.array_equal(group.velocities(), single.velocities())
+    finally:
+        single.close()
+        group.close()
+
+
+def test_group_window_exit_stops_the_group(pkg, monkeypatch):
+    """A particle of rank 0 kicked from its last own column c1 − 1 past the halo column c1 in one step has
+    left the columns rank 0 holds: no neighbour receives it from the boundary columns, so the force pass
+    raises SZ_JUMP and sph_step fails for the whole group (the flags are read two steps on), naming it."""
+    monkeypatch.setenv("SPH_RESORT", "1")
+    sc = _scenario(pkg)
+    p, dt = pkg.scenario_params(sc)
+    colw = float(np.float32(2.0) * np.float32(p.h))
+    up = int(np.argmax(np.abs(np.array(p.gravity))))
+    group = pkg.SPHSim(sc, ndev=3, rebalance_every=0)
+    try:
+        group.step(10)
+        c1 = int(group.ctx.decomposition().cut.cx_hi)
+        x = group.positions()
+        pid = _top_of_column(x, colw, c1 - 1, up)
+        f = float(x[pid, 0]) / colw - (c1 - 1)
+        group.ctx.debug_kick(pid, np.array([(3.5 - f) * colw / float(dt), 0.0, 0.0], np.float32))
+        with pytest.raises(pkg.SphError) as ei:
+            group.step(4)
+        assert ei.value.status == -3 and "left the held columns" in str(ei.value), str(ei.value)
+    finally:
+        group.close()
