@@ -9,16 +9,22 @@ the state already resident in HBM.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--no-cpu-baseline]
 
-For N > 1 it is launched by torch.distributed.run. Every rank owns an x-slab of the
-global tank and exchanges one-cell halos with its neighbours over RCCL (SPEC_SPH.md §3),
-so per-GPU work is fixed as N grows ("weak" scaling).
+`python bench.py --gpus N` measures N GPUs however it is started: under torch.distributed.run (WORLD_SIZE
+set) it is one rank; started plainly with N > 1 it launches the N rank processes itself (launch_ranks:
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT, before any GPU call in the parent),
+relays rank 0's JSON line and exits with the worst rank status. A world size other than --gpus is a failure
+line and exit status 2. Every rank owns an x-slab of the global tank and exchanges one-cell halos with its
+neighbours over RCCL (SPEC_SPH.md §3), so per-GPU work is fixed as N grows ("weak" scaling).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -77,6 +83,9 @@ def parse():
     ap.add_argument("--watchdog", type=float, default=900.0,
                     help="seconds after which a rank stuck in a phase (a peer failed inside a collective) "
                          "prints the failure and exits 3")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="N > 1: only form the process group (SPH_DIST_BACKEND) and print which ranks joined "
+                         "(tests the launcher without a GPU)")
     ap.add_argument("--table", action="store_true",
                     help="print the GPU / 1-thread / all-thread CPU rate table (SURVEY §8d) instead of the bench line")
     return ap.parse_args()
@@ -282,8 +291,83 @@ def per_step_ms(kstats: dict, steps: int) -> dict:
             for k, v in kstats.items() if v.get("timed", 0) > 0 and v["total_ms"] > 0}
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv, script=None, grace_s: float = 60.0) -> int:
+    """Start n rank processes of this script (RANK = LOCAL_RANK = r, WORLD_SIZE = n, MASTER_ADDR 127.0.0.1,
+    MASTER_PORT from the environment or a free port), as torch.distributed.run would on one node. The parent
+    makes no GPU call: it only relays rank 0's stdout and waits. When a rank fails, the others get grace_s to
+    finish (their own watchdogs end a collective a failed peer never joins), then are terminated. Returns the
+    worst exit status (a signal counts as 128 + signal); if rank 0 printed no JSON line with "metric", a
+    failure line is printed for it."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, "-u", str(script or Path(__file__).resolve()), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else None, text=True))
+    printed = []
+
+    def relay():
+        for line in procs[0].stdout:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+            try:
+                if "metric" in json.loads(line):
+                    printed.append(True)
+            except ValueError:
+                pass
+    t = threading.Thread(target=relay, daemon=True)
+    t.start()
+    first_fail = None
+    while any(p.poll() is None for p in procs):
+        codes = [p.poll() for p in procs]
+        if first_fail is None and any(c not in (None, 0) for c in codes):
+            first_fail = time.monotonic()
+        if first_fail is not None and time.monotonic() - first_fail > grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=10)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    t.join(timeout=10)
+    codes = [p.returncode for p in procs]
+    worst = max((c if c >= 0 else 128 - c) for c in codes)
+    if not printed:
+        bad = [(r, c) for r, c in enumerate(codes) if c != 0]
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "particle-steps/s", "n_gpus": n,
+                          "launch_failed": f"rank 0 printed no result line; exit status per rank {codes}",
+                          "failed_ranks": bad}), flush=True)
+        worst = worst or 1
+    return worst
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1 and not args.table:
+        # started plainly: this process becomes the launcher of the N ranks (no GPU call here)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "particle-steps/s", "n_gpus": args.gpus,
+                              "world_size_mismatch": f"--gpus {args.gpus} but WORLD_SIZE {world}"}), flush=True)
+        sys.exit(2)
     every = args.profile_every if args.profile_every > 0 else (16 if args.steps >= 160 else 4)
     prof = 0 if args.no_profile else max(1, every)
     import torch
@@ -293,11 +377,13 @@ def main():
         return
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # RCCL over xGMI between GPUs; SPH_DIST_BACKEND=gloo rehearses N ranks on one GPU
     backend = os.environ.get("SPH_DIST_BACKEND", "nccl")
+    if args.launch_check:
+        launch_check(world, rank, local, backend, dist)
+        return
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         local = local % max(1, torch.cuda.device_count())
@@ -585,6 +671,28 @@ class Watchdog:
         if self.t is not None:
             self.t.cancel()
             self.t = None
+
+
+def launch_check(world, rank, local, backend, dist):
+    """--launch-check: form the process group and report the ranks that joined (no GPU with gloo)."""
+    import torch
+    if world > 1:
+        if backend == "nccl":
+            torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local % max(1, torch.cuda.device_count())))
+        else:
+            dist.init_process_group(backend)
+        got = [None] * world
+        dist.all_gather_object(got, {"rank": rank, "local_rank": local, "pid": os.getpid()})
+        size = dist.get_world_size()
+    else:
+        got, size = [{"rank": 0, "local_rank": 0, "pid": os.getpid()}], 1
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "particle-steps/s", "n_gpus": size,
+                          "launch_check": {"backend": backend if world > 1 else None, "ranks": got}}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def agree(ok: bool, dist, dev_kind) -> bool:

@@ -120,3 +120,50 @@ def test_step_bytes_follow_survey_8d():
     assert bench.step_bytes_per_particle(22, 0, 1) == 152 + 20 * 3
     assert abs(bench.step_bytes_per_particle(22, 3663680, 1048576) - (212 + 8 * 3663680 / 1048576)) < 1e-9
     assert bench.FORCE_BYTES_PER_PARTICLE == 56.0
+
+
+def _bench_env(**extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(extra)
+    return env
+
+
+def test_plain_start_launches_the_ranks():
+    """`python bench.py --gpus 2` without torch.distributed.run starts the two ranks itself: they form one
+    process group (gloo here; no GPU call in the launcher) and rank 0's line says n_gpus 2."""
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--launch-check"],
+                       env=_bench_env(SPH_DIST_BACKEND="gloo"), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["launch_check"]["backend"] == "gloo"
+    assert sorted(x["rank"] for x in line["launch_check"]["ranks"]) == [0, 1]
+    assert sorted(x["local_rank"] for x in line["launch_check"]["ranks"]) == [0, 1]
+    assert len({x["pid"] for x in line["launch_check"]["ranks"]}) == 2
+
+
+def test_world_size_mismatch_fails():
+    """Launched as one rank of a 2-rank job while asked for 3 GPUs: a failure line and exit status 2,
+    before any process group or GPU call."""
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "3"],
+                       env=_bench_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"), capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 2
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["value"] is None and line["n_gpus"] == 3 and "WORLD_SIZE 2" in line["world_size_mismatch"]
+
+
+def test_launcher_reports_a_failed_rank(tmp_path):
+    """A rank that fails before rank 0 prints: the launcher exits with the worst status and prints a
+    failure line naming the ranks' statuses."""
+    script = tmp_path / "child.py"
+    script.write_text("import os, sys\nr = int(os.environ['RANK'])\n"
+                      "assert os.environ['WORLD_SIZE'] == '2' and os.environ['MASTER_ADDR'] == '127.0.0.1'\n"
+                      "sys.exit(5 if r == 1 else 0)\n")
+    code = ("import sys; sys.path.insert(0, %r); import bench; "
+            "sys.exit(bench.launch_ranks(2, [], script=%r, grace_s=5))") % (str(ROOT), str(script))
+    r = subprocess.run([sys.executable, "-c", code], env=_bench_env(), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 5, (r.stdout, r.stderr)
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["value"] is None and line["n_gpus"] == 2 and [1, 5] in line["failed_ranks"]
