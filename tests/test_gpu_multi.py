@@ -272,3 +272,35 @@ def test_group_window_exit_stops_the_group(pkg, monkeypatch):
         assert ei.value.status == -3 and "left the held columns" in str(ei.value), str(ei.value)
     finally:
         group.close()
+
+
+@pytest.mark.parametrize("cfg,ndev,steps", [("C4", 4, 120), ("C5", 8, 100)])
+def test_baseline_config_decomposed_full_size(pkg, oracle, cfg, ndev, steps):
+    """BASELINE's own multi-GPU configurations decomposed as they run on 4 / 8 GPUs, at full size, as a local
+    group on the test box's one device: C4 (4,194,304 particles, sloshing) in 4 slabs, C5 (16,777,216) in 8,
+    re-balanced every 20 steps. Every step's halo must reproduce the 27-cell neighbourhood at every cut
+    (SimulateParticles.compute:228-233), so the group is bit-identical to one context; then one step from the
+    decomposed state meets the oracle tolerances of test_gpu_parity_headline.compare_one_step."""
+    from test_gpu_parity_headline import compare_one_step
+    sc = pkg.config_scenario(cfg)
+    group = pkg.SPHSim(sc, ndev=ndev, rebalance_every=20)
+    try:
+        group.step(steps)
+        xg, vg = group.positions(), group.velocities()
+        d = group.ctx.decomposition()
+        assert d.world == ndev and d.owned == group.n == len(xg)
+        rebalances = d.rebalances
+    finally:
+        group.close()
+    single = pkg.SPHSim(sc)
+    try:
+        single.step(steps)
+        xs, vs = single.positions(), single.velocities()
+        same = bool(np.array_equal(xg, xs) and np.array_equal(vg, vs))
+        print({"cfg": cfg, "ndev": ndev, "steps": steps, "rebalances": rebalances, "bitwise": same,
+               "max_dx": float(np.abs(xg - xs).max())})
+        assert same
+        t = float(np.float32(single.ctx.stats().sim_time))
+        compare_one_step(pkg, oracle, single, xg, vg, f"{cfg} decomposed x{ndev}", t=t)
+    finally:
+        single.close()
