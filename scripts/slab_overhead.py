@@ -1,27 +1,60 @@
-"""The decomposition's cost on one GPU: C3 x N (bench.py's weak scenario) as one context against a local group of N
-slab contexts on the same device (sph_config.ndev = N; the halo copies are then device-local). Both do the same
-particle work; the difference is what the slab step adds (counts, packing, the halo records' re-sort, ρ halo,
-boundary force passes, bookkeeping) and the serialisation of N slabs' launches on one GPU."""
+"""The decomposition's cost per GPU, measured on one GPU.
+
+For each N: C3 x N (bench.py's weak scenario: every slab holds ~1,048,576 particles, as on N GPUs) as a local
+group of N slab contexts on the one device (sph_config.ndev = N), against C3 on one context.
+
+  * `group`:  the slabs' streams run concurrently on the device (what r03 measured: a bound, not the cost);
+  * `serial`: SPH_DEBUG_SERIAL_GROUP=1, every slab launches on slab 0's stream, so the group's step time is
+    the SUM of the N per-slab step costs; serial / N is what one GPU of an N-GPU run spends per step, minus
+    the halo copies' transport (device-local here, xGMI / RCCL there) and plus nothing else;
+  * `overhead_per_slab_ms` = serial / N − C3 single: the per-GPU cost the decomposition adds.
+
+    python scripts/slab_overhead.py [N list, default 2,4,8] [steps, default 100] [--no-concurrent]
+"""
+import os
 import sys
 import time
 from pathlib import Path
+
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
-import __graft_entry__ as GE
+import __graft_entry__ as GE  # noqa: E402
+
 pkg = GE.load_package()
-from sph_test_amd import slab
-steps = int(sys.argv[2]) if len(sys.argv) > 2 else 100
-for world in [int(w) for w in (sys.argv[1] if len(sys.argv) > 1 else "2").split(",")]:
+from sph_test_amd import slab  # noqa: E402
+
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+worlds = [int(w) for w in (args[0] if args else "2,4,8").split(",")]
+steps = int(args[1]) if len(args) > 1 else 100
+concurrent = "--no-concurrent" not in sys.argv
+
+
+def timed(sc, **kw):
+    sim = pkg.SPHSim(sc, **kw)
+    sim.step(20)
+    sim.ctx.synchronize()
+    t0 = time.perf_counter()
+    sim.step(steps)
+    host = time.perf_counter() - t0          # the host's enqueue time, until a full queue blocks it
+    sim.ctx.synchronize()
+    wall = time.perf_counter() - t0
+    sim.close()
+    return round(wall * 1e3 / steps, 4), round(host * 1e3 / steps, 4)
+
+
+c3, _ = timed(slab.weak_scenario("C3", 1))
+print({"C3_single_ms": c3}, flush=True)
+for world in worlds:
     sc = slab.weak_scenario("C3", world)
-    res = {"world": world, "particles": sc.nx * sc.ny * sc.nz}
-    for label, kw in (("single", {}), ("group", {"ndev": world, "rebalance_every": 50})):
-        sim = pkg.SPHSim(sc, **kw)
-        sim.step(20)
-        sim.ctx.synchronize()
-        t0 = time.perf_counter()
-        sim.step(steps)
-        sim.ctx.synchronize()
-        res[label + "_ms"] = round((time.perf_counter() - t0) * 1e3 / steps, 4)
-        sim.close()
-    res["overhead_ms"] = round(res["group_ms"] - res["single_ms"], 4)
-    res["overhead_per_slab_ms"] = round(res["overhead_ms"] / world, 4)
+    res = {"world": world, "particles": sc.nx * sc.ny * sc.nz, "C3_single_ms": c3}
+    res["single_ms"], _ = timed(sc)
+    if concurrent:
+        res["group_ms"], _ = timed(sc, ndev=world, rebalance_every=50)
+    os.environ["SPH_DEBUG_SERIAL_GROUP"] = "1"
+    try:
+        res["serial_ms"], res["serial_host_ms"] = timed(sc, ndev=world, rebalance_every=50)
+    finally:
+        del os.environ["SPH_DEBUG_SERIAL_GROUP"]
+    res["serial_per_slab_ms"] = round(res["serial_ms"] / world, 4)
+    res["overhead_per_slab_ms"] = round(res["serial_ms"] / world - c3, 4)
+    res["overhead_frac_of_C3_step"] = round(res["overhead_per_slab_ms"] / c3, 4)
     print(res, flush=True)

@@ -903,7 +903,8 @@ void multi_free(sph_ctx* ctx) {
     for (auto& R : M->ranks) rank_free(R);
     if (M->hist_dev) (void)hipFree(M->hist_dev);
     if (M->comm) (void)ncclCommDestroy(M->comm);
-    for (sph_ctx* k : M->kids) sph_destroy(k);
+    // in reverse: under SPH_DEBUG_SERIAL_GROUP the later slabs borrow slab 0's stream
+    for (auto k = M->kids.rbegin(); k != M->kids.rend(); ++k) sph_destroy(*k);
     delete M;
     ctx->mg = nullptr;
 }
@@ -943,7 +944,7 @@ int multi_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
     for (auto& R : M.ranks) rank_free(R);
     M.ranks.clear();
     {
-        for (sph_ctx* k : M.kids) sph_destroy(k);
+        for (auto k = M.kids.rbegin(); k != M.kids.rend(); ++k) sph_destroy(*k);
         M.kids.clear();
         int nvis = 0;
         HIPCHK(hipGetDeviceCount(&nvis));
@@ -957,6 +958,18 @@ int multi_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
             int rc = sph_create(&kc, (ctx->device + r) % nvis, &k);
             if (rc != SPH_OK) return fail(ctx, rc, "slab context %d on device %d", r, (ctx->device + r) % nvis);
             M.kids.push_back(k);
+        }
+        // measurement knob (scripts/slab_overhead.py --serial): every slab of a one-device group launches on
+        // slab 0's stream, so the slabs run one after another and the group's step time is the sum of the
+        // per-slab step costs instead of an overlapped bound
+        const char* ser = std::getenv("SPH_DEBUG_SERIAL_GROUP");
+        if (ser && std::atoi(ser) != 0) {
+            for (int r = 1; r < M.world; ++r) {
+                if (M.kids[r]->device != M.kids[0]->device)
+                    return fail(ctx, SPH_ERR_INVALID, "SPH_DEBUG_SERIAL_GROUP needs every slab on one device");
+                const int rc = sph_set_stream(M.kids[r], M.kids[0]->stream);
+                if (rc != SPH_OK) return fail(ctx, rc, "serial group: slab %d stream", r);
+            }
         }
         for (int r = 0; r + 1 < M.world; ++r) {   // halo neighbours r, r + 1
             const int rc = enable_peers(ctx, M.kids[r]->device, M.kids[r + 1]->device);
