@@ -513,8 +513,6 @@ int exchange1(Multi& M) {
     return SPH_OK;
 }
 
-constexpr int RHO_HDR = 4;   // slab.hip: 32-byte header of a ρ message, in float2
-
 int exchange2_start(Multi& M) {
     if (M.mode == 1) {
         const int r0 = M.ranks[0].rank;
@@ -633,13 +631,6 @@ int phase_assemble(RankState& R, bool exact) {
         HIPCHK(hipStreamSynchronize(s));   // nn lives on this stack frame
         R.n_ub = ctx->n;
     }
-    {   // the owned slots of the new order: the column starts the re-sort picked (k_slab_lag copies the
-        // ranges for the host at the end of the step)
-        KTimer t(ctx, "density", 24.0 * (double)R.n_ub, true);
-        launch_density_tiled(ctx->pos, ctx->cs, 0, (int32_t)R.n_ub, ctx->grid, ctx->sc, ctx->rp, hit_mask_write(ctx), path_ctr(ctx), s,
-                             DevRange{&R.dz->pick[1], &R.dz->pick[4]});
-    }
-    CKPT(R, "density");
     if (exact && (R.left >= 0 || R.right >= 0)) {   // exact ρ message sizes: this rank's own columns
         HIPCHK(hipStreamSynchronize(s));
         SlabSizes h;
@@ -652,23 +643,34 @@ int phase_assemble(RankState& R, bool exact) {
     return SPH_OK;
 }
 
-int phase_rho_out(RankState& R, Multi& M) {
+// The density pass over the owned slots of the new order (the column starts the re-sort picked; k_slab_lag
+// copies the ranges for the host at the end of the step). It also writes both ρ halo messages: the own
+// boundary columns' (ρ, P/ρ²) in slot order (RhoOut), so no packing launch follows it.
+int phase_density(RankState& R, Multi& M) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
-    for (int s = 0; s < 2; ++s) {
-        const int peer = s == 0 ? R.left : R.right;
+    RhoOut ro;
+    for (int sd = 0; sd < 2; ++sd) {
+        const int peer = sd == 0 ? R.left : R.right;
         if (peer < 0) continue;
-        int r = ensure_buf(M, ctx, &R.rho_out[s], &R.rcap_out[s], RHO_HDR + R.c2o[s]);
+        int r = ensure_buf(M, ctx, &R.rho_out[sd], &R.rcap_out[sd], RHO_HDR + R.c2o[sd]);
         if (r != SPH_OK) return r;
-        r = ensure_buf(M, ctx, &R.rho_in[s], &R.rcap_in[s], RHO_HDR + R.c2i[s]);
+        r = ensure_buf(M, ctx, &R.rho_in[sd], &R.rcap_in[sd], RHO_HDR + R.c2i[sd]);
         if (r != SPH_OK) return r;
+        // the neighbour's copy of last step's message must be done before the density pass overwrites it
         if (M.mode == 1) HIPCHK(hipStreamWaitEvent(ctx->stream, M.ranks[peer - M.ranks[0].rank].ev_rho_recv, 0));
+        ro.msg[sd] = R.rho_out[sd];
+        ro.cap[sd] = R.c2o[sd];
     }
-    launch_slab_pack_rho2(ctx->rp, R.dz, R.left >= 0 ? R.rho_out[0] : nullptr, R.c2o[0],
-                          R.right >= 0 ? R.rho_out[1] : nullptr, R.c2o[1], ctx->stream);
+    if (ro.msg[0] || ro.msg[1]) ro.dz = R.dz;
+    {
+        KTimer t(ctx, "density", 24.0 * (double)R.n_ub, true);
+        launch_density_tiled(ctx->pos, ctx->cs, 0, (int32_t)R.n_ub, ctx->grid, ctx->sc, ctx->rp, hit_mask_write(ctx),
+                             path_ctr(ctx), ctx->stream, DevRange{&R.dz->pick[1], &R.dz->pick[4]}, ro);
+    }
     HIPCHK(hipGetLastError());
     if (R.left >= 0 || R.right >= 0) HIPCHK(hipEventRecord(R.ev_rho_packed, ctx->stream));
-    CKPT(R, "rho pack");
+    CKPT(R, "density + rho pack");
     return SPH_OK;
 }
 
@@ -876,7 +878,7 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
         if ((r = phase_assemble(R, exact)) != SPH_OK) return r;
     if ((pctx->cfg.flags & SPH_FLAG_VALIDATE) && (r = validate_mid(M, pctx)) != SPH_OK) return r;
     for (auto& R : M.ranks)
-        if ((r = phase_rho_out(R, M)) != SPH_OK) return r;
+        if ((r = phase_density(R, M)) != SPH_OK) return r;
     if (M.world > 1 && (r = exchange2_start(M)) != SPH_OK) return r;
     for (auto& R : M.ranks)
         if ((r = phase_interior(R, dt)) != SPH_OK) return r;

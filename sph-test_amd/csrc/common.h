@@ -220,6 +220,15 @@ constexpr uint32_t SZ_OVF_MOVERS = 8u;    // a mover list or a re-sort destinati
 constexpr uint32_t SZ_JUMP = 16u;         // an own particle left the held window in one step (two columns or more)
 // Halo messages: one 32-byte header record, then the records. Header: (count, capacity, 0, 0 | 0...)
 constexpr int MSG_HDR_F4 = 2;
+// ρ halo messages: a 32-byte header (count, capacity) = 4 float2, then (ρ, P/ρ²) of the boundary column's slots
+constexpr int RHO_HDR = 4;
+// The slab step's ρ messages, written by the density pass itself (k_density_tiled): side s carries the own
+// boundary column [pick[1 + 2s], pick[2 + 2s]) in slot order. msg[s] null: no neighbour on that side.
+struct RhoOut {
+    float2* msg[2] = {nullptr, nullptr};
+    int32_t cap[2] = {0, 0};
+    const SlabSizes* dz = nullptr;
+};
 // What the assembled layout is computed from: the two message headers (null: no neighbour), the
 // capacities they were sent with, and the context's slot capacity.
 struct SizesIn {
@@ -438,7 +447,8 @@ struct HitMask {
     uint32_t stride = 0;
 };
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g,
-                          SphConst c, float2* rp, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr = DevRange{});
+                          SphConst c, float2* rp, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr = DevRange{},
+                          RhoOut ro = RhoOut{});
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs,
                         int32_t ib, int32_t ie, GridDesc g, SphConst c, float dt, float fext_x,
                         float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths,

@@ -416,9 +416,8 @@ void launch_slab_sizes(SlabSizes* dz, const float4* msg_l, const float4* msg_r, 
     SPH_LAUNCH(k_slab_sizes, 1, 64, 0, s, dz, SizesIn{msg_l, msg_r, cap_l, cap_r, capacity});
 }
 
-// ρ messages: a 32-byte header (count, capacity) = 4 float2, then the entries
-constexpr int RHO_HDR = 4;
-
+// ρ messages (common.h RHO_HDR): the per-phase ABI packs them here; the in-library step's density pass
+// writes them itself (RhoOut)
 // both sides in one launch (blockIdx.y = side; a side without a message has no workgroups' work)
 __global__ __launch_bounds__(SL_BLK) void k_slab_pack_rho2(const float2* __restrict__ rp, const SlabSizes* __restrict__ dz,
                                                            float2* __restrict__ msg_l, int32_t cap_l,

@@ -306,10 +306,17 @@ __device__ __forceinline__ int32_t quadrant_target(const GridDesc& g, const floa
 template <int XS>
 __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAVES))) void k_density_tiled(
     const float4* __restrict__ pos, const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c,
-    float2* __restrict__ rp, DevRange dr, HitMask hm, uint32_t* __restrict__ paths) {
+    float2* __restrict__ rp, DevRange dr, HitMask hm, uint32_t* __restrict__ paths, RhoOut ro) {
     __shared__ float4 sp[TT_GCAP + 4];
     __shared__ int32_t perm[TT_BLK];
     __shared__ uint32_t qcnt[TT_BLK / 64][5];
+    if (ro.dz && blockIdx.x == 0 && threadIdx.x < 2 && ro.msg[threadIdx.x]) {   // ρ message headers (slab step)
+        const int sd = (int)threadIdx.x;
+        const uint32_t cnt = ro.dz->pick[2 + 2 * sd] - ro.dz->pick[1 + 2 * sd];
+        float2* m = ro.msg[sd];
+        m[0] = make_float2(__uint_as_float(cnt), __uint_as_float((uint32_t)ro.cap[sd]));
+        m[1] = m[2] = m[3] = make_float2(0.f, 0.f);
+    }
     if (dr.lo) {   // device-resident bounds (slab mode); the grid is an upper bound
         ib = (int32_t)*dr.lo;
         n = (int32_t)*dr.hi;
@@ -477,7 +484,16 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
     const float tr = d * c.inv_rho0;
     const float t2 = tr * tr, t4 = t2 * t2;
     const float P = c.B * (t4 * t2 * tr - 1.0f);
-    rp[i] = make_float2(d, P / (d * d));
+    const float2 out = make_float2(d, P / (d * d));
+    rp[i] = out;
+    if (ro.dz) {   // slab step: a target of an own boundary column is also an entry of that side's ρ message
+#pragma unroll
+        for (int sd = 0; sd < 2; ++sd) {
+            const uint32_t b = ro.dz->pick[1 + 2 * sd], e = ro.dz->pick[2 + 2 * sd];
+            const uint32_t t = (uint32_t)i - b;
+            if (ro.msg[sd] && (uint32_t)i >= b && (uint32_t)i < e && t < (uint32_t)ro.cap[sd]) ro.msg[sd][RHO_HDR + t] = out;
+        }
+    }
 }
 
 struct ForceAcc {
@@ -769,13 +785,16 @@ __global__ __launch_bounds__(TF_BLK) __attribute__((amdgpu_waves_per_eu(4))) voi
 }
 
 // dr set: [ib, ie) only sizes the grid (an upper bound); the kernels read their bounds from dr
+// ro.dz set: the launch also writes the slab step's ρ messages (headers by block 0, even when the grid has no
+// targets: then ie <= ib must not skip it)
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
-                          float2* rp, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr) {
-    if (ie <= ib) return;
+                          float2* rp, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr, RhoOut ro) {
+    if (ie <= ib && !ro.dz) return;
+    const int32_t nb = ie > ib ? (ie - ib + TT_BLK - 1) / TT_BLK : 1;
     if (g.xsub == 2)
-        SPH_LAUNCH(k_density_tiled<2>, (ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s, pos, cs, ib, ie, g, c, rp, dr, hm, paths);
+        SPH_LAUNCH(k_density_tiled<2>, nb, TT_BLK, 0, s, pos, cs, ib, ie, g, c, rp, dr, hm, paths, ro);
     else
-        SPH_LAUNCH(k_density_tiled<1>, (ie - ib + TT_BLK - 1) / TT_BLK, TT_BLK, 0, s, pos, cs, ib, ie, g, c, rp, dr, hm, paths);
+        SPH_LAUNCH(k_density_tiled<1>, nb, TT_BLK, 0, s, pos, cs, ib, ie, g, c, rp, dr, hm, paths, ro);
 }
 
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,
