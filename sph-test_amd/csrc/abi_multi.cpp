@@ -675,15 +675,18 @@ int phase_density(RankState& R, Multi& M) {
 }
 
 // ---------------------------------------------------------------- phase C: force passes, finish
-// Returns whether the pass ran the column-jump guard (steady_sends).
-bool force_dev(sph_ctx* ctx, const uint32_t* lo, const uint32_t* hi, int64_t grid_ub, float dt) {
+// Returns whether the pass ran the column-jump guard (steady_sends). A second range [lo2, hi2) (at most
+// grid_ub2 slots) runs in the same launch: the two boundary columns are one launch.
+bool force_dev(sph_ctx* ctx, const uint32_t* lo, const uint32_t* hi, int64_t grid_ub, float dt,
+               const uint32_t* lo2 = nullptr, const uint32_t* hi2 = nullptr, int64_t grid_ub2 = 0) {
     MoverSink mv = mover_sink(ctx);
-    if (grid_ub <= 0) return mv.sk != nullptr;
-    KTimer t(ctx, "force_integrate", 76.0 * (double)grid_ub, true);
+    if (grid_ub <= 0 && grid_ub2 <= 0) return mv.sk != nullptr;
+    KTimer t(ctx, "force_integrate", 76.0 * (double)(std::max<int64_t>(grid_ub, 0) + grid_ub2), true);
     mv.err = &ctx->dz->flags;
     mv.jump = &ctx->dz->jump;
-    launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, (int32_t)grid_ub, ctx->grid, ctx->sc, dt, forcing(ctx),
-                       ctx->pos2, ctx->vel2, ctx->keys, mv, hit_mask_read(ctx), path_ctr(ctx), ctx->stream, DevRange{lo, hi});
+    launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, (int32_t)std::max<int64_t>(grid_ub, 0), ctx->grid, ctx->sc,
+                       dt, forcing(ctx), ctx->pos2, ctx->vel2, ctx->keys, mv, hit_mask_read(ctx), path_ctr(ctx), ctx->stream,
+                       DevRange{lo, hi}, DevRange{lo2, hi2}, (int32_t)grid_ub2);
     return mv.sk != nullptr;
 }
 
@@ -711,6 +714,9 @@ int phase_finish(RankState& R, float dt, int64_t step, bool global_flags) {
     const uint32_t* pk = R.dz->pick;
     if (one_col && (ctx->has_left || ctx->has_right)) {   // the owned column is both boundary columns
         force_dev(ctx, &pk[1], &pk[4], R.n_ub, dt);
+    } else if (ctx->has_left && ctx->has_right) {   // both boundary columns in one launch
+        force_dev(ctx, &pk[1], &pk[2], std::min<int64_t>(R.c2o[0], R.n_ub), dt, &pk[3], &pk[4],
+                  std::min<int64_t>(R.c2o[1], R.n_ub));
     } else {
         if (ctx->has_left) force_dev(ctx, &pk[1], &pk[2], std::min<int64_t>(R.c2o[0], R.n_ub), dt);
         if (ctx->has_right) force_dev(ctx, &pk[3], &pk[4], std::min<int64_t>(R.c2o[1], R.n_ub), dt);

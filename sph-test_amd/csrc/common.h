@@ -452,7 +452,7 @@ void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs,
                         int32_t ib, int32_t ie, GridDesc g, SphConst c, float dt, float fext_x,
                         float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths,
-                        hipStream_t s, DevRange dr = DevRange{});
+                        hipStream_t s, DevRange dr = DevRange{}, DevRange dr2 = DevRange{}, int32_t ie2 = 0);
 
 // slab decomposition (slab.hip)
 // Order-preserving compaction of the sorted slots [b, e) whose key column satisfies

@@ -560,15 +560,20 @@ __global__ __launch_bounds__(TF_BLK) __attribute__((amdgpu_waves_per_eu(4))) voi
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
     const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, PairK pk, float dt,
     float fext_x, float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o, MoverSink mv,
-    HitMask hm, uint32_t* __restrict__ paths, DevRange dr) {
+    HitMask hm, uint32_t* __restrict__ paths, DevRange dr, DevRange dr2, int32_t nb_a) {
     __shared__ float4 sp[TF_GCAP + 4];     // (x, y, z, ρ)
     __shared__ float4 sv[TF_GCAP + 4];     // (u, v, w, P/ρ²)
     const int tid = threadIdx.x;
+    int32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    if (dr2.lo && blk >= nb_a) {   // a second range in the same launch (the slab step's two boundary columns)
+        blk -= nb_a;
+        dr = dr2;
+    }
     if (dr.lo) {   // device-resident bounds (slab step); the grid is an upper bound
         ib = (int32_t)*dr.lo;
         n = (int32_t)*dr.hi;
     }
-    const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TF_BLK;
+    const int32_t i0 = ib + blk * TF_BLK;
     if (i0 >= n) return;   // whole workgroup: before any barrier
     SPH_BT_START;
     // Targets stay in sorted order here. Lanes ordered by quarters of fx (a dx plane's hit count follows
@@ -797,16 +802,21 @@ void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int
         SPH_LAUNCH(k_density_tiled<1>, nb, TT_BLK, 0, s, pos, cs, ib, ie, g, c, rp, dr, hm, paths, ro);
 }
 
+// dr2 set: a second device-resident range in the same launch, ie2 slots at most (its workgroups follow
+// the first range's (ie - ib) / TF_BLK)
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,
                         int32_t ie, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o,
-                        uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr) {
-    if (ie <= ib) return;
+                        uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr,
+                        DevRange dr2, int32_t ie2) {
+    const int32_t nb_a = ie > ib ? (ie - ib + TF_BLK - 1) / TF_BLK : 0;
+    const int32_t nb_b = dr2.lo && ie2 > 0 ? (ie2 + TF_BLK - 1) / TF_BLK : 0;
+    if (nb_a + nb_b == 0) return;
     if (g.xsub == 2)
-        SPH_LAUNCH(k_force_tiled<2>, (ie - ib + TF_BLK - 1) / TF_BLK, TF_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c,
-                   pair_constants(c), dt, fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr);
+        SPH_LAUNCH(k_force_tiled<2>, nb_a + nb_b, TF_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt,
+                   fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr, nb_b ? dr2 : DevRange{}, nb_a);
     else
-        SPH_LAUNCH(k_force_tiled<1>, (ie - ib + TF_BLK - 1) / TF_BLK, TF_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c,
-                   pair_constants(c), dt, fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr);
+        SPH_LAUNCH(k_force_tiled<1>, nb_a + nb_b, TF_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt,
+                   fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr, nb_b ? dr2 : DevRange{}, nb_a);
 }
 
 #ifdef SPH_BTIME
