@@ -58,7 +58,7 @@ LAYOUTS = {
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--blocks", type=int, default=300)
-    ap.add_argument("--lane-order", choices=("quadrant", "sorted"), default="quadrant")
+    ap.add_argument("--lane-order", choices=("quadrant", "sorted", "halfx", "halfy"), default="quadrant")
     args = ap.parse_args()
     O = GE.load_oracle()
     pkg = GE.load_package()
@@ -94,6 +94,9 @@ def main():
         if args.lane_order == "quadrant":
             q = (fx >= 0.5).astype(int) + 2 * (fy >= 0.5).astype(int)
             lanes = np.argsort(q, kind="stable")     # lane -> target (within the block)
+        elif args.lane_order in ("halfx", "halfy"):
+            q = ((fx if args.lane_order == "halfx" else fy) >= 0.5).astype(int)
+            lanes = np.argsort(q, kind="stable")
         else:
             lanes = np.arange(len(idx))
         kf, kl = keys[i0], keys[idx[-1]]

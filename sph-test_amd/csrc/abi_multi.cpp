@@ -38,6 +38,7 @@ struct RankState {
     hipStream_t comm = nullptr;                       // exchange 2 (overlaps the interior force pass)
     hipEvent_t ev_packed = nullptr, ev_in = nullptr;  // exchange 1: messages packed / received
     hipEvent_t ev_rho_packed = nullptr, ev_rho_recv = nullptr;
+    hipEvent_t ev_bdone = nullptr;   // the boundary force pass (comm stream) is done: the step's end waits on it
     SlabSizes* dz = nullptr;
     float4* msg_out[2] = {nullptr, nullptr};
     float4* msg_in[2] = {nullptr, nullptr};
@@ -211,7 +212,7 @@ int rank_init(RankState& R) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipStreamCreateWithFlags(&R.comm, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&R.ev_packed, &R.ev_in, &R.ev_rho_packed, &R.ev_rho_recv})
+    for (hipEvent_t* e : {&R.ev_packed, &R.ev_in, &R.ev_rho_packed, &R.ev_rho_recv, &R.ev_bdone})
         HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     for (auto& e : R.lag_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipMalloc((void**)&R.dz, sizeof(SlabSizes)));
@@ -229,7 +230,7 @@ void rank_free(RankState& R) {
     if (!R.c) return;
     (void)hipSetDevice(R.c->device);
     if (R.comm) (void)hipStreamSynchronize(R.comm);
-    for (hipEvent_t e : {R.ev_packed, R.ev_in, R.ev_rho_packed, R.ev_rho_recv})
+    for (hipEvent_t e : {R.ev_packed, R.ev_in, R.ev_rho_packed, R.ev_rho_recv, R.ev_bdone})
         if (e) (void)hipEventDestroy(e);
     for (auto e : R.lag_ev)
         if (e) (void)hipEventDestroy(e);
@@ -523,6 +524,8 @@ int exchange2_start(Multi& M) {
                 const int peer = s == 0 ? R.left : R.right;
                 if (peer < 0) continue;
                 RankState& S = M.ranks[peer - r0];
+                if (s == 0 || R.left < 0)   // once: the boundary force pass on this stream reads this rank's density
+                    HIPCHK(hipStreamWaitEvent(R.comm, R.ev_rho_packed, 0));
                 HIPCHK(hipStreamWaitEvent(R.comm, S.ev_rho_packed, 0));
                 HIPCHK(hipMemcpyPeerAsync(R.rho_in[s], ctx->device, S.rho_out[1 - s], S.c->device,
                                           (size_t)(RHO_HDR + R.c2i[s]) * sizeof(float2), R.comm));
@@ -678,15 +681,16 @@ int phase_density(RankState& R, Multi& M) {
 // Returns whether the pass ran the column-jump guard (steady_sends). A second range [lo2, hi2) (at most
 // grid_ub2 slots) runs in the same launch: the two boundary columns are one launch.
 bool force_dev(sph_ctx* ctx, const uint32_t* lo, const uint32_t* hi, int64_t grid_ub, float dt,
-               const uint32_t* lo2 = nullptr, const uint32_t* hi2 = nullptr, int64_t grid_ub2 = 0) {
+               const uint32_t* lo2 = nullptr, const uint32_t* hi2 = nullptr, int64_t grid_ub2 = 0,
+               hipStream_t st = nullptr) {
     MoverSink mv = mover_sink(ctx);
     if (grid_ub <= 0 && grid_ub2 <= 0) return mv.sk != nullptr;
     KTimer t(ctx, "force_integrate", 76.0 * (double)(std::max<int64_t>(grid_ub, 0) + grid_ub2), true);
     mv.err = &ctx->dz->flags;
     mv.jump = &ctx->dz->jump;
     launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, (int32_t)std::max<int64_t>(grid_ub, 0), ctx->grid, ctx->sc,
-                       dt, forcing(ctx), ctx->pos2, ctx->vel2, ctx->keys, mv, hit_mask_read(ctx), path_ctr(ctx), ctx->stream,
-                       DevRange{lo, hi}, DevRange{lo2, hi2}, (int32_t)grid_ub2);
+                       dt, forcing(ctx), ctx->pos2, ctx->vel2, ctx->keys, mv, hit_mask_read(ctx), path_ctr(ctx),
+                       st ? st : ctx->stream, DevRange{lo, hi}, DevRange{lo2, hi2}, (int32_t)grid_ub2);
     return mv.sk != nullptr;
 }
 
@@ -705,21 +709,29 @@ int phase_finish(RankState& R, float dt, int64_t step, bool global_flags) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
-    if (R.left >= 0 || R.right >= 0) HIPCHK(hipStreamWaitEvent(s, R.ev_rho_recv, 0));
-    CKPT(R, "exchange 2");
+    // The ghost ρ and the boundary columns' force pass run on the comm stream, behind the ρ receive (which is
+    // ordered after this rank's density pass, exchange2_start), so the boundary workgroups run alongside the
+    // interior pass and fill its tail instead of making a small launch of their own after it. The step's
+    // end (k_slab_lag, and the next step's kernels) waits for them.
+    const bool halo = R.left >= 0 || R.right >= 0;
+    hipStream_t b = halo ? R.comm : s;
     launch_slab_unpack_rho2(ctx->rp, R.dz, R.left >= 0 ? R.rho_in[0] : nullptr, R.c2i[0],
-                            R.right >= 0 ? R.rho_in[1] : nullptr, R.c2i[1], s);
+                            R.right >= 0 ? R.rho_in[1] : nullptr, R.c2i[1], b);
     CKPT(R, "rho unpack");
     const bool one_col = ctx->sl.cx_hi - ctx->sl.cx_lo == 1;
     const uint32_t* pk = R.dz->pick;
     if (one_col && (ctx->has_left || ctx->has_right)) {   // the owned column is both boundary columns
-        force_dev(ctx, &pk[1], &pk[4], R.n_ub, dt);
+        force_dev(ctx, &pk[1], &pk[4], R.n_ub, dt, nullptr, nullptr, 0, b);
     } else if (ctx->has_left && ctx->has_right) {   // both boundary columns in one launch
         force_dev(ctx, &pk[1], &pk[2], std::min<int64_t>(R.c2o[0], R.n_ub), dt, &pk[3], &pk[4],
-                  std::min<int64_t>(R.c2o[1], R.n_ub));
+                  std::min<int64_t>(R.c2o[1], R.n_ub), b);
     } else {
-        if (ctx->has_left) force_dev(ctx, &pk[1], &pk[2], std::min<int64_t>(R.c2o[0], R.n_ub), dt);
-        if (ctx->has_right) force_dev(ctx, &pk[3], &pk[4], std::min<int64_t>(R.c2o[1], R.n_ub), dt);
+        if (ctx->has_left) force_dev(ctx, &pk[1], &pk[2], std::min<int64_t>(R.c2o[0], R.n_ub), dt, nullptr, nullptr, 0, b);
+        if (ctx->has_right) force_dev(ctx, &pk[3], &pk[4], std::min<int64_t>(R.c2o[1], R.n_ub), dt, nullptr, nullptr, 0, b);
+    }
+    if (halo) {
+        HIPCHK(hipEventRecord(R.ev_bdone, b));
+        HIPCHK(hipStreamWaitEvent(s, R.ev_bdone, 0));
     }
     CKPT(R, "boundary force");
     swap_sv(ctx);
