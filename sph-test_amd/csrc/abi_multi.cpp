@@ -389,7 +389,7 @@ int validate_movers(RankState& R, int used) {
 // full-sort step (SPH_RESORT=0, or a step past the mover limit) every own slot is scanned.
 bool steady_sends(const RankState& R) { return R.since_cut >= 3 && R.jump_guard; }
 
-int phase_count(RankState& R) {
+int phase_count(RankState& R, bool exact) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
     if (!ctx->keys_valid) {   // after init or a re-cut: keys of the owned slots in the (new) window
@@ -406,7 +406,7 @@ int phase_count(RankState& R) {
     R.nb_send = slab_send_blocks(0, (int32_t)std::max<int64_t>(R.n_prev_ub, 1));
     KTimer t(ctx, "slab_count", 4.0 * R.n_prev_ub);
     launch_slab_count_dev(ctx->keys, R.dz, R.nb_send, gyz(ctx), col_le(ctx), col_ge(ctx), ctx->sblk,
-                          ctx->sdev + SDEV_TOTALS, ctx->stream, steady_sends(R));
+                          ctx->sdev + SDEV_TOTALS, ctx->stream, steady_sends(R), exact);
     CKPT(R, "count");
     return SPH_OK;
 }
@@ -423,12 +423,14 @@ int phase_pack(RankState& R, Multi& M) {
         if (r != SPH_OK) return r;
         // the neighbour's copy of last step's message must be done before it is overwritten
         if (M.mode == 1) HIPCHK(hipStreamWaitEvent(ctx->stream, M.ranks[peer - M.ranks[0].rank].ev_in, 0));
-        KTimer t(ctx, "slab_pack", 36.0 * R.c1o[s]);
-        launch_slab_pack_dev(ctx->keys, ctx->pos, ctx->vel, ctx->id, ctx->sk_valid ? ctx->sk_cur : nullptr,
-                             (uint32_t)ctx->grid.cx0 * gyz(ctx), R.dz,
-                             R.nb_send, gyz(ctx), s, col_le(ctx),
-                             col_ge(ctx), ctx->sblk, R.msg_out[s], R.c1o[s], ctx->sdev + SDEV_TOTALS + s, ctx->stream,
-                             steady_sends(R));
+    }
+    {
+        KTimer t(ctx, "slab_pack", 36.0 * (R.c1o[0] + R.c1o[1]));
+        launch_slab_pack2_dev(ctx->keys, ctx->pos, ctx->vel, ctx->id, ctx->sk_valid ? ctx->sk_cur : nullptr,
+                              (uint32_t)ctx->grid.cx0 * gyz(ctx), R.dz, R.nb_send, gyz(ctx), col_le(ctx), col_ge(ctx),
+                              ctx->sblk, R.left >= 0 ? R.msg_out[0] : nullptr, R.c1o[0],
+                              R.right >= 0 ? R.msg_out[1] : nullptr, R.c1o[1], ctx->sdev + SDEV_TOTALS, ctx->stream,
+                              steady_sends(R));
     }
     HIPCHK(hipGetLastError());
     // the peer copies of a local group wait for it (RCCL orders its sends on this stream itself); a
@@ -850,7 +852,7 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
     const bool exact = M.ranks[0].since_cut < 3;   // the same on every rank
     int r;
     for (auto& R : M.ranks)
-        if ((r = phase_count(R)) != SPH_OK) return r;
+        if ((r = phase_count(R, exact)) != SPH_OK) return r;
     if (exact) {
         if ((r = exchange_counts(M, pctx)) != SPH_OK) return r;
     } else {

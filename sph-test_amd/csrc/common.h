@@ -479,13 +479,14 @@ void launch_pick(const uint32_t* cs, const int32_t* idx, int32_t m, uint32_t* ou
 // into messages of a header and `cap[side]` records (header = true count; records past cap dropped and
 // flagged by the receiver). nb_ub: count-block upper bound (slab_send_blocks of the slot bound).
 // cand: steady state, scan only the columns a send can come from (slab.hip send_ranges)
+// exact: also the totals (host-read before packing on exact-size steps)
 void launch_slab_count_dev(const uint32_t* keys, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz, int32_t col_le,
-                           int32_t col_ge, uint32_t* blk, uint32_t* totals, hipStream_t s, bool cand);
-// total: the side's count from launch_slab_count_dev, written into the message header
-void launch_slab_pack_dev(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
-                          const uint32_t* sk, uint32_t key_base, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz,
-                          int32_t side, int32_t col_le, int32_t col_ge, const uint32_t* blk, float4* msg, int32_t cap,
-                          const uint32_t* total, hipStream_t s, bool cand);
+                           int32_t col_ge, uint32_t* blk, uint32_t* totals, hipStream_t s, bool cand, bool exact);
+// both sides in one launch from the raw per-block counts; headers and totals[2] written by the pack
+void launch_slab_pack2_dev(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
+                           const uint32_t* sk, uint32_t key_base, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz,
+                           int32_t col_le, int32_t col_ge, const uint32_t* blk, float4* msg_l, int32_t cap_l,
+                           float4* msg_r, int32_t cap_r, uint32_t* totals, hipStream_t s, bool cand);
 int32_t slab_send_blocks(int32_t b, int32_t e);
 // the received messages' counts -> dz (nl, nr clamped to the capacities, no, n, overflow flags)
 void launch_slab_sizes(SlabSizes* dz, const float4* msg_l, const float4* msg_r, int32_t cap_l, int32_t cap_r,

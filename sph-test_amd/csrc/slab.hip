@@ -111,10 +111,11 @@ __device__ __forceinline__ void write_header(float4* msg, uint32_t count, uint32
     msg[1] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// inplace 0: the totals only (the device-sized step's k_slab_pack2 takes the raw per-block counts)
 __global__ __launch_bounds__(SL_SCAN) void k_slab_scan(uint32_t* __restrict__ blk, int32_t nblk,
                                                        uint32_t* __restrict__ totals, int64_t* __restrict__ totals64,
                                                        float4* __restrict__ hdr_l, float4* __restrict__ hdr_r,
-                                                       int32_t cap_l, int32_t cap_r) {
+                                                       int32_t cap_l, int32_t cap_r, int32_t inplace = 1) {
     __shared__ uint32_t ws[SL_SCAN / 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int side = 0; side < 2; ++side) {
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(SL_SCAN) void k_slab_scan(uint32_t* __restrict__ bl
                 tot += ws[k];
             }
             __syncthreads();
-            if (i < nblk) row[i] = carry + pre + inc - v;
+            if (i < nblk && inplace) row[i] = carry + pre + inc - v;
             carry += tot;
         }
         if (threadIdx.x == 0) {
@@ -155,29 +156,14 @@ __global__ __launch_bounds__(SL_SCAN) void k_slab_scan(uint32_t* __restrict__ bl
 // the sender holds no valid sorted keys. The receiver's incremental re-sort uses it.
 constexpr uint32_t SL_NO_KEY = 0xffffffffu;
 
-__global__ __launch_bounds__(SL_BLK) void k_slab_pack(const uint32_t* __restrict__ keys,
-                                                      const float4* __restrict__ pos,
-                                                      const float4* __restrict__ vel,
-                                                      const int32_t* __restrict__ id,
-                                                      const uint32_t* __restrict__ sk, uint32_t key_base,
-                                                      int32_t b, int32_t e, uint32_t gyz, int32_t side,
-                                                      int32_t col_le, int32_t col_ge,
-                                                      const uint32_t* __restrict__ blk, int32_t nblk,
-                                                      float4* __restrict__ out, const SlabSizes* __restrict__ dz,
-                                                      uint32_t cap, float4* __restrict__ hdr,
-                                                      const uint32_t* __restrict__ total, int32_t cand) {
-    __shared__ uint32_t wc[SL_PER][SL_WAVES];
+// The compaction of one workgroup's SL_SEND slots [i0, ...) of [b, e) into records from `run` on (the side's
+// exclusive prefix of the per-block counts).
+__device__ __forceinline__ void pack_block(const uint32_t* __restrict__ keys, const float4* __restrict__ pos,
+                                           const float4* __restrict__ vel, const int32_t* __restrict__ id,
+                                           const uint32_t* __restrict__ sk, uint32_t key_base, int32_t b, int32_t e,
+                                           uint32_t gyz, int32_t side, int32_t col_le, int32_t col_ge, uint32_t run,
+                                           float4* __restrict__ out, uint32_t cap, uint32_t (*wc)[SL_WAVES]) {
     const int w = threadIdx.x >> 6;
-    // the message header (device-sized steps): the count k_slab_scan left, written by one lane here
-    // instead of by a launch of its own
-    if (hdr && blockIdx.x == 0 && threadIdx.x == 0) write_header(hdr, *total, cap);
-    if (dz) {   // device-sized step: this side's range, as k_slab_count took it
-        int32_t bl, el, br, er;
-        send_ranges(dz, cand, bl, el, br, er);
-        b = side == 0 ? bl : br;
-        e = side == 0 ? el : er;
-    }
-    if (b + (int32_t)blockIdx.x * SL_SEND >= e) return;   // whole workgroup, before the barrier
     const int32_t i0 = b + blockIdx.x * SL_SEND + threadIdx.x;
     // every key load issues before any is used; then one barrier for all sub-chunks' wave counts
     uint32_t col[SL_PER];
@@ -193,7 +179,6 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_pack(const uint32_t* __restrict
     }
     __syncthreads();
     // sub-chunks in slot order, waves in order within a sub-chunk: the records keep slot order
-    uint32_t run = blk[side * nblk + blockIdx.x];
 #pragma unroll
     for (int j = 0; j < SL_PER; ++j) {
         uint32_t before = 0, tot = 0;
@@ -214,6 +199,74 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_pack(const uint32_t* __restrict
         }
         run += tot;
     }
+}
+
+__global__ __launch_bounds__(SL_BLK) void k_slab_pack(const uint32_t* __restrict__ keys,
+                                                      const float4* __restrict__ pos,
+                                                      const float4* __restrict__ vel,
+                                                      const int32_t* __restrict__ id,
+                                                      const uint32_t* __restrict__ sk, uint32_t key_base,
+                                                      int32_t b, int32_t e, uint32_t gyz, int32_t side,
+                                                      int32_t col_le, int32_t col_ge,
+                                                      const uint32_t* __restrict__ blk, int32_t nblk,
+                                                      float4* __restrict__ out, uint32_t cap) {
+    __shared__ uint32_t wc[SL_PER][SL_WAVES];
+    if (b + (int32_t)blockIdx.x * SL_SEND >= e) return;   // whole workgroup, before the barrier
+    pack_block(keys, pos, vel, id, sk, key_base, b, e, gyz, side, col_le, col_ge, blk[side * nblk + blockIdx.x], out,
+               cap, wc);
+}
+
+// The device-sized step's pack: both sides in one launch (blockIdx.y = side), straight from k_slab_count's
+// per-block counts: each workgroup sums the counts of the blocks before it (at most a few hundred), and
+// workgroup 0 of a side writes the side's total into the message header and into totals[side] (for
+// k_slab_lag). No scan launch between count and pack.
+struct PackOut {
+    float4* msg[2];          // header + records; null: no neighbour on that side
+    uint32_t cap[2];
+    uint32_t* totals;
+};
+__global__ __launch_bounds__(SL_BLK) void k_slab_pack2(const uint32_t* __restrict__ keys, const float4* __restrict__ pos,
+                                                       const float4* __restrict__ vel, const int32_t* __restrict__ id,
+                                                       const uint32_t* __restrict__ sk, uint32_t key_base, uint32_t gyz,
+                                                       int32_t col_le, int32_t col_ge, const uint32_t* __restrict__ blk,
+                                                       int32_t nblk, const SlabSizes* __restrict__ dz, PackOut po,
+                                                       int32_t cand) {
+    __shared__ uint32_t wc[SL_PER][SL_WAVES];
+    __shared__ uint32_t red[SL_WAVES][2];
+    const int32_t side = (int32_t)blockIdx.y;
+    float4* msg = po.msg[side];
+    if (!msg) return;
+    int32_t bl, el, br, er;
+    send_ranges(dz, cand, bl, el, br, er);
+    const int32_t b = side == 0 ? bl : br, e = side == 0 ? el : er;
+    const bool work = b + (int32_t)blockIdx.x * SL_SEND < e;
+    if (!work && blockIdx.x != 0) return;   // whole workgroup, before any barrier
+    // this block's exclusive prefix (blocks < blockIdx.x) and, for block 0, the side's total
+    const uint32_t* row = blk + side * nblk;
+    uint32_t pre = 0, tot = 0;
+    for (int32_t k = threadIdx.x; k < nblk; k += SL_BLK) {
+        const uint32_t v = row[k];
+        pre += k < (int32_t)blockIdx.x ? v : 0u;
+        tot += v;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        pre += (uint32_t)__shfl_xor((int)pre, o, 64);
+        tot += (uint32_t)__shfl_xor((int)tot, o, 64);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[w][0] = pre; red[w][1] = tot; }
+    __syncthreads();
+    uint32_t run = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < SL_WAVES; ++k) { run += red[k][0]; total += red[k][1]; }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        write_header(msg, total, po.cap[side]);
+        po.totals[side] = total;
+    }
+    if (!work) return;   // block 0 of an empty side: header only (the barrier above is behind it)
+    pack_block(keys, pos, vel, id, sk, key_base, b, e, gyz, side, col_le, col_ge, run, msg + MSG_HDR_F4, po.cap[side],
+               wc);
 }
 
 __global__ __launch_bounds__(SL_BLK) void k_slab_unpack(const float4* __restrict__ rec, int32_t n,
@@ -385,21 +438,24 @@ void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel
     const int32_t nb = slab_send_blocks(b, e);
     if (e > b)
         k_slab_pack<<<nb, SL_BLK, 0, s>>>(keys, pos, vel, id, sk, key_base, b, e, gyz, side, col_le, col_ge, blk, nb,
-                                          out, nullptr, 0xffffffffu, nullptr, nullptr, 0);
+                                          out, 0xffffffffu);
 }
 
+// exact: the host reads the totals before packing (k_slab_scan, totals only); steady steps need no scan
 void launch_slab_count_dev(const uint32_t* keys, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz, int32_t col_le,
-                           int32_t col_ge, uint32_t* blk, uint32_t* totals, hipStream_t s, bool cand) {
+                           int32_t col_ge, uint32_t* blk, uint32_t* totals, hipStream_t s, bool cand, bool exact) {
     k_slab_count<<<nb_ub, SL_BLK, 0, s>>>(keys, 0, 0, gyz, col_le, col_ge, blk, nb_ub, dz, cand ? 1 : 0);
-    k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb_ub, totals, nullptr, nullptr, nullptr, 0, 0);
+    if (exact) k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb_ub, totals, nullptr, nullptr, nullptr, 0, 0, 0);
 }
 
-void launch_slab_pack_dev(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
-                          const uint32_t* sk, uint32_t key_base, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz,
-                          int32_t side, int32_t col_le, int32_t col_ge, const uint32_t* blk, float4* msg, int32_t cap,
-                          const uint32_t* total, hipStream_t s, bool cand) {
-    k_slab_pack<<<nb_ub, SL_BLK, 0, s>>>(keys, pos, vel, id, sk, key_base, 0, 0, gyz, side, col_le, col_ge, blk,
-                                         nb_ub, msg + MSG_HDR_F4, dz, (uint32_t)cap, msg, total, cand ? 1 : 0);
+void launch_slab_pack2_dev(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
+                           const uint32_t* sk, uint32_t key_base, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz,
+                           int32_t col_le, int32_t col_ge, const uint32_t* blk, float4* msg_l, int32_t cap_l,
+                           float4* msg_r, int32_t cap_r, uint32_t* totals, hipStream_t s, bool cand) {
+    if (!msg_l && !msg_r) return;
+    const PackOut po{{msg_l, msg_r}, {(uint32_t)cap_l, (uint32_t)cap_r}, totals};
+    k_slab_pack2<<<dim3(nb_ub, 2), SL_BLK, 0, s>>>(keys, pos, vel, id, sk, key_base, gyz, col_le, col_ge, blk, nb_ub, dz,
+                                                   po, cand ? 1 : 0);
 }
 
 // The assembled layout from the message headers and the owned range of the previous order (a
