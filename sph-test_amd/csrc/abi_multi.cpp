@@ -47,7 +47,8 @@ struct RankState {
     float2* rho_in[2] = {nullptr, nullptr};
     int32_t rcap_out[2] = {0, 0}, rcap_in[2] = {0, 0};
     int32_t c1o[2] = {0, 0}, c1i[2] = {0, 0}, c2o[2] = {0, 0}, c2i[2] = {0, 0};   // this step's capacities
-    uint32_t* cnt_dev = nullptr;   // [4] received counts (exact-size steps over RCCL); [2]: every rank's
+    uint32_t* cnt_dev = nullptr;   // [12] received counts [0, 2) (exact-size steps over RCCL); [4, 9): one word per
+                                   // SZ_* bit, written by the density pass and max-reduced over the ranks (an OR);
                                    // SZ_* flags, max-reduced over the communicator each step (RCCL, world > 1)
     uint32_t* lag = nullptr;       // pinned, mapped: LAG_SLOTS x LAG_WORDS (launch_slab_lag)
     hipEvent_t lag_ev[LAG_SLOTS] = {};
@@ -218,8 +219,8 @@ int rank_init(RankState& R) {
     HIPCHK(hipMalloc((void**)&R.dz, sizeof(SlabSizes)));
     HIPCHK(hipMemset(R.dz, 0, sizeof(SlabSizes)));
     R.c->dz = R.dz;
-    HIPCHK(hipMalloc((void**)&R.cnt_dev, 4 * sizeof(uint32_t)));
-    HIPCHK(hipMemset(R.cnt_dev, 0, 4 * sizeof(uint32_t)));
+    HIPCHK(hipMalloc((void**)&R.cnt_dev, 12 * sizeof(uint32_t)));
+    HIPCHK(hipMemset(R.cnt_dev, 0, 12 * sizeof(uint32_t)));
     HIPCHK(hipMemset(R.c->sdev + SDEV_TOTALS, 0, 2 * sizeof(uint32_t)));
     HIPCHK(hipHostMalloc((void**)&R.lag, LAG_SLOTS * LAG_WORDS * sizeof(uint32_t), hipHostMallocMapped));
     std::memset(R.lag, 0, LAG_SLOTS * LAG_WORDS * sizeof(uint32_t));
@@ -547,10 +548,11 @@ int exchange2_start(Multi& M) {
         NCCLCHK(ncclRecv(R.rho_in[s], (size_t)(RHO_HDR + R.c2i[s]) * sizeof(float2), ncclUint8, peer, M.comm, R.comm));
     }
     NCCLCHK(ncclGroupEnd());
-    // every rank's sticky SZ_* flags as of its density pass, max-reduced (any nonzero = a rank flagged):
-    // the step's lag record carries this value, so all ranks stop at the same later step. One word on
-    // the comm stream, in flight with the interior force pass like the ρ halo.
-    NCCLCHK(ncclAllReduce(&R.dz->flags, R.cnt_dev + 2, 1, ncclUint32, ncclMax, M.comm, R.comm));
+    // every rank's sticky SZ_* flags as of its density pass, one word per bit (the density pass wrote them),
+    // max-reduced: each bit is the OR over the ranks, so the failure message names every rank's cause. The
+    // step's lag record carries them, so all ranks stop at the same later step. In flight on the comm
+    // stream with the interior force pass, like the ρ halo.
+    NCCLCHK(ncclAllReduce(R.cnt_dev + 4, R.cnt_dev + 4, SZ_BITS, ncclUint32, ncclMax, M.comm, R.comm));
     HIPCHK(hipEventRecord(R.ev_rho_recv, R.comm));
     return SPH_OK;
 }
@@ -668,6 +670,7 @@ int phase_density(RankState& R, Multi& M) {
         ro.cap[sd] = R.c2o[sd];
     }
     if (ro.msg[0] || ro.msg[1]) ro.dz = R.dz;
+    if (M.mode == 2 && M.world > 1) ro.fbits = R.cnt_dev + 4;   // this rank's flags, one word per bit, for the OR
     {
         KTimer t(ctx, "density", 24.0 * (double)R.n_ub, true);
         launch_density_tiled(ctx->pos, ctx->cs, 0, (int32_t)R.n_ub, ctx->grid, ctx->sc, ctx->rp, hit_mask_write(ctx),
@@ -744,7 +747,7 @@ int phase_finish(RankState& R, float dt, int64_t step, bool global_flags) {
     launch_slab_lag(R.dz, ctx->has_left ? 1 : 0, ctx->has_right ? 1 : 0, ctx->sdev + SDEV_TOTALS,
                     R.left >= 0 ? R.msg_in[0] : nullptr, R.right >= 0 ? R.msg_in[1] : nullptr,
                     R.left >= 0 ? R.rho_in[0] : nullptr, R.right >= 0 ? R.rho_in[1] : nullptr,
-                    global_flags ? R.cnt_dev + 2 : nullptr, R.lag + k * LAG_WORDS, s);
+                    global_flags ? R.cnt_dev + 4 : nullptr, R.lag + k * LAG_WORDS, s);
     if (R.left >= 0 || R.right >= 0) HIPCHK(hipEventRecord(R.lag_ev[k], s));   // read two steps on
     R.cin_hist[k] = R.c1i[0] + R.c1i[1];
     R.n_prev_ub = R.n_ub;

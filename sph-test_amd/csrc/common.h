@@ -218,6 +218,7 @@ constexpr uint32_t SZ_OVF_CAP = 2u;     // the assembled slots exceed the contex
 constexpr uint32_t SZ_RHO_MISMATCH = 4u;  // a ghost column and the densities received differ in count
 constexpr uint32_t SZ_OVF_MOVERS = 8u;    // a mover list or a re-sort destination past the slot capacity
 constexpr uint32_t SZ_JUMP = 16u;         // an own particle left the held window in one step (two columns or more)
+constexpr int SZ_BITS = 5;
 // Halo messages: one 32-byte header record, then the records. Header: (count, capacity, 0, 0 | 0...)
 constexpr int MSG_HDR_F4 = 2;
 // ρ halo messages: a 32-byte header (count, capacity) = 4 float2, then (ρ, P/ρ²) of the boundary column's slots
@@ -228,6 +229,7 @@ struct RhoOut {
     float2* msg[2] = {nullptr, nullptr};
     int32_t cap[2] = {0, 0};
     const SlabSizes* dz = nullptr;
+    uint32_t* fbits = nullptr;   // RCCL step: dz->flags, one word per SZ_* bit, for the ranks' OR (abi_multi.cpp)
 };
 // What the assembled layout is computed from: the two message headers (null: no neighbour), the
 // capacities they were sent with, and the context's slot capacity.

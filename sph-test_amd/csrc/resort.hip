@@ -137,6 +137,9 @@ static __device__ __forceinline__ uint32_t lb64(const T* __restrict__ a, T v) {
 // quarter per wave), and each mover counts by three 7-probe binary searches instead of 3 x 64 compares
 // (~6.5 VALU per mover pair before, O(m^2) in the movers).
 // Also zeroes the next step's mover counter.
+// k_mv_rank's tile logic: lb64 searches exactly 64 entries, the tile is filled by threads < MV_TILE and
+// counted by MV_BLK / MV_TILE parts
+static_assert(MV_TILE == 64 && MV_BLK >= MV_TILE && MV_BLK % MV_TILE == 0, "k_mv_rank assumes 64-entry tiles");
 __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__ mtotal,
                                                     uint32_t* __restrict__ next_count,
                                                     const uint32_t* __restrict__ cs_old, ResortScratch w) {

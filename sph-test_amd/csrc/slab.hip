@@ -562,7 +562,12 @@ __global__ void k_slab_lag(SlabSizes* __restrict__ dz, int32_t has_left, int32_t
     out[6] = rho_in_l ? __float_as_uint(rho_in_l[0].x) : 0u;
     out[7] = rho_in_r ? __float_as_uint(rho_in_r[0].x) : 0u;
     out[8] = v[5];
-    out[9] = gflags ? *gflags : f;   // RCCL: every rank's flags, max-reduced (the same on all ranks)
+    uint32_t gf = f;
+    if (gflags) {   // RCCL: one word per flag bit, max-reduced over the ranks: the OR (the same on all ranks)
+        gf = 0u;
+        for (int k = 0; k < SZ_BITS; ++k) gf |= (gflags[k] != 0u ? 1u : 0u) << k;
+    }
+    out[9] = gf;
 }
 
 void launch_slab_lag(SlabSizes* dz, int32_t has_left, int32_t has_right, const uint32_t* totals,

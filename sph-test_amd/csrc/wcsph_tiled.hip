@@ -317,6 +317,11 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
         m[0] = make_float2(__uint_as_float(cnt), __uint_as_float((uint32_t)ro.cap[sd]));
         m[1] = m[2] = m[3] = make_float2(0.f, 0.f);
     }
+    if (ro.fbits && ro.dz && blockIdx.x == 0 && threadIdx.x == 0) {   // every earlier kernel of the step has set its flags
+        const uint32_t f = ro.dz->flags;
+#pragma unroll
+        for (int k = 0; k < SZ_BITS; ++k) ro.fbits[k] = (f >> k) & 1u;
+    }
     if (dr.lo) {   // device-resident bounds (slab mode); the grid is an upper bound
         ib = (int32_t)*dr.lo;
         n = (int32_t)*dr.hi;
