@@ -95,15 +95,20 @@ int32_t cap_of(uint32_t cnt) {
 }
 
 // Neighbouring slabs of a local group on different GPUs copy halos device to device: enable peer
-// access both ways so the copies go GPU to GPU over xGMI (a copy without it may be staged through host
-// memory). A pair that cannot reach each other is an error, not a silent slow path.
+// access both ways so the copies go GPU to GPU over xGMI. A pair without a peer path still works
+// (hipMemcpyPeerAsync stages such a copy through host memory) but slowly: it is reported on stderr once
+// per pair, not made an error (supported configurations).
 int enable_peers(sph_ctx* ctx, int da, int db) {
     if (da == db) return SPH_OK;
     for (int k = 0; k < 2; ++k) {
         const int from = k ? db : da, to = k ? da : db;
         int can = 0;
         HIPCHK(hipDeviceCanAccessPeer(&can, from, to));
-        if (!can) return fail(ctx, SPH_ERR_HIP, "device %d cannot access device %d (no peer path for the slab halo)", from, to);
+        if (!can) {
+            std::fprintf(stderr, "sphhip: device %d cannot access device %d: the slab halo copies between them are "
+                                 "staged through host memory (slow)\n", from, to);
+            continue;
+        }
         HIPCHK(hipSetDevice(from));
         const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
