@@ -77,11 +77,19 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_count(const uint32_t* __restric
         }
     } else {
         const int32_t l0 = bl + blockIdx.x * SL_SEND + threadIdx.x, r0 = br + blockIdx.x * SL_SEND + threadIdx.x;
+        // clamped indices: all 2 x SL_PER loads issue before any is used (conditional loads were one round trip
+        // each: 10-17 us per launch at C3 x 4, profiles/r04_slab_trace.log)
+        uint32_t kl[SL_PER], kr[SL_PER];
+        const bool any_l = l0 - (int32_t)threadIdx.x < el, any_r = r0 - (int32_t)threadIdx.x < er;
 #pragma unroll
         for (int j = 0; j < SL_PER; ++j) {
-            const int32_t il = l0 + j * SL_BLK, ir = r0 + j * SL_BLK;
-            if (il < el) cl += (int32_t)(keys[il] / gyz) <= col_le;
-            if (ir < er) cr += (int32_t)(keys[ir] / gyz) >= col_ge;
+            kl[j] = any_l ? keys[min(l0 + j * SL_BLK, el - 1)] : 0u;
+            kr[j] = any_r ? keys[min(r0 + j * SL_BLK, er - 1)] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < SL_PER; ++j) {
+            cl += l0 + j * SL_BLK < el && (int32_t)(kl[j] / gyz) <= col_le;
+            cr += r0 + j * SL_BLK < er && (int32_t)(kr[j] / gyz) >= col_ge;
         }
     }
 #pragma unroll
@@ -157,12 +165,15 @@ __global__ __launch_bounds__(SL_SCAN) void k_slab_scan(uint32_t* __restrict__ bl
 constexpr uint32_t SL_NO_KEY = 0xffffffffu;
 
 // The compaction of one workgroup's SL_SEND slots [i0, ...) of [b, e) into records from `run` on (the side's
-// exclusive prefix of the per-block counts).
+// exclusive prefix of the per-block counts). The sent slots are listed in LDS in record order first, and then every
+// thread copies list entries: the record loads of all entries issue together (one round trip) instead of one
+// dependent load-and-store round per sub-chunk (~20 us per pack launch at C3 x 4, profiles/r04_slab_trace.log).
 __device__ __forceinline__ void pack_block(const uint32_t* __restrict__ keys, const float4* __restrict__ pos,
                                            const float4* __restrict__ vel, const int32_t* __restrict__ id,
                                            const uint32_t* __restrict__ sk, uint32_t key_base, int32_t b, int32_t e,
                                            uint32_t gyz, int32_t side, int32_t col_le, int32_t col_ge, uint32_t run,
-                                           float4* __restrict__ out, uint32_t cap, uint32_t (*wc)[SL_WAVES]) {
+                                           float4* __restrict__ out, uint32_t cap, uint32_t (*wc)[SL_WAVES],
+                                           int32_t* list) {
     const int w = threadIdx.x >> 6;
     const int32_t i0 = b + blockIdx.x * SL_SEND + threadIdx.x;
     // every key load issues before any is used; then one barrier for all sub-chunks' wave counts
@@ -178,7 +189,8 @@ __device__ __forceinline__ void pack_block(const uint32_t* __restrict__ keys, co
         mine |= (uint32_t)pred << j;
     }
     __syncthreads();
-    // sub-chunks in slot order, waves in order within a sub-chunk: the records keep slot order
+    // sub-chunks in slot order, waves in order within a sub-chunk: the list keeps slot order
+    uint32_t loc = 0;
 #pragma unroll
     for (int j = 0; j < SL_PER; ++j) {
         uint32_t before = 0, tot = 0;
@@ -189,15 +201,35 @@ __device__ __forceinline__ void pack_block(const uint32_t* __restrict__ keys, co
         }
         const bool pred = (mine >> j) & 1u;
         const uint64_t m = __ballot(pred);
-        const uint32_t r = run + before + lane_prefix(m);
-        if (pred && r < cap) {   // past the message capacity: dropped; the header's count tells the receiver
-            const int32_t i = i0 + j * SL_BLK;
-            const float4 p = pos[i], v = vel[i];
-            const uint32_t ok = sk ? sk[i] + key_base : SL_NO_KEY;
-            out[2 * (size_t)r] = make_float4(p.x, p.y, p.z, __int_as_float(id[i]));
-            out[2 * (size_t)r + 1] = make_float4(v.x, v.y, v.z, __uint_as_float(ok));
+        if (pred) list[loc + before + lane_prefix(m)] = i0 + j * SL_BLK;
+        loc += tot;
+    }
+    __syncthreads();
+    // loc: the block's record count. Records past the message capacity are dropped; the header's count tells the
+    // receiver.
+    const uint32_t lim = run < cap ? min(loc, cap - run) : 0u;
+    constexpr int U = 4;
+    for (uint32_t t0 = threadIdx.x; t0 < lim; t0 += U * SL_BLK) {
+        float4 p[U], v[U];
+        int32_t q[U];
+        uint32_t ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t t = t0 + u * SL_BLK;
+            const int32_t i = list[min(t, lim - 1)];
+            p[u] = pos[i];
+            v[u] = vel[i];
+            q[u] = id[i];
+            ok[u] = sk ? sk[i] + key_base : SL_NO_KEY;
         }
-        run += tot;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t t = t0 + u * SL_BLK;
+            if (t < lim) {
+                out[2 * (size_t)(run + t)] = make_float4(p[u].x, p[u].y, p[u].z, __int_as_float(q[u]));
+                out[2 * (size_t)(run + t) + 1] = make_float4(v[u].x, v[u].y, v[u].z, __uint_as_float(ok[u]));
+            }
+        }
     }
 }
 
@@ -211,9 +243,10 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_pack(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ blk, int32_t nblk,
                                                       float4* __restrict__ out, uint32_t cap) {
     __shared__ uint32_t wc[SL_PER][SL_WAVES];
+    __shared__ int32_t list[SL_SEND];
     if (b + (int32_t)blockIdx.x * SL_SEND >= e) return;   // whole workgroup, before the barrier
     pack_block(keys, pos, vel, id, sk, key_base, b, e, gyz, side, col_le, col_ge, blk[side * nblk + blockIdx.x], out,
-               cap, wc);
+               cap, wc, list);
 }
 
 // The device-sized step's pack: both sides in one launch (blockIdx.y = side), straight from k_slab_count's
@@ -233,6 +266,7 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_pack2(const uint32_t* __restric
                                                        int32_t cand) {
     __shared__ uint32_t wc[SL_PER][SL_WAVES];
     __shared__ uint32_t red[SL_WAVES][2];
+    __shared__ int32_t list[SL_SEND];
     const int32_t side = (int32_t)blockIdx.y;
     float4* msg = po.msg[side];
     if (!msg) return;
@@ -266,7 +300,7 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_pack2(const uint32_t* __restric
     }
     if (!work) return;   // block 0 of an empty side: header only (the barrier above is behind it)
     pack_block(keys, pos, vel, id, sk, key_base, b, e, gyz, side, col_le, col_ge, run, msg + MSG_HDR_F4, po.cap[side],
-               wc);
+               wc, list);
 }
 
 __global__ __launch_bounds__(SL_BLK) void k_slab_unpack(const float4* __restrict__ rec, int32_t n,
@@ -285,15 +319,19 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_unpack(const float4* __restrict
 // order, so cs[k] shifts by nl − o0 (o0: the previous owned start). Halo columns: lower bounds in
 // the left / right blocks. cs[ncells] = cs[ncells + 1] = n. Four cells per lane: the owned cells,
 // nearly all of the table, move as one 16-byte load and store (the table is ~15 MB at C3).
-__device__ __forceinline__ uint32_t cs_old_halo(const uint32_t* __restrict__ sk, uint32_t k, uint32_t lo, uint32_t len,
-                                                uint32_t off) {
-    uint32_t a = 0u, b = len;   // lower bound of k in sk[lo, lo + len)
-    while (a < b) {
-        const uint32_t mid = (a + b) >> 1;
-        if (sk[lo + mid] < k) a = mid + 1u;
-        else b = mid;
+// A halo cell's lower bound: a binary search over every S-th key of its block, staged in LDS, then one over
+// the S − 1 keys in between in global memory (S = 8 up to 65,536 records: three dependent loads). A plain
+// binary search in global memory was 16 dependent loads per cell: ~11 us per launch at C3 x 4, most of it
+// those lanes (profiles/r04_slab_trace.log).
+constexpr int CS_SAMP = 8192;
+
+__device__ __forceinline__ uint32_t lb_range(const uint32_t* __restrict__ a, uint32_t lo, uint32_t hi, uint32_t k) {
+    while (lo < hi) {   // the first index in [lo, hi) with a[index] >= k, or hi
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < k) lo = mid + 1u;
+        else hi = mid;
     }
-    return off + a;
+    return lo;
 }
 
 __global__ __launch_bounds__(SL_BLK) void k_slab_cs_old(uint32_t* __restrict__ cs, uint32_t ncells, uint32_t gyz,
@@ -301,8 +339,8 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_cs_old(uint32_t* __restrict__ c
                                                         int32_t shift, const uint32_t* __restrict__ sk,
                                                         int32_t nl, int32_t no, int32_t nr,
                                                         const SlabSizes* __restrict__ dz) {
+    __shared__ uint32_t samp[CS_SAMP];
     const uint32_t k0 = 4u * (blockIdx.x * SL_BLK + threadIdx.x);
-    if (k0 > ncells + 1u) return;
     if (dz) {
         nl = (int32_t)dz->nl;
         no = (int32_t)dz->no;
@@ -312,6 +350,30 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_cs_old(uint32_t* __restrict__ c
     const uint32_t n = (uint32_t)(nl + no + nr);
     // the owned cells: [owned_lo, owned_hi) (halo columns are the first / last column when present)
     const uint32_t owned_lo = has_left ? gyz : 0u, owned_hi = has_right ? (gx - 1u) * gyz : ncells;
+    const uint32_t kb0 = 4u * blockIdx.x * SL_BLK, kb1 = kb0 + 4u * SL_BLK;   // this workgroup's cells
+#pragma unroll 1
+    for (int side = 0; side < 2; ++side) {   // workgroup-uniform: the halo cells of this workgroup
+        const bool here = side == 0 ? (has_left && kb0 < owned_lo) : (has_right && kb1 > owned_hi && kb0 < ncells);
+        if (!here) continue;
+        const uint32_t base = side == 0 ? 0u : (uint32_t)(nl + no), len = (uint32_t)(side == 0 ? nl : nr);
+        const uint32_t S = max(8u, (len + CS_SAMP - 1u) / CS_SAMP), ns = (len + S - 1u) / S;
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < ns; t += SL_BLK) samp[t] = sk[base + t * S];
+        __syncthreads();
+        for (uint32_t k = k0; k < k0 + 4u; ++k) {
+            const bool in = side == 0 ? k < owned_lo : (k >= owned_hi && k < ncells);
+            if (!in) continue;
+            uint32_t lo = 0u, hi = ns;   // samples below k
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (samp[mid] < k) lo = mid + 1u;
+                else hi = mid;
+            }
+            const uint32_t lb = lo == 0u ? 0u : lb_range(sk + base, (lo - 1u) * S + 1u, min(lo * S, len), k);
+            cs[k] = base + lb;
+        }
+    }
+    if (k0 > ncells + 1u) return;
     if (k0 + 3u < owned_hi && k0 >= owned_lo) {   // four owned cells (cs is 16-byte aligned)
         if (shift != 0) {
             uint4 v = reinterpret_cast<uint4*>(cs)[k0 >> 2];
@@ -326,10 +388,8 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_cs_old(uint32_t* __restrict__ c
     for (uint32_t k = k0; k < k0 + 4u && k <= ncells + 1u; ++k) {
         if (k >= ncells) {
             cs[k] = n;
-        } else if (k < owned_lo) {
-            cs[k] = cs_old_halo(sk, k, 0u, (uint32_t)nl, 0u);
-        } else if (k >= owned_hi) {
-            cs[k] = cs_old_halo(sk, k, (uint32_t)(nl + no), (uint32_t)nr, (uint32_t)(nl + no));
+        } else if (k < owned_lo || k >= owned_hi) {
+            // halo cell: written above
         } else if (shift != 0) {
             cs[k] = (uint32_t)((int32_t)cs[k] + shift);
         }
