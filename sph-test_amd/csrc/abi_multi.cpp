@@ -594,7 +594,7 @@ int phase_assemble(RankState& R, bool exact) {
         KTimer t(ctx, "resort", (double)R.n_ub * (2 * 4 + 2 * 36), true);
         if (ctx->has_left || ctx->has_right)   // without neighbours the own block keeps its cell starts
             launch_slab_cs_old(ctx->cs, ctx->grid.ncells, gyz(ctx), (uint32_t)ctx->grid.gx, ctx->has_left,
-                               ctx->has_right, 0, ctx->keys2, 0, 0, 0, s, R.dz);
+                               ctx->has_right, 0, ctx->keys2, 0, 0, 0, s, R.dz, nl_ub, nr_ub);
         CKPT(R, "cs_old");
         if (ctx->cfg.flags & SPH_FLAG_VALIDATE) {
             int r = validate_movers(R, used);
@@ -951,6 +951,19 @@ int multi_create_group(sph_ctx* ctx) {
     return SPH_OK;
 }
 
+// Test knob (tests/test_gpu_multi.py): SPH_DEBUG_CUT_SKEW=k moves every inner cut k columns right of the equal-count
+// position (every slab keeps at least one column), so the first re-balancing re-cuts the slabs of a full-size run.
+void skew_cuts(std::vector<sph_slab>& cuts) {
+    const char* e = std::getenv("SPH_DEBUG_CUT_SKEW");
+    const int k = e ? std::atoi(e) : 0;
+    if (k == 0) return;
+    for (size_t r = 0; r + 1 < cuts.size(); ++r) {
+        const int c = std::max(cuts[r].cx_lo + 1, std::min(cuts[r].cx_hi + k, cuts[r + 1].cx_hi - 1));
+        cuts[r].cx_hi = c;
+        cuts[r + 1].cx_lo = c;
+    }
+}
+
 // Distribute a scenario over a local group: equal-count cuts, one slab context per GPU.
 int multi_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
     Multi& M = *ctx->mg;
@@ -961,6 +974,7 @@ int multi_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
     if (G < 2 * M.world) return fail(ctx, SPH_ERR_INVALID, "%d columns cannot be cut into %d slabs", G, M.world);
     const std::vector<int64_t> per = lattice_columns(*sc, p);
     M.cuts = balanced_cuts(per, M.world);
+    skew_cuts(M.cuts);
     M.n_total = (int64_t)sc->nx * sc->ny * (sc->dim == 3 ? sc->nz : 1);
     const int64_t per_x = (int64_t)sc->ny * (sc->dim == 3 ? sc->nz : 1);
     int64_t maxcol = 0;
@@ -1188,6 +1202,7 @@ int sph::multi_init_rank(sph_ctx* ctx, const sph_scenario* sc) {
     if (G < 2 * M.world) return fail(ctx, SPH_ERR_INVALID, "%d columns cannot be cut into %d slabs", G, M.world);
     const std::vector<int64_t> per = lattice_columns(*sc, p);
     M.cuts = balanced_cuts(per, M.world);
+    skew_cuts(M.cuts);
     M.n_total = (int64_t)sc->nx * sc->ny * (sc->dim == 3 ? sc->nz : 1);
     const int64_t per_x = (int64_t)sc->ny * (sc->dim == 3 ? sc->nz : 1);
     int64_t maxcol = 0, own = 0;

@@ -275,21 +275,26 @@ def test_group_window_exit_stops_the_group(pkg, monkeypatch):
 
 
 @pytest.mark.parametrize("cfg,ndev,steps", [("C4", 4, 120), ("C5", 8, 100)])
-def test_baseline_config_decomposed_full_size(pkg, oracle, cfg, ndev, steps):
+def test_baseline_config_decomposed_full_size(pkg, oracle, monkeypatch, cfg, ndev, steps):
     """BASELINE's own multi-GPU configurations decomposed as they run on 4 / 8 GPUs, at full size, as a local
     group on the test box's one device: C4 (4,194,304 particles, sloshing) in 4 slabs, C5 (16,777,216) in 8,
-    re-balanced every 20 steps. Every step's halo must reproduce the 27-cell neighbourhood at every cut
+    re-balanced every 20 steps. The cuts start one column right of the equal-count position
+    (SPH_DEBUG_CUT_SKEW=1), so the first re-balancing re-cuts every slab at full size (a full radix sort and three
+    exact-size steps follow). Every step's halo must reproduce the 27-cell neighbourhood at every cut
     (SimulateParticles.compute:228-233), so the group is bit-identical to one context; then one step from the
     decomposed state meets the oracle tolerances of test_gpu_parity_headline.compare_one_step."""
     from test_gpu_parity_headline import compare_one_step
     sc = pkg.config_scenario(cfg)
+    monkeypatch.setenv("SPH_DEBUG_CUT_SKEW", "1")
     group = pkg.SPHSim(sc, ndev=ndev, rebalance_every=20)
+    monkeypatch.delenv("SPH_DEBUG_CUT_SKEW")
     try:
         group.step(steps)
         xg, vg = group.positions(), group.velocities()
         d = group.ctx.decomposition()
         assert d.world == ndev and d.owned == group.n == len(xg)
         rebalances = d.rebalances
+        assert rebalances > 0
     finally:
         group.close()
     single = pkg.SPHSim(sc)
