@@ -594,7 +594,7 @@ int phase_assemble(RankState& R, bool exact) {
         KTimer t(ctx, "resort", (double)R.n_ub * (2 * 4 + 2 * 36), true);
         if (ctx->has_left || ctx->has_right)   // without neighbours the own block keeps its cell starts
             launch_slab_cs_old(ctx->cs, ctx->grid.ncells, gyz(ctx), (uint32_t)ctx->grid.gx, ctx->has_left,
-                               ctx->has_right, 0, ctx->keys2, 0, 0, 0, s, R.dz, nl_ub, nr_ub);
+                               ctx->has_right, 0, ctx->keys2, 0, 0, 0, s, R.dz);
         CKPT(R, "cs_old");
         if (ctx->cfg.flags & SPH_FLAG_VALIDATE) {
             int r = validate_movers(R, used);

@@ -470,10 +470,9 @@ void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel
                       int32_t col_le, int32_t col_ge, const uint32_t* blk, float4* out, hipStream_t s);
 void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, int32_t* id, hipStream_t s);
 // cell starts of the assembled old keys, in place from the previous table (ncells + 2 entries)
-// dz: sizes on the device, nl_ub / nr_ub bound the halo blocks (the message capacities)
 void launch_slab_cs_old(uint32_t* cs, uint32_t ncells, uint32_t gyz, uint32_t gx, bool has_left, bool has_right,
                         int32_t shift, const uint32_t* sk, int32_t nl, int32_t no, int32_t nr, hipStream_t s,
-                        const SlabSizes* dz = nullptr, int32_t nl_ub = 0, int32_t nr_ub = 0);
+                        const SlabSizes* dz = nullptr);
 void launch_column_starts(const uint32_t* cs, uint32_t gyz, int32_t c0, int32_t m, uint32_t* out, hipStream_t s);
 void launch_pick(const uint32_t* cs, const int32_t* idx, int32_t m, uint32_t* out, hipStream_t s,
                  uint32_t* out_host = nullptr);
