@@ -47,6 +47,8 @@ struct SphConst {
     float Lx, Ly, Lz;
     float wall_e;
     float inv_h2;   // 1/h², the neighbour passes' q = sqrt(r²/h²)
+    // the neighbour passes in units of r (wcsph_tiled.hip SPH_RUNITS): 2h, −6h, 4h³ and the density scale m·σ/(4h³)
+    float two_h, m6h, four_h3, rho_scale;
 };
 
 // Model R uniforms (SimulateParticles.compute:89-100) + DragInput (:70-74).

@@ -142,6 +142,10 @@ int derive(sph_ctx* ctx) {
         s.Lx = p.box[0]; s.Ly = p.box[1]; s.Lz = ctx->cfg.dim == 3 ? p.box[2] : 0.f;
         s.wall_e = p.wall_restitution;
         s.inv_h2 = s.inv_h * s.inv_h;
+        s.two_h = 2.0f * h;
+        s.m6h = -6.0f * h;
+        s.four_h3 = 4.0f * h * h * h;
+        s.rho_scale = s.mass * s.sigma / s.four_h3;
     }
     g.cx0 = 0;
     g.gx_all = g.gx;

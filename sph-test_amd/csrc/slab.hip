@@ -382,8 +382,16 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_cs_old(uint32_t* __restrict__ c
         const uint32_t ws = j0 == 0u ? 0u : (j0 - 1u) * S + 1u, we = min(j1 * S, len);
         const uint32_t wn = we > ws ? we - ws : 0u;
         const bool staged = wn <= (uint32_t)CS_WIN;
-        if (staged)
-            for (uint32_t t = threadIdx.x; t < wn; t += SL_BLK) win[t] = a[ws + t];
+        if (staged) {   // eight loads in flight per lane (a plain loop issued one load per round trip)
+            for (uint32_t t0 = threadIdx.x; t0 < wn; t0 += 8u * SL_BLK) {
+                uint32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = a[ws + min(t0 + u * SL_BLK, wn - 1u)];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (t0 + u * SL_BLK < wn) win[t0 + u * SL_BLK] = v[u];
+            }
+        }
         __syncthreads();
         for (uint32_t k = max(k0, c0); k < min(k0 + 4u, c1); ++k) {
             uint32_t lb;

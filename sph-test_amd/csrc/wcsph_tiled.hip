@@ -182,6 +182,29 @@ __device__ __forceinline__ float dist2(float4 a, float4 b) {
     return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
 }
 
+// SPH_RUNITS (default 1): both passes evaluate the kernel in units of r instead of q = r/h: the powers of h go
+// into per-launch constants (SphConst two_h, m6h, four_h3, rho_scale; PairK), which takes the r²·(1/h²) multiply
+// out of pass 1's candidate loop and q, q² and one h factor out of pass 2's pair body. 0: the q forms below.
+#ifndef SPH_RUNITS
+#define SPH_RUNITS 1
+#endif
+
+#if SPH_RUNITS
+// h³·4·w(q) of the unnormalised cubic spline (W = σ·w), r = |x_i − x_j|: min(4h³ + r²(3r − 6h), max(2h − r, 0)³),
+// the q form below times h³. v = 2h − r comes back: its sign bit is set exactly for the candidates that are NOT
+// neighbours (r > 2h, with r = sqrt(r²) rounded as here), the hit bit pass 1 records and is_hit tests.
+__device__ __forceinline__ float spline_w4(const SphConst& c, float r2, float& v) {
+    const float r = __builtin_amdgcn_sqrtf(r2);
+    v = c.two_h - r;
+    const float t = __builtin_amdgcn_fmed3f(v, 0.0f, c.two_h);   // max(v, 0) (v ≤ 2h); fmaxf adds a canonicalize
+    return fminf(fmaf(r2, fmaf(3.0f, r, c.m6h), c.four_h3), t * t * t);
+}
+
+// The neighbour test of both passes, for paths without the hit mask: the bit pass 1 records.
+__device__ __forceinline__ bool is_hit(const SphConst& c, float r2) {
+    return (__float_as_uint(c.two_h - __builtin_amdgcn_sqrtf(r2)) >> 31) == 0u;
+}
+#else
 // 4·w(q) of the unnormalised cubic spline (W = σ·w) for q ≤ 2, else 0. Branchless: both arms
 // are computed and selected (a ?: over expressions compiles to an exec branch per candidate).
 // Scaling by 4 (and the final 0.25) is exact in binary floating point: no rounding is added.
@@ -205,6 +228,7 @@ __device__ __forceinline__ float spline_w4(const SphConst& c, float r2, float& v
 __device__ __forceinline__ bool is_hit(const SphConst& c, float r2) {
     return (__float_as_uint(2.0f - __builtin_amdgcn_sqrtf(r2 * c.inv_h2)) >> 31) == 0u;
 }
+#endif
 
 // The scans use x, y, z only, and the compiler then narrows the float4 LDS read to
 // ds_read_b96: 8 LDS cycles per wave with 32-bank grouping, against 4 for ds_read_b128
@@ -485,7 +509,11 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
     if (!valid) return;
     if (mn > 0 && wp < wend)   // the last, partial word: bits [0, mn), zeros above
         *wp = __builtin_bitreverse32(~ml << (32 - mn));
+#if SPH_RUNITS
+    const float d = c.rho_scale * s;   // m·σ·(h³·4w)/(4h³)
+#else
     const float d = c.mass * (c.sigma * (0.25f * s));
+#endif
     const float tr = d * c.inv_rho0;
     const float t2 = tr * tr, t4 = t2 * t2;
     const float P = c.B * (t4 * t2 * tr - 1.0f);
@@ -516,6 +544,7 @@ struct ForceAcc {
 // splash particles past the parity bound (tests/test_gpu_parity_headline.py).
 struct PairK {
     float inv_h, h, kvisc, eta2, kf, kx;
+    float two_h, m6h, four_h3, m2h;
 };
 
 static PairK pair_constants(const SphConst& c) {
@@ -524,8 +553,18 @@ static PairK pair_constants(const SphConst& c) {
     k.h = c.h;
     k.kvisc = -2.0f * c.ac0 * c.h;            // inv_rbar = 2/(ρi + ρj)
     k.eta2 = c.eta2;
+#if SPH_RUNITS
+    // r units: the pair body's G and w4 carry one and three more factors of h than their q forms
+    k.kf = 0.75f * c.mass * c.sigma_h2 * c.inv_h;
+    k.kx = 0.5f * c.eps * c.mass * c.sigma / c.four_h3 * 4.0f;
+#else
     k.kf = 0.75f * c.mass * c.sigma_h2;
     k.kx = 0.5f * c.eps * c.mass * c.sigma;
+#endif
+    k.two_h = c.two_h;
+    k.m6h = c.m6h;
+    k.four_h3 = c.four_h3;
+    k.m2h = -c.two_h;
     return k;
 }
 
@@ -537,6 +576,16 @@ __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi,
     const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
     const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));   // explicit chains: the same rounding on every path
     const float rs = __builtin_amdgcn_rsqf(fmaxf(r2, 1e-30f));
+#if SPH_RUNITS
+    // r units: w4·h³ = 4h³ + r²(3r − 6h) or (2h − r)³, G·h = 4h − 3r or (2h − r)²/r
+    const float r = r2 * rs;
+    const float t = k.two_h - r;
+    const float t2 = t * t;
+    const bool inner = r < k.h;
+    const float c36 = fmaf(3.0f, r, k.m6h);
+    const float w_in = fmaf(r2, c36, k.four_h3), w_out = t2 * t;
+    const float g_in = k.m2h - c36, g_out = t2 * rs;
+#else
     const float q = r2 * rs * k.inv_h;
     const float t = 2.0f - q;
     const float t2 = t * t;
@@ -545,6 +594,7 @@ __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi,
     const float c36 = fmaf(3.0f, q, -6.0f);
     const float w_in = fmaf(q * q, c36, 4.0f), w_out = t2 * t;
     const float g_in = -2.0f - c36, g_out = t2 * rs * k.h;
+#endif
     const float w4 = inner ? w_in : w_out;
     const float G = inner ? g_in : g_out;
     const float du = vi.x - vj.x, dv = vi.y - vj.y, dw = vi.z - vj.z;
