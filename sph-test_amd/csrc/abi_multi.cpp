@@ -586,16 +586,20 @@ int phase_assemble(RankState& R, bool exact) {
                            (uint32_t)std::max(ctx->capacity, 1), &R.dz->flags};
         const uint32_t key_base = (uint32_t)ctx->grid.cx0 * gyz(ctx);
         CKPT(R, "exchange 1");
-        if (nl_ub + nr_ub > 0) {   // every rank with a neighbour (capacities are >= 512)
-            KTimer t(ctx, "slab_assemble", 40.0 * (double)(nl_ub + nr_ub));
-            launch_slab_rec(src, n_ub, ctx->grid, key_base, ctx->vals, ctx->keys2, mv, s, &sizes);  // grid: nl_ub + nr_ub
-        }
-        CKPT(R, "sizes + slab_rec");
         KTimer t(ctx, "resort", (double)R.n_ub * (2 * 4 + 2 * 36), true);
-        if (ctx->has_left || ctx->has_right)   // without neighbours the own block keeps its cell starts
-            launch_slab_cs_old(ctx->cs, ctx->grid.ncells, gyz(ctx), (uint32_t)ctx->grid.gx, ctx->has_left,
-                               ctx->has_right, 0, ctx->keys2, 0, 0, 0, s, R.dz);
-        CKPT(R, "cs_old");
+        if (nl_ub + nr_ub > 0) {   // every rank with a neighbour (capacities are >= 512)
+            // the records' keys and movers, the sizes, and the old cell-start table in one launch (without
+            // neighbours the own block keeps its cell starts)
+            CsOld csp;
+            csp.cs = ctx->cs;
+            csp.ncells = ctx->grid.ncells;
+            csp.gyz = gyz(ctx);
+            csp.gx = (uint32_t)ctx->grid.gx;
+            csp.has_left = ctx->has_left ? 1 : 0;
+            csp.has_right = ctx->has_right ? 1 : 0;
+            launch_slab_rec(src, n_ub, ctx->grid, key_base, ctx->vals, ctx->keys2, mv, s, &sizes, csp);  // grid: nl_ub + nr_ub
+        }
+        CKPT(R, "sizes + slab_rec + cs_old");
         if (ctx->cfg.flags & SPH_FLAG_VALIDATE) {
             int r = validate_movers(R, used);
             if (r != SPH_OK) return r;

@@ -357,7 +357,104 @@ struct AsmSrc {
     int32_t nl, nre;
     const SlabSizes* dz;    // non-null: nl, nre, o_off (and the slot count) live on the device
 };
+// The old cell-start table of the assembled layout (slab.hip k_slab_cs_old), as extra workgroups of a launch.
+struct CsOld {
+    uint32_t* cs = nullptr;   // null: none
+    uint32_t ncells = 0, gyz = 0, gx = 0;
+    int32_t has_left = 0, has_right = 0;
+};
 #if defined(__HIPCC__)
+// The cell-start table of the assembled old keys [left | own | right], for the incremental re-sort, made from the
+// previous step's table in place, by the workgroup `blk` (four cells per lane; 1,024 per workgroup). Owned columns:
+// the own block kept its order, so cs[k] shifts by nl − o0 (o0: the previous owned start), one 16-byte load and
+// store per lane (the table is ~15 MB at C3). cs[ncells] = cs[ncells + 1] = n. Halo columns: the lower bound of
+// cell k in its block's sorted old keys key(side, t): the workgroup stages every S-th key in LDS (S >= 64, at most
+// CS_SAMP samples), finds from them a record window holding the lower bounds of all its cells, stages that
+// window's keys (eight loads in flight per lane) and searches in LDS: about three global round trips. Measured
+// against (profiles/r04_slab_trace.log, C3 x 4): a binary search per cell in global memory, 16 dependent loads
+// (11 us per launch), and a gap fill by one lane per record (225 us: a lane before an empty stretch of rows
+// writes thousands of cells alone).
+constexpr int CS_SAMP = 1024;
+constexpr int CS_WIN = 6144;
+template <typename K>
+__device__ __forceinline__ void cs_old_block(const CsOld& p, uint32_t blk, uint32_t nl, uint32_t no, uint32_t nr,
+                                             int32_t shift, K key, uint32_t* samp, uint32_t* win) {
+    const uint32_t n = nl + no + nr, ncells = p.ncells;
+    const uint32_t owned_lo = p.has_left ? p.gyz : 0u, owned_hi = p.has_right ? (p.gx - 1u) * p.gyz : ncells;
+    const uint32_t k0 = 4u * (blk * blockDim.x + threadIdx.x);
+    const uint32_t kb0 = 4u * blk * blockDim.x, kb1 = kb0 + 4u * blockDim.x;   // this workgroup's cells
+#pragma unroll 1
+    for (int side = 0; side < 2; ++side) {   // workgroup-uniform
+        const uint32_t r0 = side == 0 ? 0u : owned_hi, r1 = side == 0 ? owned_lo : ncells;   // halo cells
+        if (!(side == 0 ? p.has_left : p.has_right) || kb1 <= r0 || kb0 >= r1) continue;
+        const uint32_t c0 = max(kb0, r0), c1 = min(kb1, r1);
+        const uint32_t base = side == 0 ? 0u : nl + no, len = side == 0 ? nl : nr;
+        const uint32_t S = max(64u, (len + CS_SAMP - 1u) / CS_SAMP), ns = (len + S - 1u) / S;
+        __syncthreads();
+        for (uint32_t t0 = threadIdx.x; t0 < ns; t0 += 4u * blockDim.x) {
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = key(side, min(t0 + u * blockDim.x, ns - 1u) * S);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (t0 + u * blockDim.x < ns) samp[t0 + u * blockDim.x] = v[u];
+        }
+        __syncthreads();
+        uint32_t j0, j1;   // samples below c0 / c1: lb(c0) >= (j0 - 1)·S + 1 (or 0), lb(c1) <= min(j1·S, len)
+        {
+            uint32_t lo = 0u, hi = ns;
+            while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (samp[m] < c0) lo = m + 1u; else hi = m; }
+            j0 = lo;
+            hi = ns;
+            while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (samp[m] < c1) lo = m + 1u; else hi = m; }
+            j1 = lo;
+        }
+        const uint32_t ws = j0 == 0u ? 0u : (j0 - 1u) * S + 1u, we = min(j1 * S, len);
+        const uint32_t wn = we > ws ? we - ws : 0u;
+        const bool staged = wn <= (uint32_t)CS_WIN;
+        if (staged) {
+            for (uint32_t t0 = threadIdx.x; t0 < wn; t0 += 8u * blockDim.x) {
+                uint32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = key(side, ws + min(t0 + u * blockDim.x, wn - 1u));
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (t0 + u * blockDim.x < wn) win[t0 + u * blockDim.x] = v[u];
+            }
+        }
+        __syncthreads();
+        for (uint32_t k = max(k0, c0); k < min(k0 + 4u, c1); ++k) {
+            uint32_t lo = ws, hi = we;
+            if (staged) {
+                lo = 0u;
+                hi = wn;
+                while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (win[m] < k) lo = m + 1u; else hi = m; }
+                lo += ws;
+            } else {
+                while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (key(side, m) < k) lo = m + 1u; else hi = m; }
+            }
+            p.cs[k] = base + lo;
+        }
+    }
+    if (k0 > ncells + 1u) return;
+    if (k0 + 3u < owned_hi && k0 >= owned_lo) {   // four owned cells (cs is 16-byte aligned)
+        if (shift != 0) {
+            uint4 v = reinterpret_cast<uint4*>(p.cs)[k0 >> 2];
+            v.x = (uint32_t)((int32_t)v.x + shift);
+            v.y = (uint32_t)((int32_t)v.y + shift);
+            v.z = (uint32_t)((int32_t)v.z + shift);
+            v.w = (uint32_t)((int32_t)v.w + shift);
+            reinterpret_cast<uint4*>(p.cs)[k0 >> 2] = v;
+        }
+        return;
+    }
+    for (uint32_t k = k0; k < k0 + 4u && k <= ncells + 1u; ++k) {
+        if (k >= ncells) p.cs[k] = n;
+        else if (k >= owned_lo && k < owned_hi && shift != 0) p.cs[k] = (uint32_t)((int32_t)p.cs[k] + shift);
+    }
+}
+inline int32_t cs_old_blocks(uint32_t ncells, int32_t blk) { return (int32_t)(((ncells + 2u + 3u) / 4u + blk - 1) / blk); }
+
 // the device-sized slab step: the assembled array's layout from SlabSizes (see AsmSrc)
 __device__ __forceinline__ void resolve_sizes(AsmSrc& a, ResortScratch& w, int32_t& n) {
     if (!a.dz) return;
@@ -376,8 +473,9 @@ inline AsmSrc asm_plain(const float4* pos, const float4* vel, const int32_t* id,
 // the slab step's halo records (slots [0, nl) and [nre, n)): new keys (window sentinel) into
 // src.keyr, old keys moved into this window and clamped into src.skr, and every record whose key
 // changed appended to the sink (mi = slot | MV_REC) after the own movers the force pass appended
+// cs (optional): the device-sized step's old cell-start table in the same launch, from the messages' old keys
 void launch_slab_rec(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base, uint32_t* keyr, uint32_t* skr,
-                     MoverSink sink, hipStream_t s, const SizesIn* sizes = nullptr);
+                     MoverSink sink, hipStream_t s, const SizesIn* sizes = nullptr, CsOld cs = CsOld{});
 // cell-start values to pick once the table is final: out[t] = cs[idx[t]] (device), and the same
 // into out_host (mapped pinned memory) when given; m = 0: none
 struct CsPick {

@@ -351,15 +351,40 @@ constexpr int MV_DET_PER = 4;
 constexpr int MV_DET = MV_BLK * MV_DET_PER;
 constexpr uint32_t REC_NO_KEY = 0xffffffffu;   // slab.hip SL_NO_KEY
 
+// A record's old key moved into this window and clamped into [0, ncells - 1] (the clamp in 64-bit: the u32 form
+// `og < base ? 0 : min(og - base, ncells - 1)` compiled to a plain subtract + min on ROCm 7.2, so keys below the
+// window wrapped); a record without an old key takes its side's bound.
+__device__ __forceinline__ uint32_t rec_old_key(uint32_t og, bool left, uint32_t key_base, uint32_t ncells) {
+    if (og == REC_NO_KEY) return left ? 0u : ncells - 1u;
+    const int64_t d = (int64_t)og - (int64_t)key_base;
+    return (uint32_t)(d < 0 ? 0 : (d > (int64_t)ncells - 1 ? (int64_t)ncells - 1 : d));
+}
+
+// Workgroups [nb_rec, nb_rec + cs_old_blocks) build the old cell-start table (common.h cs_old_block) in the same
+// launch, from the messages' old keys: no launch between the records and the re-sort (profiles/r04_slab_trace.log).
 __global__ __launch_bounds__(MV_BLK) void k_slab_rec(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base,
                                                      uint32_t* __restrict__ keyr, uint32_t* __restrict__ skr,
-                                                     MoverSink sink, SizesIn in, int32_t from_headers) {
+                                                     MoverSink sink, SizesIn in, int32_t from_headers, CsOld csp,
+                                                     int32_t nb_rec) {
     __shared__ uint32_t wsum[MV_BLK / 64];
     __shared__ uint32_t base_s;
+    __shared__ uint32_t samp[CS_SAMP];
+    __shared__ uint32_t win[CS_WIN];
     if (from_headers) {   // device-sized slab step: every workgroup derives the layout from the headers,
         uint32_t nl, no, nr, f;   // the first stores it for the kernels after this one
         slab_sizes_from(src.dz, in, nl, no, nr, f);
         if (blockIdx.x == 0 && threadIdx.x == 0) slab_sizes_store(const_cast<SlabSizes*>(src.dz), nl, no, nr, f);
+        if (csp.cs && (int32_t)blockIdx.x >= nb_rec) {   // the old cell-start table
+            const float4* rl = src.rl;
+            const float4* rr = src.rr;
+            const uint32_t ncells = g.ncells;
+            auto key = [&](int side, uint32_t t) {
+                const float4* rec = side == 0 ? rl : rr;
+                return rec_old_key(__float_as_uint(rec[2 * (size_t)t + 1].w), side == 0, key_base, ncells);
+            };
+            cs_old_block(csp, blockIdx.x - (uint32_t)nb_rec, nl, no, nr, (int32_t)nl - (int32_t)src.dz->o0, key, samp, win);
+            return;
+        }
         src.nl = (int32_t)nl;
         src.nre = (int32_t)(nl + no);
         n = (int32_t)(nl + no + nr);
@@ -388,12 +413,7 @@ __global__ __launch_bounds__(MV_BLK) void k_slab_rec(AsmSrc src, int32_t n, Grid
     for (int j = 0; j < MV_DET_PER; ++j) {
         const bool left = xs[j] < src.nl;
         kn[j] = window_key(g, pv[j].x, pv[j].y, pv[j].z);
-        if (og[j] == REC_NO_KEY) ko[j] = left ? 0u : g.ncells - 1u;
-        else {   // clamp og - key_base into [0, ncells - 1] in 64-bit (the u32 form `og < base ? 0 : min(og - base,
-                 // ncells - 1)` compiled to a plain subtract + min on ROCm 7.2, so keys below the window wrapped)
-            const int64_t d = (int64_t)og[j] - (int64_t)key_base;
-            ko[j] = (uint32_t)(d < 0 ? 0 : (d > (int64_t)g.ncells - 1 ? (int64_t)g.ncells - 1 : d));
-        }
+        ko[j] = rec_old_key(og[j], left, key_base, g.ncells);
         if (r0 + j * MV_BLK < nrec) {
             keyr[xs[j]] = kn[j];
             skr[xs[j]] = ko[j];
@@ -439,11 +459,13 @@ __global__ __launch_bounds__(MV_BLK) void k_slab_rec(AsmSrc src, int32_t n, Grid
 }
 
 void launch_slab_rec(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base, uint32_t* keyr, uint32_t* skr,
-                     MoverSink sink, hipStream_t s, const SizesIn* sizes) {
+                     MoverSink sink, hipStream_t s, const SizesIn* sizes, CsOld cs) {
     const int32_t nrec = src.nl + (n - src.nre);
-    if (nrec > 0)
-        k_slab_rec<<<(nrec + MV_DET - 1) / MV_DET, MV_BLK, 0, s>>>(src, n, g, key_base, keyr, skr, sink,
-                                                                  sizes ? *sizes : SizesIn{}, sizes ? 1 : 0);
+    const int32_t nb_rec = (nrec + MV_DET - 1) / MV_DET;
+    const int32_t nb_cs = cs.cs && sizes ? cs_old_blocks(g.ncells, MV_BLK) : 0;   // the fused table: device-sized steps
+    if (nb_rec + nb_cs > 0)
+        k_slab_rec<<<nb_rec + nb_cs, MV_BLK, 0, s>>>(src, n, g, key_base, keyr, skr, sink, sizes ? *sizes : SizesIn{},
+                                                     sizes ? 1 : 0, nb_cs ? cs : CsOld{}, nb_rec);
 }
 
 void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* count,

@@ -314,114 +314,22 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_unpack(const float4* __restrict
     id[i] = __float_as_int(a.w);
 }
 
-// The cell-start table of the assembled old keys [left | own | right] (sk), for the incremental
-// re-sort, made from the previous step's table in place. Owned columns: the own block kept its
-// order, so cs[k] shifts by nl − o0 (o0: the previous owned start); four cells per lane, one 16-byte
-// load and store (the table is ~15 MB at C3). cs[ncells] = cs[ncells + 1] = n.
-// Halo columns: the lower bound of cell k in the block's sorted old keys. A workgroup (1,024 cells) stages every
-// S-th key of the block in LDS (S >= 64, at most 1,024 samples), finds from them a record window that holds the
-// lower bounds of all its cells, stages that window's keys in LDS (coalesced), and searches there: about three
-// global round trips per workgroup. Measured against (profiles/r04_slab_trace*.log, C3 x 4): a binary search per
-// cell in global memory, 16 dependent loads (11 us per launch), and a gap fill by one lane per record, whose lane
-// before an empty stretch of rows wrote thousands of cells alone (225 us).
-constexpr int CS_SAMP = 1024;
-constexpr int CS_WIN = 6144;
-
-__device__ __forceinline__ uint32_t lb_range(const uint32_t* __restrict__ a, uint32_t lo, uint32_t hi, uint32_t k) {
-    while (lo < hi) {   // the first index in [lo, hi) with a[index] >= k, or hi
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a[mid] < k) lo = mid + 1u;
-        else hi = mid;
-    }
-    return lo;
-}
-
-__global__ __launch_bounds__(SL_BLK) void k_slab_cs_old(uint32_t* __restrict__ cs, uint32_t ncells, uint32_t gyz,
-                                                        uint32_t gx, int32_t has_left, int32_t has_right,
-                                                        int32_t shift, const uint32_t* __restrict__ sk,
+// The per-phase path's old cell-start table (common.h cs_old_block; the in-library step runs the same body inside
+// k_slab_rec, reading the old keys from the messages).
+__global__ __launch_bounds__(SL_BLK) void k_slab_cs_old(CsOld p, int32_t shift, const uint32_t* __restrict__ sk,
                                                         int32_t nl, int32_t no, int32_t nr,
                                                         const SlabSizes* __restrict__ dz) {
     __shared__ uint32_t samp[CS_SAMP];
     __shared__ uint32_t win[CS_WIN];
-    const uint32_t k0 = 4u * (blockIdx.x * SL_BLK + threadIdx.x);
     if (dz) {
         nl = (int32_t)dz->nl;
         no = (int32_t)dz->no;
         nr = (int32_t)dz->nr;
         shift = nl - (int32_t)dz->o0;
     }
-    const uint32_t n = (uint32_t)(nl + no + nr);
-    // the owned cells: [owned_lo, owned_hi) (halo columns are the first / last column when present)
-    const uint32_t owned_lo = has_left ? gyz : 0u, owned_hi = has_right ? (gx - 1u) * gyz : ncells;
-    const uint32_t kb0 = 4u * blockIdx.x * SL_BLK, kb1 = kb0 + 4u * SL_BLK;   // this workgroup's cells
-#pragma unroll 1
-    for (int side = 0; side < 2; ++side) {   // workgroup-uniform
-        const uint32_t r0 = side == 0 ? 0u : owned_hi, r1 = side == 0 ? owned_lo : ncells;   // halo cells
-        if (!(side == 0 ? has_left : has_right) || kb1 <= r0 || kb0 >= r1) continue;
-        const uint32_t c0 = max(kb0, r0), c1 = min(kb1, r1);   // this workgroup's halo cells
-        const uint32_t base = side == 0 ? 0u : (uint32_t)(nl + no), len = (uint32_t)(side == 0 ? nl : nr);
-        const uint32_t* a = sk + base;
-        const uint32_t S = max(64u, (len + CS_SAMP - 1u) / CS_SAMP), ns = (len + S - 1u) / S;
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < CS_SAMP / SL_BLK; ++u) {
-            const uint32_t t = threadIdx.x + u * SL_BLK;
-            if (t < ns) samp[t] = a[t * S];
-        }
-        __syncthreads();
-        // samples below c0 / c1: lb(c0) >= (j0 - 1)·S + 1 (or 0), lb(c1) <= min(j1·S, len)
-        uint32_t j0 = 0u, j1 = ns;
-        {
-            uint32_t lo = 0u, hi = ns;
-            while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (samp[m] < c0) lo = m + 1u; else hi = m; }
-            j0 = lo;
-            hi = ns;
-            while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (samp[m] < c1) lo = m + 1u; else hi = m; }
-            j1 = lo;
-        }
-        const uint32_t ws = j0 == 0u ? 0u : (j0 - 1u) * S + 1u, we = min(j1 * S, len);
-        const uint32_t wn = we > ws ? we - ws : 0u;
-        const bool staged = wn <= (uint32_t)CS_WIN;
-        if (staged) {   // eight loads in flight per lane (a plain loop issued one load per round trip)
-            for (uint32_t t0 = threadIdx.x; t0 < wn; t0 += 8u * SL_BLK) {
-                uint32_t v[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = a[ws + min(t0 + u * SL_BLK, wn - 1u)];
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (t0 + u * SL_BLK < wn) win[t0 + u * SL_BLK] = v[u];
-            }
-        }
-        __syncthreads();
-        for (uint32_t k = max(k0, c0); k < min(k0 + 4u, c1); ++k) {
-            uint32_t lb;
-            if (staged) {
-                uint32_t lo = 0u, hi = wn;
-                while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (win[m] < k) lo = m + 1u; else hi = m; }
-                lb = ws + lo;
-            } else {
-                lb = lb_range(a, ws, we, k);
-            }
-            cs[k] = base + lb;
-        }
-    }
-    if (k0 > ncells + 1u) return;
-    if (k0 + 3u < owned_hi && k0 >= owned_lo) {   // four owned cells (cs is 16-byte aligned)
-        if (shift != 0) {
-            uint4 v = reinterpret_cast<uint4*>(cs)[k0 >> 2];
-            v.x = (uint32_t)((int32_t)v.x + shift);
-            v.y = (uint32_t)((int32_t)v.y + shift);
-            v.z = (uint32_t)((int32_t)v.z + shift);
-            v.w = (uint32_t)((int32_t)v.w + shift);
-            reinterpret_cast<uint4*>(cs)[k0 >> 2] = v;
-        }
-        return;
-    }
-    for (uint32_t k = k0; k < k0 + 4u && k <= ncells + 1u; ++k) {
-        if (k >= ncells) cs[k] = n;
-        else if (k >= owned_lo && k < owned_hi && shift != 0) cs[k] = (uint32_t)((int32_t)cs[k] + shift);
-        // halo cells: written above
-    }
+    const uint32_t rbase = (uint32_t)(nl + no);
+    auto key = [&](int side, uint32_t t) { return sk[(side == 0 ? 0u : rbase) + t]; };
+    cs_old_block(p, blockIdx.x, (uint32_t)nl, (uint32_t)no, (uint32_t)nr, shift, key, samp, win);
 }
 
 // ---- init-time selection of owned columns (global grid in `g`)
@@ -671,9 +579,14 @@ void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, 
 void launch_slab_cs_old(uint32_t* cs, uint32_t ncells, uint32_t gyz, uint32_t gx, bool has_left, bool has_right,
                         int32_t shift, const uint32_t* sk, int32_t nl, int32_t no, int32_t nr, hipStream_t s,
                         const SlabSizes* dz) {
-    const uint32_t m = (ncells + 2u + 3u) / 4u;   // four cells per lane
-    SPH_LAUNCH(k_slab_cs_old, (m + SL_BLK - 1) / SL_BLK, SL_BLK, 0, s, cs, ncells, gyz, gx, has_left ? 1 : 0,
-               has_right ? 1 : 0, shift, sk, nl, no, nr, dz);
+    CsOld p;
+    p.cs = cs;
+    p.ncells = ncells;
+    p.gyz = gyz;
+    p.gx = gx;
+    p.has_left = has_left ? 1 : 0;
+    p.has_right = has_right ? 1 : 0;
+    SPH_LAUNCH(k_slab_cs_old, cs_old_blocks(ncells, SL_BLK), SL_BLK, 0, s, p, shift, sk, nl, no, nr, dz);
 }
 
 void launch_slab_select_columns(const float4* pos, const float4* vel, const int32_t* id, int32_t n, GridDesc g,
