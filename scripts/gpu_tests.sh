@@ -1,5 +1,8 @@
+# The GPU suite and smoke on the current head.
 set +e
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=600 -x > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
-exit $rc
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout=600 --timeout-method thread -rA > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc"; grep -E "passed|failed|FAILED" gpurun_out/pytest_gpu.log | tail -5
+[ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; echo "smoke rc=$?"; tail -1 gpurun_out/smoke.log
+exit 0
