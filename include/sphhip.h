@@ -262,7 +262,9 @@ int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int3
                          uint32_t* perm_out, uint32_t* sorted_keys_out);
 /* Test hook, Model S: add dv to the velocity of particle `id` between steps, in every context of a
  * group that holds it (tests/test_gpu_multi.py: a particle made to cross several slab columns in one
- * step, the decomposition's column-jump fallback and its window-exit stop). Not a Unity call. */
+ * step, the decomposition's column-jump fallback and its window-exit stop). Not a Unity call.
+ * On an RCCL rank every rank calls it between the same two steps (the next step then re-packs its
+ * halo messages instead of using the ones sent during the last step, on every rank alike). */
 int sph_debug_kick(sph_ctx* ctx, int32_t id, const float dv[3]);
 
 /* ---- slab decomposition (multi-GPU; SPEC_SPH.md §3). New capability: the reference is one

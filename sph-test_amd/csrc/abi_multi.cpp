@@ -30,7 +30,10 @@ namespace sph {
 
 constexpr int LAG_SLOTS = 4;
 constexpr int LAG_WORDS = 16;
-constexpr int SDEV_TOTALS = 10;   // sdev[10..11]: this step's send counts (sdev[0..7] picks, [8..9] gap counters)
+constexpr int SDEV_TOTALS = 10;   // sdev[10..13]: send counts, two slots by step parity (sdev[0..7] picks, [8..9] gaps)
+// The send counts of step `step` (the early sends of step s + 1 are packed while step s's bookkeeping still reads
+// step s's counts, so the two live in different slots).
+uint32_t* totals_slot(sph_ctx* c, int64_t step) { return c->sdev + SDEV_TOTALS + 2 * (int)(step & 1); }
 
 struct RankState {
     sph_ctx* c = nullptr;
@@ -39,6 +42,10 @@ struct RankState {
     hipEvent_t ev_packed = nullptr, ev_in = nullptr;  // exchange 1: messages packed / received
     hipEvent_t ev_rho_packed = nullptr, ev_rho_recv = nullptr;
     hipEvent_t ev_bdone = nullptr;   // the boundary force pass (comm stream) is done: the step's end waits on it
+    hipEvent_t ev_sent = nullptr;    // early sends: the next step's messages have arrived (comm stream)
+    hipEvent_t ev_fdone = nullptr;   // early sends without the jump guard: the interior force pass is done
+    int32_t e_c1o[2] = {0, 0}, e_c1i[2] = {0, 0};   // the next step's message capacities (early sends)
+    int32_t g2[2] = {0, 0};          // grid bounds of the two-column boundary ranges (early sends), 0: n_ub
     SlabSizes* dz = nullptr;
     float4* msg_out[2] = {nullptr, nullptr};
     float4* msg_in[2] = {nullptr, nullptr};
@@ -75,6 +82,8 @@ struct Multi {
     int64_t n_total = 0;
     bool ready = false;
     int64_t steps = 0;
+    bool early = false;              // this step's messages were packed and exchanged during the previous step
+    int hold_early = 0;              // steps to run without early sends (after a host-side state change)
 };
 
 namespace {
@@ -218,7 +227,7 @@ int rank_init(RankState& R) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipStreamCreateWithFlags(&R.comm, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&R.ev_packed, &R.ev_in, &R.ev_rho_packed, &R.ev_rho_recv, &R.ev_bdone})
+    for (hipEvent_t* e : {&R.ev_packed, &R.ev_in, &R.ev_rho_packed, &R.ev_rho_recv, &R.ev_bdone, &R.ev_sent, &R.ev_fdone})
         HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     for (auto& e : R.lag_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipMalloc((void**)&R.dz, sizeof(SlabSizes)));
@@ -226,7 +235,7 @@ int rank_init(RankState& R) {
     R.c->dz = R.dz;
     HIPCHK(hipMalloc((void**)&R.cnt_dev, 12 * sizeof(uint32_t)));
     HIPCHK(hipMemset(R.cnt_dev, 0, 12 * sizeof(uint32_t)));
-    HIPCHK(hipMemset(R.c->sdev + SDEV_TOTALS, 0, 2 * sizeof(uint32_t)));
+    HIPCHK(hipMemset(R.c->sdev + SDEV_TOTALS, 0, 4 * sizeof(uint32_t)));
     HIPCHK(hipHostMalloc((void**)&R.lag, LAG_SLOTS * LAG_WORDS * sizeof(uint32_t), hipHostMallocMapped));
     std::memset(R.lag, 0, LAG_SLOTS * LAG_WORDS * sizeof(uint32_t));
     return SPH_OK;
@@ -236,7 +245,7 @@ void rank_free(RankState& R) {
     if (!R.c) return;
     (void)hipSetDevice(R.c->device);
     if (R.comm) (void)hipStreamSynchronize(R.comm);
-    for (hipEvent_t e : {R.ev_packed, R.ev_in, R.ev_rho_packed, R.ev_rho_recv, R.ev_bdone})
+    for (hipEvent_t e : {R.ev_packed, R.ev_in, R.ev_rho_packed, R.ev_rho_recv, R.ev_bdone, R.ev_sent, R.ev_fdone})
         if (e) (void)hipEventDestroy(e);
     for (auto e : R.lag_ev)
         if (e) (void)hipEventDestroy(e);
@@ -395,7 +404,7 @@ int validate_movers(RankState& R, int used) {
 // full-sort step (SPH_RESORT=0, or a step past the mover limit) every own slot is scanned.
 bool steady_sends(const RankState& R) { return R.since_cut >= 3 && R.jump_guard; }
 
-int phase_count(RankState& R, bool exact) {
+int phase_count(RankState& R, bool exact, int64_t step) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
     if (!ctx->keys_valid) {   // after init or a re-cut: keys of the owned slots in the (new) window
@@ -412,12 +421,12 @@ int phase_count(RankState& R, bool exact) {
     R.nb_send = slab_send_blocks(0, (int32_t)std::max<int64_t>(R.n_prev_ub, 1));
     KTimer t(ctx, "slab_count", 4.0 * R.n_prev_ub);
     launch_slab_count_dev(ctx->keys, R.dz, R.nb_send, gyz(ctx), col_le(ctx), col_ge(ctx), ctx->sblk,
-                          ctx->sdev + SDEV_TOTALS, ctx->stream, steady_sends(R), exact);
+                          totals_slot(ctx, step), ctx->stream, steady_sends(R), exact);
     CKPT(R, "count");
     return SPH_OK;
 }
 
-int phase_pack(RankState& R, Multi& M) {
+int phase_pack(RankState& R, Multi& M, int64_t step) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
     for (int s = 0; s < 2; ++s) {
@@ -435,7 +444,7 @@ int phase_pack(RankState& R, Multi& M) {
         launch_slab_pack2_dev(ctx->keys, ctx->pos, ctx->vel, ctx->id, ctx->sk_valid ? ctx->sk_cur : nullptr,
                               (uint32_t)ctx->grid.cx0 * gyz(ctx), R.dz, R.nb_send, gyz(ctx), col_le(ctx), col_ge(ctx),
                               ctx->sblk, R.left >= 0 ? R.msg_out[0] : nullptr, R.c1o[0],
-                              R.right >= 0 ? R.msg_out[1] : nullptr, R.c1o[1], ctx->sdev + SDEV_TOTALS, ctx->stream,
+                              R.right >= 0 ? R.msg_out[1] : nullptr, R.c1o[1], totals_slot(ctx, step), ctx->stream,
                               steady_sends(R));
     }
     HIPCHK(hipGetLastError());
@@ -447,14 +456,14 @@ int phase_pack(RankState& R, Multi& M) {
 }
 
 // ---------------------------------------------------------------- exchanges
-int exchange_counts(Multi& M, sph_ctx* pctx) {
+int exchange_counts(Multi& M, sph_ctx* pctx, int64_t step) {
     // exact-size steps: the host reads every local rank's send counts, then learns the neighbours'
     for (auto& R : M.ranks) {
         sph_ctx* ctx = R.c;
         HIPCHK(hipSetDevice(ctx->device));
         uint32_t t[2] = {0, 0};
         if (R.left >= 0 || R.right >= 0) {
-            HIPCHK(hipMemcpyAsync(t, ctx->sdev + SDEV_TOTALS, 8, hipMemcpyDeviceToHost, ctx->stream));
+            HIPCHK(hipMemcpyAsync(t, totals_slot(ctx, step), 8, hipMemcpyDeviceToHost, ctx->stream));
             HIPCHK(hipStreamSynchronize(ctx->stream));
         }
         R.c1o[0] = R.left >= 0 ? (int32_t)t[0] : 0;
@@ -473,11 +482,11 @@ int exchange_counts(Multi& M, sph_ctx* pctx) {
     (void)pctx;
     NCCLCHK(ncclGroupStart());
     if (R.left >= 0) {
-        NCCLCHK(ncclSend(ctx->sdev + SDEV_TOTALS, 1, ncclUint32, R.left, M.comm, ctx->stream));
+        NCCLCHK(ncclSend(totals_slot(ctx, step), 1, ncclUint32, R.left, M.comm, ctx->stream));
         NCCLCHK(ncclRecv(R.cnt_dev + 0, 1, ncclUint32, R.left, M.comm, ctx->stream));
     }
     if (R.right >= 0) {
-        NCCLCHK(ncclSend(ctx->sdev + SDEV_TOTALS + 1, 1, ncclUint32, R.right, M.comm, ctx->stream));
+        NCCLCHK(ncclSend(totals_slot(ctx, step) + 1, 1, ncclUint32, R.right, M.comm, ctx->stream));
         NCCLCHK(ncclRecv(R.cnt_dev + 1, 1, ncclUint32, R.right, M.comm, ctx->stream));
     }
     NCCLCHK(ncclGroupEnd());
@@ -696,45 +705,64 @@ int phase_density(RankState& R, Multi& M) {
 // grid_ub2 slots) runs in the same launch: the two boundary columns are one launch.
 bool force_dev(sph_ctx* ctx, const uint32_t* lo, const uint32_t* hi, int64_t grid_ub, float dt,
                const uint32_t* lo2 = nullptr, const uint32_t* hi2 = nullptr, int64_t grid_ub2 = 0,
-               hipStream_t st = nullptr) {
+               hipStream_t st = nullptr, bool jump_err = false) {
     MoverSink mv = mover_sink(ctx);
     if (grid_ub <= 0 && grid_ub2 <= 0) return mv.sk != nullptr;
     KTimer t(ctx, "force_integrate", 76.0 * (double)(std::max<int64_t>(grid_ub, 0) + grid_ub2), true);
     mv.err = &ctx->dz->flags;
     mv.jump = &ctx->dz->jump;
+    mv.jump_err = jump_err ? 1 : 0;
     launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, (int32_t)std::max<int64_t>(grid_ub, 0), ctx->grid, ctx->sc,
                        dt, forcing(ctx), ctx->pos2, ctx->vel2, ctx->keys, mv, hit_mask_read(ctx), path_ctr(ctx),
                        st ? st : ctx->stream, DevRange{lo, hi}, DevRange{lo2, hi2}, (int32_t)grid_ub2);
     return mv.sk != nullptr;
 }
 
-int phase_interior(RankState& R, float dt) {
+// early: the next step's messages are packed right after the boundary pass, so that pass takes the two columns at
+// each side a send can come from (lo, lo + 1 | hi − 2, hi − 1; slab.hip send_ranges) and the interior pass the
+// rest; an interior particle that moves two or more columns could then be missed by the sends, so the interior pass
+// reports it (SZ_JUMP_EARLY stops every rank) instead of asking for a full scan.
+int phase_interior(RankState& R, float dt, bool early) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
     // interior columns: [pick[2] or pick[1], pick[3] or pick[4]) (empty when a one-column slab has both
-    // neighbours: then the bound is below the start and every workgroup exits)
+    // neighbours: then the bound is below the start and every workgroup exits); early: [pick[6], pick[7])
     const uint32_t* pk = R.dz->pick;
-    R.jump_guard = force_dev(ctx, ctx->has_left ? &pk[2] : &pk[1], ctx->has_right ? &pk[3] : &pk[4], R.n_ub, dt);
+    if (early)
+        R.jump_guard = force_dev(ctx, ctx->has_left ? &pk[6] : &pk[1], ctx->has_right ? &pk[7] : &pk[4], R.n_ub, dt,
+                                 nullptr, nullptr, 0, nullptr, true);
+    else
+        R.jump_guard = force_dev(ctx, ctx->has_left ? &pk[2] : &pk[1], ctx->has_right ? &pk[3] : &pk[4], R.n_ub, dt);
+    if (early && !R.jump_guard) HIPCHK(hipEventRecord(R.ev_fdone, ctx->stream));   // the early sends scan all slots
     CKPT(R, "interior force");
     return SPH_OK;
 }
 
-int phase_finish(RankState& R, float dt, int64_t step, bool global_flags) {
+// The ghost ρ and the boundary columns' force pass run on the comm stream, behind the ρ receive (which is ordered
+// after this rank's density pass, exchange2_start), so the boundary workgroups run alongside the interior pass and
+// fill its tail instead of making a small launch of their own after it. early: the two columns at each side, then
+// the next step's counts and messages on the same stream (phase_interior).
+int phase_boundary(RankState& R, Multi& M, float dt, bool early) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
-    hipStream_t s = ctx->stream;
-    // The ghost ρ and the boundary columns' force pass run on the comm stream, behind the ρ receive (which is
-    // ordered after this rank's density pass, exchange2_start), so the boundary workgroups run alongside the
-    // interior pass and fill its tail instead of making a small launch of their own after it. The step's
-    // end (k_slab_lag, and the next step's kernels) waits for them.
     const bool halo = R.left >= 0 || R.right >= 0;
-    hipStream_t b = halo ? R.comm : s;
+    hipStream_t b = halo ? R.comm : ctx->stream;
     launch_slab_unpack_rho2(ctx->rp, R.dz, R.left >= 0 ? R.rho_in[0] : nullptr, R.c2i[0],
                             R.right >= 0 ? R.rho_in[1] : nullptr, R.c2i[1], b);
     CKPT(R, "rho unpack");
     const bool one_col = ctx->sl.cx_hi - ctx->sl.cx_lo == 1;
     const uint32_t* pk = R.dz->pick;
-    if (one_col && (ctx->has_left || ctx->has_right)) {   // the owned column is both boundary columns
+    if (early) {   // lo, lo + 1 | hi − 2, hi − 1 (every slab has at least four columns)
+        const int64_t gl = R.g2[0] > 0 ? std::min<int64_t>(R.g2[0], R.n_ub) : R.n_ub;
+        const int64_t gr = R.g2[1] > 0 ? std::min<int64_t>(R.g2[1], R.n_ub) : R.n_ub;
+        // a boundary particle that moves two columns can leave the candidate columns of the other side too
+        if (ctx->has_left && ctx->has_right)
+            force_dev(ctx, &pk[1], &pk[6], gl, dt, &pk[7], &pk[4], gr, b, true);
+        else if (ctx->has_left)
+            force_dev(ctx, &pk[1], &pk[6], gl, dt, nullptr, nullptr, 0, b, true);
+        else if (ctx->has_right)
+            force_dev(ctx, &pk[7], &pk[4], gr, dt, nullptr, nullptr, 0, b, true);
+    } else if (one_col && (ctx->has_left || ctx->has_right)) {   // the owned column is both boundary columns
         force_dev(ctx, &pk[1], &pk[4], R.n_ub, dt, nullptr, nullptr, 0, b);
     } else if (ctx->has_left && ctx->has_right) {   // both boundary columns in one launch
         force_dev(ctx, &pk[1], &pk[2], std::min<int64_t>(R.c2o[0], R.n_ub), dt, &pk[3], &pk[4],
@@ -743,18 +771,100 @@ int phase_finish(RankState& R, float dt, int64_t step, bool global_flags) {
         if (ctx->has_left) force_dev(ctx, &pk[1], &pk[2], std::min<int64_t>(R.c2o[0], R.n_ub), dt, nullptr, nullptr, 0, b);
         if (ctx->has_right) force_dev(ctx, &pk[3], &pk[4], std::min<int64_t>(R.c2o[1], R.n_ub), dt, nullptr, nullptr, 0, b);
     }
-    if (halo) {
-        HIPCHK(hipEventRecord(R.ev_bdone, b));
-        HIPCHK(hipStreamWaitEvent(s, R.ev_bdone, 0));
-    }
+    if (halo) HIPCHK(hipEventRecord(R.ev_bdone, b));
     CKPT(R, "boundary force");
+    if (!early || !halo) return SPH_OK;
+    // the next step's sends, from this step's order and new positions: capacities from the counts two steps before
+    // the next step (as multi_one_step derives them), one count launch and one pack launch
+    int r = SPH_OK;
+    const uint32_t* L = lag_slot(R, M.steps - 1, ctx, &r);
+    if (r != SPH_OK) return r;
+    R.e_c1o[0] = R.left >= 0 ? cap_of(L[0]) : 0;
+    R.e_c1o[1] = R.right >= 0 ? cap_of(L[1]) : 0;
+    R.e_c1i[0] = R.left >= 0 ? cap_of(L[2]) : 0;
+    R.e_c1i[1] = R.right >= 0 ? cap_of(L[3]) : 0;
+    for (int sd = 0; sd < 2; ++sd) {
+        const int peer = sd == 0 ? R.left : R.right;
+        if (peer < 0) continue;
+        if ((r = ensure_buf(M, ctx, &R.msg_out[sd], &R.mcap_out[sd], MSG_HDR_F4 + 2 * R.e_c1o[sd])) != SPH_OK) return r;
+        if ((r = ensure_buf(M, ctx, &R.msg_in[sd], &R.mcap_in[sd], MSG_HDR_F4 + 2 * R.e_c1i[sd])) != SPH_OK) return r;
+        // the neighbour's copy of this step's message must be done before it is overwritten
+        if (M.mode == 1) HIPCHK(hipStreamWaitEvent(b, M.ranks[peer - M.ranks[0].rank].ev_in, 0));
+    }
+    // without the jump guard (a full-sort step) the sends scan every own slot, after the interior pass
+    const bool cand = R.jump_guard;
+    if (!cand) HIPCHK(hipStreamWaitEvent(b, R.ev_fdone, 0));
+    R.nb_send = slab_send_blocks(0, (int32_t)std::max<int64_t>(R.n_ub, 1));
+    {
+        KTimer t(ctx, "slab_count", 4.0 * R.n_ub);
+        launch_slab_count_dev(ctx->keys, R.dz, R.nb_send, gyz(ctx), col_le(ctx), col_ge(ctx), ctx->sblk,
+                              totals_slot(ctx, M.steps + 1), b, cand, false, true);
+    }
+    {
+        KTimer t(ctx, "slab_pack", 36.0 * (R.e_c1o[0] + R.e_c1o[1]));
+        launch_slab_pack2_dev(ctx->keys, ctx->pos2, ctx->vel2, ctx->id, ctx->sk_valid ? ctx->sk_cur : nullptr,
+                              (uint32_t)ctx->grid.cx0 * gyz(ctx), R.dz, R.nb_send, gyz(ctx), col_le(ctx), col_ge(ctx),
+                              ctx->sblk, R.left >= 0 ? R.msg_out[0] : nullptr, R.e_c1o[0],
+                              R.right >= 0 ? R.msg_out[1] : nullptr, R.e_c1o[1], totals_slot(ctx, M.steps + 1), b, cand,
+                              true);
+    }
+    HIPCHK(hipGetLastError());
+    if (M.mode == 1) HIPCHK(hipEventRecord(R.ev_packed, b));
+    CKPT(R, "early pack");
+    return SPH_OK;
+}
+
+// The next step's halo messages, on the comm streams (early sends): peer copies in a local group, one RCCL group
+// per rank otherwise. The next step's assemble waits for ev_sent.
+int exchange1_early(Multi& M) {
+    if (M.mode == 1) {
+        const int r0 = M.ranks[0].rank;
+        for (auto& R : M.ranks) {
+            sph_ctx* ctx = R.c;
+            HIPCHK(hipSetDevice(ctx->device));
+            for (int s = 0; s < 2; ++s) {
+                const int peer = s == 0 ? R.left : R.right;
+                if (peer < 0) continue;
+                RankState& S = M.ranks[peer - r0];
+                const size_t bytes = (size_t)(MSG_HDR_F4 + 2 * R.e_c1i[s]) * sizeof(float4);
+                HIPCHK(hipStreamWaitEvent(R.comm, S.ev_packed, 0));
+                HIPCHK(hipMemcpyPeerAsync(R.msg_in[s], ctx->device, S.msg_out[1 - s], S.c->device, bytes, R.comm));
+            }
+            if (R.left >= 0 || R.right >= 0) {
+                HIPCHK(hipEventRecord(R.ev_in, R.comm));
+                HIPCHK(hipEventRecord(R.ev_sent, R.comm));
+            }
+        }
+        return SPH_OK;
+    }
+    RankState& R = M.ranks[0];
+    if (R.left < 0 && R.right < 0) return SPH_OK;
+    sph_ctx* ctx = R.c;
+    NCCLCHK(ncclGroupStart());
+    for (int s = 0; s < 2; ++s) {
+        const int peer = s == 0 ? R.left : R.right;
+        if (peer < 0) continue;
+        NCCLCHK(ncclSend(R.msg_out[s], (size_t)(MSG_HDR_F4 + 2 * R.e_c1o[s]) * sizeof(float4), ncclUint8, peer, M.comm,
+                         R.comm));
+        NCCLCHK(ncclRecv(R.msg_in[s], (size_t)(MSG_HDR_F4 + 2 * R.e_c1i[s]) * sizeof(float4), ncclUint8, peer, M.comm,
+                         R.comm));
+    }
+    NCCLCHK(ncclGroupEnd());
+    HIPCHK(hipEventRecord(R.ev_sent, R.comm));
+    return SPH_OK;
+}
+
+int phase_finish(RankState& R, float dt, int64_t step, bool global_flags) {
+    sph_ctx* ctx = R.c;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    if (R.left >= 0 || R.right >= 0) HIPCHK(hipStreamWaitEvent(s, R.ev_bdone, 0));
     swap_sv(ctx);
     ctx->keys_valid = true;
     ctx->steps++;
     ctx->sim_time += (double)dt;
     const int k = (int)(step % LAG_SLOTS);
-    launch_slab_lag(R.dz, ctx->has_left ? 1 : 0, ctx->has_right ? 1 : 0, ctx->sdev + SDEV_TOTALS,
-                    R.left >= 0 ? R.msg_in[0] : nullptr, R.right >= 0 ? R.msg_in[1] : nullptr,
+    launch_slab_lag(R.dz, ctx->has_left ? 1 : 0, ctx->has_right ? 1 : 0, totals_slot(ctx, step),
                     R.left >= 0 ? R.rho_in[0] : nullptr, R.right >= 0 ? R.rho_in[1] : nullptr,
                     global_flags ? R.cnt_dev + 4 : nullptr, R.lag + k * LAG_WORDS, s);
     if (R.left >= 0 || R.right >= 0) HIPCHK(hipEventRecord(R.lag_ev[k], s));   // read two steps on
@@ -764,6 +874,20 @@ int phase_finish(RankState& R, float dt, int64_t step, bool global_flags) {
     ctx->dz_ahead = true;   // o0 / o1 / n / rng on the host are last step's until slab_sync_ranges
     HIPCHK(hipGetLastError());
     return SPH_OK;
+}
+
+// Early sends for the next step: every rank decides alike from state all ranks share (the cut age, the re-balancing
+// schedule, the cuts, the re-sort mode), so the exchanges issued early are matched on every rank.
+bool early_next(const Multi& M) {
+    if (M.world < 2 || M.ranks.empty()) return false;
+    if (M.hold_early > 0 || std::getenv("SPH_NO_EARLY_SENDS")) return false;
+    const RankState& R0 = M.ranks[0];
+    if (R0.since_cut + 1 < 3) return false;   // the next step sizes its messages exactly
+    if (M.rebalance_every > 0 && (M.steps + 1) % M.rebalance_every == 0) return false;   // it may re-cut
+    if (R0.c->resort_mode == 0) return false;   // no jump guard anywhere
+    for (const sph_slab& c : M.cuts)
+        if (c.cx_hi - c.cx_lo < 4) return false;
+    return true;
 }
 
 // ---------------------------------------------------------------- re-balancing
@@ -811,6 +935,7 @@ int rebalance(Multi& M, sph_ctx* pctx) {
     if (!changed) return SPH_OK;
     M.cuts = nc;
     M.rebalances++;
+    M.early = false;
     for (auto& R : M.ranks) {
         int r = sph_slab_recut(R.c, &M.cuts[R.rank]);
         if (r != SPH_OK) return r;
@@ -862,14 +987,18 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
     // exact sizes for three steps after a cut: the lagged counts of step s come from step s - 2, and the
     // first step after a re-cut carries the migration to the new cut, not the new steady halo
     const bool exact = M.ranks[0].since_cut < 3;   // the same on every rank
+    // early: this step's messages were packed and exchanged during the previous step (never on an exact step)
+    const bool early = M.early && !exact;
+    M.early = false;
     int r;
-    for (auto& R : M.ranks)
-        if ((r = phase_count(R, exact)) != SPH_OK) return r;
+    if (!early)
+        for (auto& R : M.ranks)
+            if ((r = phase_count(R, exact, M.steps)) != SPH_OK) return r;
     if (exact) {
-        if ((r = exchange_counts(M, pctx)) != SPH_OK) return r;
+        if ((r = exchange_counts(M, pctx, M.steps)) != SPH_OK) return r;
     } else {
         // an overflow flagged two steps ago (or earlier; flags are sticky) stops every rank at this same
-        // step, before any exchange: over RCCL the lag record holds the flags max-reduced over all ranks
+        // step, before any exchange: over RCCL the lag record holds the flags OR-reduced over all ranks
         // (exchange2_start), in a local group the host ORs its ranks' own
         uint32_t flags = 0;
         for (auto& R : M.ranks) {
@@ -879,12 +1008,13 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
             flags |= L[9];
         }
         if (flags)
-            return fail(pctx, SPH_ERR_CAPACITY, "slab step %lld: a rank flagged%s%s%s%s%s (flags %#x, seen two steps on)",
+            return fail(pctx, SPH_ERR_CAPACITY, "slab step %lld: a rank flagged%s%s%s%s%s%s (flags %#x, seen two steps on)",
                         (long long)M.steps, (flags & SZ_OVF_MSG) ? " a halo message overflow" : "",
                         (flags & SZ_OVF_CAP) ? " slots over capacity" : "",
                         (flags & SZ_RHO_MISMATCH) ? " a ghost density count mismatch" : "",
                         (flags & SZ_OVF_MOVERS) ? " a mover list / re-sort destination out of range" : "",
-                        (flags & SZ_JUMP) ? " a particle that left the held columns in one step" : "", flags);
+                        (flags & SZ_JUMP) ? " a particle that left the held columns in one step" : "",
+                        (flags & SZ_JUMP_EARLY) ? " a particle that moved two or more columns in one step" : "", flags);
         for (auto& R : M.ranks) {
             if (R.left < 0 && R.right < 0) continue;   // no messages: nothing to size
             // the counts of two steps before: both neighbours read the same numbers
@@ -898,24 +1028,45 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
             R.c2o[1] = R.right >= 0 ? cap_of(L[5]) : 0;
             R.c2i[0] = R.left >= 0 ? cap_of(L[6]) : 0;
             R.c2i[1] = R.right >= 0 ? cap_of(L[7]) : 0;
+            R.g2[0] = R.left >= 0 ? cap_of(L[10]) : 0;
+            R.g2[1] = R.right >= 0 ? cap_of(L[11]) : 0;
             // slot bound: the assembled count two steps ago plus every record received since
             const int64_t km1 = (M.steps - 1) % LAG_SLOTS;
             R.n_prev_ub = std::min<int64_t>(R.n_prev_ub, (int64_t)L[8] + R.cin_hist[km1]);
         }
     }
-    for (auto& R : M.ranks)
-        if ((r = phase_pack(R, M)) != SPH_OK) return r;
-    if ((r = exchange1(M)) != SPH_OK) return r;
+    if (early) {   // the messages the previous step sent: their capacities, and wait for them
+        for (auto& R : M.ranks) {
+            if (R.left < 0 && R.right < 0) continue;
+            for (int sd = 0; sd < 2; ++sd) {
+                R.c1o[sd] = R.e_c1o[sd];
+                R.c1i[sd] = R.e_c1i[sd];
+            }
+            sph_ctx* ctx = R.c;
+            HIPCHK(hipSetDevice(ctx->device));
+            HIPCHK(hipStreamWaitEvent(ctx->stream, R.ev_sent, 0));
+        }
+    } else {
+        for (auto& R : M.ranks)
+            if ((r = phase_pack(R, M, M.steps)) != SPH_OK) return r;
+        if ((r = exchange1(M)) != SPH_OK) return r;
+    }
     for (auto& R : M.ranks)
         if ((r = phase_assemble(R, exact)) != SPH_OK) return r;
     if ((pctx->cfg.flags & SPH_FLAG_VALIDATE) && (r = validate_mid(M, pctx)) != SPH_OK) return r;
     for (auto& R : M.ranks)
         if ((r = phase_density(R, M)) != SPH_OK) return r;
     if (M.world > 1 && (r = exchange2_start(M)) != SPH_OK) return r;
+    const bool nxt = early_next(M);   // decided before the force passes, whose ranges depend on it
     for (auto& R : M.ranks)
-        if ((r = phase_interior(R, dt)) != SPH_OK) return r;
+        if ((r = phase_interior(R, dt, nxt)) != SPH_OK) return r;
+    for (auto& R : M.ranks)
+        if ((r = phase_boundary(R, M, dt, nxt)) != SPH_OK) return r;
+    if (nxt && (r = exchange1_early(M)) != SPH_OK) return r;
     for (auto& R : M.ranks)
         if ((r = phase_finish(R, dt, M.steps, M.mode == 2 && M.world > 1)) != SPH_OK) return r;
+    M.early = nxt;
+    if (M.hold_early > 0) M.hold_early--;
     M.steps++;
     return SPH_OK;
 }
@@ -944,6 +1095,15 @@ void multi_free(sph_ctx* ctx) {
 }
 
 bool is_group(const sph_ctx* ctx) { return ctx->mg && ctx->mg->mode == 1; }
+// The next step packs and exchanges its messages itself: the ones sent during the last step hold the state
+// before the change (over RCCL every rank must make the same change between the same steps: the exchanges pair up).
+// The step after the change runs without early sends too, so its force passes keep the graceful column-jump guard
+// (an external velocity change is what can move a particle two columns in one step).
+void multi_state_changed(sph_ctx* ctx) {
+    if (!ctx || !ctx->mg) return;
+    ctx->mg->early = false;
+    ctx->mg->hold_early = 1;
+}
 
 std::vector<sph_ctx*> multi_kids(const sph_ctx* ctx) { return ctx->mg ? ctx->mg->kids : std::vector<sph_ctx*>{}; }
 

@@ -214,13 +214,15 @@ struct SlabSizes {
     uint32_t flags;           // sticky: SZ_* bits
     uint32_t jump;            // this step's force pass moved an own particle by more than one column (the next
                               // step's sends then scan every own slot; cleared when the sizes are derived)
+    uint32_t hl_raw, hr_raw;  // this step's received message header counts (before clamping), for k_slab_lag
 };
 constexpr uint32_t SZ_OVF_MSG = 1u;     // a halo message held more records than its capacity
 constexpr uint32_t SZ_OVF_CAP = 2u;     // the assembled slots exceed the context's capacity
 constexpr uint32_t SZ_RHO_MISMATCH = 4u;  // a ghost column and the densities received differ in count
 constexpr uint32_t SZ_OVF_MOVERS = 8u;    // a mover list or a re-sort destination past the slot capacity
 constexpr uint32_t SZ_JUMP = 16u;         // an own particle left the held window in one step (two columns or more)
-constexpr int SZ_BITS = 5;
+constexpr uint32_t SZ_JUMP_EARLY = 32u;   // early sends: an interior particle moved two or more columns in one step
+constexpr int SZ_BITS = 6;
 // Halo messages: one 32-byte header record, then the records. Header: (count, capacity, 0, 0 | 0...)
 constexpr int MSG_HDR_F4 = 2;
 // ρ halo messages: a 32-byte header (count, capacity) = 4 float2, then (ρ, P/ρ²) of the boundary column's slots
@@ -244,8 +246,9 @@ struct SizesIn {
 __device__ __forceinline__ uint32_t header_count(const float4* msg) { return __float_as_uint(msg[0].x); }
 // nl, no, nr and the flags of the assembled [left | own | right] (slab.hip k_slab_sizes; k_slab_rec)
 __device__ __forceinline__ void slab_sizes_from(const SlabSizes* dz, const SizesIn& in, uint32_t& nl, uint32_t& no,
-                                                uint32_t& nr, uint32_t& f) {
-    const uint32_t hl = in.hl ? header_count(in.hl) : 0u, hr = in.hr ? header_count(in.hr) : 0u;
+                                                uint32_t& nr, uint32_t& f, uint32_t& hl, uint32_t& hr) {
+    hl = in.hl ? header_count(in.hl) : 0u;
+    hr = in.hr ? header_count(in.hr) : 0u;
     nl = min(hl, (uint32_t)in.cap_l);
     nr = min(hr, (uint32_t)in.cap_r);
     f = dz->flags;
@@ -257,7 +260,10 @@ __device__ __forceinline__ void slab_sizes_from(const SlabSizes* dz, const Sizes
         if (no > (uint32_t)in.capacity) no = 0;
     }
 }
-__device__ __forceinline__ void slab_sizes_store(SlabSizes* dz, uint32_t nl, uint32_t no, uint32_t nr, uint32_t f) {
+__device__ __forceinline__ void slab_sizes_store(SlabSizes* dz, uint32_t nl, uint32_t no, uint32_t nr, uint32_t f,
+                                                 uint32_t hl, uint32_t hr) {
+    dz->hl_raw = hl;
+    dz->hr_raw = hr;
     dz->nl = nl;
     dz->nr = nr;
     dz->no = no;
@@ -279,6 +285,7 @@ struct MoverSink {
     uint32_t cap;
     uint32_t* err = nullptr;   // SZ_OVF_MOVERS is or-ed here if the list would pass cap (entries dropped)
     uint32_t* jump = nullptr;  // slab step: SlabSizes.jump (a column jump > 1), SZ_JUMP into err (window exit)
+    int32_t jump_err = 0;      // early sends (abi_multi.cpp): a column jump > 1 is SZ_JUMP_EARLY in err, not jump
 };
 
 #if defined(__HIPCC__)
@@ -581,14 +588,17 @@ void launch_pick(const uint32_t* cs, const int32_t* idx, int32_t m, uint32_t* ou
 // into messages of a header and `cap[side]` records (header = true count; records past cap dropped and
 // flagged by the receiver). nb_ub: count-block upper bound (slab_send_blocks of the slot bound).
 // cand: steady state, scan only the columns a send can come from (slab.hip send_ranges)
-// exact: also the totals (host-read before packing on exact-size steps)
+// exact: also the totals (host-read before packing on exact-size steps). early: the sends of the NEXT step,
+// packed right after this step's boundary force pass (slab.hip send_ranges)
 void launch_slab_count_dev(const uint32_t* keys, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz, int32_t col_le,
-                           int32_t col_ge, uint32_t* blk, uint32_t* totals, hipStream_t s, bool cand, bool exact);
+                           int32_t col_ge, uint32_t* blk, uint32_t* totals, hipStream_t s, bool cand, bool exact,
+                           bool early = false);
 // both sides in one launch from the raw per-block counts; headers and totals[2] written by the pack
 void launch_slab_pack2_dev(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
                            const uint32_t* sk, uint32_t key_base, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz,
                            int32_t col_le, int32_t col_ge, const uint32_t* blk, float4* msg_l, int32_t cap_l,
-                           float4* msg_r, int32_t cap_r, uint32_t* totals, hipStream_t s, bool cand);
+                           float4* msg_r, int32_t cap_r, uint32_t* totals, hipStream_t s, bool cand,
+                           bool early = false);
 int32_t slab_send_blocks(int32_t b, int32_t e);
 // the received messages' counts -> dz (nl, nr clamped to the capacities, no, n, overflow flags)
 void launch_slab_sizes(SlabSizes* dz, const float4* msg_l, const float4* msg_r, int32_t cap_l, int32_t cap_r,
@@ -604,9 +614,10 @@ void launch_slab_unpack_rho2(float2* rp, SlabSizes* dz, const float2* msg_l, int
 // per-step counts for the host's lagged capacity choice, written to mapped pinned memory:
 // out[0..1] sent records (left, right), out[2..3] received headers, out[4..5] ρ sent, out[6..7] ρ received,
 // out[8] assembled slots, out[9] flags (gflags non-null: that word instead, every rank's flags reduced)
+// totals: this step's send counts (k_slab_pack2 / k_slab_scan wrote them into the step's slot)
 void launch_slab_lag(SlabSizes* dz, int32_t has_left, int32_t has_right, const uint32_t* totals,
-                     const float4* msg_in_l, const float4* msg_in_r, const float2* rho_in_l, const float2* rho_in_r,
-                     const uint32_t* gflags, uint32_t* out, hipStream_t s);
+                     const float2* rho_in_l, const float2* rho_in_r, const uint32_t* gflags, uint32_t* out,
+                     hipStream_t s);
 
 // owned slots [o0, o0+n) -> records of 8 floats (x,y,z,u,v,w,id-bits,ρ)
 void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, const float2* rp,

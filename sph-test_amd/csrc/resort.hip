@@ -371,9 +371,10 @@ __global__ __launch_bounds__(MV_BLK) void k_slab_rec(AsmSrc src, int32_t n, Grid
     __shared__ uint32_t samp[CS_SAMP];
     __shared__ uint32_t win[CS_WIN];
     if (from_headers) {   // device-sized slab step: every workgroup derives the layout from the headers,
-        uint32_t nl, no, nr, f;   // the first stores it for the kernels after this one
-        slab_sizes_from(src.dz, in, nl, no, nr, f);
-        if (blockIdx.x == 0 && threadIdx.x == 0) slab_sizes_store(const_cast<SlabSizes*>(src.dz), nl, no, nr, f);
+        uint32_t nl, no, nr, f, hl, hr;   // the first stores it for the kernels after this one
+        slab_sizes_from(src.dz, in, nl, no, nr, f, hl, hr);
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            slab_sizes_store(const_cast<SlabSizes*>(src.dz), nl, no, nr, f, hl, hr);
         if (csp.cs && (int32_t)blockIdx.x >= nb_rec) {   // the old cell-start table
             const float4* rl = src.rl;
             const float4* rr = src.rr;

@@ -48,11 +48,14 @@ int32_t slab_send_blocks(int32_t b, int32_t e) { return e > b ? (e - b + SL_SEND
 // the picks), only the columns a send can come from: a particle moves less than a column per step, so one
 // that is now in column <= lo was in lo or lo + 1 (left), >= hi - 1 in hi - 2 or hi - 1 (right). A force
 // pass that moved an own particle further sets dz->jump, and the next sends scan every own slot again.
+// Early sends (the next step's, packed right after this step's boundary force pass, abi_multi.cpp): the owned range is
+// this step's [pick[1], pick[4]) (k_slab_lag has not run yet), and dz->jump is not consulted: the boundary pass that
+// moved the candidate columns has finished, and the interior pass reports its jumps as SZ_JUMP_EARLY instead.
 __device__ __forceinline__ void send_ranges(const SlabSizes* __restrict__ dz, int32_t cand, int32_t& bl, int32_t& el,
-                                            int32_t& br, int32_t& er) {
-    bl = br = (int32_t)dz->o0;
-    el = er = (int32_t)dz->o1;
-    if (cand && dz->jump == 0u) {
+                                            int32_t& br, int32_t& er, int32_t early = 0) {
+    bl = br = (int32_t)(early ? dz->pick[1] : dz->o0);
+    el = er = (int32_t)(early ? dz->pick[4] : dz->o1);
+    if (cand && (early || dz->jump == 0u)) {
         el = max(bl, min(el, (int32_t)dz->pick[6]));
         br = min(er, max(br, (int32_t)dz->pick[7]));
     }
@@ -61,10 +64,10 @@ __device__ __forceinline__ void send_ranges(const SlabSizes* __restrict__ dz, in
 __global__ __launch_bounds__(SL_BLK) void k_slab_count(const uint32_t* __restrict__ keys, int32_t b, int32_t e,
                                                        uint32_t gyz, int32_t col_le, int32_t col_ge,
                                                        uint32_t* __restrict__ blk, int32_t nblk,
-                                                       const SlabSizes* __restrict__ dz, int32_t cand) {
+                                                       const SlabSizes* __restrict__ dz, int32_t cand, int32_t early) {
     __shared__ uint32_t wl[SL_WAVES], wr[SL_WAVES];
     int32_t bl = b, el = e, br = b, er = e;
-    if (dz) send_ranges(dz, cand, bl, el, br, er);   // device-sized step; nblk is an upper bound
+    if (dz) send_ranges(dz, cand, bl, el, br, er, early);   // device-sized step; nblk is an upper bound
     uint32_t cl = 0, cr = 0;
     if (bl == br && el == er) {   // one range for both sides
         const int32_t i0 = bl + blockIdx.x * SL_SEND + threadIdx.x;
@@ -263,7 +266,7 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_pack2(const uint32_t* __restric
                                                        const uint32_t* __restrict__ sk, uint32_t key_base, uint32_t gyz,
                                                        int32_t col_le, int32_t col_ge, const uint32_t* __restrict__ blk,
                                                        int32_t nblk, const SlabSizes* __restrict__ dz, PackOut po,
-                                                       int32_t cand) {
+                                                       int32_t cand, int32_t early) {
     __shared__ uint32_t wc[SL_PER][SL_WAVES];
     __shared__ uint32_t red[SL_WAVES][2];
     __shared__ int32_t list[SL_SEND];
@@ -271,7 +274,7 @@ __global__ __launch_bounds__(SL_BLK) void k_slab_pack2(const uint32_t* __restric
     float4* msg = po.msg[side];
     if (!msg) return;
     int32_t bl, el, br, er;
-    send_ranges(dz, cand, bl, el, br, er);
+    send_ranges(dz, cand, bl, el, br, er, early);
     const int32_t b = side == 0 ? bl : br, e = side == 0 ? el : er;
     const bool work = b + (int32_t)blockIdx.x * SL_SEND < e;
     if (!work && blockIdx.x != 0) return;   // whole workgroup, before any barrier
@@ -424,7 +427,7 @@ void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, 
 void launch_slab_count(const uint32_t* keys, int32_t b, int32_t e, uint32_t gyz, int32_t col_le, int32_t col_ge,
                        uint32_t* blk, uint32_t* totals, hipStream_t s, int64_t* totals64) {
     const int32_t nb = slab_send_blocks(b, e);
-    k_slab_count<<<nb, SL_BLK, 0, s>>>(keys, b, e, gyz, col_le, col_ge, blk, nb, nullptr, 0);
+    k_slab_count<<<nb, SL_BLK, 0, s>>>(keys, b, e, gyz, col_le, col_ge, blk, nb, nullptr, 0, 0);
     k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb, totals, totals64, nullptr, nullptr, 0, 0);
 }
 
@@ -439,28 +442,29 @@ void launch_slab_pack(const uint32_t* keys, const float4* pos, const float4* vel
 
 // exact: the host reads the totals before packing (k_slab_scan, totals only); steady steps need no scan
 void launch_slab_count_dev(const uint32_t* keys, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz, int32_t col_le,
-                           int32_t col_ge, uint32_t* blk, uint32_t* totals, hipStream_t s, bool cand, bool exact) {
-    k_slab_count<<<nb_ub, SL_BLK, 0, s>>>(keys, 0, 0, gyz, col_le, col_ge, blk, nb_ub, dz, cand ? 1 : 0);
+                           int32_t col_ge, uint32_t* blk, uint32_t* totals, hipStream_t s, bool cand, bool exact,
+                           bool early) {
+    k_slab_count<<<nb_ub, SL_BLK, 0, s>>>(keys, 0, 0, gyz, col_le, col_ge, blk, nb_ub, dz, cand ? 1 : 0, early ? 1 : 0);
     if (exact) k_slab_scan<<<1, SL_SCAN, 0, s>>>(blk, nb_ub, totals, nullptr, nullptr, nullptr, 0, 0, 0);
 }
 
 void launch_slab_pack2_dev(const uint32_t* keys, const float4* pos, const float4* vel, const int32_t* id,
                            const uint32_t* sk, uint32_t key_base, const SlabSizes* dz, int32_t nb_ub, uint32_t gyz,
                            int32_t col_le, int32_t col_ge, const uint32_t* blk, float4* msg_l, int32_t cap_l,
-                           float4* msg_r, int32_t cap_r, uint32_t* totals, hipStream_t s, bool cand) {
+                           float4* msg_r, int32_t cap_r, uint32_t* totals, hipStream_t s, bool cand, bool early) {
     if (!msg_l && !msg_r) return;
     const PackOut po{{msg_l, msg_r}, {(uint32_t)cap_l, (uint32_t)cap_r}, totals};
     k_slab_pack2<<<dim3(nb_ub, 2), SL_BLK, 0, s>>>(keys, pos, vel, id, sk, key_base, gyz, col_le, col_ge, blk, nb_ub, dz,
-                                                   po, cand ? 1 : 0);
+                                                   po, cand ? 1 : 0, early ? 1 : 0);
 }
 
 // The assembled layout from the message headers and the owned range of the previous order (a
 // host-sized step; device-sized steps compute it in k_slab_rec).
 __global__ void k_slab_sizes(SlabSizes* __restrict__ dz, SizesIn in) {
     if (threadIdx.x != 0) return;
-    uint32_t nl, no, nr, f;
-    slab_sizes_from(dz, in, nl, no, nr, f);
-    slab_sizes_store(dz, nl, no, nr, f);
+    uint32_t nl, no, nr, f, hl, hr;
+    slab_sizes_from(dz, in, nl, no, nr, f, hl, hr);
+    slab_sizes_store(dz, nl, no, nr, f, hl, hr);
 }
 
 void launch_slab_sizes(SlabSizes* dz, const float4* msg_l, const float4* msg_r, int32_t cap_l, int32_t cap_r,
@@ -521,9 +525,11 @@ void launch_slab_unpack_rho2(float2* rp, SlabSizes* dz, const float2* msg_l, int
 // kernels of this step read the picks themselves; these copies are for the host and the next step),
 // the next step's owned range, the sizes of a rank without neighbours (no message will set them), and
 // this step's counts for the capacities two steps on (mapped pinned memory).
+// out[2], out[3]: the header counts of this step's received messages as the record kernel saw them (the message
+// buffers may hold the next step's early messages by now); out[10], out[11]: the two columns at each side (the early
+// boundary pass's ranges), for the next grids.
 __global__ void k_slab_lag(SlabSizes* __restrict__ dz, int32_t has_left, int32_t has_right,
-                           const uint32_t* __restrict__ totals, const float4* __restrict__ msg_in_l,
-                           const float4* __restrict__ msg_in_r, const float2* __restrict__ rho_in_l,
+                           const uint32_t* __restrict__ totals, const float2* __restrict__ rho_in_l,
                            const float2* __restrict__ rho_in_r, const uint32_t* __restrict__ gflags,
                            uint32_t* __restrict__ out) {
     if (threadIdx.x != 0) return;
@@ -551,8 +557,8 @@ __global__ void k_slab_lag(SlabSizes* __restrict__ dz, int32_t has_left, int32_t
     }
     out[0] = totals[0];
     out[1] = totals[1];
-    out[2] = msg_in_l ? header_count(msg_in_l) : 0u;
-    out[3] = msg_in_r ? header_count(msg_in_r) : 0u;
+    out[2] = has_left ? dz->hl_raw : 0u;
+    out[3] = has_right ? dz->hr_raw : 0u;
     out[4] = v[2] - v[1];
     out[5] = v[4] - v[3];
     out[6] = rho_in_l ? __float_as_uint(rho_in_l[0].x) : 0u;
@@ -564,12 +570,14 @@ __global__ void k_slab_lag(SlabSizes* __restrict__ dz, int32_t has_left, int32_t
         for (int k = 0; k < SZ_BITS; ++k) gf |= (gflags[k] != 0u ? 1u : 0u) << k;
     }
     out[9] = gf;
+    out[10] = v[6] - v[1];
+    out[11] = v[4] - v[7];
 }
 
 void launch_slab_lag(SlabSizes* dz, int32_t has_left, int32_t has_right, const uint32_t* totals,
-                     const float4* msg_in_l, const float4* msg_in_r, const float2* rho_in_l, const float2* rho_in_r,
-                     const uint32_t* gflags, uint32_t* out, hipStream_t s) {
-    k_slab_lag<<<1, 64, 0, s>>>(dz, has_left, has_right, totals, msg_in_l, msg_in_r, rho_in_l, rho_in_r, gflags, out);
+                     const float2* rho_in_l, const float2* rho_in_r, const uint32_t* gflags, uint32_t* out,
+                     hipStream_t s) {
+    k_slab_lag<<<1, 64, 0, s>>>(dz, has_left, has_right, totals, rho_in_l, rho_in_r, gflags, out);
 }
 
 void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, int32_t* id, hipStream_t s) {

@@ -620,13 +620,17 @@ __global__ __launch_bounds__(TF_BLK) __attribute__((amdgpu_waves_per_eu(4))) voi
     __shared__ float4 sv[TF_GCAP + 4];     // (u, v, w, P/ρ²)
     const int tid = threadIdx.x;
     int32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    int32_t nb_r = nb_a;   // this range's workgroups
     if (dr2.lo && blk >= nb_a) {   // a second range in the same launch (the slab step's two boundary columns)
         blk -= nb_a;
+        nb_r = (int32_t)gridDim.x - nb_a;
         dr = dr2;
     }
     if (dr.lo) {   // device-resident bounds (slab step); the grid is an upper bound
         ib = (int32_t)*dr.lo;
         n = (int32_t)*dr.hi;
+        // a range past its grid (a bound from an earlier step's count) stops every rank, as a message overflow does
+        if (blk == 0 && tid == 0 && mv.err && n - ib > nb_r * TF_BLK) atomicOr(mv.err, SZ_OVF_CAP);
     }
     const int32_t i0 = ib + blk * TF_BLK;
     if (i0 >= n) return;   // whole workgroup: before any barrier
@@ -838,7 +842,8 @@ __global__ __launch_bounds__(TF_BLK) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (wk >= g.ncells) {
             if (mv.err) atomicOr(mv.err, SZ_JUMP);   // left the held window: it reaches no neighbour
         } else if (d > 1 || d < -1) {
-            *mv.jump = 1u;
+            if (mv.jump_err) atomicOr(mv.err, SZ_JUMP_EARLY);
+            else *mv.jump = 1u;
         }
     }
     append_mover(mv, i, wk);
@@ -868,10 +873,10 @@ void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, 
     if (nb_a + nb_b == 0) return;
     if (g.xsub == 2)
         SPH_LAUNCH(k_force_tiled<2>, nb_a + nb_b, TF_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt,
-                   fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr, nb_b ? dr2 : DevRange{}, nb_a);
+                   fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr, nb_b ? dr2 : DevRange{}, nb_b ? nb_a : nb_a + nb_b);
     else
         SPH_LAUNCH(k_force_tiled<1>, nb_a + nb_b, TF_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt,
-                   fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr, nb_b ? dr2 : DevRange{}, nb_a);
+                   fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr, nb_b ? dr2 : DevRange{}, nb_b ? nb_a : nb_a + nb_b);
 }
 
 #ifdef SPH_BTIME

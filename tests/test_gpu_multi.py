@@ -206,16 +206,20 @@ def _top_of_column(x, colw, col, up):
     return int(sel[np.argmax(x[sel, up])])
 
 
-@pytest.mark.parametrize("resort", ["1", "0"])
-def test_group_column_jump_falls_back_to_full_sends(pkg, monkeypatch, resort):
+@pytest.mark.parametrize("resort,early", [("1", True), ("1", False), ("0", True)])
+def test_group_column_jump_falls_back_to_full_sends(pkg, monkeypatch, resort, early):
     """A particle of rank 0 kicked from column c1 − 3 across two columns in one step, into its last own
     column or the halo column c1 (rank 0 owns [0, c1)): it must be sent to rank 1, although the steady-
     state sends scan only the old columns c1 − 2 and c1 − 1. With the incremental re-sort (SPH_RESORT=1)
     the force pass's column-jump guard flags the move and the next sends scan every own slot; with the
     full sort (SPH_RESORT=0) the guard cannot run (it reads the previous order's keys) and the sends scan
     every own slot on every step (abi_multi.cpp steady_sends). Either way the group stays bit-identical
-    to one context. The kick is taken back after the jump, so the run goes on in the steady state."""
+    to one context. The kick is taken back after the jump, so the run goes on in the steady state.
+    A kick drops the messages sent early (during the step before it) and holds the early sends for one
+    step, so the jump step keeps the graceful guard; early=False runs the whole test without early sends."""
     monkeypatch.setenv("SPH_RESORT", resort)
+    if not early:
+        monkeypatch.setenv("SPH_NO_EARLY_SENDS", "1")
     sc = _scenario(pkg)
     p, dt = pkg.scenario_params(sc)
     colw = float(np.float32(2.0) * np.float32(p.h))
@@ -270,6 +274,36 @@ def test_group_window_exit_stops_the_group(pkg, monkeypatch):
         with pytest.raises(pkg.SphError) as ei:
             group.step(4)
         assert ei.value.status == -3 and "left the held columns" in str(ei.value), str(ei.value)
+    finally:
+        group.close()
+
+
+def test_group_early_sends_two_column_jump_stops_the_group(pkg, monkeypatch):
+    """Early sends (the next step's halo messages packed during this step, abi_multi.cpp phase_boundary) scan
+    only the two columns at each side; a particle that moves two or more columns while they are packed could be
+    missed, so the force pass raises SZ_JUMP_EARLY and the group stops, naming it. A particle of rank 0 kicked
+    to about 2.8 columns per step from column c1 − 7: the kick step runs without early sends (the graceful guard,
+    test above), the step after it with them, and its second jump stops the group."""
+    monkeypatch.setenv("SPH_RESORT", "1")
+    sc = _scenario(pkg)
+    p, dt = pkg.scenario_params(sc)
+    colw = float(np.float32(2.0) * np.float32(p.h))
+    up = int(np.argmax(np.abs(np.array(p.gravity))))
+    group = pkg.SPHSim(sc, ndev=2, rebalance_every=0)   # two slabs: rank 0 holds about nine columns
+    try:
+        group.step(10)
+        c1 = int(group.ctx.decomposition().cut.cx_hi)
+        if c1 < 8:
+            pytest.skip(f"rank 0 holds {c1} columns")
+        x = group.positions()
+        pid = _top_of_column(x, colw, c1 - 7, up)
+        group.ctx.debug_kick(pid, np.array([2.8 * colw / float(dt), 0.0, 0.0], np.float32))
+        group.step(1)   # the kick step: graceful
+        x1 = group.positions()
+        print({"c1": c1, "pid": pid, "col0": float(x[pid, 0]) / colw, "col1": float(x1[pid, 0]) / colw})
+        with pytest.raises(pkg.SphError) as ei:
+            group.step(4)
+        assert ei.value.status == -3 and "two or more columns" in str(ei.value), str(ei.value)
     finally:
         group.close()
 
