@@ -845,7 +845,10 @@ int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int3
 int sph_debug_kick(sph_ctx* ctx, int32_t id, const float dv[3]) {
     if (!ctx || !dv) return SPH_ERR_INVALID;
     if (is_contact(ctx)) return fail(ctx, SPH_ERR_STATE, "sph_debug_kick is Model S only");
-    multi_state_changed(ctx);   // a slab step's early messages hold the velocities before the kick
+    {   // a slab step's early messages hold the velocities before the kick
+        const int r = multi_state_changed(ctx);
+        if (r != SPH_OK) return r;
+    }
     std::vector<sph_ctx*> cs = is_group(ctx) ? multi_kids(ctx) : std::vector<sph_ctx*>{ctx};
     for (sph_ctx* k : cs) {   // every slot up to the capacity: ghosts and stale slots are overwritten before use
         HIPCHK(hipSetDevice(k->device));

@@ -45,6 +45,8 @@ struct RankState {
     hipEvent_t ev_sent = nullptr;    // early sends: the next step's messages have arrived (comm stream)
     hipEvent_t ev_fdone = nullptr;   // early sends without the jump guard: the interior force pass is done
     int32_t e_c1o[2] = {0, 0}, e_c1i[2] = {0, 0};   // the next step's message capacities (early sends)
+    bool comm_borrowed = false;      // SPH_DEBUG_SERIAL_GROUP: slab 0's comm stream
+    bool sent_pending = false;       // ev_sent closes comm-stream work the main stream has not waited for yet
     int32_t g2[2] = {0, 0};          // grid bounds of the two-column boundary ranges (early sends), 0: n_ub
     SlabSizes* dz = nullptr;
     float4* msg_out[2] = {nullptr, nullptr};
@@ -257,7 +259,7 @@ void rank_free(RankState& R) {
     dfree(R.dz);
     dfree(R.cnt_dev);
     if (R.lag) (void)hipHostFree(R.lag);
-    if (R.comm) (void)hipStreamDestroy(R.comm);
+    if (R.comm && !R.comm_borrowed) (void)hipStreamDestroy(R.comm);
     R = RankState{};
 }
 
@@ -815,7 +817,8 @@ int phase_boundary(RankState& R, Multi& M, float dt, bool early) {
 }
 
 // The next step's halo messages, on the comm streams (early sends): peer copies in a local group, one RCCL group
-// per rank otherwise. The next step's assemble waits for ev_sent.
+// per rank otherwise. The step's bookkeeping follows them there (phase_finish), and the next step's first launch
+// waits for ev_sent.
 int exchange1_early(Multi& M) {
     if (M.mode == 1) {
         const int r0 = M.ranks[0].rank;
@@ -830,10 +833,7 @@ int exchange1_early(Multi& M) {
                 HIPCHK(hipStreamWaitEvent(R.comm, S.ev_packed, 0));
                 HIPCHK(hipMemcpyPeerAsync(R.msg_in[s], ctx->device, S.msg_out[1 - s], S.c->device, bytes, R.comm));
             }
-            if (R.left >= 0 || R.right >= 0) {
-                HIPCHK(hipEventRecord(R.ev_in, R.comm));
-                HIPCHK(hipEventRecord(R.ev_sent, R.comm));
-            }
+            if (R.left >= 0 || R.right >= 0) HIPCHK(hipEventRecord(R.ev_in, R.comm));
         }
         return SPH_OK;
     }
@@ -850,15 +850,21 @@ int exchange1_early(Multi& M) {
                          R.comm));
     }
     NCCLCHK(ncclGroupEnd());
-    HIPCHK(hipEventRecord(R.ev_sent, R.comm));
     return SPH_OK;
 }
 
-int phase_finish(RankState& R, float dt, int64_t step, bool global_flags) {
+// early (the next step's messages went out on the comm stream): the bookkeeping kernel follows them there, so the
+// main stream runs from this step's interior pass into the next step's assemble behind one wait (ev_sent,
+// multi_join) instead of a wait for the boundary pass plus a launch of its own. Its flags word then holds what the
+// interior pass of this step flagged only if that pass has finished; the flags are sticky, so the next step's record
+// carries them (an RCCL rank's flags are the all-reduced ones of the density pass either way).
+int phase_finish(RankState& R, float dt, int64_t step, bool global_flags, bool early) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
-    hipStream_t s = ctx->stream;
-    if (R.left >= 0 || R.right >= 0) HIPCHK(hipStreamWaitEvent(s, R.ev_bdone, 0));
+    const bool halo = R.left >= 0 || R.right >= 0;
+    const bool on_comm = early && halo;
+    hipStream_t s = on_comm ? R.comm : ctx->stream;
+    if (halo && !on_comm) HIPCHK(hipStreamWaitEvent(s, R.ev_bdone, 0));
     swap_sv(ctx);
     ctx->keys_valid = true;
     ctx->steps++;
@@ -867,12 +873,30 @@ int phase_finish(RankState& R, float dt, int64_t step, bool global_flags) {
     launch_slab_lag(R.dz, ctx->has_left ? 1 : 0, ctx->has_right ? 1 : 0, totals_slot(ctx, step),
                     R.left >= 0 ? R.rho_in[0] : nullptr, R.right >= 0 ? R.rho_in[1] : nullptr,
                     global_flags ? R.cnt_dev + 4 : nullptr, R.lag + k * LAG_WORDS, s);
-    if (R.left >= 0 || R.right >= 0) HIPCHK(hipEventRecord(R.lag_ev[k], s));   // read two steps on
+    if (halo) HIPCHK(hipEventRecord(R.lag_ev[k], s));   // read two steps on
+    if (on_comm) {
+        HIPCHK(hipEventRecord(R.ev_sent, s));
+        R.sent_pending = true;
+    }
     R.cin_hist[k] = R.c1i[0] + R.c1i[1];
     R.n_prev_ub = R.n_ub;
     R.since_cut++;
     ctx->dz_ahead = true;   // o0 / o1 / n / rng on the host are last step's until slab_sync_ranges
     HIPCHK(hipGetLastError());
+    return SPH_OK;
+}
+
+// The main streams wait for the comm-stream work of the last step (its boundary pass, early sends and bookkeeping):
+// at the next step's start, at the end of every sph_step call (so reads, kicks and re-cuts see the whole step), and
+// before a host-side state change.
+int multi_join(Multi& M) {
+    for (auto& R : M.ranks) {
+        if (!R.sent_pending) continue;
+        sph_ctx* ctx = R.c;
+        HIPCHK(hipSetDevice(ctx->device));
+        HIPCHK(hipStreamWaitEvent(ctx->stream, R.ev_sent, 0));
+        R.sent_pending = false;
+    }
     return SPH_OK;
 }
 
@@ -980,8 +1004,10 @@ int validate_mid(Multi& M, sph_ctx* pctx) {
 }
 
 int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
+    int r = multi_join(M);
+    if (r != SPH_OK) return r;
     if (M.rebalance_every > 0 && M.world > 1 && M.steps > 0 && M.steps % M.rebalance_every == 0) {
-        int r = rebalance(M, pctx);
+        r = rebalance(M, pctx);
         if (r != SPH_OK) return r;
     }
     // exact sizes for three steps after a cut: the lagged counts of step s come from step s - 2, and the
@@ -990,7 +1016,6 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
     // early: this step's messages were packed and exchanged during the previous step (never on an exact step)
     const bool early = M.early && !exact;
     M.early = false;
-    int r;
     if (!early)
         for (auto& R : M.ranks)
             if ((r = phase_count(R, exact, M.steps)) != SPH_OK) return r;
@@ -1035,16 +1060,13 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
             R.n_prev_ub = std::min<int64_t>(R.n_prev_ub, (int64_t)L[8] + R.cin_hist[km1]);
         }
     }
-    if (early) {   // the messages the previous step sent: their capacities, and wait for them
+    if (early) {   // the messages the previous step sent (multi_join waited for them): their capacities
         for (auto& R : M.ranks) {
             if (R.left < 0 && R.right < 0) continue;
             for (int sd = 0; sd < 2; ++sd) {
                 R.c1o[sd] = R.e_c1o[sd];
                 R.c1i[sd] = R.e_c1i[sd];
             }
-            sph_ctx* ctx = R.c;
-            HIPCHK(hipSetDevice(ctx->device));
-            HIPCHK(hipStreamWaitEvent(ctx->stream, R.ev_sent, 0));
         }
     } else {
         for (auto& R : M.ranks)
@@ -1064,7 +1086,7 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
         if ((r = phase_boundary(R, M, dt, nxt)) != SPH_OK) return r;
     if (nxt && (r = exchange1_early(M)) != SPH_OK) return r;
     for (auto& R : M.ranks)
-        if ((r = phase_finish(R, dt, M.steps, M.mode == 2 && M.world > 1)) != SPH_OK) return r;
+        if ((r = phase_finish(R, dt, M.steps, M.mode == 2 && M.world > 1, nxt)) != SPH_OK) return r;
     M.early = nxt;
     if (M.hold_early > 0) M.hold_early--;
     M.steps++;
@@ -1099,10 +1121,11 @@ bool is_group(const sph_ctx* ctx) { return ctx->mg && ctx->mg->mode == 1; }
 // before the change (over RCCL every rank must make the same change between the same steps: the exchanges pair up).
 // The step after the change runs without early sends too, so its force passes keep the graceful column-jump guard
 // (an external velocity change is what can move a particle two columns in one step).
-void multi_state_changed(sph_ctx* ctx) {
-    if (!ctx || !ctx->mg) return;
+int multi_state_changed(sph_ctx* ctx) {
+    if (!ctx || !ctx->mg) return SPH_OK;
     ctx->mg->early = false;
     ctx->mg->hold_early = 1;
+    return multi_join(*ctx->mg);
 }
 
 std::vector<sph_ctx*> multi_kids(const sph_ctx* ctx) { return ctx->mg ? ctx->mg->kids : std::vector<sph_ctx*>{}; }
@@ -1193,6 +1216,17 @@ int multi_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
             if (rc == SPH_OK) rc = put_dz(M.ranks[r]);
             if (rc != SPH_OK) return fail(ctx, rc, "slab %d: %s", r, sph_last_error(k));
         }
+        // ... and every slab's halo work on slab 0's comm stream: two streams in all, as on each GPU of a real
+        // group (more streams than the device's hardware queues would share queues and order unrelated work)
+        if (ser && std::atoi(ser) != 0) {
+            HIPCHK(hipDeviceSynchronize());
+            for (int r = 1; r < M.world; ++r) {
+                RankState& R = M.ranks[r];
+                HIPCHK(hipStreamDestroy(R.comm));
+                R.comm = M.ranks[0].comm;
+                R.comm_borrowed = true;
+            }
+        }
     }
     M.steps = 0;
     M.ready = true;
@@ -1243,12 +1277,15 @@ int multi_step(sph_ctx* ctx, float dt, int32_t nsteps) {
                              (long long)R.n_ub, (long long)R.since_cut);
             }
         if (r != SPH_OK) {
+            (void)multi_join(M);
             if (M.mode == 1)   // a slab context's message on the group
                 for (auto& R : M.ranks)
                     if (R.c && !R.c->err.empty()) ctx->err = R.c->err;
             return r;
         }
     }
+    int r = multi_join(M);
+    if (r != SPH_OK) return r;
     if (M.mode == 1) {
         ctx->steps = M.ranks[0].c->steps;
         ctx->sim_time = M.ranks[0].c->sim_time;

@@ -274,7 +274,7 @@ int slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void* de
 // multi-GPU step (abi_multi.cpp)
 void multi_free(sph_ctx* ctx);
 bool is_group(const sph_ctx* ctx);   // sph_config.ndev > 1: the context holds one slab context per GPU
-void multi_state_changed(sph_ctx* ctx);   // host-side state changed between steps: no early sends for the next step
+int multi_state_changed(sph_ctx* ctx);   // host-side state changed between steps: no early sends for the next step
 int multi_create_group(sph_ctx* ctx);
 int multi_init_scenario(sph_ctx* ctx, const sph_scenario* sc);   // local group
 int multi_init_rank(sph_ctx* ctx, const sph_scenario* sc);       // RCCL rank
