@@ -1021,6 +1021,7 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
             if ((r = phase_count(R, exact, M.steps)) != SPH_OK) return r;
     if (exact) {
         if ((r = exchange_counts(M, pctx, M.steps)) != SPH_OK) return r;
+        for (auto& R : M.ranks) R.g2[0] = R.g2[1] = 0;   // no lagged column counts of the new cut yet: grids of n_ub
     } else {
         // an overflow flagged two steps ago (or earlier; flags are sticky) stops every rank at this same
         // step, before any exchange: over RCCL the lag record holds the flags OR-reduced over all ranks

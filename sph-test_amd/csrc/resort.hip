@@ -238,6 +238,9 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_place(const uint32_t* __restrict_
 // workgroup. A workgroup whose counts agree at its start and that holds no mover key leaves its cells.
 // Runs as extra workgroups of k_mv_merge (it needs only k_mv_place's tables), beside the scatter.
 constexpr int MV_CS_CELLS = 4 * MV_BLK;
+#ifndef SPH_MERGE_PREFETCH
+#define SPH_MERGE_PREFETCH 1
+#endif
 // movers staged in LDS for the merge's binary searches (a workgroup's cells or slots rarely hold more)
 constexpr uint32_t MV_LDS = 1024;
 
@@ -315,6 +318,12 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
     }
     const uint32_t ko = i < n ? asm_sk(src, i) : 0u;
     const bool stay = i < n && asm_key(src, i) == ko;
+#if SPH_MERGE_PREFETCH
+    // the slot's particle loads issue before the searches' dependent loads and the barrier (a mover's are unused)
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f), v = p;
+    int32_t pid = 0;
+    if (i < n) asm_load(src, i, p, v, pid);
+#endif
     __syncthreads();
     const uint32_t a = movers_before(i < n && !stay, b[0], wc);
     const uint32_t lo = b[1], hi = b[2];
@@ -331,9 +340,11 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
         if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
         return;
     }
+#if !SPH_MERGE_PREFETCH
     float4 p, v;
     int32_t pid;
     asm_load(src, i, p, v, pid);
+#endif
     pos_o[dst] = p;
     vel_o[dst] = v;
     id_o[dst] = pid;
