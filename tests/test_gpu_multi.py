@@ -343,3 +343,30 @@ def test_baseline_config_decomposed_full_size(pkg, oracle, monkeypatch, cfg, nde
         compare_one_step(pkg, oracle, single, xg, vg, f"{cfg} decomposed x{ndev}", t=t)
     finally:
         single.close()
+
+
+def test_group_through_the_collapse_bitwise(pkg):
+    """C3 x 4 (4,194,304 particles, dam-break) in 4 slabs for 5,000 steps, re-balanced every 50: from rest through
+    the collapse to the surge front running along the floor (bench.py's mid-collapse state), so the steady-state
+    steps with early sends meet the splash, thousands of movers per step (steps past the re-sort's
+    mover limit take the full sort and send from every own slot) and the re-cuts that follow the moving fluid. The
+    group stays bit-identical to one context."""
+    from sph_test_amd import slab
+    sc = slab.weak_scenario("C3", 4)
+    steps = 5000
+    group = pkg.SPHSim(sc, ndev=4, rebalance_every=50)
+    try:
+        group.step(steps)
+        xg, vg = group.positions(), group.velocities()
+        rebalances = group.ctx.decomposition().rebalances
+    finally:
+        group.close()
+    single = pkg.SPHSim(sc)
+    try:
+        single.step(steps)
+        xs, vs = single.positions(), single.velocities()
+    finally:
+        single.close()
+    same = bool(np.array_equal(xg, xs) and np.array_equal(vg, vs))
+    print({"steps": steps, "rebalances": rebalances, "bitwise": same, "max_dx": float(np.abs(xg - xs).max())})
+    assert rebalances > 0 and same
