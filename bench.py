@@ -386,6 +386,10 @@ def main():
         return
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if os.environ.get("SPH_RCCL_HOST_PER_RANK"):
+            # rehearsal of the in-library RCCL step with every rank on one GPU: RCCL refuses two ranks of one host
+            # on one device, so each rank poses as a host of its own and the exchanges take RCCL's socket transport
+            os.environ["NCCL_HOSTID"] = f"sph-rank-{rank}"
         local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         if backend == "nccl":

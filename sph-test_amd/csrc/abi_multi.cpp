@@ -26,6 +26,8 @@
 
 #include <rccl/rccl.h>
 
+#include <chrono>
+
 namespace sph {
 
 constexpr int LAG_SLOTS = 4;
@@ -291,9 +293,21 @@ int col_le(const sph_ctx* c) { return c->has_left ? c->sl.cx_lo - c->grid.cx0 : 
 int col_ge(const sph_ctx* c) { return c->has_right ? c->sl.cx_hi - 1 - c->grid.cx0 : 0x7fffffff; }
 uint32_t gyz(const sph_ctx* c) { return col_keys(c->grid); }
 
+// SPH_HOST_TIMING=1 (measurement): host time per step in multi_one_step and the part of it spent blocked on lag
+// events, printed when the context is destroyed (the issue rate a rank's host sustains against its GPU)
+struct HostTiming {
+    bool on = std::getenv("SPH_HOST_TIMING") != nullptr;
+    double total = 0.0, wait = 0.0;
+    int64_t steps = 0;
+};
+HostTiming g_ht;
+double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
 const uint32_t* lag_slot(RankState& R, int64_t step, sph_ctx* ctx, int* rc) {
     const int k = (int)(step % LAG_SLOTS);
+    const double t0 = g_ht.on ? now_s() : 0.0;
     const hipError_t e = hipEventSynchronize(R.lag_ev[k]);   // done long ago unless the host runs 2 steps ahead
+    if (g_ht.on) g_ht.wait += now_s() - t0;
     if (e != hipSuccess) *rc = fail(ctx, SPH_ERR_HIP, "lag event: %s", hipGetErrorString(e));
     return R.lag + k * LAG_WORDS;
 }
@@ -1108,6 +1122,10 @@ int rank_setup(Multi& M, RankState& R, sph_ctx* c, int rank) {
 void multi_free(sph_ctx* ctx) {
     Multi* M = ctx->mg;
     if (!M) return;
+    if (g_ht.on && g_ht.steps > 0)
+        std::fprintf(stderr, "[host] world %d ranks here %zu: %lld steps, %.1f us/step on the host, %.1f us/step of it blocked on "
+                     "lag events\n", M->world, M->ranks.size(), (long long)g_ht.steps, 1e6 * g_ht.total / (double)g_ht.steps,
+                     1e6 * g_ht.wait / (double)g_ht.steps);
     for (auto& R : M->ranks) rank_free(R);
     if (M->hist_dev) (void)hipFree(M->hist_dev);
     if (M->comm) (void)ncclCommDestroy(M->comm);
@@ -1266,7 +1284,12 @@ int multi_step(sph_ctx* ctx, float dt, int32_t nsteps) {
             int r = validate(M, ctx);
             if (r != SPH_OK) return r;
         }
+        const double t0 = g_ht.on ? now_s() : 0.0;
         int r = multi_one_step(M, ctx, dt);
+        if (g_ht.on) {
+            g_ht.total += now_s() - t0;
+            g_ht.steps++;
+        }
         static const bool trace = std::getenv("SPH_TRACE_LAG") != nullptr;
         if (r == SPH_OK && trace && (ctx->cfg.flags & SPH_FLAG_VALIDATE))
             for (auto& R : M.ranks) {
