@@ -49,6 +49,9 @@ struct RankState {
     int32_t e_c1o[2] = {0, 0}, e_c1i[2] = {0, 0};   // the next step's message capacities (early sends)
     bool comm_borrowed = false;      // SPH_DEBUG_SERIAL_GROUP: slab 0's comm stream
     bool sent_pending = false;       // ev_sent closes comm-stream work the main stream has not waited for yet
+    uint32_t* ebins = nullptr;       // early sends: the boundary pass's send counts (SendBins), 2 x ebin_cap words
+    int32_t ebin_cap = 0;
+    bool ebins_used = false;         // this step's boundary pass counted into ebins (k_slab_lag clears them)
     int32_t g2[2] = {0, 0};          // grid bounds of the two-column boundary ranges (early sends), 0: n_ub
     SlabSizes* dz = nullptr;
     float4* msg_out[2] = {nullptr, nullptr};
@@ -227,10 +230,38 @@ int ensure_buf(Multi& M, sph_ctx* ctx, T** p, int32_t* cap, int32_t need) {
     return SPH_OK;
 }
 
+// a switch in the environment: set and not "0"
+bool env_on(const char* name) {
+    const char* v = std::getenv(name);
+    return v && *v && std::atoi(v) != 0;
+}
+
+// the early sends' count bins (SendBins): both sides' send blocks, zeroed; allocated once per slot capacity
+int ensure_ebins(Multi& M, RankState& R, int32_t nb) {
+    if (nb <= R.ebin_cap && R.ebins) return SPH_OK;
+    sph_ctx* ctx = R.c;
+    int r = sync_all(M, ctx);
+    if (r != SPH_OK) return r;
+    dfree(R.ebins);
+    const int32_t cap = std::max(nb, slab_send_blocks(0, std::max(ctx->capacity, 1)));
+    HIPCHK(hipMalloc((void**)&R.ebins, 2 * (size_t)cap * sizeof(uint32_t)));
+    HIPCHK(hipMemset(R.ebins, 0, 2 * (size_t)cap * sizeof(uint32_t)));
+    HIPCHK(hipDeviceSynchronize());
+    R.ebin_cap = cap;
+    return SPH_OK;
+}
+
 int rank_init(RankState& R) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipStreamCreateWithFlags(&R.comm, hipStreamNonBlocking));
+    // the comm stream's work (ρ halo, boundary force pass, the next step's sends) must end under the interior
+    // pass: at the device's highest stream priority its workgroups dispatch ahead of the interior pass's pending
+    // ones (SPH_COMM_PRIORITY=0: default priority)
+    int prio_lo = 0, prio_hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    const char* pe = std::getenv("SPH_COMM_PRIORITY");
+    const bool high = !(pe && std::atoi(pe) == 0);
+    HIPCHK(hipStreamCreateWithPriority(&R.comm, hipStreamNonBlocking, high ? prio_hi : prio_lo));
     for (hipEvent_t* e : {&R.ev_packed, &R.ev_in, &R.ev_rho_packed, &R.ev_rho_recv, &R.ev_bdone, &R.ev_sent, &R.ev_fdone})
         HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     for (auto& e : R.lag_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -260,6 +291,7 @@ void rank_free(RankState& R) {
     R.c->dz_ahead = false;
     dfree(R.dz);
     dfree(R.cnt_dev);
+    dfree(R.ebins);
     if (R.lag) (void)hipHostFree(R.lag);
     if (R.comm && !R.comm_borrowed) (void)hipStreamDestroy(R.comm);
     R = RankState{};
@@ -721,7 +753,7 @@ int phase_density(RankState& R, Multi& M) {
 // grid_ub2 slots) runs in the same launch: the two boundary columns are one launch.
 bool force_dev(sph_ctx* ctx, const uint32_t* lo, const uint32_t* hi, int64_t grid_ub, float dt,
                const uint32_t* lo2 = nullptr, const uint32_t* hi2 = nullptr, int64_t grid_ub2 = 0,
-               hipStream_t st = nullptr, bool jump_err = false) {
+               hipStream_t st = nullptr, bool jump_err = false, SendBins sb = SendBins{}) {
     MoverSink mv = mover_sink(ctx);
     if (grid_ub <= 0 && grid_ub2 <= 0) return mv.sk != nullptr;
     KTimer t(ctx, "force_integrate", 76.0 * (double)(std::max<int64_t>(grid_ub, 0) + grid_ub2), true);
@@ -730,7 +762,7 @@ bool force_dev(sph_ctx* ctx, const uint32_t* lo, const uint32_t* hi, int64_t gri
     mv.jump_err = jump_err ? 1 : 0;
     launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, 0, (int32_t)std::max<int64_t>(grid_ub, 0), ctx->grid, ctx->sc,
                        dt, forcing(ctx), ctx->pos2, ctx->vel2, ctx->keys, mv, hit_mask_read(ctx), path_ctr(ctx),
-                       st ? st : ctx->stream, DevRange{lo, hi}, DevRange{lo2, hi2}, (int32_t)grid_ub2);
+                       st ? st : ctx->stream, DevRange{lo, hi}, DevRange{lo2, hi2}, (int32_t)grid_ub2, sb);
     return mv.sk != nullptr;
 }
 
@@ -768,16 +800,32 @@ int phase_boundary(RankState& R, Multi& M, float dt, bool early) {
     CKPT(R, "rho unpack");
     const bool one_col = ctx->sl.cx_hi - ctx->sl.cx_lo == 1;
     const uint32_t* pk = R.dz->pick;
+    R.ebins_used = false;
     if (early) {   // lo, lo + 1 | hi − 2, hi − 1 (every slab has at least four columns)
         const int64_t gl = R.g2[0] > 0 ? std::min<int64_t>(R.g2[0], R.n_ub) : R.n_ub;
         const int64_t gr = R.g2[1] > 0 ? std::min<int64_t>(R.g2[1], R.n_ub) : R.n_ub;
+        // with the jump guard the next step's sends come from exactly these columns, so this pass counts them per
+        // send block (SendBins: no count launch); without it they come from every own slot (phase_boundary below)
+        SendBins sb;
+        R.nb_send = slab_send_blocks(0, (int32_t)std::max<int64_t>(R.n_ub, 1));
+        if (halo && R.jump_guard && !env_on("SPH_NO_FOLDED_COUNT")) {
+            int r = ensure_ebins(M, R, R.nb_send);
+            if (r != SPH_OK) return r;
+            sb.bins = R.ebins;
+            sb.nblk = R.nb_send;
+            sb.col_le = col_le(ctx);
+            sb.col_ge = col_ge(ctx);
+            sb.side[0] = ctx->has_left ? 0 : 1;
+            sb.side[1] = ctx->has_left && ctx->has_right ? 1 : -1;
+            R.ebins_used = true;
+        }
         // a boundary particle that moves two columns can leave the candidate columns of the other side too
         if (ctx->has_left && ctx->has_right)
-            force_dev(ctx, &pk[1], &pk[6], gl, dt, &pk[7], &pk[4], gr, b, true);
+            force_dev(ctx, &pk[1], &pk[6], gl, dt, &pk[7], &pk[4], gr, b, true, sb);
         else if (ctx->has_left)
-            force_dev(ctx, &pk[1], &pk[6], gl, dt, nullptr, nullptr, 0, b, true);
+            force_dev(ctx, &pk[1], &pk[6], gl, dt, nullptr, nullptr, 0, b, true, sb);
         else if (ctx->has_right)
-            force_dev(ctx, &pk[7], &pk[4], gr, dt, nullptr, nullptr, 0, b, true);
+            force_dev(ctx, &pk[7], &pk[4], gr, dt, nullptr, nullptr, 0, b, true, sb);
     } else if (one_col && (ctx->has_left || ctx->has_right)) {   // the owned column is both boundary columns
         force_dev(ctx, &pk[1], &pk[4], R.n_ub, dt, nullptr, nullptr, 0, b);
     } else if (ctx->has_left && ctx->has_right) {   // both boundary columns in one launch
@@ -810,8 +858,7 @@ int phase_boundary(RankState& R, Multi& M, float dt, bool early) {
     // without the jump guard (a full-sort step) the sends scan every own slot, after the interior pass
     const bool cand = R.jump_guard;
     if (!cand) HIPCHK(hipStreamWaitEvent(b, R.ev_fdone, 0));
-    R.nb_send = slab_send_blocks(0, (int32_t)std::max<int64_t>(R.n_ub, 1));
-    {
+    if (!R.ebins_used) {
         KTimer t(ctx, "slab_count", 4.0 * R.n_ub);
         launch_slab_count_dev(ctx->keys, R.dz, R.nb_send, gyz(ctx), col_le(ctx), col_ge(ctx), ctx->sblk,
                               totals_slot(ctx, M.steps + 1), b, cand, false, true);
@@ -820,7 +867,7 @@ int phase_boundary(RankState& R, Multi& M, float dt, bool early) {
         KTimer t(ctx, "slab_pack", 36.0 * (R.e_c1o[0] + R.e_c1o[1]));
         launch_slab_pack2_dev(ctx->keys, ctx->pos2, ctx->vel2, ctx->id, ctx->sk_valid ? ctx->sk_cur : nullptr,
                               (uint32_t)ctx->grid.cx0 * gyz(ctx), R.dz, R.nb_send, gyz(ctx), col_le(ctx), col_ge(ctx),
-                              ctx->sblk, R.left >= 0 ? R.msg_out[0] : nullptr, R.e_c1o[0],
+                              R.ebins_used ? R.ebins : ctx->sblk, R.left >= 0 ? R.msg_out[0] : nullptr, R.e_c1o[0],
                               R.right >= 0 ? R.msg_out[1] : nullptr, R.e_c1o[1], totals_slot(ctx, M.steps + 1), b, cand,
                               true);
     }
@@ -884,9 +931,13 @@ int phase_finish(RankState& R, float dt, int64_t step, bool global_flags, bool e
     ctx->steps++;
     ctx->sim_time += (double)dt;
     const int k = (int)(step % LAG_SLOTS);
+    // the count bins the boundary pass filled and the pack read (on this same stream) are cleared for the next use
+    const bool clear = on_comm && R.ebins_used;
     launch_slab_lag(R.dz, ctx->has_left ? 1 : 0, ctx->has_right ? 1 : 0, totals_slot(ctx, step),
                     R.left >= 0 ? R.rho_in[0] : nullptr, R.right >= 0 ? R.rho_in[1] : nullptr,
-                    global_flags ? R.cnt_dev + 4 : nullptr, R.lag + k * LAG_WORDS, s);
+                    global_flags ? R.cnt_dev + 4 : nullptr, R.lag + k * LAG_WORDS, s, clear ? R.ebins : nullptr,
+                    clear ? 2 * R.nb_send : 0);
+    R.ebins_used = false;
     if (halo) HIPCHK(hipEventRecord(R.lag_ev[k], s));   // read two steps on
     if (on_comm) {
         HIPCHK(hipEventRecord(R.ev_sent, s));
@@ -918,7 +969,7 @@ int multi_join(Multi& M) {
 // schedule, the cuts, the re-sort mode), so the exchanges issued early are matched on every rank.
 bool early_next(const Multi& M) {
     if (M.world < 2 || M.ranks.empty()) return false;
-    if (M.hold_early > 0 || std::getenv("SPH_NO_EARLY_SENDS")) return false;
+    if (M.hold_early > 0 || env_on("SPH_NO_EARLY_SENDS")) return false;
     const RankState& R0 = M.ranks[0];
     if (R0.since_cut + 1 < 3) return false;   // the next step sizes its messages exactly
     if (M.rebalance_every > 0 && (M.steps + 1) % M.rebalance_every == 0) return false;   // it may re-cut

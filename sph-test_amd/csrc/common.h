@@ -199,6 +199,19 @@ struct DevRange {
     const uint32_t* hi = nullptr;
 };
 
+// The slab step's send blocks: the count / pack pair takes SEND_SLOTS consecutive owned slots per workgroup (slab.hip).
+constexpr int32_t SEND_SLOTS = 4096;
+// Early sends (abi_multi.cpp phase_boundary): the boundary force pass counts the next step's sends itself, per send
+// block, into bins[side * nblk + block] (zeroed by the step's k_slab_lag after the pack has read them). Range r of the
+// launch (0: dr, 1: dr2) starts a side's send range and counts for side[r] (−1: none): new column <= col_le (left)
+// or >= col_ge (right).
+struct SendBins {
+    uint32_t* bins = nullptr;   // null: no count
+    int32_t nblk = 0;
+    int32_t side[2] = {-1, -1};
+    int32_t col_le = 0, col_ge = 0;
+};
+
 // The in-library slab step (abi_multi.cpp) keeps every per-step size on the device: the counts of
 // the halo messages arrive in their headers, the slot ranges come out of the re-sort's cell table,
 // and every kernel reads them here (launch grids are host upper bounds). No host read per step.
@@ -561,7 +574,8 @@ void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs,
                         int32_t ib, int32_t ie, GridDesc g, SphConst c, float dt, float fext_x,
                         float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths,
-                        hipStream_t s, DevRange dr = DevRange{}, DevRange dr2 = DevRange{}, int32_t ie2 = 0);
+                        hipStream_t s, DevRange dr = DevRange{}, DevRange dr2 = DevRange{}, int32_t ie2 = 0,
+                        SendBins sb = SendBins{});
 
 // slab decomposition (slab.hip)
 // Order-preserving compaction of the sorted slots [b, e) whose key column satisfies
@@ -615,9 +629,10 @@ void launch_slab_unpack_rho2(float2* rp, SlabSizes* dz, const float2* msg_l, int
 // out[0..1] sent records (left, right), out[2..3] received headers, out[4..5] ρ sent, out[6..7] ρ received,
 // out[8] assembled slots, out[9] flags (gflags non-null: that word instead, every rank's flags reduced)
 // totals: this step's send counts (k_slab_pack2 / k_slab_scan wrote them into the step's slot)
+// zero/nzero: words to clear (the early sends' count bins, after the pack read them); null: none
 void launch_slab_lag(SlabSizes* dz, int32_t has_left, int32_t has_right, const uint32_t* totals,
                      const float2* rho_in_l, const float2* rho_in_r, const uint32_t* gflags, uint32_t* out,
-                     hipStream_t s);
+                     hipStream_t s, uint32_t* zero = nullptr, int32_t nzero = 0);
 
 // owned slots [o0, o0+n) -> records of 8 floats (x,y,z,u,v,w,id-bits,ρ)
 void launch_pack_owned(const float4* pos, const float4* vel, const int32_t* id, const float2* rp,

@@ -40,6 +40,7 @@ __device__ __forceinline__ uint32_t block_ballot_count(bool pred, uint32_t* wcnt
 // single-workgroup scan between them sees few entries (one pass per side at C3).
 constexpr int SL_PER = 16;
 constexpr int SL_SEND = SL_BLK * SL_PER;
+static_assert(SL_SEND == SEND_SLOTS, "send blocks: common.h SEND_SLOTS");
 
 int32_t slab_send_blocks(int32_t b, int32_t e) { return e > b ? (e - b + SL_SEND - 1) / SL_SEND : 1; }
 
@@ -531,7 +532,8 @@ void launch_slab_unpack_rho2(float2* rp, SlabSizes* dz, const float2* msg_l, int
 __global__ void k_slab_lag(SlabSizes* __restrict__ dz, int32_t has_left, int32_t has_right,
                            const uint32_t* __restrict__ totals, const float2* __restrict__ rho_in_l,
                            const float2* __restrict__ rho_in_r, const uint32_t* __restrict__ gflags,
-                           uint32_t* __restrict__ out) {
+                           uint32_t* __restrict__ out, uint32_t* __restrict__ zero, int32_t nzero) {
+    for (int32_t t = (int32_t)threadIdx.x; t < nzero; t += (int32_t)blockDim.x) zero[t] = 0u;
     if (threadIdx.x != 0) return;
     const uint32_t* v = dz->pick;
     const uint32_t rg[10] = {v[0], v[1], v[1], v[4], v[4], v[5], v[1], v[2], v[3], v[4]};
@@ -576,8 +578,9 @@ __global__ void k_slab_lag(SlabSizes* __restrict__ dz, int32_t has_left, int32_t
 
 void launch_slab_lag(SlabSizes* dz, int32_t has_left, int32_t has_right, const uint32_t* totals,
                      const float2* rho_in_l, const float2* rho_in_r, const uint32_t* gflags, uint32_t* out,
-                     hipStream_t s) {
-    k_slab_lag<<<1, 64, 0, s>>>(dz, has_left, has_right, totals, rho_in_l, rho_in_r, gflags, out);
+                     hipStream_t s, uint32_t* zero, int32_t nzero) {
+    k_slab_lag<<<1, 256, 0, s>>>(dz, has_left, has_right, totals, rho_in_l, rho_in_r, gflags, out, zero,
+                                 zero ? nzero : 0);
 }
 
 void launch_slab_unpack(const float4* rec, int32_t n, float4* pos, float4* vel, int32_t* id, hipStream_t s) {

@@ -55,6 +55,7 @@ constexpr int TF_FALLBACK = 4 * TF_GCAP;
 #define SPH_TF_BLK 256
 #endif
 constexpr int TF_BLK = SPH_TF_BLK;
+static_assert(SEND_SLOTS % TF_BLK == 0, "a force workgroup lies in one send block (SendBins)");
 // Slots each thread stages per round (loads in flight together): pass 1 up to 1,350 slots in 256 threads
 // takes all of a plane in one or two rounds; pass 2 holds 40 B per slot in registers.
 #ifndef SPH_TT_STAGE_U
@@ -615,16 +616,18 @@ __global__ __launch_bounds__(TF_BLK) __attribute__((amdgpu_waves_per_eu(4))) voi
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
     const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, PairK pk, float dt,
     float fext_x, float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o, MoverSink mv,
-    HitMask hm, uint32_t* __restrict__ paths, DevRange dr, DevRange dr2, int32_t nb_a) {
+    HitMask hm, uint32_t* __restrict__ paths, DevRange dr, DevRange dr2, int32_t nb_a, SendBins sb) {
     __shared__ float4 sp[TF_GCAP + 4];     // (x, y, z, ρ)
     __shared__ float4 sv[TF_GCAP + 4];     // (u, v, w, P/ρ²)
     const int tid = threadIdx.x;
     int32_t blk = xcd_block(blockIdx.x, gridDim.x);
     int32_t nb_r = nb_a;   // this range's workgroups
+    int32_t rng = 0;       // which range (SendBins.side)
     if (dr2.lo && blk >= nb_a) {   // a second range in the same launch (the slab step's two boundary columns)
         blk -= nb_a;
         nb_r = (int32_t)gridDim.x - nb_a;
         dr = dr2;
+        rng = 1;
     }
     if (dr.lo) {   // device-resident bounds (slab step); the grid is an upper bound
         ib = (int32_t)*dr.lo;
@@ -846,6 +849,13 @@ __global__ __launch_bounds__(TF_BLK) __attribute__((amdgpu_waves_per_eu(4))) voi
             else *mv.jump = 1u;
         }
     }
+    if (sb.bins && sb.side[rng] >= 0) {   // early sends: this wave's count for its send block (workgroup-uniform test)
+        const int32_t sd = sb.side[rng], col = (int32_t)(key / col_keys<XS>(g));
+        const bool snd = sd == 0 ? col <= sb.col_le : col >= sb.col_ge;
+        const uint64_t act = __ballot(1), m = __ballot(snd);
+        if (m != 0ull && lane_id() == (uint32_t)(__ffsll((long long)act) - 1))
+            atomicAdd(sb.bins + sd * sb.nblk + (blk * TF_BLK) / SEND_SLOTS, (uint32_t)__popcll(m));
+    }
     append_mover(mv, i, wk);
 }
 
@@ -867,16 +877,16 @@ void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,
                         int32_t ie, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o,
                         uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr,
-                        DevRange dr2, int32_t ie2) {
+                        DevRange dr2, int32_t ie2, SendBins sb) {
     const int32_t nb_a = ie > ib ? (ie - ib + TF_BLK - 1) / TF_BLK : 0;
     const int32_t nb_b = dr2.lo && ie2 > 0 ? (ie2 + TF_BLK - 1) / TF_BLK : 0;
     if (nb_a + nb_b == 0) return;
     if (g.xsub == 2)
         SPH_LAUNCH(k_force_tiled<2>, nb_a + nb_b, TF_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt,
-                   fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr, nb_b ? dr2 : DevRange{}, nb_b ? nb_a : nb_a + nb_b);
+                   fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr, nb_b ? dr2 : DevRange{}, nb_b ? nb_a : nb_a + nb_b, sb);
     else
         SPH_LAUNCH(k_force_tiled<1>, nb_a + nb_b, TF_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt,
-                   fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr, nb_b ? dr2 : DevRange{}, nb_b ? nb_a : nb_a + nb_b);
+                   fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr, nb_b ? dr2 : DevRange{}, nb_b ? nb_a : nb_a + nb_b, sb);
 }
 
 #ifdef SPH_BTIME
