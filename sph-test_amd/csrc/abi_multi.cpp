@@ -256,12 +256,15 @@ int rank_init(RankState& R) {
     HIPCHK(hipSetDevice(ctx->device));
     // the comm stream's work (ρ halo, boundary force pass, the next step's sends) must end under the interior
     // pass: at the device's highest stream priority its workgroups dispatch ahead of the interior pass's pending
-    // ones (SPH_COMM_PRIORITY=0: default priority)
-    int prio_lo = 0, prio_hi = 0;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    // ones. Serialised C3 x 2 / x 4 (profiles/r04_comm_priority_ab.log): the comm work's slack under the interior
+    // passes 43 -> 55 / 39 -> 84 us. SPH_COMM_PRIORITY=0: normal priority
+    int prio_least = 0, prio_greatest = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
     const char* pe = std::getenv("SPH_COMM_PRIORITY");
-    const bool high = !(pe && std::atoi(pe) == 0);
-    HIPCHK(hipStreamCreateWithPriority(&R.comm, hipStreamNonBlocking, high ? prio_hi : prio_lo));
+    if (pe && std::atoi(pe) == 0)
+        HIPCHK(hipStreamCreateWithFlags(&R.comm, hipStreamNonBlocking));
+    else
+        HIPCHK(hipStreamCreateWithPriority(&R.comm, hipStreamNonBlocking, prio_greatest));
     for (hipEvent_t* e : {&R.ev_packed, &R.ev_in, &R.ev_rho_packed, &R.ev_rho_recv, &R.ev_bdone, &R.ev_sent, &R.ev_fdone})
         HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     for (auto& e : R.lag_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));

@@ -269,6 +269,11 @@ __device__ __forceinline__ void stage_run(int32_t src0, int32_t ln, L&& load, W&
     stage_plane<U, BLK>(c0, len, ln, load, write);
 }
 
+// a[r] for a runtime r in 0..2 as selects: an array indexed by a runtime value lives in scratch memory for the whole
+// kernel (pass 1 kept its lane windows there: three scratch stores per plane and a scratch load after each staging
+// barrier, before the scan could start)
+__device__ __forceinline__ int32_t pick3(const int32_t (&a)[3], int r) { return r == 0 ? a[0] : (r == 1 ? a[1] : a[2]); }
+
 // A plane whose three intervals exceed the LDS budget: consecutive rows that fit together are staged as
 // one group (rows 0+1 or 1+2), the others one by one; a row past the budget goes to big_row (chunks or
 // global memory). Groups run in visit order, so the hit mask's bits are taken in order. At C3 ~10% of
@@ -484,19 +489,20 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
         };
         // a row past the budget: in chunks, or straight from global memory
         auto big_row = [&](int r) {
-            if (len[r] > TT_FALLBACK) {
+            const int32_t lr = pick3(len, r), a0 = pick3(r0, r), a1 = pick3(r1, r), b0 = pick3(c0, r), b1 = pick3(c1, r);
+            if (lr > TT_FALLBACK) {
                 count_path(paths, 1);
-                for (int32_t j = r0[r]; j < r1[r]; ++j) one(dist2(pi, pos[j]));
+                for (int32_t j = a0; j < a1; ++j) one(dist2(pi, pos[j]));
                 return;
             }
 #pragma unroll 1
-            for (int32_t base = c0[r]; base < c1[r]; base += TT_GCAP) {
-                const int32_t ln = min(TT_GCAP, c1[r] - base);
+            for (int32_t base = b0; base < b1; base += TT_GCAP) {
+                const int32_t ln = min(TT_GCAP, b1 - base);
                 __syncthreads();
                 stage_run<TT_STAGE_U>(base, ln, load_p, write_p);
                 __syncthreads();
-                const int32_t lo = max(r0[r], base) - base;
-                scan(lo, max(min(r1[r], base + ln) - base - lo, 0));
+                const int32_t lo = max(a0, base) - base;
+                scan(lo, max(min(a1, base + ln) - base - lo, 0));
             }
         };
         if (total <= TT_GCAP) {
@@ -784,10 +790,11 @@ __global__ __launch_bounds__(TF_BLK) __attribute__((amdgpu_waves_per_eu(4))) voi
         // a row past the budget: in chunks (the chunks take the row's bits in order), or straight from
         // global memory
         auto big_row = [&](int r) {
-            if (len[r] > TF_FALLBACK) {
+            const int32_t lr = pick3(len, r), a0 = pick3(r0, r), a1 = pick3(r1, r), b0 = pick3(c0, r), b1 = pick3(c1, r);
+            if (lr > TF_FALLBACK) {
                 count_path(paths, 3);
-                if (by_mask) skip(r1[r] - r0[r]);
-                for (int32_t j = r0[r]; j < r1[r]; ++j) {
+                if (by_mask) skip(a1 - a0);
+                for (int32_t j = a0; j < a1; ++j) {
                     const float4 pj = pos[j];
                     if (j != i && is_hit(c, dist2(pi, pj))) {
                         const float4 vj = vel[j];
@@ -799,13 +806,13 @@ __global__ __launch_bounds__(TF_BLK) __attribute__((amdgpu_waves_per_eu(4))) voi
                 return;
             }
 #pragma unroll 1
-            for (int32_t base = c0[r]; base < c1[r]; base += TF_GCAP) {
-                const int32_t ln = min(TF_GCAP, c1[r] - base);
+            for (int32_t base = b0; base < b1; base += TF_GCAP) {
+                const int32_t ln = min(TF_GCAP, b1 - base);
                 __syncthreads();
                 stage_run<TF_STAGE_U, TF_BLK>(base, ln, load_f, write_f);
                 __syncthreads();
-                const int32_t lo = max(r0[r], base) - base;
-                const int32_t wl = max(min(r1[r], base + ln) - base - lo, 0);
+                const int32_t lo = max(a0, base) - base;
+                const int32_t wl = max(min(a1, base + ln) - base - lo, 0);
                 if (by_mask)
                     walk(wl, wl, wl, lo, 0, 0);
                 else
