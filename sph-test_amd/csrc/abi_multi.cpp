@@ -391,6 +391,25 @@ int validate_movers(RankState& R, int used) {
                         h.o1, ncells);
         by_slot.push_back(Ent{(uint32_t)x, mo[r], r});
     }
+    if (g_ht.on) {   // measurement (SPH_HOST_TIMING with SPH_FLAG_VALIDATE): the movers by origin and column move
+        const uint32_t gyz = col_keys(ctx->grid);
+        uint32_t own = 0, rec = 0, rec_clamped = 0, rec_col0 = 0, rec_col1 = 0, rec_colx = 0, own_col0 = 0;
+        for (uint32_t r = 0; r < m; ++r) {
+            const bool isr = (mi[r] & MV_REC) != 0;
+            const int32_t dc = (int32_t)(mk[r] / gyz) - (int32_t)(mo[r] / gyz);
+            if (isr) {
+                ++rec;
+                if (mo[r] == 0u || mo[r] == ncells - 1u) ++rec_clamped;
+                if (dc == 0) ++rec_col0; else if (dc == 1 || dc == -1) ++rec_col1; else ++rec_colx;
+            } else {
+                ++own;
+                if (dc == 0) ++own_col0;
+            }
+        }
+        std::fprintf(stderr, "[movers] rank %d step %lld: own %u (same column %u), records %u (clamped old key %u; same column "
+                     "%u, one column %u, more %u) of nl %u nr %u\n", R.rank, (long long)ctx->steps, own, own_col0, rec,
+                     rec_clamped, rec_col0, rec_col1, rec_colx, h.nl, h.nr);
+    }
     // the assembled old keys (records: keys2, own: sk_cur) and new keys (records: vals, own: keys)
     const uint32_t n = h.n;
     std::vector<uint32_t> skr(n), keyr(n), sko(h.no), keyo(h.no);
