@@ -52,6 +52,9 @@ struct RankState {
     uint32_t* ebins = nullptr;       // early sends: the boundary pass's send counts (SendBins), 2 x ebin_cap words
     int32_t ebin_cap = 0;
     bool ebins_used = false;         // this step's boundary pass counted into ebins (k_slab_lag clears them)
+    uint32_t* cs_alt = nullptr;      // pre-issued records: the next step's old cell-start table, built beside ctx->cs
+    uint32_t cs_alt_cap = 0;
+    bool pre_rec = false;            // the next step's k_slab_rec ran at the end of this step (comm stream)
     int32_t g2[2] = {0, 0};          // grid bounds of the two-column boundary ranges (early sends), 0: n_ub
     SlabSizes* dz = nullptr;
     float4* msg_out[2] = {nullptr, nullptr};
@@ -295,6 +298,7 @@ void rank_free(RankState& R) {
     dfree(R.dz);
     dfree(R.cnt_dev);
     dfree(R.ebins);
+    dfree(R.cs_alt);
     if (R.lag) (void)hipHostFree(R.lag);
     if (R.comm && !R.comm_borrowed) (void)hipStreamDestroy(R.comm);
     R = RankState{};
@@ -652,8 +656,11 @@ int phase_assemble(RankState& R, bool exact) {
     const SizesIn sizes{R.left >= 0 ? R.msg_in[0] : nullptr, R.right >= 0 ? R.msg_in[1] : nullptr, R.c1i[0], R.c1i[1],
                         ctx->capacity};
     R.n_ub = std::min<int64_t>(R.c1i[0] + R.n_prev_ub + R.c1i[1], ctx->capacity);
-    const bool many = ctx->resort_mode == 1 && *(volatile uint32_t*)ctx->mv_host > resort_limit((int32_t)R.n_ub);
-    if (ctx->resort_mode != 0 && !many && ctx->sk_valid && R.n_ub > 0) {
+    const bool pre = R.pre_rec;   // the record kernel ran at the end of the last step (pre_rec)
+    R.pre_rec = false;
+    ctx->dz_next = false;
+    const bool many = !pre && ctx->resort_mode == 1 && *(volatile uint32_t*)ctx->mv_host > resort_limit((int32_t)R.n_ub);
+    if (pre || (ctx->resort_mode != 0 && !many && ctx->sk_valid && R.n_ub > 0)) {
         // incremental re-sort over [left records | own slots | right records], sizes on the device
         const int32_t nl_ub = R.c1i[0], nr_ub = R.c1i[1], n_ub = (int32_t)R.n_ub;
         const AsmSrc src{ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->keys, 0,
@@ -666,7 +673,10 @@ int phase_assemble(RankState& R, bool exact) {
         const uint32_t key_base = (uint32_t)ctx->grid.cx0 * gyz(ctx);
         CKPT(R, "exchange 1");
         KTimer t(ctx, "resort", (double)R.n_ub * (2 * 4 + 2 * 36), true);
-        if (nl_ub + nr_ub > 0) {   // every rank with a neighbour (capacities are >= 512)
+        if (pre) {   // its old cell-start table becomes the table of this step
+            std::swap(ctx->cs, R.cs_alt);
+            std::swap(ctx->cs_cap, R.cs_alt_cap);
+        } else if (nl_ub + nr_ub > 0) {   // every rank with a neighbour (capacities are >= 512)
             // the records' keys and movers, the sizes, and the old cell-start table in one launch (without
             // neighbours the own block keeps its cell starts)
             CsOld csp;
@@ -941,7 +951,54 @@ int exchange1_early(Multi& M) {
 // multi_join) instead of a wait for the boundary pass plus a launch of its own. Its flags word then holds what the
 // interior pass of this step flagged only if that pass has finished; the flags are sticky, so the next step's record
 // carries them (an RCCL rank's flags are the all-reduced ones of the density pass either way).
-int phase_finish(RankState& R, float dt, int64_t step, bool global_flags, bool early) {
+// The next step's record kernel, issued at the end of this one (early sends: the messages it reads have arrived on
+// the comm stream): the records' keys and movers, the assembled sizes and the old cell-start table leave the compute
+// stream's critical path (~12 µs per step at C3) for the comm stream, which runs under the interior force pass. The
+// table is built into a second buffer (the interior pass still reads ctx->cs), swapped in by the next assemble. The
+// records' movers join the force passes' in the same counter (the re-sort does not depend on the list order), and
+// its size store clears SlabSizes.jump, which this step's passes do not set (early sends report jumps as
+// SZ_JUMP_EARLY). A host-side change between the steps (sph_debug_kick) keeps it valid: the messages the next step
+// re-packs hold the same particles at the same positions.
+int pre_rec(Multi& M, RankState& R) {
+    sph_ctx* ctx = R.c;
+    if (env_on("SPH_NO_PRE_REC") || ctx->resort_mode == 0 || !ctx->sk_valid) return SPH_OK;
+    const int32_t nl_ub = R.e_c1i[0], nr_ub = R.e_c1i[1];
+    if (nl_ub + nr_ub <= 0) return SPH_OK;
+    const int64_t n_ub = std::min<int64_t>(nl_ub + R.n_ub + nr_ub, ctx->capacity);   // a bound: sizes come from headers
+    if (ctx->resort_mode == 1 && *(volatile uint32_t*)ctx->mv_host > resort_limit((int32_t)n_ub)) return SPH_OK;
+    const uint32_t need = ctx->grid.ncells + 2;
+    if (need > R.cs_alt_cap || !R.cs_alt) {
+        int r = sync_all(M, ctx);
+        if (r != SPH_OK) return r;
+        dfree(R.cs_alt);
+        HIPCHK(hipMalloc((void**)&R.cs_alt, (size_t)need * sizeof(uint32_t)));
+        R.cs_alt_cap = need;
+    }
+    const SizesIn sizes{R.left >= 0 ? R.msg_in[0] : nullptr, R.right >= 0 ? R.msg_in[1] : nullptr, nl_ub, nr_ub,
+                        ctx->capacity};
+    const AsmSrc src{ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->keys, 0,
+                     R.left >= 0 ? (const float4*)(R.msg_in[0] + MSG_HDR_F4) : nullptr,
+                     R.right >= 0 ? (const float4*)(R.msg_in[1] + MSG_HDR_F4) : nullptr,
+                     ctx->keys2, ctx->vals, nl_ub, (int32_t)n_ub - nr_ub, R.dz};
+    const MoverSink mv{ctx->keys2, ctx->mv_count + ctx->mv_par, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_rank,
+                       (uint32_t)std::max(ctx->capacity, 1), &R.dz->flags};
+    CsOld csp;
+    csp.cs = R.cs_alt;
+    csp.src = ctx->cs;
+    csp.ncells = ctx->grid.ncells;
+    csp.gyz = gyz(ctx);
+    csp.gx = (uint32_t)ctx->grid.gx;
+    csp.has_left = ctx->has_left ? 1 : 0;
+    csp.has_right = ctx->has_right ? 1 : 0;
+    launch_slab_rec(src, (int32_t)n_ub, ctx->grid, (uint32_t)ctx->grid.cx0 * gyz(ctx), ctx->vals, ctx->keys2, mv, R.comm,
+                    &sizes, csp);
+    HIPCHK(hipGetLastError());
+    R.pre_rec = true;
+    ctx->dz_next = true;
+    return SPH_OK;
+}
+
+int phase_finish(Multi& M, RankState& R, float dt, int64_t step, bool global_flags, bool early) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
     const bool halo = R.left >= 0 || R.right >= 0;
@@ -962,6 +1019,8 @@ int phase_finish(RankState& R, float dt, int64_t step, bool global_flags, bool e
     R.ebins_used = false;
     if (halo) HIPCHK(hipEventRecord(R.lag_ev[k], s));   // read two steps on
     if (on_comm) {
+        int r = pre_rec(M, R);
+        if (r != SPH_OK) return r;
         HIPCHK(hipEventRecord(R.ev_sent, s));
         R.sent_pending = true;
     }
@@ -1047,6 +1106,7 @@ int rebalance(Multi& M, sph_ctx* pctx) {
     M.cuts = nc;
     M.rebalances++;
     M.early = false;
+    for (auto& R : M.ranks) R.pre_rec = R.c->dz_next = false;
     for (auto& R : M.ranks) {
         int r = sph_slab_recut(R.c, &M.cuts[R.rank]);
         if (r != SPH_OK) return r;
@@ -1174,7 +1234,7 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
         if ((r = phase_boundary(R, M, dt, nxt)) != SPH_OK) return r;
     if (nxt && (r = exchange1_early(M)) != SPH_OK) return r;
     for (auto& R : M.ranks)
-        if ((r = phase_finish(R, dt, M.steps, M.mode == 2 && M.world > 1, nxt)) != SPH_OK) return r;
+        if ((r = phase_finish(M, R, dt, M.steps, M.mode == 2 && M.world > 1, nxt)) != SPH_OK) return r;
     M.early = nxt;
     if (M.hold_early > 0) M.hold_early--;
     M.steps++;
@@ -1335,9 +1395,11 @@ int validate(Multi& M, sph_ctx* pctx) {
         SlabSizes h;
         HIPCHK(hipMemcpy(&h, R.dz, sizeof h, hipMemcpyDeviceToHost));
         const uint32_t cap = (uint32_t)ctx->capacity;
-        bool ok = h.flags == 0 && h.n <= cap && h.o0 <= h.o1 && h.o1 <= h.n && h.rg[0] <= h.rg[1] &&
-                  h.rg[1] <= h.rg[3] && h.rg[3] <= h.rg[5] && h.rg[5] <= h.n && (int64_t)h.n <= R.n_ub;
-        for (int k = 0; k < 6; k += 2) ok = ok && h.fr[k] <= h.fr[k + 1] && h.fr[k + 1] <= h.n;
+        // the slots of the last step's order; SlabSizes.n already holds the next layout's when its record kernel ran
+        const uint32_t n = R.pre_rec ? h.rg[5] : h.n;
+        bool ok = h.flags == 0 && h.n <= cap && n <= cap && h.o0 <= h.o1 && h.o1 <= n && h.rg[0] <= h.rg[1] &&
+                  h.rg[1] <= h.rg[3] && h.rg[3] <= h.rg[5] && h.rg[5] <= n && (int64_t)n <= R.n_ub;
+        for (int k = 0; k < 6; k += 2) ok = ok && h.fr[k] <= h.fr[k + 1] && h.fr[k + 1] <= n;
         if (!ok)
             return fail(pctx, SPH_ERR_STATE,
                         "validate rank %d step %lld: flags %u n %u (ub %lld, cap %u) o %u..%u rg %u %u %u %u %u %u "

@@ -382,10 +382,12 @@ struct CsOld {
     uint32_t* cs = nullptr;   // null: none
     uint32_t ncells = 0, gyz = 0, gx = 0;
     int32_t has_left = 0, has_right = 0;
+    const uint32_t* src = nullptr;   // the previous table when it is not cs itself (then every cell is written)
 };
 #if defined(__HIPCC__)
 // The cell-start table of the assembled old keys [left | own | right], for the incremental re-sort, made from the
-// previous step's table in place, by the workgroup `blk` (four cells per lane; 1,024 per workgroup). Owned columns:
+// previous step's table in place (or, with CsOld.src, into a second table while passes still read the first), by the
+// workgroup `blk` (four cells per lane; 1,024 per workgroup). Owned columns:
 // the own block kept its order, so cs[k] shifts by nl − o0 (o0: the previous owned start), one 16-byte load and
 // store per lane (the table is ~15 MB at C3). cs[ncells] = cs[ncells + 1] = n. Halo columns: the lower bound of
 // cell k in its block's sorted old keys key(side, t): the workgroup stages every S-th key in LDS (S >= 64, at most
@@ -457,9 +459,11 @@ __device__ __forceinline__ void cs_old_block(const CsOld& p, uint32_t blk, uint3
         }
     }
     if (k0 > ncells + 1u) return;
+    const uint32_t* in = p.src ? p.src : p.cs;
+    const bool write = shift != 0 || p.src != nullptr;   // in place, unshifted owned cells stay as they are
     if (k0 + 3u < owned_hi && k0 >= owned_lo) {   // four owned cells (cs is 16-byte aligned)
-        if (shift != 0) {
-            uint4 v = reinterpret_cast<uint4*>(p.cs)[k0 >> 2];
+        if (write) {
+            uint4 v = reinterpret_cast<const uint4*>(in)[k0 >> 2];
             v.x = (uint32_t)((int32_t)v.x + shift);
             v.y = (uint32_t)((int32_t)v.y + shift);
             v.z = (uint32_t)((int32_t)v.z + shift);
@@ -470,7 +474,7 @@ __device__ __forceinline__ void cs_old_block(const CsOld& p, uint32_t blk, uint3
     }
     for (uint32_t k = k0; k < k0 + 4u && k <= ncells + 1u; ++k) {
         if (k >= ncells) p.cs[k] = n;
-        else if (k >= owned_lo && k < owned_hi && shift != 0) p.cs[k] = (uint32_t)((int32_t)p.cs[k] + shift);
+        else if (k >= owned_lo && k < owned_hi && write) p.cs[k] = (uint32_t)((int32_t)in[k] + shift);
     }
 }
 inline int32_t cs_old_blocks(uint32_t ncells, int32_t blk) { return (int32_t)(((ncells + 2u + 3u) / 4u + blk - 1) / blk); }
