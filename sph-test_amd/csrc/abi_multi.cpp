@@ -656,7 +656,7 @@ int phase_assemble(RankState& R, bool exact) {
     const SizesIn sizes{R.left >= 0 ? R.msg_in[0] : nullptr, R.right >= 0 ? R.msg_in[1] : nullptr, R.c1i[0], R.c1i[1],
                         ctx->capacity};
     R.n_ub = std::min<int64_t>(R.c1i[0] + R.n_prev_ub + R.c1i[1], ctx->capacity);
-    const bool pre = R.pre_rec;   // the record kernel ran at the end of the last step (pre_rec)
+    const bool pre = R.pre_rec;   // the record kernel ran at the end of the last step (issue_next_rec)
     R.pre_rec = false;
     ctx->dz_next = false;
     const bool many = !pre && ctx->resort_mode == 1 && *(volatile uint32_t*)ctx->mv_host > resort_limit((int32_t)R.n_ub);
@@ -959,7 +959,7 @@ int exchange1_early(Multi& M) {
 // its size store clears SlabSizes.jump, which this step's passes do not set (early sends report jumps as
 // SZ_JUMP_EARLY). A host-side change between the steps (sph_debug_kick) keeps it valid: the messages the next step
 // re-packs hold the same particles at the same positions.
-int pre_rec(Multi& M, RankState& R) {
+int issue_next_rec(Multi& M, RankState& R) {
     sph_ctx* ctx = R.c;
     if (env_on("SPH_NO_PRE_REC") || ctx->resort_mode == 0 || !ctx->sk_valid) return SPH_OK;
     const int32_t nl_ub = R.e_c1i[0], nr_ub = R.e_c1i[1];
@@ -1019,7 +1019,7 @@ int phase_finish(Multi& M, RankState& R, float dt, int64_t step, bool global_fla
     R.ebins_used = false;
     if (halo) HIPCHK(hipEventRecord(R.lag_ev[k], s));   // read two steps on
     if (on_comm) {
-        int r = pre_rec(M, R);
+        int r = issue_next_rec(M, R);
         if (r != SPH_OK) return r;
         HIPCHK(hipEventRecord(R.ev_sent, s));
         R.sent_pending = true;

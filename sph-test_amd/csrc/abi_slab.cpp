@@ -22,7 +22,7 @@ int sph::slab_sync_ranges(sph_ctx* ctx) {
         for (int k = 0; k < 10; ++k) ctx->rng[k] = (int32_t)h.rg[k];
         ctx->o0 = (int32_t)h.o0;
         ctx->o1 = (int32_t)h.o1;
-        // the slots of the last step's order; after the next step's record kernel ran (abi_multi.cpp pre_rec),
+        // the slots of the last step's order; after the next step's record kernel ran (abi_multi.cpp issue_next_rec),
         // SlabSizes.n holds the next assembled layout's and rg[5] (k_slab_lag) this order's
         ctx->n = (int32_t)(ctx->dz_next ? h.rg[5] : h.n);
         ctx->dropped = (int32_t)h.dropped;

@@ -92,7 +92,7 @@ struct sph_ctx {
     void* staging = nullptr;
     size_t staging_bytes = 0;
     bool keys_valid = false;
-    bool dz_next = false;   // multi-GPU step: SlabSizes n / nl / no / nr hold the next step's layout (abi_multi.cpp pre_rec)
+    bool dz_next = false;   // multi-GPU step: SlabSizes n / nl / no / nr hold the next step's layout (abi_multi.cpp issue_next_rec)
     int32_t keys_active = -1;
     // incremental re-sort (resort.hip): sorted keys of the current slot order, and scratch
     uint32_t *sk_cur = nullptr, *sk_next = nullptr;
