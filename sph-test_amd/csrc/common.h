@@ -199,8 +199,12 @@ struct DevRange {
     const uint32_t* hi = nullptr;
 };
 
-// The slab step's send blocks: the count / pack pair takes SEND_SLOTS consecutive owned slots per workgroup (slab.hip).
-constexpr int32_t SEND_SLOTS = 4096;
+// The slab step's send blocks: the count / pack pair takes SEND_SLOTS consecutive owned slots per workgroup (slab.hip):
+// SPH_SL_PER slots per thread of 256.
+#ifndef SPH_SL_PER
+#define SPH_SL_PER 16
+#endif
+constexpr int32_t SEND_SLOTS = 256 * SPH_SL_PER;
 // Early sends (abi_multi.cpp phase_boundary): the boundary force pass counts the next step's sends itself, per send
 // block, into bins[side * nblk + block] (zeroed by the step's k_slab_lag after the pack has read them). Range r of the
 // launch (0: dr, 1: dr2) starts a side's send range and counts for side[r] (−1: none): new column <= col_le (left)

@@ -38,7 +38,7 @@ __device__ __forceinline__ uint32_t block_ballot_count(bool pred, uint32_t* wcnt
 
 // Send lists: each workgroup of the count / pack pair takes SL_SEND consecutive owned slots, so the
 // single-workgroup scan between them sees few entries (one pass per side at C3).
-constexpr int SL_PER = 16;
+constexpr int SL_PER = SPH_SL_PER;
 constexpr int SL_SEND = SL_BLK * SL_PER;
 static_assert(SL_SEND == SEND_SLOTS, "send blocks: common.h SEND_SLOTS");
 
