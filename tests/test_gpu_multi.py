@@ -370,3 +370,27 @@ def test_group_through_the_collapse_bitwise(pkg):
     same = bool(np.array_equal(xg, xs) and np.array_equal(vg, vs))
     print({"steps": steps, "rebalances": rebalances, "bitwise": same, "max_dx": float(np.abs(xg - xs).max())})
     assert rebalances > 0 and same
+
+
+def test_group_sloshing_long_run_bitwise(pkg):
+    """BASELINE's C4 (4,194,304 particles, sloshing: lateral forcing, the fastest x motion of the configurations) in 4
+    slabs for 2,000 steps, re-balanced every 50: the early sends' two-column scan never misses a particle (a miss would
+    stop the group with SZ_JUMP_EARLY or break the identity), and the group stays bit-identical to one context."""
+    sc = pkg.config_scenario("C4")
+    steps = 2000
+    group = pkg.SPHSim(sc, ndev=4, rebalance_every=50)
+    try:
+        group.step(steps)
+        xg, vg = group.positions(), group.velocities()
+        rebalances = group.ctx.decomposition().rebalances
+    finally:
+        group.close()
+    single = pkg.SPHSim(sc)
+    try:
+        single.step(steps)
+        xs, vs = single.positions(), single.velocities()
+    finally:
+        single.close()
+    same = bool(np.array_equal(xg, xs) and np.array_equal(vg, vs))
+    print({"steps": steps, "rebalances": rebalances, "bitwise": same, "max_dx": float(np.abs(xg - xs).max())})
+    assert same
