@@ -56,10 +56,6 @@ struct RankState {
     uint32_t* cs_alt = nullptr;      // pre-issued records: the next step's old cell-start table, built beside ctx->cs
     uint32_t cs_alt_cap = 0;
     bool pre_rec = false;            // the next step's k_slab_rec ran at the end of this step (comm stream)
-    bool rec_on_comm = true;         // the comm-path probe's verdict: the comm work ends under the interior pass
-    hipEvent_t ev_t_int = nullptr, ev_t_comm = nullptr;   // the probe's timing events (interior end, comm end)
-    bool probing = false;            // this step records the probe
-    bool probe_pending = false;      // recorded, not yet read
     int32_t g2[2] = {0, 0};          // grid bounds of the two-column boundary ranges (early sends), 0: n_ub
     SlabSizes* dz = nullptr;
     float4* msg_out[2] = {nullptr, nullptr};
@@ -99,7 +95,6 @@ struct Multi {
     int64_t steps = 0;
     bool early = false;              // this step's messages were packed and exchanged during the previous step
     int hold_early = 0;              // steps to run without early sends (after a host-side state change)
-    bool serial = false;             // SPH_DEBUG_SERIAL_GROUP: every slab on one compute and one comm stream
 };
 
 namespace {
@@ -276,8 +271,6 @@ int rank_init(RankState& R) {
         HIPCHK(hipStreamCreateWithPriority(&R.comm, hipStreamNonBlocking, prio_greatest));
     for (hipEvent_t* e : {&R.ev_packed, &R.ev_in, &R.ev_rho_packed, &R.ev_rho_recv, &R.ev_bdone, &R.ev_sent, &R.ev_fdone})
         HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    HIPCHK(hipEventCreate(&R.ev_t_int));
-    HIPCHK(hipEventCreate(&R.ev_t_comm));
     for (auto& e : R.lag_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipMalloc((void**)&R.dz, sizeof(SlabSizes)));
     HIPCHK(hipMemset(R.dz, 0, sizeof(SlabSizes)));
@@ -294,8 +287,7 @@ void rank_free(RankState& R) {
     if (!R.c) return;
     (void)hipSetDevice(R.c->device);
     if (R.comm) (void)hipStreamSynchronize(R.comm);
-    for (hipEvent_t e : {R.ev_packed, R.ev_in, R.ev_rho_packed, R.ev_rho_recv, R.ev_bdone, R.ev_sent, R.ev_fdone,
-                         R.ev_t_int, R.ev_t_comm})
+    for (hipEvent_t e : {R.ev_packed, R.ev_in, R.ev_rho_packed, R.ev_rho_recv, R.ev_bdone, R.ev_sent, R.ev_fdone})
         if (e) (void)hipEventDestroy(e);
     for (auto e : R.lag_ev)
         if (e) (void)hipEventDestroy(e);
@@ -823,7 +815,6 @@ int phase_interior(RankState& R, float dt, bool early) {
     else
         R.jump_guard = force_dev(ctx, ctx->has_left ? &pk[2] : &pk[1], ctx->has_right ? &pk[3] : &pk[4], R.n_ub, dt);
     if (early && !R.jump_guard) HIPCHK(hipEventRecord(R.ev_fdone, ctx->stream));   // the early sends scan all slots
-    if (R.probing) HIPCHK(hipEventRecord(R.ev_t_int, ctx->stream));
     CKPT(R, "interior force");
     return SPH_OK;
 }
@@ -971,7 +962,7 @@ int exchange1_early(Multi& M) {
 // re-packs hold the same particles at the same positions.
 int issue_next_rec(Multi& M, RankState& R) {
     sph_ctx* ctx = R.c;
-    if (env_on("SPH_NO_PRE_REC") || !R.rec_on_comm || ctx->resort_mode == 0 || !ctx->sk_valid) return SPH_OK;
+    if (env_on("SPH_NO_PRE_REC") || ctx->resort_mode == 0 || !ctx->sk_valid) return SPH_OK;
     const int32_t nl_ub = R.e_c1i[0], nr_ub = R.e_c1i[1];
     if (nl_ub + nr_ub <= 0) return SPH_OK;
     const int64_t n_ub = std::min<int64_t>(nl_ub + R.n_ub + nr_ub, ctx->capacity);   // a bound: sizes come from headers
@@ -1008,26 +999,6 @@ int issue_next_rec(Multi& M, RankState& R) {
     return SPH_OK;
 }
 
-// The comm-path probe (every 64 steps with early sends): the comm work's end against the interior pass's end, from
-// timing events, read once both have completed (no wait). The record kernel stays on the comm stream while the comm
-// work ends under the interior pass, and goes back to the compute stream when it does not (then the comm work is the
-// step's critical path and the kernel would lengthen it); it returns once the comm work, without it, leaves 25 µs.
-// Per rank: no exchange depends on where the kernel runs.
-void read_probe(RankState& R) {
-    if (!R.probe_pending) return;
-    if (hipEventQuery(R.ev_t_comm) != hipSuccess || hipEventQuery(R.ev_t_int) != hipSuccess) return;
-    R.probe_pending = false;
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, R.ev_t_int, R.ev_t_comm) != hipSuccess) return;
-    const bool was = R.rec_on_comm;
-    if (R.rec_on_comm && ms > 0.f) R.rec_on_comm = false;
-    else if (!R.rec_on_comm && ms < -0.025f) R.rec_on_comm = true;
-    if (g_ht.on && was != R.rec_on_comm)
-        std::fprintf(stderr, "[probe] rank %d step %lld: comm work ends %.1f us %s the interior pass: record kernel on the %s "
-                     "stream\n", R.rank, (long long)R.c->steps, 1e3 * std::fabs(ms), ms > 0.f ? "after" : "before",
-                     R.rec_on_comm ? "comm" : "compute");
-}
-
 int phase_finish(Multi& M, RankState& R, float dt, int64_t step, bool global_flags, bool early) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
@@ -1051,14 +1022,9 @@ int phase_finish(Multi& M, RankState& R, float dt, int64_t step, bool global_fla
     if (on_comm) {
         int r = issue_next_rec(M, R);
         if (r != SPH_OK) return r;
-        if (R.probing) {
-            HIPCHK(hipEventRecord(R.ev_t_comm, s));
-            R.probe_pending = true;
-        }
         HIPCHK(hipEventRecord(R.ev_sent, s));
         R.sent_pending = true;
     }
-    R.probing = false;
     R.cin_hist[k] = R.c1i[0] + R.c1i[1];
     R.n_prev_ub = R.n_ub;
     R.since_cut++;
@@ -1263,12 +1229,6 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
         if ((r = phase_density(R, M)) != SPH_OK) return r;
     if (M.world > 1 && (r = exchange2_start(M)) != SPH_OK) return r;
     const bool nxt = early_next(M);   // decided before the force passes, whose ranges depend on it
-    for (auto& R : M.ranks) {
-        read_probe(R);
-        // not in the serialised measurement group: its one comm stream carries every slab's comm work, so a slab's
-        // comm end says nothing about the one GPU per slab the measurement stands for
-        R.probing = nxt && !M.serial && !R.probe_pending && (R.left >= 0 || R.right >= 0) && M.steps % 64 == 8;
-    }
     for (auto& R : M.ranks)
         if ((r = phase_interior(R, dt, nxt)) != SPH_OK) return r;
     for (auto& R : M.ranks)
@@ -1419,7 +1379,6 @@ int multi_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
                 R.comm = M.ranks[0].comm;
                 R.comm_borrowed = true;
             }
-            M.serial = true;
         }
     }
     M.steps = 0;

@@ -69,6 +69,29 @@ def test_group_bitwise_vs_python_slab_path(pkg, tmp_path):
         sim.close()
 
 
+@pytest.mark.parametrize("switch", ["SPH_NO_PRE_REC", "SPH_NO_EARLY_SENDS"])
+def test_group_step_placement_is_bitwise_neutral(pkg, monkeypatch, switch):
+    """Where the slab step runs its work never changes results: a 3-slab group with re-balancing every 40
+    steps, 160 steps with the next step's record kernel on the comm stream and early sends (the default),
+    against the same run with the record kernel at each step's start (SPH_NO_PRE_REC) or without early sends
+    (SPH_NO_EARLY_SENDS): bit-identical positions, velocities and densities."""
+    sc = _scenario(pkg)
+
+    def run():
+        sim = pkg.SPHSim(sc, ndev=3, rebalance_every=40)
+        try:
+            sim.step(160)
+            return sim.positions(), sim.velocities(), sim.density()
+        finally:
+            sim.close()
+
+    base = run()
+    monkeypatch.setenv(switch, "1")
+    alt = run()
+    for a, b in zip(base, alt):
+        assert a.tobytes() == b.tobytes()
+
+
 def test_group_long_run_lag_sizes(pkg):
     """300 steps of a 2-slab group with re-balancing every 50: the lag-sized messages never overflow
     (a flagged overflow would fail sph_step with SPH_ERR_CAPACITY), no particle is lost, and the result
