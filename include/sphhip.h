@@ -256,6 +256,9 @@ int sph_read_path_counts(sph_ctx* ctx, uint32_t counts[4], int32_t reset);
  * last change of the slot order), [1] waves run (3 planes each).
  * reset != 0 zeroes them after the read. */
 int sph_read_hit_mask_counts(sph_ctx* ctx, uint32_t counts[2], int32_t reset);
+/* Model S: particles whose cell key changed in the last step (the movers the next incremental re-sort
+ * places; 0 with SPH_RESORT=0). Waits for the context's stream. */
+int sph_read_mover_count(sph_ctx* ctx, uint32_t* movers);
 /* stable LSD radix sort of (key, index) on the device: the sort of the step, exposed for
  * bit-exact parity tests. perm[i] = source index of sorted slot i. */
 int sph_debug_radix_sort(sph_ctx* ctx, const uint32_t* keys, int32_t count, int32_t key_bits,

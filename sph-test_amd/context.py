@@ -237,6 +237,12 @@ class Context:
         self._chk("sph_read_path_counts", self._L.sph_read_path_counts(self._h, A.ptr(out), 1 if reset else 0))
         return out
 
+    def mover_count(self) -> int:
+        """Particles whose cell key changed in the last step (sph_read_mover_count; Model S, single context)."""
+        out = np.zeros(1, np.uint32)
+        self._chk("sph_read_mover_count", self._L.sph_read_mover_count(self._h, A.ptr(out)))
+        return int(out[0])
+
     def debug_kick(self, pid: int, dv) -> None:
         """Test hook (sph_debug_kick): add dv to particle pid's velocity, in every slab that holds it."""
         d = np.ascontiguousarray(dv, dtype=np.float32)

@@ -114,6 +114,7 @@ int sph_get_stream(sph_ctx* ctx, void** s) {
 int sph_set_params(sph_ctx* ctx, const sph_params* params) {
     if (!ctx || !params) return SPH_ERR_INVALID;
     HIPCHK(hipSetDevice(ctx->device));
+    if (int r = multi_params_changing(ctx, *params)) return r;
     if (is_group(ctx)) {   // kept for the slab contexts (made at sph_init_scenario), applied to existing ones
         if (!(params->h > 0.f) || !(params->dx > 0.f) || !(params->rho0 > 0.f))
             return fail(ctx, SPH_ERR_INVALID, "Model S needs dx, h, rho0 > 0");
@@ -798,6 +799,17 @@ extern "C" {
 int sph_read_path_counts(sph_ctx* ctx, uint32_t counts[4], int32_t reset) {
     if (!ctx || !counts) return SPH_ERR_INVALID;
     return read_paths(ctx, 0, 4, counts, reset);
+}
+
+int sph_read_mover_count(sph_ctx* ctx, uint32_t* movers) {
+    if (!ctx || !movers) return SPH_ERR_INVALID;
+    if (ctx->mg) return fail(ctx, SPH_ERR_STATE, "sph_read_mover_count: single contexts only");
+    if (is_contact(ctx) || !ctx->mv_count) return fail(ctx, SPH_ERR_STATE, "sph_read_mover_count: Model S only");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    // the last force pass appended into the counter the next re-sort reads (mv_par)
+    HIPCHK(hipMemcpy(movers, ctx->mv_count + ctx->mv_par, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return SPH_OK;
 }
 
 int sph_read_hit_mask_counts(sph_ctx* ctx, uint32_t counts[2], int32_t reset) {

@@ -95,6 +95,10 @@ struct Multi {
     int64_t steps = 0;
     bool early = false;              // this step's messages were packed and exchanged during the previous step
     int hold_early = 0;              // steps to run without early sends (after a host-side state change)
+    // switches every rank must agree on (they decide the exchange sequence and the message sizes): read from the
+    // environment once per scenario and, over RCCL, max-reduced over the ranks (agree_switches)
+    bool no_early = false;           // SPH_NO_EARLY_SENDS
+    int32_t msg_cap = 0;             // SPH_DEBUG_MSG_CAP (tests): > 0 caps every lag-sized message
 };
 
 namespace {
@@ -105,12 +109,11 @@ namespace {
         if (r_ != ncclSuccess) return fail(ctx, SPH_ERR_HIP, "%s: %s", #call, ncclGetErrorString(r_)); \
     } while (0)
 
-int32_t cap_of(uint32_t cnt) {
-    // the count two steps ago + 25% + 512 (a one-column halo changes by far less in two steps), whole 256s
+int32_t cap_of(const Multi& M, uint32_t cnt) {
+    // the count two or three steps ago + 25% + 512 (a one-column halo changes by far less in three steps), whole 256s
     const int64_t c = (int64_t)cnt + cnt / 4 + 512;
     // SPH_DEBUG_MSG_CAP (tests only): cap every lag-sized message, to force the overflow path
-    if (const char* e = std::getenv("SPH_DEBUG_MSG_CAP"))
-        if (std::atoll(e) > 0) return (int32_t)std::atoll(e);
+    if (M.msg_cap > 0) return M.msg_cap;
     return (int32_t)std::min<int64_t>((c + 255) / 256 * 256, INT32_MAX / 4);
 }
 
@@ -346,7 +349,8 @@ double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock:
 const uint32_t* lag_slot(RankState& R, int64_t step, sph_ctx* ctx, int* rc) {
     const int k = (int)(step % LAG_SLOTS);
     const double t0 = g_ht.on ? now_s() : 0.0;
-    const hipError_t e = hipEventSynchronize(R.lag_ev[k]);   // done long ago unless the host runs 2 steps ahead
+    // the step two steps back: done unless the host runs more than a step ahead of the GPU
+    const hipError_t e = hipEventSynchronize(R.lag_ev[k]);
     if (g_ht.on) g_ht.wait += now_s() - t0;
     if (e != hipSuccess) *rc = fail(ctx, SPH_ERR_HIP, "lag event: %s", hipGetErrorString(e));
     return R.lag + k * LAG_WORDS;
@@ -637,11 +641,6 @@ int exchange2_start(Multi& M) {
         NCCLCHK(ncclRecv(R.rho_in[s], (size_t)(RHO_HDR + R.c2i[s]) * sizeof(float2), ncclUint8, peer, M.comm, R.comm));
     }
     NCCLCHK(ncclGroupEnd());
-    // every rank's sticky SZ_* flags as of its density pass, one word per bit (the density pass wrote them),
-    // max-reduced: each bit is the OR over the ranks, so the failure message names every rank's cause. The
-    // step's lag record carries them, so all ranks stop at the same later step. In flight on the comm
-    // stream with the interior force pass, like the ρ halo.
-    NCCLCHK(ncclAllReduce(R.cnt_dev + 4, R.cnt_dev + 4, SZ_BITS, ncclUint32, ncclMax, M.comm, R.comm));
     HIPCHK(hipEventRecord(R.ev_rho_recv, R.comm));
     return SPH_OK;
 }
@@ -871,33 +870,42 @@ int phase_boundary(RankState& R, Multi& M, float dt, bool early) {
     if (halo) HIPCHK(hipEventRecord(R.ev_bdone, b));
     CKPT(R, "boundary force");
     if (!early || !halo) return SPH_OK;
-    // the next step's sends, from this step's order and new positions: capacities from the counts two steps before
-    // the next step (as multi_one_step derives them), one count launch and one pack launch
+    // An error below leaves the counts the boundary pass added into ebins (only k_slab_lag clears them): cleared
+    // here on the comm stream, so that a later early step cannot add to stale counts.
+    auto bail = [&](int rc) {
+        if (R.ebins_used) (void)hipMemsetAsync(R.ebins, 0, 2 * (size_t)R.nb_send * sizeof(uint32_t), b);
+        R.ebins_used = false;
+        return rc;
+    };
+    // the next step's sends, from this step's order and new positions: capacities from the counts three steps before
+    // the next step, i.e. the lag record multi_one_step waited for at this step's start (reading the previous
+    // step's would block the host until the GPU finished that step's comm work: one step ahead instead of two),
+    // one count launch and one pack launch. Both neighbours derive them from the same record.
     int r = SPH_OK;
-    const uint32_t* L = lag_slot(R, M.steps - 1, ctx, &r);
-    if (r != SPH_OK) return r;
-    R.e_c1o[0] = R.left >= 0 ? cap_of(L[0]) : 0;
-    R.e_c1o[1] = R.right >= 0 ? cap_of(L[1]) : 0;
-    R.e_c1i[0] = R.left >= 0 ? cap_of(L[2]) : 0;
-    R.e_c1i[1] = R.right >= 0 ? cap_of(L[3]) : 0;
+    const uint32_t* L = lag_slot(R, M.steps - 2, ctx, &r);
+    if (r != SPH_OK) return bail(r);
+    R.e_c1o[0] = R.left >= 0 ? cap_of(M, L[0]) : 0;
+    R.e_c1o[1] = R.right >= 0 ? cap_of(M, L[1]) : 0;
+    R.e_c1i[0] = R.left >= 0 ? cap_of(M, L[2]) : 0;
+    R.e_c1i[1] = R.right >= 0 ? cap_of(M, L[3]) : 0;
     for (int sd = 0; sd < 2; ++sd) {
         const int peer = sd == 0 ? R.left : R.right;
         if (peer < 0) continue;
-        if ((r = ensure_buf(M, ctx, &R.msg_out[sd], &R.mcap_out[sd], MSG_HDR_F4 + 2 * R.e_c1o[sd])) != SPH_OK) return r;
-        if ((r = ensure_buf(M, ctx, &R.msg_in[sd], &R.mcap_in[sd], MSG_HDR_F4 + 2 * R.e_c1i[sd])) != SPH_OK) return r;
+        if ((r = ensure_buf(M, ctx, &R.msg_out[sd], &R.mcap_out[sd], MSG_HDR_F4 + 2 * R.e_c1o[sd])) != SPH_OK) return bail(r);
+        if ((r = ensure_buf(M, ctx, &R.msg_in[sd], &R.mcap_in[sd], MSG_HDR_F4 + 2 * R.e_c1i[sd])) != SPH_OK) return bail(r);
         // the neighbour's copy of this step's message must be done before it is overwritten
         if (M.mode == 1) HIPCHK(hipStreamWaitEvent(b, M.ranks[peer - M.ranks[0].rank].ev_in, 0));
     }
     // without the jump guard (a full-sort step) the sends scan every own slot, after the interior pass
     const bool cand = R.jump_guard;
-    if (!cand) HIPCHK(hipStreamWaitEvent(b, R.ev_fdone, 0));
+    if (!cand && hipStreamWaitEvent(b, R.ev_fdone, 0) != hipSuccess) return bail(fail(ctx, SPH_ERR_HIP, "wait ev_fdone"));
     if (!R.ebins_used) {
-        KTimer t(ctx, "slab_count", 4.0 * R.n_ub);
+        KTimer t(ctx, "slab_count", 4.0 * R.n_ub, false, b);
         launch_slab_count_dev(ctx->keys, R.dz, R.nb_send, gyz(ctx), col_le(ctx), col_ge(ctx), ctx->sblk,
                               totals_slot(ctx, M.steps + 1), b, cand, false, true);
     }
     {
-        KTimer t(ctx, "slab_pack", 36.0 * (R.e_c1o[0] + R.e_c1o[1]));
+        KTimer t(ctx, "slab_pack", 36.0 * (R.e_c1o[0] + R.e_c1o[1]), false, b);
         launch_slab_pack2_dev(ctx->keys, ctx->pos2, ctx->vel2, ctx->id, ctx->sk_valid ? ctx->sk_cur : nullptr,
                               (uint32_t)ctx->grid.cx0 * gyz(ctx), R.dz, R.nb_send, gyz(ctx), col_le(ctx), col_ge(ctx),
                               R.ebins_used ? R.ebins : ctx->sblk, R.left >= 0 ? R.msg_out[0] : nullptr, R.e_c1o[0],
@@ -999,7 +1007,7 @@ int issue_next_rec(Multi& M, RankState& R) {
     return SPH_OK;
 }
 
-int phase_finish(Multi& M, RankState& R, float dt, int64_t step, bool global_flags, bool early) {
+int phase_finish(Multi& M, RankState& R, float dt, int64_t step, bool early) {
     sph_ctx* ctx = R.c;
     HIPCHK(hipSetDevice(ctx->device));
     const bool halo = R.left >= 0 || R.right >= 0;
@@ -1013,9 +1021,18 @@ int phase_finish(Multi& M, RankState& R, float dt, int64_t step, bool global_fla
     const int k = (int)(step % LAG_SLOTS);
     // the count bins the boundary pass filled and the pack read (on this same stream) are cleared for the next use
     const bool clear = on_comm && R.ebins_used;
+    // flags: a local group's host ORs its ranks' own. RCCL ranks: every rank's sticky SZ_* flags as of its density
+    // pass, one word per bit, max-reduced, i.e. each bit is the OR over the ranks (the failure message names every
+    // rank's cause); the step's lag record carries them, so every rank stops two steps on, at the same step. The
+    // all-reduce runs behind this step's exchanges (early sends: at the end of the comm stream's work), where no pass
+    // of the step waits on it; it sat between the ρ halo and the boundary force pass before. It stays per step: with
+    // a reduction only every few steps, ranks ran on for up to that many steps on a state whose sizes had overflowed,
+    // and a two-rank overflow run did not finish (tests/test_gpu_rccl.py).
+    const bool gflags = M.mode == 2 && M.world > 1;
+    if (gflags) NCCLCHK(ncclAllReduce(R.cnt_dev + 4, R.cnt_dev + 4, SZ_BITS, ncclUint32, ncclMax, M.comm, s));
     launch_slab_lag(R.dz, ctx->has_left ? 1 : 0, ctx->has_right ? 1 : 0, totals_slot(ctx, step),
                     R.left >= 0 ? R.rho_in[0] : nullptr, R.right >= 0 ? R.rho_in[1] : nullptr,
-                    global_flags ? R.cnt_dev + 4 : nullptr, R.lag + k * LAG_WORDS, s, clear ? R.ebins : nullptr,
+                    gflags ? R.cnt_dev + 4 : nullptr, R.lag + k * LAG_WORDS, s, clear ? R.ebins : nullptr,
                     clear ? 2 * R.nb_send : 0);
     R.ebins_used = false;
     if (halo) HIPCHK(hipEventRecord(R.lag_ev[k], s));   // read two steps on
@@ -1051,7 +1068,7 @@ int multi_join(Multi& M) {
 // schedule, the cuts, the re-sort mode), so the exchanges issued early are matched on every rank.
 bool early_next(const Multi& M) {
     if (M.world < 2 || M.ranks.empty()) return false;
-    if (M.hold_early > 0 || env_on("SPH_NO_EARLY_SENDS")) return false;
+    if (M.hold_early > 0 || M.no_early) return false;
     const RankState& R0 = M.ranks[0];
     if (R0.since_cut + 1 < 3) return false;   // the next step sizes its messages exactly
     if (M.rebalance_every > 0 && (M.steps + 1) % M.rebalance_every == 0) return false;   // it may re-cut
@@ -1173,7 +1190,7 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
     } else {
         // an overflow flagged two steps ago (or earlier; flags are sticky) stops every rank at this same
         // step, before any exchange: over RCCL the lag record holds the flags OR-reduced over all ranks
-        // (exchange2_start), in a local group the host ORs its ranks' own
+        // (phase_finish), in a local group the host ORs its ranks' own
         uint32_t flags = 0;
         for (auto& R : M.ranks) {
             if (R.left < 0 && R.right < 0) continue;
@@ -1194,16 +1211,16 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
             // the counts of two steps before: both neighbours read the same numbers
             const uint32_t* L = lag_slot(R, M.steps - 2, R.c, &r);
             if (r != SPH_OK) return r;
-            R.c1o[0] = R.left >= 0 ? cap_of(L[0]) : 0;
-            R.c1o[1] = R.right >= 0 ? cap_of(L[1]) : 0;
-            R.c1i[0] = R.left >= 0 ? cap_of(L[2]) : 0;
-            R.c1i[1] = R.right >= 0 ? cap_of(L[3]) : 0;
-            R.c2o[0] = R.left >= 0 ? cap_of(L[4]) : 0;
-            R.c2o[1] = R.right >= 0 ? cap_of(L[5]) : 0;
-            R.c2i[0] = R.left >= 0 ? cap_of(L[6]) : 0;
-            R.c2i[1] = R.right >= 0 ? cap_of(L[7]) : 0;
-            R.g2[0] = R.left >= 0 ? cap_of(L[10]) : 0;
-            R.g2[1] = R.right >= 0 ? cap_of(L[11]) : 0;
+            R.c1o[0] = R.left >= 0 ? cap_of(M, L[0]) : 0;
+            R.c1o[1] = R.right >= 0 ? cap_of(M, L[1]) : 0;
+            R.c1i[0] = R.left >= 0 ? cap_of(M, L[2]) : 0;
+            R.c1i[1] = R.right >= 0 ? cap_of(M, L[3]) : 0;
+            R.c2o[0] = R.left >= 0 ? cap_of(M, L[4]) : 0;
+            R.c2o[1] = R.right >= 0 ? cap_of(M, L[5]) : 0;
+            R.c2i[0] = R.left >= 0 ? cap_of(M, L[6]) : 0;
+            R.c2i[1] = R.right >= 0 ? cap_of(M, L[7]) : 0;
+            R.g2[0] = R.left >= 0 ? cap_of(M, L[10]) : 0;
+            R.g2[1] = R.right >= 0 ? cap_of(M, L[11]) : 0;
             // slot bound: the assembled count two steps ago plus every record received since
             const int64_t km1 = (M.steps - 1) % LAG_SLOTS;
             R.n_prev_ub = std::min<int64_t>(R.n_prev_ub, (int64_t)L[8] + R.cin_hist[km1]);
@@ -1235,7 +1252,7 @@ int multi_one_step(Multi& M, sph_ctx* pctx, float dt) {
         if ((r = phase_boundary(R, M, dt, nxt)) != SPH_OK) return r;
     if (nxt && (r = exchange1_early(M)) != SPH_OK) return r;
     for (auto& R : M.ranks)
-        if ((r = phase_finish(M, R, dt, M.steps, M.mode == 2 && M.world > 1, nxt)) != SPH_OK) return r;
+        if ((r = phase_finish(M, R, dt, M.steps, nxt)) != SPH_OK) return r;
     M.early = nxt;
     if (M.hold_early > 0) M.hold_early--;
     M.steps++;
@@ -1281,6 +1298,18 @@ int multi_state_changed(sph_ctx* ctx) {
     return multi_join(*ctx->mg);
 }
 
+int multi_params_changing(sph_ctx* ctx, const sph_params& next) {
+    if (!ctx || !ctx->mg || !ctx->mg->ready) return SPH_OK;
+    const sph_params& o = ctx->prm;
+    // the grid (cell size 2h, the box) sizes every slab's window, cell-start tables and message columns
+    if (next.h != o.h || next.box[0] != o.box[0] || next.box[1] != o.box[1] || next.box[2] != o.box[2])
+        return fail(ctx, SPH_ERR_STATE, "multi-GPU context: h and the box are fixed once the scenario is initialised "
+                    "(sph_init_scenario again)");
+    // the messages sent during the last step and the pre-issued record kernel stay valid (same particles, same
+    // grid); the next step's force passes keep the graceful column-jump guard
+    return multi_state_changed(ctx);
+}
+
 std::vector<sph_ctx*> multi_kids(const sph_ctx* ctx) { return ctx->mg ? ctx->mg->kids : std::vector<sph_ctx*>{}; }
 
 int multi_create_group(sph_ctx* ctx) {
@@ -1291,11 +1320,39 @@ int multi_create_group(sph_ctx* ctx) {
     return SPH_OK;
 }
 
+// Switches that decide the exchange sequence, the message sizes or the cuts, read from the environment once per
+// scenario. Over RCCL every rank must hold the same values: a rank alone with SPH_NO_EARLY_SENDS would issue its
+// exchanges at other points of the step than its neighbours, and both would wait in mismatched send / receive
+// sequences until the watchdog fired. So they are compared with one all-reduce (max of v and of -v) and a mismatch
+// fails every rank's init alike. Returns SPH_DEBUG_CUT_SKEW.
+int read_switches(Multi& M, sph_ctx* ctx, int* skew) {
+    M.no_early = env_on("SPH_NO_EARLY_SENDS");
+    const char* mc = std::getenv("SPH_DEBUG_MSG_CAP");
+    M.msg_cap = mc ? std::max(0, std::atoi(mc)) : 0;
+    const char* sk = std::getenv("SPH_DEBUG_CUT_SKEW");
+    *skew = sk ? std::atoi(sk) : 0;
+    if (M.mode != 2 || M.world < 2) return SPH_OK;
+    int32_t v[6] = {M.no_early ? 1 : 0, M.msg_cap, *skew, M.no_early ? -1 : 0, -M.msg_cap, -*skew};
+    int32_t* d = nullptr;
+    HIPCHK(hipMalloc((void**)&d, sizeof v));
+    hipError_t he = hipMemcpy(d, v, sizeof v, hipMemcpyHostToDevice);
+    ncclResult_t nr = ncclSuccess;
+    if (he == hipSuccess) nr = ncclAllReduce(d, d, 6, ncclInt32, ncclMax, M.comm, ctx->stream);
+    if (he == hipSuccess && nr == ncclSuccess) he = hipMemcpyAsync(v, d, sizeof v, hipMemcpyDeviceToHost, ctx->stream);
+    if (he == hipSuccess && nr == ncclSuccess) he = hipStreamSynchronize(ctx->stream);
+    (void)hipFree(d);
+    if (nr != ncclSuccess) return fail(ctx, SPH_ERR_HIP, "switch agreement: %s", ncclGetErrorString(nr));
+    if (he != hipSuccess) return fail(ctx, SPH_ERR_HIP, "switch agreement: %s", hipGetErrorString(he));
+    for (int k = 0; k < 3; ++k)
+        if (v[k] != -v[k + 3])
+            return fail(ctx, SPH_ERR_INVALID, "ranks disagree on SPH_NO_EARLY_SENDS / SPH_DEBUG_MSG_CAP / "
+                        "SPH_DEBUG_CUT_SKEW (max %d %d %d, min %d %d %d)", v[0], v[1], v[2], -v[3], -v[4], -v[5]);
+    return SPH_OK;
+}
+
 // Test knob (tests/test_gpu_multi.py): SPH_DEBUG_CUT_SKEW=k moves every inner cut k columns right of the equal-count
 // position (every slab keeps at least one column), so the first re-balancing re-cuts the slabs of a full-size run.
-void skew_cuts(std::vector<sph_slab>& cuts) {
-    const char* e = std::getenv("SPH_DEBUG_CUT_SKEW");
-    const int k = e ? std::atoi(e) : 0;
+void skew_cuts(std::vector<sph_slab>& cuts, int k) {
     if (k == 0) return;
     for (size_t r = 0; r + 1 < cuts.size(); ++r) {
         const int c = std::max(cuts[r].cx_lo + 1, std::min(cuts[r].cx_hi + k, cuts[r + 1].cx_hi - 1));
@@ -1313,8 +1370,10 @@ int multi_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
     const int G = global_columns(p);
     if (G < 2 * M.world) return fail(ctx, SPH_ERR_INVALID, "%d columns cannot be cut into %d slabs", G, M.world);
     const std::vector<int64_t> per = lattice_columns(*sc, p);
+    int skew = 0;
+    if (int r = read_switches(M, ctx, &skew)) return r;
     M.cuts = balanced_cuts(per, M.world);
-    skew_cuts(M.cuts);
+    skew_cuts(M.cuts, skew);
     M.n_total = (int64_t)sc->nx * sc->ny * (sc->dim == 3 ? sc->nz : 1);
     const int64_t per_x = (int64_t)sc->ny * (sc->dim == 3 ? sc->nz : 1);
     int64_t maxcol = 0;
@@ -1562,8 +1621,10 @@ int sph::multi_init_rank(sph_ctx* ctx, const sph_scenario* sc) {
     const int G = global_columns(p);
     if (G < 2 * M.world) return fail(ctx, SPH_ERR_INVALID, "%d columns cannot be cut into %d slabs", G, M.world);
     const std::vector<int64_t> per = lattice_columns(*sc, p);
+    int skew = 0;
+    if (int r = read_switches(M, ctx, &skew)) return r;
     M.cuts = balanced_cuts(per, M.world);
-    skew_cuts(M.cuts);
+    skew_cuts(M.cuts, skew);
     M.n_total = (int64_t)sc->nx * sc->ny * (sc->dim == 3 ? sc->nz : 1);
     const int64_t per_x = (int64_t)sc->ny * (sc->dim == 3 ? sc->nz : 1);
     int64_t maxcol = 0, own = 0;

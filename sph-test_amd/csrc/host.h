@@ -203,19 +203,21 @@ int kstat_index(sph_ctx* c, const char* name);
 hipEvent_t take_event(sph_ctx* c);
 void resolve_pending(sph_ctx* c);
 
-// Times a scope of launches on the context's stream when profiling. ext: the scope's kernels launch
-// through SPH_LAUNCH, and the events ride in their dispatch packets (common.h LaunchEvents); otherwise
-// the events are recorded around the scope.
+// Times a scope of launches when profiling. ext: the scope's kernels launch through SPH_LAUNCH, and the
+// events ride in their dispatch packets (common.h LaunchEvents); otherwise the events are recorded around
+// the scope on `st` (the stream the scope launches on; default the context's).
 struct KTimer {
     sph_ctx* c;
     int k;
     bool ext, on;
+    hipStream_t s;
     hipEvent_t a = nullptr;
     LaunchEvents le;
     LaunchEvents* prev = nullptr;
-    KTimer(sph_ctx* ctx, const char* name, double bytes, bool ext_events = false)
+    KTimer(sph_ctx* ctx, const char* name, double bytes, bool ext_events = false, hipStream_t st = nullptr)
         : c(ctx), k(kstat_index(ctx, name)), ext(ext_events),
-          on(ctx->profiling && (ctx->prof_every <= 1 || ctx->steps % ctx->prof_every == 0)) {
+          on(ctx->profiling && (ctx->prof_every <= 1 || ctx->steps % ctx->prof_every == 0)),
+          s(st ? st : ctx->stream) {
         c->kstats[k].launches++;
         c->kstats[k].bytes = bytes;
         if (!on) return;
@@ -226,7 +228,7 @@ struct KTimer {
             prev = g_launch_events;
             g_launch_events = &le;
         } else {
-            (void)hipEventRecord(a, c->stream);
+            (void)hipEventRecord(a, s);
         }
     }
     ~KTimer() {
@@ -241,7 +243,7 @@ struct KTimer {
             c->pending.push_back({k, le.start, le.stop});
         } else {
             hipEvent_t b = take_event(c);
-            (void)hipEventRecord(b, c->stream);
+            (void)hipEventRecord(b, s);
             c->pending.push_back({k, a, b});
         }
         if (c->pending.size() > 8192) resolve_pending(c);
@@ -276,6 +278,9 @@ int slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const void* de
 void multi_free(sph_ctx* ctx);
 bool is_group(const sph_ctx* ctx);   // sph_config.ndev > 1: the context holds one slab context per GPU
 int multi_state_changed(sph_ctx* ctx);   // host-side state changed between steps: no early sends for the next step
+// sph_set_params on a multi-GPU context whose scenario is initialised: grid-changing updates are refused
+// (re-initialise the scenario), others hold the next step's early sends and drop the pre-issued record kernel
+int multi_params_changing(sph_ctx* ctx, const sph_params& next);
 int multi_create_group(sph_ctx* ctx);
 int multi_init_scenario(sph_ctx* ctx, const sph_scenario* sc);   // local group
 int multi_init_rank(sph_ctx* ctx, const sph_scenario* sc);       // RCCL rank
