@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model-r", type=int, default=0)
+    ap.add_argument("--scenario", default="", help="kind,dim,nx,ny,nz,tx,ty,tz (dx 0.01) instead of --config, e.g. a "
+                    "C5/8 rank's cross-section: 0,3,16,256,512,64,512,512")
     args = ap.parse_args()
     pkg = GE.load_package()
     if args.model_r:
@@ -27,7 +29,11 @@ def main():
         ctl.context.synchronize()
         ctl.OnDestroy()
         return
-    sim = pkg.SPHSim.from_config(args.config)
+    if args.scenario:
+        v = [int(t) for t in args.scenario.split(",")]
+        sim = pkg.SPHSim(pkg.make_scenario(*v, dx=0.01, seed=1234))
+    else:
+        sim = pkg.SPHSim.from_config(args.config)
     sim.step(args.warmup)
     sim.step(args.steps)
     sim.ctx.synchronize()

@@ -9,7 +9,11 @@ group of N slab contexts on the one device (sph_config.ndev = N), against C3 on 
     the halo copies' transport (device-local here, xGMI / RCCL there) and plus nothing else;
   * `overhead_per_slab_ms` = serial / N − C3 single: the per-GPU cost the decomposition adds.
 
-    python scripts/slab_overhead.py [N list, default 2,4,8] [steps, default 100] [--no-concurrent]
+  * `--own-comm`: SPH_DEBUG_SERIAL_GROUP=2, the compute work serialised as above but each slab keeps its own comm
+    stream, as each GPU of a real group does (with 1 all slabs' comm work queues on one stream, and a slab's halo work
+    waits behind every other slab's). Run it with GPU_MAX_HW_QUEUES >= N + 2 so each stream has a hardware queue.
+
+    python scripts/slab_overhead.py [N list, default 2,4,8] [steps, default 100] [--no-concurrent] [--own-comm]
 """
 import os
 import sys
@@ -26,6 +30,7 @@ args = [a for a in sys.argv[1:] if not a.startswith("--")]
 worlds = [int(w) for w in (args[0] if args else "2,4,8").split(",")]
 steps = int(args[1]) if len(args) > 1 else 100
 concurrent = "--no-concurrent" not in sys.argv
+serial_mode = "2" if "--own-comm" in sys.argv else "1"
 
 
 def timed(sc, **kw):
@@ -49,7 +54,9 @@ for world in worlds:
     res["single_ms"], _ = timed(sc)
     if concurrent:
         res["group_ms"], _ = timed(sc, ndev=world, rebalance_every=50)
-    os.environ["SPH_DEBUG_SERIAL_GROUP"] = "1"
+    os.environ["SPH_DEBUG_SERIAL_GROUP"] = serial_mode
+    res["serial_mode"] = int(serial_mode)
+    res["hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES")
     try:
         res["serial_ms"], res["serial_host_ms"] = timed(sc, ndev=world, rebalance_every=50)
     finally:

@@ -14,7 +14,7 @@ steps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 pkg = GE.load_package()
 from sph_test_amd import slab  # noqa: E402
 if n > 1:
-    os.environ["SPH_DEBUG_SERIAL_GROUP"] = "1"
+    os.environ.setdefault("SPH_DEBUG_SERIAL_GROUP", "1")
     sim = pkg.SPHSim(slab.weak_scenario("C3", n), ndev=n, rebalance_every=0)
 else:
     sim = pkg.SPHSim.from_config("C3")

@@ -45,11 +45,16 @@ def timed(step, sync, n, label):
            "host_us_per_step": round(host * 1e6 / steps, 2), "particle_steps_per_s": round(n * steps / wall)}, flush=True)
 
 
+import os  # noqa: E402
 for n in (4096, 32768):
-    ctl = pkg.ParticleSystemController(particleCount=n)
-    ctl.Start(sphere(n))
-    timed(lambda k: ctl.context.step(0.01, k), ctl.context.synchronize, n, f"R sphere N={n}")
-    ctl.OnDestroy()
+    for team in ("", "65"):   # the default lanes per target, and the flat form (contact.hip CT_FLAT)
+        if team:
+            os.environ["SPH_CT_TEAM"] = team
+        ctl = pkg.ParticleSystemController(particleCount=n)
+        ctl.Start(sphere(n))
+        timed(lambda k: ctl.context.step(0.01, k), ctl.context.synchronize, n, f"R sphere N={n} team {team or 'default'}")
+        ctl.OnDestroy()
+        os.environ.pop("SPH_CT_TEAM", None)
 for cfg in ("C1",):
     sim = pkg.SPHSim.from_config(cfg)
     timed(sim.step, sim.ctx.synchronize, sim.n, f"S {cfg}")

@@ -668,7 +668,7 @@ int phase_assemble(RankState& R, bool exact) {
                          R.right >= 0 ? (const float4*)(R.msg_in[1] + MSG_HDR_F4) : nullptr,
                          ctx->keys2, ctx->vals, nl_ub, n_ub - nr_ub, R.dz};
         const int used = ctx->mv_par;
-        const MoverSink mv{ctx->keys2, ctx->mv_count + used, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_rank,
+        const MoverSink mv{ctx->keys2, ctx->mv_count + used, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo,
                            (uint32_t)std::max(ctx->capacity, 1), &R.dz->flags};
         const uint32_t key_base = (uint32_t)ctx->grid.cx0 * gyz(ctx);
         CKPT(R, "exchange 1");
@@ -989,7 +989,7 @@ int issue_next_rec(Multi& M, RankState& R) {
                      R.left >= 0 ? (const float4*)(R.msg_in[0] + MSG_HDR_F4) : nullptr,
                      R.right >= 0 ? (const float4*)(R.msg_in[1] + MSG_HDR_F4) : nullptr,
                      ctx->keys2, ctx->vals, nl_ub, (int32_t)n_ub - nr_ub, R.dz};
-    const MoverSink mv{ctx->keys2, ctx->mv_count + ctx->mv_par, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_rank,
+    const MoverSink mv{ctx->keys2, ctx->mv_count + ctx->mv_par, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo,
                        (uint32_t)std::max(ctx->capacity, 1), &R.dz->flags};
     CsOld csp;
     csp.cs = R.cs_alt;
@@ -1404,9 +1404,12 @@ int multi_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
         }
         // measurement knob (scripts/slab_overhead.py --serial): every slab of a one-device group launches on
         // slab 0's stream, so the slabs run one after another and the group's step time is the sum of the
-        // per-slab step costs instead of an overlapped bound
+        // per-slab step costs instead of an overlapped bound. 1: every slab's comm work on slab 0's comm stream as
+        // well (two streams in all); 2: each slab keeps its own comm stream, as on the GPUs of a real group (run
+        // with GPU_MAX_HW_QUEUES >= slabs + 2, or streams share hardware queues and order unrelated work)
         const char* ser = std::getenv("SPH_DEBUG_SERIAL_GROUP");
-        if (ser && std::atoi(ser) != 0) {
+        const int ser_mode = ser ? std::atoi(ser) : 0;
+        if (ser_mode != 0) {
             for (int r = 1; r < M.world; ++r) {
                 if (M.kids[r]->device != M.kids[0]->device)
                     return fail(ctx, SPH_ERR_INVALID, "SPH_DEBUG_SERIAL_GROUP needs every slab on one device");
@@ -1430,7 +1433,7 @@ int multi_init_scenario(sph_ctx* ctx, const sph_scenario* sc) {
         }
         // ... and every slab's halo work on slab 0's comm stream: two streams in all, as on each GPU of a real
         // group (more streams than the device's hardware queues would share queues and order unrelated work)
-        if (ser && std::atoi(ser) != 0) {
+        if (ser_mode == 1) {
             HIPCHK(hipDeviceSynchronize());
             for (int r = 1; r < M.world; ++r) {
                 RankState& R = M.ranks[r];

@@ -271,7 +271,7 @@ int sph::slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const voi
         const AsmSrc src{ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->keys, ctx->o0 - nl, (const float4*)dev_left,
                          (const float4*)dev_right, ctx->keys2, ctx->vals, nl, nl + no};
         const int used = ctx->mv_par;
-        const MoverSink mv{ctx->keys2, ctx->mv_count + used, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_rank,
+        const MoverSink mv{ctx->keys2, ctx->mv_count + used, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo,
                            (uint32_t)std::max(ctx->capacity, 1)};
         {
             KTimer t(ctx, "slab_assemble", 40.0 * (double)(nl + nr));

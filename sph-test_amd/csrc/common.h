@@ -298,7 +298,6 @@ struct MoverSink {
     uint32_t* mi;         // slot index
     uint32_t* mk;         // new key
     uint32_t* mo;         // old key
-    uint32_t* rank;       // 3 x cap rank accumulators, zeroed here
     uint32_t cap;
     uint32_t* err = nullptr;   // SZ_OVF_MOVERS is or-ed here if the list would pass cap (entries dropped)
     uint32_t* jump = nullptr;  // slab step: SlabSizes.jump (a column jump > 1), SZ_JUMP into err (window exit)
@@ -326,9 +325,6 @@ __device__ __forceinline__ void append_mover(const MoverSink& s, int32_t i, uint
         s.mi[r] = (uint32_t)i;
         s.mk[r] = key;
         s.mo[r] = ko;
-        s.rank[r] = 0u;
-        s.rank[s.cap + r] = 0u;
-        s.rank[2 * s.cap + r] = 0u;
     }
 }
 #endif
@@ -352,7 +348,7 @@ void launch_sort_small(const uint32_t* keys_in, int32_t n, int32_t key_bits, uin
 // sk: sorted keys of the slot order; cs: its cell starts, updated in place; count: the movers'
 // counter, count_other: the next step's counter (zeroed here). Writes the re-sorted state to *_o.
 struct ResortScratch {
-    uint32_t *mi, *mk, *mo, *rank;   // appended movers (MoverSink), rank: 3 x cap
+    uint32_t *mi, *mk, *mo, *rank;   // appended movers (MoverSink); rank: 2 x cap (k_mv_rank: rk, insertion slot q)
     uint64_t* ms;                    // movers by (new key, slot)
     uint32_t *mx, *mos;              // movers by slot: slot, old key
     uint32_t cap;

@@ -200,6 +200,161 @@ __device__ __forceinline__ void contact_accumulate_team(const float4* __restrict
     w = A.omg + (totalTorque / wa.w) * dt;
 }
 
+// Flat form (team code CT_FLAT): one wave per target over the target's candidates flattened across the nine rows
+// (candidate f = row k's j = rj0_k + f − P_k, P the rows' exclusive length prefix), for the reference's scale where a
+// target has ~500 candidates in ~9 rows of ~56: the team form walks the rows one after another, a dependent global
+// load of positions, then of the touching candidates' velocities, per row. Here one round prefetches the positions of
+// CF_CHUNKS x 64 candidates, finds the touching ones (the reject test of :253, the same expressions), loads the
+// velocities of a lane's (at most CF_SLOTS) touching candidates together, evaluates both pair bodies, and adds the
+// hits' F and TA in flattened order, i.e. rows in order and j increasing within a row: the serial order, bit for bit.
+// A round where a lane touches more than CF_SLOTS candidates (never at the reference's packing) takes its chunks
+// one at a time instead: same order, same sums.
+constexpr int CT_FLAT = 65;
+constexpr int CF_CHUNKS = 8, CF_SLOTS = 3;
+__device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict__ pos, const float4* __restrict__ vel,
+                                                        const float4* __restrict__ omg, const uint32_t* __restrict__ cs,
+                                                        const GridDesc& g, const ContactConst& c, int32_t a, float4 pa,
+                                                        float4 va, float4 wa, f3& v, f3& w, uint32_t tq[3]) {
+    const int lane = (int)(threadIdx.x & 63u);
+    const Body A{xyz(pa), xyz(va), xyz(wa), pa.w};
+    const float dt = c.dt;
+    f3 totalForce = mk(0, 0, 0), totalTorque = mk(0, 0, 0);
+    uint32_t q0 = 0u, q1 = 0u, q2 = 0u;
+    const int32_t cx = cell_cx(g, pa.x);
+    const int32_t cy = cell_coord(pa.y, g.oy, g.inv_cell, g.gy);
+    const int32_t cz = cell_coord(pa.z, g.oz, g.inv_cz, g.gz);
+    const int32_t z0 = cz > 0 ? cz - 1 : 0, z1 = cz < g.gz - 1 ? cz + 1 : g.gz - 1;
+    uint32_t rj0 = 0u, rlen = 0u;
+    if (lane < 9) {
+        const int32_t xx = cx + lane / 3 - 1, yy = cy + lane % 3 - 1;
+        if (xx >= 0 && xx < g.gx && yy >= 0 && yy < g.gy) {
+            const uint32_t rowk = ((uint32_t)xx * (uint32_t)g.gy + (uint32_t)yy) * (uint32_t)g.gz;
+            rj0 = cs[rowk + (uint32_t)z0];
+            rlen = cs[rowk + (uint32_t)z1 + 1u] - rj0;
+        }
+    }
+    uint32_t incl = rlen;   // inclusive prefix over lanes 0..8 (lanes >= 9 hold 0)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    const uint32_t excl = incl - rlen;
+    // the rows' flattened starts, wave-uniform (scalar registers)
+    uint32_t P[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) P[k] = (uint32_t)__builtin_amdgcn_readlane((int)excl, k);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 8);
+    // candidate f -> sorted slot: its row k counts the starts at or below f; the row's first slot and flattened start
+    // come from lane k (a per-lane select chain over P / J compiled to a scratch-memory table)
+    auto slot_of = [&](uint32_t f) __attribute__((always_inline)) {
+        int k = 0;
+#pragma unroll
+        for (int r = 1; r < 9; ++r) k += f >= P[r] ? 1 : 0;
+        return (uint32_t)__shfl((int)rj0, k, 64) + (f - (uint32_t)__shfl((int)excl, k, 64));
+    };
+    // the hit's F and TA (TA = 0 for a repulsion-only contact) and the int torque b scatters into a (:291)
+    auto body = [&](uint32_t j, f3& F, f3& TA) __attribute__((always_inline)) {
+        const float4 pb = pos[j], vb = vel[j], wb = omg[j];
+        const Body B{xyz(pb), xyz(vb), xyz(wb), pb.w};
+        f3 TB;
+        const int h = contact_pair(c, A, B, F, TA, TB);
+        if (h != 2) TA = mk(0, 0, 0);
+        if (h == 0) F = mk(0, 0, 0);
+        if (h != 0) {
+            f3 F2, TA2, TB2;
+            if (contact_pair(c, B, A, F2, TA2, TB2) == 2) {
+                const f3 sc = TB2 * dt * TORQUE_SCALE;
+                q0 += (uint32_t)ftoi(sc.x);
+                q1 += (uint32_t)ftoi(sc.y);
+                q2 += (uint32_t)ftoi(sc.z);
+            }
+        }
+    };
+    auto add_hit = [&](const f3& F, const f3& TA, int src) __attribute__((always_inline)) {
+        totalForce = add_exact(totalForce, mk(__shfl(F.x, src, 64), __shfl(F.y, src, 64), __shfl(F.z, src, 64)));
+        totalTorque = add_exact(totalTorque, mk(__shfl(TA.x, src, 64), __shfl(TA.y, src, 64), __shfl(TA.z, src, 64)));
+    };
+#pragma unroll 1
+    for (uint32_t round = 0; round < total; round += 64u * CF_CHUNKS) {
+        uint32_t jj[CF_CHUNKS];
+        float4 pb[CF_CHUNKS];
+#pragma unroll
+        for (int ch = 0; ch < CF_CHUNKS; ++ch) {   // every position load of the round in flight together
+            const uint32_t f = round + (uint32_t)(ch * 64 + lane);
+            jj[ch] = slot_of(min(f, total - 1u));
+            pb[ch] = pos[jj[ch]];
+        }
+        uint32_t touch = 0u;   // bit ch: candidate (round, ch, lane) touches a (:240, :253)
+#pragma unroll
+        for (int ch = 0; ch < CF_CHUNKS; ++ch) {
+            const uint32_t f = round + (uint32_t)(ch * 64 + lane);
+            const f3 d = A.pos - xyz(pb[ch]);
+            const float reff = A.r * 0.5f + pb[ch].w * 0.5f;
+            if (f < total && (int32_t)jj[ch] != a && reff - len(d) > 0.001f) touch |= 1u << ch;
+        }
+        if (__any(__popc(touch) > CF_SLOTS)) {   // wave-uniform: chunk by chunk
+#pragma unroll
+            for (int ch = 0; ch < CF_CHUNKS; ++ch) {
+                f3 F = mk(0, 0, 0), TA = mk(0, 0, 0);
+                const bool hit = (touch >> ch) & 1u;
+                if (hit) body(jj[ch], F, TA);
+                for (uint64_t m = __ballot(hit); m; m &= m - 1ull) add_hit(F, TA, __builtin_ctzll(m));
+            }
+            continue;
+        }
+        // this lane's touching candidates in chunk order into three slots, then their bodies (loads in flight
+        // together). Named registers throughout: an array indexed by a lane's running count (or a select chain
+        // over one) compiles to a scratch-memory table.
+        uint32_t j0 = 0u, j1 = 0u, j2 = 0u;
+        int cnt = 0;
+#pragma unroll
+        for (int ch = 0; ch < CF_CHUNKS; ++ch)
+            if ((touch >> ch) & 1u) {
+                j2 = cnt == 2 ? jj[ch] : j2;
+                j1 = cnt == 1 ? jj[ch] : j1;
+                j0 = cnt == 0 ? jj[ch] : j0;
+                ++cnt;
+            }
+        f3 F0 = mk(0, 0, 0), T0 = F0, F1 = F0, T1 = F0, F2 = F0, T2 = F0;
+        if (cnt > 0) body(j0, F0, T0);
+        if (cnt > 1) body(j1, F1, T1);
+        if (cnt > 2) body(j2, F2, T2);
+        // the hits in flattened order: chunk by chunk, lowest lane first; a lane's next hit is always slot 0
+#pragma unroll
+        for (int ch = 0; ch < CF_CHUNKS; ++ch) {
+            const bool hc = (touch >> ch) & 1u;
+            for (uint64_t m = __ballot(hc); m; m &= m - 1ull) add_hit(F0, T0, __builtin_ctzll(m));
+            if (hc) {
+                F0 = F1; T0 = T1;
+                F1 = F2; T1 = T2;
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        q0 += (uint32_t)__shfl_xor((int)q0, o, 64);
+        q1 += (uint32_t)__shfl_xor((int)q1, o, 64);
+        q2 += (uint32_t)__shfl_xor((int)q2, o, 64);
+    }
+    tq[0] = q0; tq[1] = q1; tq[2] = q2;
+    v = A.vel + (totalForce / va.w) * dt;                                    // :302-306
+    w = A.omg + (totalTorque / wa.w) * dt;
+}
+
+// T lanes per target: 16 or 64 (team form) or CT_FLAT (one wave, flat form); lanes of a target for the launch mapping
+template <int T> constexpr int team_lanes() { return T == CT_FLAT ? 64 : T; }
+template <int T>
+__device__ __forceinline__ void contact_accumulate_lanes(const float4* __restrict__ pos, const float4* __restrict__ vel,
+                                                         const float4* __restrict__ omg, const uint32_t* __restrict__ cs,
+                                                         const GridDesc& g, const ContactConst& c, int32_t a, float4 pa,
+                                                         float4 va, float4 wa, f3& v, f3& w, uint32_t tq[3]) {
+    if constexpr (T == CT_FLAT)
+        contact_accumulate_flat(pos, vel, omg, cs, g, c, a, pa, va, wa, v, w, tq);
+    else
+        contact_accumulate_team<T>(pos, vel, omg, cs, g, c, a, pa, va, wa, v, w, tq);
+}
+
 // ApplyDragForce (compute:316-323; selectedID is a particle index). The reference applies it
 // to any particle below particleBuffer.Length, active or not.
 __device__ __forceinline__ f3 apply_drag(const ContactConst& c, int32_t pid, f3 p, f3 v, float mass) {
@@ -293,8 +448,9 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step_team(
     const uint32_t* __restrict__ cs, int32_t n_active, int32_t n, GridDesc g, ContactConst c,
     float4* __restrict__ pos_o, float4* __restrict__ vel_o, float4* __restrict__ omg_o,
     float4* __restrict__ rot_o, int32_t* __restrict__ torque_o, uint32_t* __restrict__ keys_o, MoverSink mv) {
-    const int32_t a = blockIdx.x * (CT_BLK / T) + (int32_t)(threadIdx.x / T);
-    const bool lead = (threadIdx.x & (T - 1)) == 0;
+    constexpr int L = team_lanes<T>();
+    const int32_t a = blockIdx.x * (CT_BLK / L) + (int32_t)(threadIdx.x / L);
+    const bool lead = (threadIdx.x & (L - 1)) == 0;
     if (a >= n) return;                                                      // team-uniform
     const float4 pa = pos[a], va = vel[a], wa = omg[a];
     if (a >= n_active) {
@@ -309,7 +465,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step_team(
     }
     f3 v, w;
     uint32_t tq[3];
-    contact_accumulate_team<T>(pos, vel, omg, cs, g, c, a, pa, va, wa, v, w, tq);
+    contact_accumulate_lanes<T>(pos, vel, omg, cs, g, c, a, pa, va, wa, v, w, tq);
     if (!lead) return;
     f3 p;
     float4 q;
@@ -332,13 +488,14 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_forces_team(
     const int32_t* __restrict__ id, const uint32_t* __restrict__ cs, int32_t n_active, int32_t n, GridDesc g,
     ContactConst c, float4* __restrict__ vel_o, float4* __restrict__ omg_o, int32_t* __restrict__ torque_o,
     int32_t* __restrict__ slot_of) {
-    const int32_t a = blockIdx.x * (CT_BLK / T) + (int32_t)(threadIdx.x / T);
-    const bool lead = (threadIdx.x & (T - 1)) == 0;
+    constexpr int L = team_lanes<T>();
+    const int32_t a = blockIdx.x * (CT_BLK / L) + (int32_t)(threadIdx.x / L);
+    const bool lead = (threadIdx.x & (L - 1)) == 0;
     if (a >= n) return;                                                      // team-uniform
     const float4 pa = pos[a], va = vel[a], wa = omg[a];
     f3 v = xyz(va), w = xyz(wa);
     uint32_t tq[3] = {0u, 0u, 0u};
-    if (a < n_active) contact_accumulate_team<T>(pos, vel, omg, cs, g, c, a, pa, va, wa, v, w, tq);
+    if (a < n_active) contact_accumulate_lanes<T>(pos, vel, omg, cs, g, c, a, pa, va, wa, v, w, tq);
     if (!lead) return;
     const int32_t pid = id[a];
     if ((uint32_t)pid < (uint32_t)n) slot_of[pid] = a;
@@ -405,7 +562,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_finish(
 // splitting thin candidate lists. A forced choice (1, 16, 64) wins; every choice gives bit-identical
 // results (contact_accumulate_team).
 static int contact_team(int32_t n, int forced) {
-    if (forced == 1 || forced == 16 || forced == 64) return forced;
+    if (forced == 1 || forced == 16 || forced == 64 || forced == CT_FLAT) return forced;
     if (n <= 32768) return 64;
     if (n <= 262144) return 16;
     return 1;
@@ -420,9 +577,10 @@ void launch_contact_step(const float4* pos, const float4* vel, const float4* omg
     switch (contact_team(n, team)) {
 #define SPH_CT_STEP(T)                                                                                        \
     case T:                                                                                                   \
-        k_contact_step_team<T><<<(n + CT_BLK / T - 1) / (CT_BLK / T), CT_BLK, 0, s>>>(                          \
+        k_contact_step_team<T><<<(n + CT_BLK / team_lanes<T>() - 1) / (CT_BLK / team_lanes<T>()), CT_BLK, 0, s>>>(  \
             pos, vel, omg, rot, aux, id, cs, n_active, n, g, c, pos_o, vel_o, omg_o, rot_o, torque_o, keys_o, mv);  \
         break;
+        SPH_CT_STEP(CT_FLAT)
         SPH_CT_STEP(64)
         SPH_CT_STEP(16)
 #undef SPH_CT_STEP
@@ -440,9 +598,10 @@ void launch_contact_forces(const float4* pos, const float4* vel, const float4* o
     switch (contact_team(n, team)) {
 #define SPH_CT_FORCES(T)                                                                                      \
     case T:                                                                                                   \
-        k_contact_forces_team<T><<<(n + CT_BLK / T - 1) / (CT_BLK / T), CT_BLK, 0, s>>>(                        \
+        k_contact_forces_team<T><<<(n + CT_BLK / team_lanes<T>() - 1) / (CT_BLK / team_lanes<T>()), CT_BLK, 0, s>>>( \
             pos, vel, omg, id, cs, n_active, n, g, c, vel_o, omg_o, torque_o, slot_of);                         \
         break;
+        SPH_CT_FORCES(CT_FLAT)
         SPH_CT_FORCES(64)
         SPH_CT_FORCES(16)
 #undef SPH_CT_FORCES

@@ -52,7 +52,7 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
     }
     // incremental re-sort (both models)
     AL(sk_cur, n); AL(sk_next, n);
-    AL(mv_mi, n); AL(mv_mk, n); AL(mv_mo, n); AL(mv_rank, 3 * n); AL(mv_mx, n); AL(mv_mos, n); AL(mv_ms, n);
+    AL(mv_mi, n); AL(mv_mk, n); AL(mv_mo, n); AL(mv_rank, 2 * n); AL(mv_mx, n); AL(mv_mos, n); AL(mv_ms, n);
     AL(mv_count, 2);
     HIPCHK(hipMemset(ctx->mv_count, 0, 2 * sizeof(uint32_t)));
 #undef AL

@@ -84,16 +84,18 @@ ResortScratch resort_scratch(sph_ctx* ctx) {
 // The force pass appends movers for the next step's incremental re-sort.
 MoverSink mover_sink(sph_ctx* ctx) {
     if (ctx->resort_mode == 0 || !ctx->sk_valid) return MoverSink{};
-    return MoverSink{ctx->sk_cur, ctx->mv_count + ctx->mv_par, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_rank,
+    return MoverSink{ctx->sk_cur, ctx->mv_count + ctx->mv_par, ctx->mv_mi, ctx->mv_mk, ctx->mv_mo,
                      (uint32_t)std::max(ctx->capacity, 1)};
 }
 
 // Bring the slots into stable (key, index) order: the incremental re-sort when the previous
 // step's sorted keys and cell starts describe the current slot order, else the full radix sort.
-// Movers above which the full radix sort is cheaper than the incremental re-sort: k_mv_rank's
-// all-pairs counts grow as m², the full sort as n (C3: ~12k movers, where the two cross).
+// Movers above which the full radix sort is taken instead of the incremental re-sort. Until r4 k_mv_rank counted
+// all pairs of movers (m², crossing the full sort's cost at ~12k movers at C3, the limit was 12·√n); its ranges are
+// O(m) per workgroup now, and the re-sort's cost is the stayers' scatter (n) plus a few passes over the movers, so the
+// full sort (three 8-bit passes, a gather and the cell starts over n) pays only when a large share moves.
 uint32_t resort_limit(int32_t n) {
-    return std::max<uint32_t>(4096u, (uint32_t)(12.0 * std::sqrt((double)std::max(n, 0))));
+    return std::max<uint32_t>(4096u, (uint32_t)std::max(n, 0) / 16u);
 }
 
 int sort_wcsph(sph_ctx* ctx) {

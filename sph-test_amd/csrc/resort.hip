@@ -20,22 +20,17 @@
 // for bit with the full sort.
 //
 // Kernels:
-//   k_mv_rank        counts per mover against every 64-mover tile (sorted in LDS, binary searches):
-//                    (key, index) rank, index rank, A(q)
-//   k_mv_place       movers: scatter of (pos, vel, id, key); tables by (key, index) and by index
-//   k_mv_merge       stayers: scatter of (pos, vel, id, key); extra workgroups update the cell
-//                    starts in place: cs[k] += #{movers: new key < k} − #{movers: old key < k}
+//   k_mv_rank        per mover its (key, index) rank and insertion slot q, and the tables by (key, index) and by
+//                    index, each workgroup over its own range of slots and of new keys: O(m) per workgroup
+//   k_mv_merge       stayers: scatter of (pos, vel, id, key); extra workgroups place the movers (A(q) from the
+//                    table by index) and update the cell starts in place:
+//                    cs[k] += #{movers: new key < k} − #{movers: old key < k}
 // The scatters replace the permutation gather, and the update the cell-start rebuild, of the full path.
 #include "common.h"
 
 namespace sph {
 
 constexpr int MV_BLK = 256;
-// movers per rank tile: 64 gives ~4x the work items of 256 for a few more atomics (256 -> 64 was
-// faster in every paired round, C3 re-sort ~42 -> ~39 us; 32 and 128 are within the run-to-run noise
-// of 64, profiles/r01_mv_tile_ab.log)
-constexpr int MV_TILE = 64;
-constexpr int MV_RANK_GRID = 2048;
 
 static __device__ __forceinline__ uint64_t comp(uint32_t key, uint32_t idx) { return (uint64_t)key << 32 | idx; }
 
@@ -121,102 +116,154 @@ static __device__ __forceinline__ uint32_t movers_before(bool mv, uint32_t block
     return off + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
 }
 
-// #entries below v in a sorted 64-entry LDS array (branchless; pads sort last and are never below v)
-template <typename T>
-static __device__ __forceinline__ uint32_t lb64(const T* __restrict__ a, T v) {
-    uint32_t p = 0;
+// Mover ranks in O(m) per workgroup (replaces the all-pairs tile counts of r1-r4, whose work grew as m²: the C3
+// re-sort chain went from 27.7 us from rest to 41.5 us mid-collapse). Workgroup b of G owns the slots
+// [x0, x1) = [b·n/G, (b+1)·n/G) of the assembled old order and the new keys [kd0, kd1) = [sk(x0), sk(x1)) (the
+// old sorted keys at those slots, so every workgroup's key range holds about n/G particles and ~m/G movers; the
+// ranges partition all keys, sentinels included). It streams the whole mover list once (U per lane in flight):
+//   rk(x) = #{y : k_y < kd0} + #{y with k_y in [kd0, kd1) : (k_y, y) < (k_x, x)}   for its dest entries (k_x in range)
+//   ri(x) = #{y : y < x0} + #{y with slot in [x0, x1) : y < x}                    for its source entries (x in range)
+// the first terms counted while streaming, the second by comparisons among the entries staged in LDS (~m/G each).
+// It writes the sorted tables the merge reads, ms[rk] = (k, x), mx[ri] = x, mos[ri] = old key, and per mover rk and
+// its insertion slot q = clamp(x, cs_old[k], cs_old[k + 1]) (rank[r], rank[cap + r]) for the placement, so no kernel
+// after this one reads cs_old while the merge updates it in place. A range with more entries than LDS holds (a
+// state where most particles move, only under SPH_RESORT=2) counts them against the whole list instead: slow, same
+// result. Also zeroes the next step's mover counter.
+constexpr int MV_RANK_GRID = 256;                 // workgroups at most; one per CU
+constexpr int MV_RANK_U = 16;                     // movers per lane per streaming round
+constexpr int MV_RK_CAP = 4096, MV_RS_CAP = 4096;  // entries staged per workgroup (80 KB of LDS)
+
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
 #pragma unroll
-    for (uint32_t s = 32; s > 0; s >>= 1) p += a[p + s - 1] < v ? s : 0u;
-    return p + (a[p] < v ? 1u : 0u);
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+    __syncthreads();
+    if (lane_id() == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < MV_BLK / 64; ++k) t += red[k];
+    return t;
 }
 
-// Per mover x (append order): rank[x] = #{y : (k_y, i_y) < (k_x, i_x)}, rank[cap + x] =
-// #{y : i_y < i_x}, rank[2cap + x] = A(q_x) = #{y : i_y < q_x}. Work items = (MV_BLK movers) x
-// (MV_TILE-mover tile); partial counts are added atomically (integers: order-independent).
-// The tile is sorted twice in LDS (by (key, index) and by index: each entry's rank among the 64, counted a
-// quarter per wave), and each mover counts by three 7-probe binary searches instead of 3 x 64 compares
-// (~6.5 VALU per mover pair before, O(m^2) in the movers).
-// Also zeroes the next step's mover counter.
-// k_mv_rank's tile logic: lb64 searches exactly 64 entries, the tile is filled by threads < MV_TILE and
-// counted by MV_BLK / MV_TILE parts
-static_assert(MV_TILE == 64 && MV_BLK >= MV_TILE && MV_BLK % MV_TILE == 0, "k_mv_rank assumes 64-entry tiles");
-__global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__ mtotal,
-                                                    uint32_t* __restrict__ next_count,
-                                                    const uint32_t* __restrict__ cs_old, ResortScratch w) {
-    constexpr int NPART = MV_BLK / MV_TILE;                  // waves counting one quarter of the tile each
-    __shared__ uint64_t tile[MV_TILE];                       // (key, index) in append order; pads ~0
-    __shared__ uint64_t sc[MV_TILE];                         // sorted by (key, index)
-    __shared__ uint32_t si[MV_TILE];                         // indices, sorted
-    __shared__ uint32_t part_c[NPART][MV_TILE], part_i[NPART][MV_TILE];
-    if (w.dz) w.mi_off = (int32_t)w.dz->nl - (int32_t)w.dz->o0;
+__global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__ mtotal, uint32_t* __restrict__ next_count,
+                                                    const uint32_t* __restrict__ cs_old, ResortScratch w, AsmSrc src,
+                                                    int32_t n) {
+    __shared__ uint64_t dk[MV_RK_CAP];   // (new key, slot) of this workgroup's dest entries
+    __shared__ uint32_t dr[MV_RK_CAP];   // their mover index
+    __shared__ uint32_t sx[MV_RS_CAP];   // slots of its source entries
+    __shared__ uint32_t sr[MV_RS_CAP];
+    __shared__ uint32_t cnt[2], red[MV_BLK / 64];
+    resolve_sizes(src, w, n);
     if (blockIdx.x == 0 && threadIdx.x == 0) *next_count = 0u;
-    const uint32_t m = *mtotal;
-    const uint64_t nr = (m + MV_BLK - 1) / MV_BLK, nt = (m + MV_TILE - 1) / MV_TILE;
-    const int e = threadIdx.x % MV_TILE, part = threadIdx.x / MV_TILE;
-    for (uint64_t item = blockIdx.x; item < nr * nt; item += gridDim.x) {
-        const uint32_t ir = (uint32_t)(item % nr), it = (uint32_t)(item / nr);
-        __syncthreads();
-        if (threadIdx.x < MV_TILE) {
-            const uint32_t y = it * MV_TILE + threadIdx.x;
-            tile[threadIdx.x] = y < m ? comp(w.mk[y], mv_slot(w, w.mi[y])) : ~0ull;
-        }
-        __syncthreads();
-        {   // entry e's rank among the tile, over this wave's quarter (ties, i.e. pads, by position)
-            const uint64_t c = tile[e];
-            const uint32_t i = (uint32_t)c;
-            uint32_t rc = 0, ri = 0;
-#pragma unroll 4
-            for (int u = part * (MV_TILE / NPART); u < (part + 1) * (MV_TILE / NPART); ++u) {
-                const uint64_t cu = tile[u];
-                const uint32_t iu = (uint32_t)cu;
-                rc += (cu < c || (cu == c && u < e)) ? 1u : 0u;
-                ri += (iu < i || (iu == i && u < e)) ? 1u : 0u;
-            }
-            part_c[part][e] = rc;
-            part_i[part][e] = ri;
-        }
-        __syncthreads();
-        if (threadIdx.x < MV_TILE) {
-            uint32_t rc = 0, ri = 0;
+    if (threadIdx.x < 2) cnt[threadIdx.x] = 0u;
+    const uint32_t m = *mtotal, G = gridDim.x, b = blockIdx.x;
+    const uint32_t x0 = (uint32_t)((uint64_t)(uint32_t)n * b / G), x1 = (uint32_t)((uint64_t)(uint32_t)n * (b + 1) / G);
+    const uint32_t kd0 = b == 0 ? 0u : (x0 < (uint32_t)n ? asm_sk(src, (int32_t)x0) : 0xffffffffu);
+    const uint32_t kd1 = b == G - 1 ? 0xffffffffu : (x1 < (uint32_t)n ? asm_sk(src, (int32_t)x1) : 0xffffffffu);
+    __syncthreads();
+    uint32_t below_k = 0, below_x = 0;
+    for (uint32_t base = 0; base < m; base += MV_BLK * MV_RANK_U) {
+        uint32_t xs[MV_RANK_U], ks[MV_RANK_U];
 #pragma unroll
-            for (int k = 0; k < NPART; ++k) {
-                rc += part_c[k][threadIdx.x];
-                ri += part_i[k][threadIdx.x];
-            }
-            const uint64_t c = tile[threadIdx.x];
-            sc[rc] = c;
-            si[ri] = (uint32_t)c;
+        for (int u = 0; u < MV_RANK_U; ++u) {   // every load of the round issues before any is used
+            const uint32_t r = min(base + u * MV_BLK + threadIdx.x, m - 1u);
+            xs[u] = w.mi[r];
+            ks[u] = w.mk[r];
         }
-        __syncthreads();
-        const uint32_t x = ir * MV_BLK + threadIdx.x;
-        if (x < m) {
-            const uint32_t ix = mv_slot(w, w.mi[x]), k = w.mk[x];
-            const uint64_t cx = comp(k, ix);
-            const uint32_t c0 = cs_old[k], c1 = cs_old[k + 1];
-            const uint32_t q = ix < c0 ? c0 : (ix > c1 ? c1 : ix);
-            const uint32_t nk = lb64(sc, cx), ni = lb64(si, ix), nq = lb64(si, q);
-            if (nk) atomicAdd(&w.rank[x], nk);
-            if (ni) atomicAdd(&w.rank[w.cap + x], ni);
-            if (nq) atomicAdd(&w.rank[2 * w.cap + x], nq);
+#pragma unroll
+        for (int u = 0; u < MV_RANK_U; ++u) {
+            const uint32_t r = base + u * MV_BLK + threadIdx.x;
+            if (r >= m) break;
+            const uint32_t x = mv_slot(w, xs[u]), k = ks[u];
+            below_k += k < kd0 ? 1u : 0u;
+            below_x += x < x0 ? 1u : 0u;
+            if (k >= kd0 && k < kd1) {
+                const uint32_t p = atomicAdd(&cnt[0], 1u);
+                if (p < MV_RK_CAP) { dk[p] = comp(k, x); dr[p] = r; }
+            }
+            if (x >= x0 && x < x1) {
+                const uint32_t p = atomicAdd(&cnt[1], 1u);
+                if (p < MV_RS_CAP) { sx[p] = x; sr[p] = r; }
+            }
+        }
+    }
+    below_k = block_sum(below_k, red);   // (its barriers also publish the staged entries and counts)
+    below_x = block_sum(below_x, red);
+    const uint32_t nd = cnt[0], ns = cnt[1];
+    auto dest = [&](uint32_t r, uint64_t c, uint32_t lr) {
+        const uint32_t rk = below_k + lr, k = (uint32_t)(c >> 32), x = (uint32_t)c;
+        const uint32_t c0 = cs_old[k], c1 = cs_old[k + 1];
+        if (rk >= w.cap) {   // inconsistent tables: flag, never write past them
+            if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
+            return;
+        }
+        w.ms[rk] = c;
+        w.rank[r] = rk;
+        w.rank[w.cap + r] = x < c0 ? c0 : (x > c1 ? c1 : x);
+    };
+    auto source = [&](uint32_t r, uint32_t x, uint32_t lr) {
+        const uint32_t ri = below_x + lr;
+        if (ri >= w.cap) {
+            if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
+            return;
+        }
+        w.mx[ri] = x;
+        w.mos[ri] = w.mo[r];   // old keys by slot: ascending
+    };
+    if (nd <= MV_RK_CAP) {
+        for (uint32_t e = threadIdx.x; e < nd; e += MV_BLK) {
+            const uint64_t c = dk[e];
+            uint32_t lr = 0;
+            for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < c ? 1u : 0u;
+            dest(dr[e], c, lr);
+        }
+    } else {   // more dest entries than LDS holds: each one counted against the whole list
+        for (uint32_t r = threadIdx.x; r < m; r += MV_BLK) {
+            const uint32_t k = w.mk[r];
+            if (!(k >= kd0 && k < kd1)) continue;
+            const uint64_t c = comp(k, mv_slot(w, w.mi[r]));
+            uint32_t lr = 0;
+            for (uint32_t f = 0; f < m; ++f) {
+                const uint32_t kf = w.mk[f];
+                lr += (kf >= kd0 && kf < kd1 && comp(kf, mv_slot(w, w.mi[f])) < c) ? 1u : 0u;
+            }
+            dest(r, c, lr);
+        }
+    }
+    if (ns <= MV_RS_CAP) {
+        for (uint32_t e = threadIdx.x; e < ns; e += MV_BLK) {
+            const uint32_t x = sx[e];
+            uint32_t lr = 0;
+            for (uint32_t f = 0; f < ns; ++f) lr += sx[f] < x ? 1u : 0u;
+            source(sr[e], x, lr);
+        }
+    } else {
+        for (uint32_t r = threadIdx.x; r < m; r += MV_BLK) {
+            const uint32_t x = mv_slot(w, w.mi[r]);
+            if (!(x >= x0 && x < x1)) continue;
+            uint32_t lr = 0;
+            for (uint32_t f = 0; f < m; ++f) {
+                const uint32_t xf = mv_slot(w, w.mi[f]);
+                lr += (xf >= x0 && xf < x) ? 1u : 0u;
+            }
+            source(r, x, lr);
         }
     }
 }
 
-__global__ __launch_bounds__(MV_BLK) void k_mv_place(const uint32_t* __restrict__ mtotal,
-                                                     const uint32_t* __restrict__ cs_old, ResortScratch w, AsmSrc src,
-                                                     float4* __restrict__ pos_o, float4* __restrict__ vel_o,
-                                                     int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o,
-                                                     ResortExtra ex) {
-    int32_t n_unused = 0;
-    resolve_sizes(src, w, n_unused);
-    const uint32_t m = *mtotal;
-    for (uint32_t r = blockIdx.x * MV_BLK + threadIdx.x; r < m; r += gridDim.x * MV_BLK) {
+// The movers' scatter, as extra workgroups of k_mv_merge (after k_mv_rank): dst = (q − A(q)) + rk with A(q) =
+// #{movers with slot < q} from the slot-sorted table mx. It reads no cell start (q was taken by k_mv_rank), so it
+// runs beside the merge's in-place cell-start update.
+constexpr int MV_PLACE_BLOCKS = 64;
+static __device__ void mv_place(uint32_t m, const ResortScratch& w, const AsmSrc& src, float4* __restrict__ pos_o,
+                                float4* __restrict__ vel_o, int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o,
+                                const ResortExtra& ex, uint32_t blk) {
+    for (uint32_t r = blk * MV_BLK + threadIdx.x; r < m; r += MV_PLACE_BLOCKS * MV_BLK) {
         const uint32_t x = mv_slot(w, w.mi[r]), k = w.mk[r];
-        const uint32_t c0 = cs_old[k], c1 = cs_old[k + 1];
-        const uint32_t q = x < c0 ? c0 : (x > c1 ? c1 : x);
-        const uint32_t rk = w.rank[r], ri = w.rank[w.cap + r], aq = w.rank[2 * w.cap + r];
+        const uint32_t rk = w.rank[r], q = w.rank[w.cap + r];
+        const uint32_t aq = lower_bound(w.mx, m, q);
         const uint32_t dst = (q - aq) + rk;
-        if (dst >= w.cap || rk >= w.cap || ri >= w.cap) {   // inconsistent tables: flag, never write past them
+        if (dst >= w.cap || rk >= w.cap) {   // inconsistent tables: flag, never write past them
             if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
             continue;
         }
@@ -228,15 +275,12 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_place(const uint32_t* __restrict_
         id_o[dst] = pid;
         sk_o[dst] = k;
         move_extra(ex, x, dst);
-        w.ms[rk] = comp(k, x);
-        w.mx[ri] = x;
-        w.mos[ri] = w.mo[r];   // old keys by slot: ascending
     }
 }
 
 // cs[k] += #{movers: new key < k} − #{movers: old key < k}, for k in [0, ncells]; 1024 cells per
 // workgroup. A workgroup whose counts agree at its start and that holds no mover key leaves its cells.
-// Runs as extra workgroups of k_mv_merge (it needs only k_mv_place's tables), beside the scatter.
+// Runs as extra workgroups of k_mv_merge (it needs only k_mv_rank's tables), beside the scatter.
 constexpr int MV_CS_CELLS = 4 * MV_BLK;
 #ifndef SPH_MERGE_PREFETCH
 #define SPH_MERGE_PREFETCH 1
@@ -295,11 +339,15 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
     __shared__ uint32_t b[4];
     __shared__ uint64_t lms[MV_LDS];
     __shared__ uint32_t lmo[MV_LDS];
-    if ((int32_t)blockIdx.x >= nb) {   // the cell-start workgroups
-        mv_cell_start(cs, ncells, *mtotal, w, blockIdx.x - nb, b, pick, lms, lmo);
+    if ((int32_t)blockIdx.x >= nb + MV_PLACE_BLOCKS) {   // the cell-start workgroups
+        mv_cell_start(cs, ncells, *mtotal, w, blockIdx.x - nb - MV_PLACE_BLOCKS, b, pick, lms, lmo);
         return;
     }
     resolve_sizes(src, w, n);          // device-sized slab step: nb is an upper bound
+    if ((int32_t)blockIdx.x >= nb) {   // the movers' scatter
+        mv_place(*mtotal, w, src, pos_o, vel_o, id_o, sk_o, ex, blockIdx.x - nb);
+        return;
+    }
     const int32_t i0 = xcd_block(blockIdx.x, nb) * MV_BLK;
     if (i0 >= n) return;               // whole workgroup, before any barrier
     const int32_t i = i0 + threadIdx.x;
@@ -463,9 +511,6 @@ __global__ __launch_bounds__(MV_BLK) void k_slab_rec(AsmSrc src, int32_t n, Grid
         sink.mi[q] = (uint32_t)xs[j] | MV_REC;
         sink.mk[q] = kn[j];
         sink.mo[q] = ko[j];
-        sink.rank[q] = 0u;
-        sink.rank[sink.cap + q] = 0u;
-        sink.rank[2 * sink.cap + q] = 0u;
         ++q;
     }
 }
@@ -485,11 +530,12 @@ void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const u
                    uint32_t* sk_o, hipStream_t s, CsPick pick, ResortExtra ex) {
     if (n <= 0) return;
     const int32_t nb = (n + MV_BLK - 1) / MV_BLK;
-    SPH_LAUNCH(k_mv_rank, MV_RANK_GRID, MV_BLK, 0, s, count, count_other, cs, w);
-    SPH_LAUNCH(k_mv_place, std::min(nb, 1024), MV_BLK, 0, s, count, cs, w, src, pos_o, vel_o, id_o, sk_o, ex);
-    // + the cell-start update, after every reader of cs_old (k_mv_rank, k_mv_place)
+    // n is an upper bound of the slots on device-sized steps: the rank kernel's ranges split the device count
+    SPH_LAUNCH(k_mv_rank, std::min(MV_RANK_GRID, nb), MV_BLK, 0, s, count, count_other, cs, w, src, n);
+    // the stayers' scatter, the movers' and the cell-start update (after k_mv_rank, the last reader of cs_old)
     const int32_t ncs = (int32_t)((ncells + MV_CS_CELLS) / MV_CS_CELLS);
-    SPH_LAUNCH(k_mv_merge, nb + ncs, MV_BLK, 0, s, src, n, count, w, pos_o, vel_o, id_o, sk_o, nb, cs, ncells, pick, ex);
+    SPH_LAUNCH(k_mv_merge, nb + MV_PLACE_BLOCKS + ncs, MV_BLK, 0, s, src, n, count, w, pos_o, vel_o, id_o, sk_o, nb, cs,
+               ncells, pick, ex);
 }
 
 }  // namespace sph

@@ -42,7 +42,7 @@ def _run(pkg, monkeypatch, team, parts, steps, conns=None, active=None):
 def test_team_sizes_bit_identical(pkg, monkeypatch, n, steps, active):
     parts = random_sphere(pkg.PARTICLE84, n, seed=11)
     ref, tq_ref = _run(pkg, monkeypatch, 1, parts, steps, active=active)
-    for team in (16, 64):
+    for team in (16, 64, 65):   # 65: the flat form (one wave per target, contact.hip CT_FLAT)
         got, tq = _run(pkg, monkeypatch, team, parts, steps, active=active)
         assert got.tobytes() == ref.tobytes(), f"team {team}"
         assert np.array_equal(tq, tq_ref), f"team {team}"
@@ -52,7 +52,7 @@ def test_team_sizes_bit_identical_with_bonds(pkg, monkeypatch):
     parts, conns = bonded_sphere(pkg.PARTICLE84, pkg.ADHESION84, 4096, seed=7)
     conns = conns[:4096]
     ref, tq_ref = _run(pkg, monkeypatch, 1, parts, 3, conns=conns)
-    for team in (16, 64):
+    for team in (16, 64, 65):   # 65: the flat form (one wave per target, contact.hip CT_FLAT)
         got, tq = _run(pkg, monkeypatch, team, parts, 3, conns=conns)
         assert got.tobytes() == ref.tobytes(), f"team {team}"
         assert np.array_equal(tq, tq_ref), f"team {team}"

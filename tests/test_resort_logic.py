@@ -53,3 +53,46 @@ def test_resort_formulas_match_stable_sort(frac):
         ref = np.argsort(newk, kind="stable")
         assert np.array_equal(perm, ref)
         assert np.array_equal(cs_new, np.searchsorted(newk[ref], np.arange(nc + 1), side="left"))
+
+
+def range_ranks(ks, newk, G):
+    """resort.hip k_mv_rank restated: workgroup b owns the old slots [x0, x1) = [b·n/G, (b+1)·n/G) and the new keys
+    [ks[x0], ks[x1]) (first range from 0, last to infinity); rk counts the movers below the key range plus those in
+    range with a smaller (key, slot), ri the movers below the slot range plus those in range with a smaller slot."""
+    n = len(ks)
+    movers = np.nonzero(newk != ks)[0]
+    mk = newk[movers]
+    rk = np.full(len(movers), -1, np.int64)
+    ri = np.full(len(movers), -1, np.int64)
+    for b in range(G):
+        x0, x1 = n * b // G, n * (b + 1) // G
+        kd0 = 0 if b == 0 else (ks[x0] if x0 < n else np.iinfo(np.int64).max)
+        kd1 = np.iinfo(np.int64).max if b == G - 1 else (ks[x1] if x1 < n else np.iinfo(np.int64).max)
+        ind = (mk >= kd0) & (mk < kd1)
+        ins = (movers >= x0) & (movers < x1)
+        below_k, below_x = int((mk < kd0).sum()), int((movers < x0).sum())
+        c = _comp(mk, movers)
+        for e in np.nonzero(ind)[0]:
+            assert rk[e] < 0, "a mover in two key ranges"
+            rk[e] = below_k + int((c[ind] < c[e]).sum())
+        for e in np.nonzero(ins)[0]:
+            assert ri[e] < 0, "a mover in two slot ranges"
+            ri[e] = below_x + int((movers[ins] < movers[e]).sum())
+    return movers, mk, rk, ri
+
+
+@pytest.mark.parametrize("frac", [0.0, 0.01, 0.3, 1.0])
+@pytest.mark.parametrize("G", [1, 3, 16, 256])
+def test_range_ranks_equal_global_ranks(frac, G):
+    rng = np.random.default_rng(int(frac * 1000) + G)
+    for _ in range(20):
+        n = int(rng.integers(1, 1500))
+        nc = int(rng.integers(1, 300))
+        ks = np.sort(rng.integers(0, nc, n)).astype(np.int64)
+        newk = ks.copy()
+        mv = rng.random(n) < frac
+        newk[mv] = rng.integers(0, nc + 1, int(mv.sum()))    # nc: the sentinel key (inactive / left the window)
+        movers, mk, rk, ri = range_ranks(ks, newk, min(G, max(n // 256, 1)) if G == 256 else G)
+        c = _comp(mk, movers)
+        assert np.array_equal(rk, np.argsort(np.argsort(c, kind="stable"), kind="stable"))
+        assert np.array_equal(ri, np.arange(len(movers)))
