@@ -575,6 +575,14 @@ struct HitMask {
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g,
                           SphConst c, float2* rp, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr = DevRange{},
                           RhoOut ro = RhoOut{});
+// Model S at small N (wcsph_tiled.hip): one wave per target, the tiled passes' sums bit for bit; single context,
+// targets [0, n); pass 2 takes its hits by distance (no hit mask)
+constexpr int32_t SMALL_N = 16384;
+void launch_density_small(const float4* pos, const uint32_t* cs, int32_t n, GridDesc g, SphConst c, float2* rp,
+                          hipStream_t s);
+void launch_force_small(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t n, GridDesc g,
+                        SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv,
+                        hipStream_t s);
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs,
                         int32_t ib, int32_t ie, GridDesc g, SphConst c, float dt, float fext_x,
                         float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths,

@@ -105,6 +105,7 @@ struct sph_ctx {
     // seen mover count exceeds resort_limit(n), 2 incremental whenever possible (tests)
     int resort_mode = 1;
     int ct_team = 0;                // env SPH_CT_TEAM: Model R lanes per target (0 = by size; tests)
+    int small_mode = 1;             // env SPH_SMALL: Model S wave-per-target passes, 0 never, 1 up to SMALL_N (default), 2 always
     uint32_t* mv_host = nullptr;    // pinned: the mover count of the latest step copied back
     int64_t steps = 0;
     double sim_time = 0.0;

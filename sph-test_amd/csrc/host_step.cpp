@@ -131,12 +131,22 @@ int step_wcsph(sph_ctx* ctx, float dt) {
     const int32_t n = ctx->n;
     int r = sort_wcsph(ctx);
     if (r != SPH_OK) return r;
-    {
-        KTimer t(ctx, "density", 24.0 * n, true);
-        density_range(ctx, 0, n);
-    }
     const MoverSink mv = mover_sink(ctx);
-    {
+    // the reference's scale: one wave per target (bit-identical to the tiled passes, wcsph_tiled.hip small N)
+    const bool small = ctx->small_mode == 2 || (ctx->small_mode == 1 && n <= SMALL_N);
+    if (small) {
+        {
+            KTimer t(ctx, "density", 24.0 * n, true);
+            launch_density_small(ctx->pos, ctx->cs, n, ctx->grid, ctx->sc, ctx->rp, ctx->stream);
+        }
+        KTimer t(ctx, "force_integrate", 56.0 * n, true);
+        launch_force_small(ctx->pos, ctx->vel, ctx->rp, ctx->cs, n, ctx->grid, ctx->sc, dt, forcing(ctx), ctx->pos2,
+                           ctx->vel2, ctx->keys, mv, ctx->stream);
+    } else {
+        {
+            KTimer t(ctx, "density", 24.0 * n, true);
+            density_range(ctx, 0, n);
+        }
         KTimer t(ctx, "force_integrate", 76.0 * n, true);
         force_range(ctx, 0, n, dt, forcing(ctx), mv);
     }

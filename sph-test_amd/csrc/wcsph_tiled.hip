@@ -231,6 +231,19 @@ __device__ __forceinline__ bool is_hit(const SphConst& c, float r2) {
 }
 #endif
 
+// ρ and P/ρ² from the kernel sum (Tait EOS, SPEC_SPH.md §2), both forms of pass 1
+__device__ __forceinline__ float2 density_eos(const SphConst& c, float s) {
+#if SPH_RUNITS
+    const float d = c.rho_scale * s;   // m·σ·(h³·4w)/(4h³)
+#else
+    const float d = c.mass * (c.sigma * (0.25f * s));
+#endif
+    const float tr = d * c.inv_rho0;
+    const float t2 = tr * tr, t4 = t2 * t2;
+    const float P = c.B * (t4 * t2 * tr - 1.0f);
+    return make_float2(d, P / (d * d));
+}
+
 // The scans use x, y, z only, and the compiler then narrows the float4 LDS read to
 // ds_read_b96: 8 LDS cycles per wave with 32-bank grouping, against 4 for ds_read_b128
 // (MI355X_MICROARCH.md §LDS). The empty asm consumes .w at no instruction cost so the 16-B read stays.
@@ -516,15 +529,7 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
     if (!valid) return;
     if (mn > 0 && wp < wend)   // the last, partial word: bits [0, mn), zeros above
         *wp = __builtin_bitreverse32(~ml << (32 - mn));
-#if SPH_RUNITS
-    const float d = c.rho_scale * s;   // m·σ·(h³·4w)/(4h³)
-#else
-    const float d = c.mass * (c.sigma * (0.25f * s));
-#endif
-    const float tr = d * c.inv_rho0;
-    const float t2 = tr * tr, t4 = t2 * t2;
-    const float P = c.B * (t4 * t2 * tr - 1.0f);
-    const float2 out = make_float2(d, P / (d * d));
+    const float2 out = density_eos(c, s);
     rp[i] = out;
     if (ro.dz) {   // slab step: a target of an own boundary column is also an entry of that side's ρ message
 #pragma unroll
@@ -577,9 +582,13 @@ static PairK pair_constants(const SphConst& c) {
 
 // Pair body (SPEC_SPH.md §2). pj = (x, y, z, ρ_j), vj = (u, v, w, P_j/ρ_j²). Branchless, for
 // pairs with q ≤ 2: one rsq gives r and 1/r; r = 0 (the target itself, or coincident distinct
-// particles) gives q = 0 and adds ±0 along dx = 0.
-__device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi, float rhoi, float prhoi, float4 pj,
-                                           float4 vj, ForceAcc& a) {
+// particles) gives q = 0 and adds ±0 along dx = 0. pair_terms evaluates a pair, pair_add adds it to the target's
+// sums (the small-N pass evaluates pairs on many lanes and adds them in visit order on one, with the same roundings).
+struct PairTerms {
+    float cf, dx, dy, dz, cx, du, dv, dw;
+};
+__device__ __forceinline__ PairTerms pair_terms(const PairK& k, float4 pi, float4 vi, float rhoi, float prhoi, float4 pj,
+                                                float4 vj) {
     const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
     const float r2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));   // explicit chains: the same rounding on every path
     const float rs = __builtin_amdgcn_rsqf(fmaxf(r2, 1e-30f));
@@ -612,9 +621,41 @@ __device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi,
     const float inv_s = e * inv_es;
     const float pij = fminf(vr, 0.0f) * k.kvisc * inv_es;
     const float cf = (prhoi + vj.w + pij) * G;
-    a.ax += cf * dx; a.ay += cf * dy; a.az += cf * dz;
     const float cx = inv_s * w4;
-    a.sx -= cx * du; a.sy -= cx * dv; a.sz -= cx * dw;
+    return PairTerms{cf, dx, dy, dz, cx, du, dv, dw};
+}
+// the sums (the compiler contracts each into one fma: one rounding per term, in both forms)
+__device__ __forceinline__ void pair_add(const PairTerms& t, ForceAcc& a) {
+    a.ax += t.cf * t.dx; a.ay += t.cf * t.dy; a.az += t.cf * t.dz;
+    a.sx -= t.cx * t.du; a.sy -= t.cx * t.dv; a.sz -= t.cx * t.dw;
+}
+__device__ __forceinline__ void pair_force(const PairK& k, float4 pi, float4 vi, float rhoi, float prhoi, float4 pj,
+                                           float4 vj, ForceAcc& a) {
+    pair_add(pair_terms(k, pi, vi, rhoi, prhoi, pj, vj), a);
+}
+
+// The end of pass 2 for target i in the small-N form (single context: no slab guard): the arithmetic of
+// k_force_tiled's tail, expression for expression (the sums scaled once, KDK with the box walls, the next cell key).
+template <int XS>
+__device__ __forceinline__ uint32_t integrate_target(ForceAcc acc, const PairK& pk, const SphConst& c, const GridDesc& g,
+                                                     float4 pi, float4 vi, float dt, float fext_x, int32_t i,
+                                                     float4* __restrict__ pos_o, float4* __restrict__ vel_o,
+                                                     uint32_t* __restrict__ keys_o) {
+    acc.ax *= pk.kf; acc.ay *= pk.kf; acc.az *= pk.kf;
+    acc.sx *= pk.kx; acc.sy *= pk.kx; acc.sz *= pk.kx;
+    float nv[3] = {vi.x + (acc.ax + c.gx + fext_x) * dt, vi.y + (acc.ay + c.gy) * dt, vi.z + (acc.az + c.gz) * dt};
+    float np[3] = {pi.x + (nv[0] + acc.sx) * dt, pi.y + (nv[1] + acc.sy) * dt, pi.z + (nv[2] + acc.sz) * dt};
+    const float L[3] = {c.Lx, c.Ly, c.Lz};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (np[a] < 0.0f) { np[a] = 0.0f; if (nv[a] < 0.0f) nv[a] = -c.wall_e * nv[a]; }
+        if (np[a] > L[a]) { np[a] = L[a]; if (nv[a] > 0.0f) nv[a] = -c.wall_e * nv[a]; }
+    }
+    pos_o[i] = make_float4(np[0], np[1], np[2], 0.f);
+    vel_o[i] = make_float4(nv[0], nv[1], nv[2], 0.f);
+    const uint32_t key = cell_key<XS>(g, np[0], np[1], np[2]);
+    keys_o[i] = key;
+    return key;
 }
 
 template <int XS>
@@ -829,6 +870,7 @@ __global__ __launch_bounds__(TF_BLK) __attribute__((amdgpu_waves_per_eu(4))) voi
     count_wave(paths, 5);   // waves (3 planes each)
     SPH_BT_END(1);
     if (!valid) return;
+    // integrate_target's arithmetic, kept inline here: as a call the kernel's scalar arguments spilled to lanes
     acc.ax *= pk.kf; acc.ay *= pk.kf; acc.az *= pk.kf;
     acc.sx *= pk.kx; acc.sy *= pk.kx; acc.sz *= pk.kx;
     float nv[3] = {vi.x + (acc.ax + c.gx + fext_x) * dt, vi.y + (acc.ay + c.gy) * dt, vi.z + (acc.az + c.gz) * dt};
@@ -864,6 +906,136 @@ __global__ __launch_bounds__(TF_BLK) __attribute__((amdgpu_waves_per_eu(4))) voi
             atomicAdd(sb.bins + sd * sb.nblk + (blk * TF_BLK) / SEND_SLOTS, (uint32_t)__popcll(m));
     }
     append_mover(mv, i, wk);
+}
+
+// ---------------------------------------------------------------- small N
+// At the reference's own scale (a few thousand particles, ParticleSystemController.cs:12) the tiled passes run a
+// handful of 256-target workgroups on a 256-CU chip (C1: 16), each walking its planes one after another. The small
+// form gives every target one wave: lane k < rows finds row k's trimmed window (lane_window, the tiled passes'
+// windows), the rows' windows back to back are the visit order, and each 64-candidate chunk of it is evaluated one
+// candidate per lane, its loads in flight together. The sums are then taken in visit order from the lanes
+// (readlane): pass 1 adds every candidate's w (non-neighbours add +0), pass 2 adds the hits' pair terms, each with
+// the tiled passes' expression, so the results are bit-identical to theirs (tests/test_gpu_small.py). Pass 2 takes
+// its hits by distance (is_hit: the bit pass 1 records), so no hit mask passes between the two.
+template <int XS>
+struct SmallRows {
+    static constexpr int NR = 3 * (2 * XS + 1);   // rows in visit order
+    uint32_t rj0 = 0u, excl = 0u, total = 0u;     // lane k < NR: row k's first slot and flattened start
+    uint32_t P[NR];                               // the rows' flattened starts (wave-uniform)
+    __device__ __forceinline__ SmallRows(const GridDesc& g, const uint32_t* __restrict__ cs, float4 pi, int lane) {
+        BlockRows b;
+        b.cx = cell_cxs<XS>(g, pi.x);
+        b.cy = cell_coord(pi.y, g.oy, g.inv_cell, g.gy);
+        cell_fracs<XS>(g, pi.x, pi.y, pi.z, b.cx, b.cy, b.fx, b.fy, b.gzf);
+        uint32_t len = 0u;
+        if (lane < NR) {
+            int32_t r0, r1;
+            lane_window<XS>(g, cs, b, true, lane, r0, r1);
+            rj0 = (uint32_t)r0;
+            len = (uint32_t)(r1 - r0);
+        }
+        uint32_t incl = len;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
+            if (lane >= o) incl += t;
+        }
+        excl = incl - len;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) P[k] = (uint32_t)__builtin_amdgcn_readlane((int)excl, k);
+        total = (uint32_t)__builtin_amdgcn_readlane((int)incl, NR - 1);
+    }
+    // flattened candidate f -> sorted slot (the row's first slot and start from its lane, not a per-lane select
+    // chain: that compiles to a scratch-memory table)
+    __device__ __forceinline__ uint32_t slot(uint32_t f) const {
+        int k = 0;
+#pragma unroll
+        for (int r = 1; r < NR; ++r) k += f >= P[r] ? 1 : 0;
+        return (uint32_t)__shfl((int)rj0, k, 64) + (f - (uint32_t)__shfl((int)excl, k, 64));
+    }
+};
+
+__device__ __forceinline__ float lanef(float v, uint32_t src) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)src));
+}
+
+template <int XS>
+__global__ __launch_bounds__(256) void k_density_small(const float4* __restrict__ pos, const uint32_t* __restrict__ cs,
+                                                       int32_t n, GridDesc g, SphConst c, float2* __restrict__ rp) {
+    const int lane = (int)lane_id();
+    const int32_t i = (int32_t)blockIdx.x * 4 + (int32_t)(threadIdx.x >> 6);
+    if (i >= n) return;   // wave-uniform
+    const float4 pi = pos[i];
+    const SmallRows<XS> R(g, cs, pi, lane);
+    float s = 0.0f;
+#pragma unroll 1
+    for (uint32_t base = 0; base < R.total; base += 64u) {
+        const uint32_t f = base + (uint32_t)lane;
+        float v;
+        const float w4 = spline_w4(c, dist2(pi, pos[R.slot(min(f, R.total - 1u))]), v);
+        const float w = f < R.total ? w4 : 0.0f;
+#pragma unroll
+        for (int t = 0; t < 64; ++t) s += lanef(w, (uint32_t)t);   // visit order; past the end +0
+    }
+    if (lane == 0) rp[i] = density_eos(c, s);
+}
+
+template <int XS>
+__global__ __launch_bounds__(256) void k_force_small(const float4* __restrict__ pos, const float4* __restrict__ vel,
+                                                     const float2* __restrict__ rp, const uint32_t* __restrict__ cs,
+                                                     int32_t n, GridDesc g, SphConst c, PairK pk, float dt, float fext_x,
+                                                     float4* __restrict__ pos_o, float4* __restrict__ vel_o,
+                                                     uint32_t* __restrict__ keys_o, MoverSink mv) {
+    const int lane = (int)lane_id();
+    const int32_t i = (int32_t)blockIdx.x * 4 + (int32_t)(threadIdx.x >> 6);
+    if (i >= n) return;   // wave-uniform
+    const float4 pi = pos[i], vi = vel[i];
+    const float2 ri = rp[i];
+    const SmallRows<XS> R(g, cs, pi, lane);
+    ForceAcc acc{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (uint32_t base = 0; base < R.total; base += 64u) {
+        const uint32_t f = base + (uint32_t)lane;
+        const uint32_t j = R.slot(min(f, R.total - 1u));
+        const float4 pj = pos[j];
+        const bool hit = f < R.total && is_hit(c, dist2(pi, pj));
+        PairTerms t{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (hit) {
+            const float4 vj = vel[j];
+            const float2 rj = rp[j];
+            t = pair_terms(pk, pi, vi, ri.x, ri.y, make_float4(pj.x, pj.y, pj.z, rj.x), make_float4(vj.x, vj.y, vj.z, rj.y));
+        }
+        for (uint64_t m = __ballot(hit); m; m &= m - 1ull) {   // the hits in visit order
+            const uint32_t src = (uint32_t)__builtin_ctzll(m);
+            const PairTerms u{lanef(t.cf, src), lanef(t.dx, src), lanef(t.dy, src), lanef(t.dz, src),
+                              lanef(t.cx, src), lanef(t.du, src), lanef(t.dv, src), lanef(t.dw, src)};
+            pair_add(u, acc);
+        }
+    }
+    if (lane != 0) return;
+    const uint32_t key = integrate_target<XS>(acc, pk, c, g, pi, vi, dt, fext_x, i, pos_o, vel_o, keys_o);
+    append_mover(mv, i, key);   // one lane: window_key = cell_key in a single domain
+}
+
+void launch_density_small(const float4* pos, const uint32_t* cs, int32_t n, GridDesc g, SphConst c, float2* rp,
+                          hipStream_t s) {
+    if (n <= 0) return;
+    if (g.xsub == 2)
+        SPH_LAUNCH(k_density_small<2>, (n + 3) / 4, 256, 0, s, pos, cs, n, g, c, rp);
+    else
+        SPH_LAUNCH(k_density_small<1>, (n + 3) / 4, 256, 0, s, pos, cs, n, g, c, rp);
+}
+
+void launch_force_small(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t n, GridDesc g,
+                        SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv,
+                        hipStream_t s) {
+    if (n <= 0) return;
+    if (g.xsub == 2)
+        SPH_LAUNCH(k_force_small<2>, (n + 3) / 4, 256, 0, s, pos, vel, rp, cs, n, g, c, pair_constants(c), dt, fext_x,
+                   pos_o, vel_o, keys_o, mv);
+    else
+        SPH_LAUNCH(k_force_small<1>, (n + 3) / 4, 256, 0, s, pos, vel, rp, cs, n, g, c, pair_constants(c), dt, fext_x,
+                   pos_o, vel_o, keys_o, mv);
 }
 
 // dr set: [ib, ie) only sizes the grid (an upper bound); the kernels read their bounds from dr

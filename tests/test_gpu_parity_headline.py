@@ -227,12 +227,13 @@ def test_c2_three_steps_mid_collapse(pkg, oracle):
         sim.close()
 
 
-def test_hit_mask_budget_fallback(pkg, oracle):
+def test_hit_mask_budget_fallback(pkg, oracle, monkeypatch):
     """A block of fluid compressed to 0.75 dx spacing (~2.4x the candidates per target, past the hit mask's
     256) beside fluid at rest spacing: pass 2 scans the compressed waves' planes by distance and takes the
     others from the mask (sph_read_hit_mask_counts: both kinds occur), and the step still meets the
     tolerances above."""
     sc = pkg.make_scenario(pkg.SPH_SCENARIO_DAMBREAK, 3, 24, 20, 16, 40, 40, 40, dx=0.01, seed=5)
+    monkeypatch.setenv("SPH_SMALL", "0")           # the tiled passes (8,736 particles would take the small form)
     sim = pkg.SPHSim(sc, capacity=40_000)
     try:
         def block(x0, n, s, ny, nz):
