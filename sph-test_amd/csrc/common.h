@@ -572,9 +572,19 @@ struct HitMask {
     uint32_t* w = nullptr;   // HM_WORDS * stride words; nullptr: no mask (pass 2 scans by distance)
     uint32_t stride = 0;
 };
+// The neighbour passes' y-band schedule (schedule.hip): table[0] header, table[1 + d] workgroup d's target range;
+// entries = the launch's workgroups. Single-context launches over [0, n) only.
+constexpr int SCHED_BANDS = 8;
+struct Sched {
+    const uint2* table = nullptr;
+    int32_t entries = 0;
+};
+int32_t schedule_entries(int32_t n, const GridDesc& g);
+bool schedule_fits(const GridDesc& g);
+void launch_schedule(const uint32_t* cs, GridDesc g, int32_t n, uint2* table, int32_t entries, hipStream_t s);
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g,
                           SphConst c, float2* rp, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr = DevRange{},
-                          RhoOut ro = RhoOut{});
+                          RhoOut ro = RhoOut{}, Sched sch = Sched{});
 // Model S at small N (wcsph_tiled.hip): one wave per target, the tiled passes' sums bit for bit; single context,
 // targets [0, n); pass 2 takes its hits by distance (no hit mask)
 constexpr int32_t SMALL_N = 16384;
@@ -587,7 +597,7 @@ void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, 
                         int32_t ib, int32_t ie, GridDesc g, SphConst c, float dt, float fext_x,
                         float4* pos_o, float4* vel_o, uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths,
                         hipStream_t s, DevRange dr = DevRange{}, DevRange dr2 = DevRange{}, int32_t ie2 = 0,
-                        SendBins sb = SendBins{});
+                        SendBins sb = SendBins{}, Sched sch = Sched{});
 
 // slab decomposition (slab.hip)
 // Order-preserving compaction of the sorted slots [b, e) whose key column satisfies

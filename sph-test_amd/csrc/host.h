@@ -106,6 +106,12 @@ struct sph_ctx {
     int resort_mode = 1;
     int ct_team = 0;                // env SPH_CT_TEAM: Model R lanes per target (0 = by size; tests)
     int small_mode = 1;             // env SPH_SMALL: Model S wave-per-target passes, 0 never, 1 up to SMALL_N (default), 2 always
+    // the tiled passes' y-band schedule (schedule.hip): env SPH_SCHED 0 off, 1 on (default); rebuilt every
+    // SCHED_EVERY steps and whenever the slot count or the grid changed (any table is a partition of [0, n))
+    int sched_mode = 1;
+    uint2* sched = nullptr;
+    int32_t sched_cap = 0, sched_ent = 0, sched_n = -1;
+    bool sched_valid = false;
     uint32_t* mv_host = nullptr;    // pinned: the mover count of the latest step copied back
     int64_t steps = 0;
     double sim_time = 0.0;
@@ -260,8 +266,8 @@ int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id, const uint32_t** sorted_
 HitMask hit_mask_write(sph_ctx* ctx);
 HitMask hit_mask_read(const sph_ctx* ctx);
 inline uint32_t* path_ctr(const sph_ctx* ctx) { return ctx->count_paths ? ctx->paths : nullptr; }
-void density_range(sph_ctx* ctx, int32_t b, int32_t e);
-void force_range(sph_ctx* ctx, int32_t b, int32_t e, float dt, float fext, MoverSink mv = MoverSink{});
+void density_range(sph_ctx* ctx, int32_t b, int32_t e, Sched sch = Sched{});
+void force_range(sph_ctx* ctx, int32_t b, int32_t e, float dt, float fext, MoverSink mv = MoverSink{}, Sched sch = Sched{});
 ResortScratch resort_scratch(sph_ctx* ctx);
 MoverSink mover_sink(sph_ctx* ctx);
 uint32_t resort_limit(int32_t n);

@@ -16,6 +16,9 @@ void free_all(sph_ctx* c) {
     dfree(c->sk_cur); dfree(c->sk_next);
     dfree(c->mv_mi); dfree(c->mv_mk); dfree(c->mv_mo); dfree(c->mv_rank); dfree(c->mv_mx); dfree(c->mv_mos);
     dfree(c->mv_ms); dfree(c->mv_count);
+    dfree(c->sched);
+    c->sched_cap = 0;
+    c->sched_valid = false;
     c->sk_valid = false;
     if (c->staging) (void)hipFree(c->staging);
     c->staging = nullptr;
@@ -160,6 +163,7 @@ void invalidate_sort(sph_ctx* c) {
     c->keys_valid = false;
     c->sk_valid = false;
     c->hm_valid = false;
+    c->sched_valid = false;
 }
 
 // ---------------------------------------------------------------- profiling

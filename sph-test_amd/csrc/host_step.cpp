@@ -60,13 +60,36 @@ HitMask hit_mask_read(const sph_ctx* ctx) {
     return ctx->hm_valid ? HitMask{ctx->hmask, (uint32_t)std::max(ctx->capacity, 1)} : HitMask{};
 }
 
-void density_range(sph_ctx* ctx, int32_t b, int32_t e) {
-    launch_density_tiled(ctx->pos, ctx->cs, b, e, ctx->grid, ctx->sc, ctx->rp, hit_mask_write(ctx), path_ctr(ctx), ctx->stream);
+void density_range(sph_ctx* ctx, int32_t b, int32_t e, Sched sch) {
+    launch_density_tiled(ctx->pos, ctx->cs, b, e, ctx->grid, ctx->sc, ctx->rp, hit_mask_write(ctx), path_ctr(ctx), ctx->stream,
+                         DevRange{}, RhoOut{}, sch);
 }
 
-void force_range(sph_ctx* ctx, int32_t b, int32_t e, float dt, float fext, MoverSink mv) {
+void force_range(sph_ctx* ctx, int32_t b, int32_t e, float dt, float fext, MoverSink mv, Sched sch) {
     launch_force_tiled(ctx->pos, ctx->vel, ctx->rp, ctx->cs, b, e, ctx->grid, ctx->sc, dt, fext, ctx->pos2, ctx->vel2,
-                       ctx->keys, mv, hit_mask_read(ctx), path_ctr(ctx), ctx->stream);
+                       ctx->keys, mv, hit_mask_read(ctx), path_ctr(ctx), ctx->stream, DevRange{}, DevRange{}, 0, SendBins{},
+                       sch);
+}
+
+// The single context's y-band schedule for the tiled passes of this step (schedule.hip), or none.
+constexpr int64_t SCHED_EVERY = 8;
+Sched step_schedule(sph_ctx* ctx) {
+    const int32_t n = ctx->n;
+    if (ctx->sched_mode == 0 || n <= 0 || !schedule_fits(ctx->grid)) return Sched{};
+    const int32_t ent = schedule_entries(n, ctx->grid);
+    if (ent + 1 > ctx->sched_cap) {
+        if (dalloc(ctx, &ctx->sched, (size_t)ent + 1) != SPH_OK) return Sched{};
+        ctx->sched_cap = ent + 1;
+        ctx->sched_valid = false;
+    }
+    if (!ctx->sched_valid || ctx->sched_n != n || ctx->sched_ent != ent || ctx->steps % SCHED_EVERY == 0) {
+        KTimer t(ctx, "schedule", 4.0 * ctx->grid.gx * ctx->grid.xsub * ctx->grid.gy + 8.0 * ent, true);
+        launch_schedule(ctx->cs, ctx->grid, n, ctx->sched, ent, ctx->stream);
+        ctx->sched_valid = true;
+        ctx->sched_n = n;
+        ctx->sched_ent = ent;
+    }
+    return Sched{ctx->sched, ent};
 }
 
 // f_ext(t) of SPEC_SPH.md §2 at the context's simulated time (sloshing; 0 otherwise)
@@ -143,12 +166,13 @@ int step_wcsph(sph_ctx* ctx, float dt) {
         launch_force_small(ctx->pos, ctx->vel, ctx->rp, ctx->cs, n, ctx->grid, ctx->sc, dt, forcing(ctx), ctx->pos2,
                            ctx->vel2, ctx->keys, mv, ctx->stream);
     } else {
+        const Sched sch = step_schedule(ctx);
         {
             KTimer t(ctx, "density", 24.0 * n, true);
-            density_range(ctx, 0, n);
+            density_range(ctx, 0, n, sch);
         }
         KTimer t(ctx, "force_integrate", 76.0 * n, true);
-        force_range(ctx, 0, n, dt, forcing(ctx), mv);
+        force_range(ctx, 0, n, dt, forcing(ctx), mv, sch);
     }
     // this step's mover count, for the next steps' sort choice (no host wait); every 8th step, as the
     // copy is a ~4 us blit and the count drifts slowly

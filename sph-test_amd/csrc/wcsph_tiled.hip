@@ -346,10 +346,33 @@ __device__ __forceinline__ int32_t quadrant_target(const GridDesc& g, const floa
     return perm[threadIdx.x];
 }
 
+// This workgroup's targets [i0, iend): entry blockIdx.x of the y-band table (schedule.hip) when one is given and fits,
+// else runs of blocks dealt to the XCDs (xcd_block) over [ib, n). false: no targets (exit before any barrier).
+template <int BLK>
+__device__ __forceinline__ bool block_range(const uint2* __restrict__ sch, int32_t ib, int32_t n, int32_t& i0,
+                                            int32_t& iend) {
+    int32_t nb = (int32_t)gridDim.x;
+    if (sch) {
+        const uint2 h = sch[0];
+        if (h.x) {
+            const uint2 e = sch[1 + blockIdx.x];
+            i0 = (int32_t)e.x;
+            iend = (int32_t)e.y;
+            return i0 < iend;
+        }
+        nb = (n - ib + BLK - 1) / BLK;   // the table did not fit: the plain mapping over the first nb workgroups
+        if ((int32_t)blockIdx.x >= nb) return false;
+    }
+    i0 = ib + xcd_block((int32_t)blockIdx.x, nb) * BLK;
+    iend = min(i0 + BLK, n);
+    return i0 < n;
+}
+
 template <int XS>
 __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAVES))) void k_density_tiled(
     const float4* __restrict__ pos, const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c,
-    float2* __restrict__ rp, DevRange dr, HitMask hm, uint32_t* __restrict__ paths, RhoOut ro) {
+    float2* __restrict__ rp, DevRange dr, HitMask hm, uint32_t* __restrict__ paths, RhoOut ro,
+    const uint2* __restrict__ sch) {
     __shared__ float4 sp[TT_GCAP + 4];
     __shared__ int32_t perm[TT_BLK];
     __shared__ uint32_t qcnt[TT_BLK / 64][5];
@@ -369,14 +392,14 @@ __global__ __launch_bounds__(TT_BLK) __attribute__((amdgpu_waves_per_eu(SPH_DWAV
         ib = (int32_t)*dr.lo;
         n = (int32_t)*dr.hi;
     }
-    const int32_t i0 = ib + xcd_block(blockIdx.x, gridDim.x) * TT_BLK;
-    if (i0 >= n) return;   // whole workgroup: before any barrier
+    int32_t i0, iend;
+    if (!block_range<TT_BLK>(sch, ib, n, i0, iend)) return;   // whole workgroup: before any barrier
     SPH_BT_START;
     // quadrant order, measured against plain sorted order (138 -> 154 us) and halves by fx or by fy
     // (+1 to +2 us) at C3 (profiles/r02_pass1_lane_order_ab.log)
-    const int32_t i = quadrant_target<XS>(g, pos, i0, n, perm, qcnt);
-    const bool valid = i < n;
-    const int32_t ilast = min(i0 + TT_BLK, n) - 1;
+    const int32_t i = quadrant_target<XS>(g, pos, i0, iend, perm, qcnt);
+    const bool valid = i < iend;
+    const int32_t ilast = iend - 1;
     const float4 pi = pos[valid ? i : ilast];
     const BlockRows b = block_rows<XS>(g, pos, i0, ilast, pi);
     float s = 0.0f;
@@ -663,35 +686,42 @@ __global__ __launch_bounds__(TF_BLK) __attribute__((amdgpu_waves_per_eu(4))) voi
     const float4* __restrict__ pos, const float4* __restrict__ vel, const float2* __restrict__ rp,
     const uint32_t* __restrict__ cs, int32_t ib, int32_t n, GridDesc g, SphConst c, PairK pk, float dt,
     float fext_x, float4* __restrict__ pos_o, float4* __restrict__ vel_o, uint32_t* __restrict__ keys_o, MoverSink mv,
-    HitMask hm, uint32_t* __restrict__ paths, DevRange dr, DevRange dr2, int32_t nb_a, SendBins sb) {
+    HitMask hm, uint32_t* __restrict__ paths, DevRange dr, DevRange dr2, int32_t nb_a, SendBins sb,
+    const uint2* __restrict__ sch) {
     __shared__ float4 sp[TF_GCAP + 4];     // (x, y, z, ρ)
     __shared__ float4 sv[TF_GCAP + 4];     // (u, v, w, P/ρ²)
     const int tid = threadIdx.x;
-    int32_t blk = xcd_block(blockIdx.x, gridDim.x);
-    int32_t nb_r = nb_a;   // this range's workgroups
+    int32_t blk = 0, i0, iend;
     int32_t rng = 0;       // which range (SendBins.side)
-    if (dr2.lo && blk >= nb_a) {   // a second range in the same launch (the slab step's two boundary columns)
-        blk -= nb_a;
-        nb_r = (int32_t)gridDim.x - nb_a;
-        dr = dr2;
-        rng = 1;
+    if (sch) {   // single context: the y-band table (schedule.hip)
+        if (!block_range<TF_BLK>(sch, ib, n, i0, iend)) return;   // whole workgroup: before any barrier
+    } else {
+        blk = xcd_block(blockIdx.x, gridDim.x);
+        int32_t nb_r = nb_a;   // this range's workgroups
+        if (dr2.lo && blk >= nb_a) {   // a second range in the same launch (the slab step's two boundary columns)
+            blk -= nb_a;
+            nb_r = (int32_t)gridDim.x - nb_a;
+            dr = dr2;
+            rng = 1;
+        }
+        if (dr.lo) {   // device-resident bounds (slab step); the grid is an upper bound
+            ib = (int32_t)*dr.lo;
+            n = (int32_t)*dr.hi;
+            // a range past its grid (a bound from an earlier step's count) stops every rank, as a message overflow does
+            if (blk == 0 && tid == 0 && mv.err && n - ib > nb_r * TF_BLK) atomicOr(mv.err, SZ_OVF_CAP);
+        }
+        i0 = ib + blk * TF_BLK;
+        if (i0 >= n) return;   // whole workgroup: before any barrier
+        iend = min(i0 + TF_BLK, n);
     }
-    if (dr.lo) {   // device-resident bounds (slab step); the grid is an upper bound
-        ib = (int32_t)*dr.lo;
-        n = (int32_t)*dr.hi;
-        // a range past its grid (a bound from an earlier step's count) stops every rank, as a message overflow does
-        if (blk == 0 && tid == 0 && mv.err && n - ib > nb_r * TF_BLK) atomicOr(mv.err, SZ_OVF_CAP);
-    }
-    const int32_t i0 = ib + blk * TF_BLK;
-    if (i0 >= n) return;   // whole workgroup: before any barrier
     SPH_BT_START;
     // Targets stay in sorted order here. Lanes ordered by quarters of fx (a dx plane's hit count follows
     // fx) fill the plane loop better (66% -> 80% of lanes busy at C3) but run slower, 206 -> 246 us, and
     // by halves of fx (83%) 190 -> 229 us: the lanes of a wave then come from more z layers and read
     // scattered LDS slots (profiles/r02_direct_plane_ab.log, r02_fx2_noself_ab.log).
     const int32_t i = i0 + tid;
-    const bool valid = i < n;
-    const int32_t ilast = min(i0 + TF_BLK, n) - 1;
+    const bool valid = i < iend;
+    const int32_t ilast = iend - 1;
     const int32_t ii = valid ? i : ilast;
     const float4 pi = pos[ii], vi = vel[ii];
     const float2 ri = rp[ii];
@@ -1042,13 +1072,15 @@ void launch_force_small(const float4* pos, const float4* vel, const float2* rp, 
 // ro.dz set: the launch also writes the slab step's ρ messages (headers by block 0, even when the grid has no
 // targets: then ie <= ib must not skip it)
 void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int32_t ie, GridDesc g, SphConst c,
-                          float2* rp, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr, RhoOut ro) {
+                          float2* rp, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr, RhoOut ro, Sched sch) {
     if (ie <= ib && !ro.dz) return;
-    const int32_t nb = ie > ib ? (ie - ib + TT_BLK - 1) / TT_BLK : 1;
+    const bool tab = sch.table && !dr.lo && ib == 0;
+    const int32_t nb = tab ? sch.entries : (ie > ib ? (ie - ib + TT_BLK - 1) / TT_BLK : 1);
+    const uint2* t = tab ? sch.table : nullptr;
     if (g.xsub == 2)
-        SPH_LAUNCH(k_density_tiled<2>, nb, TT_BLK, 0, s, pos, cs, ib, ie, g, c, rp, dr, hm, paths, ro);
+        SPH_LAUNCH(k_density_tiled<2>, nb, TT_BLK, 0, s, pos, cs, ib, ie, g, c, rp, dr, hm, paths, ro, t);
     else
-        SPH_LAUNCH(k_density_tiled<1>, nb, TT_BLK, 0, s, pos, cs, ib, ie, g, c, rp, dr, hm, paths, ro);
+        SPH_LAUNCH(k_density_tiled<1>, nb, TT_BLK, 0, s, pos, cs, ib, ie, g, c, rp, dr, hm, paths, ro, t);
 }
 
 // dr2 set: a second device-resident range in the same launch, ie2 slots at most (its workgroups follow
@@ -1056,16 +1088,20 @@ void launch_density_tiled(const float4* pos, const uint32_t* cs, int32_t ib, int
 void launch_force_tiled(const float4* pos, const float4* vel, const float2* rp, const uint32_t* cs, int32_t ib,
                         int32_t ie, GridDesc g, SphConst c, float dt, float fext_x, float4* pos_o, float4* vel_o,
                         uint32_t* keys_o, MoverSink mv, HitMask hm, uint32_t* paths, hipStream_t s, DevRange dr,
-                        DevRange dr2, int32_t ie2, SendBins sb) {
+                        DevRange dr2, int32_t ie2, SendBins sb, Sched sch) {
     const int32_t nb_a = ie > ib ? (ie - ib + TF_BLK - 1) / TF_BLK : 0;
     const int32_t nb_b = dr2.lo && ie2 > 0 ? (ie2 + TF_BLK - 1) / TF_BLK : 0;
     if (nb_a + nb_b == 0) return;
+    // the table's blocks hold up to 256 targets: a build with other force workgroups (make variants) keeps its mapping
+    const bool tab = sch.table && TF_BLK == 256 && !dr.lo && !dr2.lo && ib == 0 && !sb.bins;
+    const int32_t nb = tab ? sch.entries : nb_a + nb_b;
+    const uint2* t = tab ? sch.table : nullptr;
     if (g.xsub == 2)
-        SPH_LAUNCH(k_force_tiled<2>, nb_a + nb_b, TF_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt,
-                   fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr, nb_b ? dr2 : DevRange{}, nb_b ? nb_a : nb_a + nb_b, sb);
+        SPH_LAUNCH(k_force_tiled<2>, nb, TF_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt,
+                   fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr, nb_b ? dr2 : DevRange{}, nb_b ? nb_a : nb_a + nb_b, sb, t);
     else
-        SPH_LAUNCH(k_force_tiled<1>, nb_a + nb_b, TF_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt,
-                   fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr, nb_b ? dr2 : DevRange{}, nb_b ? nb_a : nb_a + nb_b, sb);
+        SPH_LAUNCH(k_force_tiled<1>, nb, TF_BLK, 0, s, pos, vel, rp, cs, ib, ie, g, c, pair_constants(c), dt,
+                   fext_x, pos_o, vel_o, keys_o, mv, hm, paths, dr, nb_b ? dr2 : DevRange{}, nb_b ? nb_a : nb_a + nb_b, sb, t);
 }
 
 #ifdef SPH_BTIME
