@@ -349,7 +349,8 @@ double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock:
 const uint32_t* lag_slot(RankState& R, int64_t step, sph_ctx* ctx, int* rc) {
     const int k = (int)(step % LAG_SLOTS);
     const double t0 = g_ht.on ? now_s() : 0.0;
-    // the step two steps back: done unless the host runs more than a step ahead of the GPU
+    // waits for the step's comm work: at a step's start for the step two back (done unless the host runs more than a
+    // step ahead), in an early-send boundary phase for the previous step
     const hipError_t e = hipEventSynchronize(R.lag_ev[k]);
     if (g_ht.on) g_ht.wait += now_s() - t0;
     if (e != hipSuccess) *rc = fail(ctx, SPH_ERR_HIP, "lag event: %s", hipGetErrorString(e));
@@ -877,12 +878,13 @@ int phase_boundary(RankState& R, Multi& M, float dt, bool early) {
         R.ebins_used = false;
         return rc;
     };
-    // the next step's sends, from this step's order and new positions: capacities from the counts three steps before
-    // the next step, i.e. the lag record multi_one_step waited for at this step's start (reading the previous
-    // step's would block the host until the GPU finished that step's comm work: one step ahead instead of two),
-    // one count launch and one pack launch. Both neighbours derive them from the same record.
+    // the next step's sends, from this step's order and new positions: capacities from the counts two steps before
+    // the next step (as multi_one_step derives them), one count launch and one pack launch. Both neighbours derive
+    // them from the same record. The host waits here for the previous step's comm work, so it runs at most one step
+    // ahead of the GPU. (Three steps before, from the record already waited for at this step's start, overflowed a
+    // message after a re-cut: the record of the first step after a cut holds the migration, not the new halo.)
     int r = SPH_OK;
-    const uint32_t* L = lag_slot(R, M.steps - 2, ctx, &r);
+    const uint32_t* L = lag_slot(R, M.steps - 1, ctx, &r);
     if (r != SPH_OK) return bail(r);
     R.e_c1o[0] = R.left >= 0 ? cap_of(M, L[0]) : 0;
     R.e_c1o[1] = R.right >= 0 ? cap_of(M, L[1]) : 0;

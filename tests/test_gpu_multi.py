@@ -142,9 +142,10 @@ def test_group_overflow_stops_the_group(pkg, monkeypatch):
     fails with SPH_ERR_CAPACITY for the whole group at the step the flag is read: the first lag-sized
     step is 3 (three exact-size steps after the initial cut), its flags are read two steps on."""
     sc = _scenario(pkg)
+    # read once when the scenario is cut (abi_multi.cpp read_switches: over RCCL every rank must agree on it)
+    monkeypatch.setenv("SPH_DEBUG_MSG_CAP", "256")
     sim = pkg.SPHSim(sc, ndev=3, rebalance_every=0)
     try:
-        monkeypatch.setenv("SPH_DEBUG_MSG_CAP", "256")
         with pytest.raises(pkg.SphError) as ei:
             sim.step(20)
         msg = str(ei.value)
