@@ -8,10 +8,10 @@ timeout -k 10 1000 python -u -m pytest -x -v -s -m gpu --timeout 300 --timeout-m
 echo "pytest rc=$rc"; grep -E " passed| failed|FAILED|ERROR" $O/pytest.log | tail -15
 [ $rc -ne 0 ] && { grep -B5 -A40 "Error\|FAILED\|assert" $O/pytest.log | tail -80; exit $rc; }
 timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench.log 2>&1; echo "bench rc=$?"; tail -c 1500 $O/bench.log
-for r in 1 2; do for sc in 0 1; do
-  SPH_SCHED=$sc timeout -k 10 300 python bench.py --no-cpu-baseline --steps 200 > $O/bench_sched$sc.log 2>&1; echo "sched=$sc rc=$?"
-  python3 -c "import json,sys; d=json.loads(open('$O/bench_sched$sc.log').read().strip().splitlines()[-1]); print('sched', $sc, d['ms_per_step'], d['kernels_ms_per_step'], d.get('ms_per_step_mid_collapse'), d.get('kernels_ms_per_step_mid_collapse'))"
-done; done
+for sc in 0 1; do
+  SPH_SCHED=$sc timeout -k 10 300 python bench.py --strong --config C5 --steps 20 --warmup 3 --no-cpu-baseline --mid-steps 0 > $O/bench_c5_sched$sc.log 2>&1; echo "C5 sched=$sc rc=$?"
+  python3 -c "import json,sys; d=json.loads(open('$O/bench_c5_sched$sc.log').read().strip().splitlines()[-1]); print('C5 sched', $sc, d['ms_per_step'], d.get('kernels_ms_per_step'))"
+done
 timeout -k 10 200 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$O/mid" -o run --output-format csv -- python3 scripts/mid_trace.py > $O/mid.log 2>&1; rc=$?
 echo "mid trace rc=$rc"; grep -v amdgpu.ids $O/mid.log; [ $rc -ne 0 ] && exit $rc
 f=$(find $O/mid -name "*kernel_trace.csv" | head -1)

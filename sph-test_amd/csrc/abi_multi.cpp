@@ -704,9 +704,7 @@ int phase_assemble(RankState& R, bool exact) {
         w.err = &R.dz->flags;
         launch_resort(src, ctx->cs, ctx->grid.ncells, n_ub, ctx->mv_count + used, ctx->mv_count + (1 - used), w,
                       ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, s, pick);
-        CKPT(R, "resort");
-        if ((ctx->steps & 7) == 0)
-            HIPCHK(hipMemcpyAsync(ctx->mv_host, ctx->mv_count + used, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        CKPT(R, "resort");   // (k_mv_rank stored the mover count for the host)
         ctx->mv_par = 1 - used;
         swap_sv(ctx);
         std::swap(ctx->id, ctx->id2);

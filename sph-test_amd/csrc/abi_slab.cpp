@@ -286,9 +286,7 @@ int sph::slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const voi
         w.mi_off = nl - ctx->o0;   // own movers were appended by slot in the previous order
         launch_resort(src, ctx->cs, ctx->grid.ncells, (int32_t)n, ctx->mv_count + used, ctx->mv_count + (1 - used), w,
                       ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, s, pick);
-        if ((ctx->steps & 7) == 0)
-            HIPCHK(hipMemcpyAsync(ctx->mv_host, ctx->mv_count + used, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        ctx->mv_par = 1 - used;
+        ctx->mv_par = 1 - used;   // (k_mv_rank stored the mover count for the host)
         swap_sv(ctx);
         std::swap(ctx->id, ctx->id2);
         std::swap(ctx->sk_cur, ctx->sk_next);

@@ -348,13 +348,14 @@ void launch_sort_small(const uint32_t* keys_in, int32_t n, int32_t key_bits, uin
 // sk: sorted keys of the slot order; cs: its cell starts, updated in place; count: the movers'
 // counter, count_other: the next step's counter (zeroed here). Writes the re-sorted state to *_o.
 struct ResortScratch {
-    uint32_t *mi, *mk, *mo, *rank;   // appended movers (MoverSink); rank: 2 x cap (k_mv_rank: rk, insertion slot q)
+    uint32_t *mi, *mk, *mo;          // appended movers (MoverSink)
     uint64_t* ms;                    // movers by (new key, slot)
     uint32_t *mx, *mos;              // movers by slot: slot, old key
     uint32_t cap;
     int32_t mi_off;                  // slab step: an own mover's slot is mi + mi_off (MV_REC: records' slot)
     const SlabSizes* dz = nullptr;   // non-null: mi_off = nl - o0 from the device sizes
     uint32_t* err = nullptr;         // SZ_OVF_MOVERS if a destination would pass cap (never written)
+    uint32_t* host_count = nullptr;  // mapped host memory: k_mv_rank stores the mover count there (the host's sort choice)
 };
 // a mover entry whose mi has this bit holds a slot of the assembled array (a halo record's);
 // without it, mi is the force pass's slot and the assembled slot is mi + mi_off

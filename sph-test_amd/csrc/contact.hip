@@ -559,11 +559,13 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_finish(
 }
 
 // Lanes per target: enough teams to fill the chip (256 CUs × 8 waves × 64 lanes ≈ 131k lanes) without
-// splitting thin candidate lists. A forced choice (1, 16, 64) wins; every choice gives bit-identical
+// splitting thin candidate lists. A forced choice (1, 16, 64, CT_FLAT) wins; every choice gives bit-identical
 // results (contact_accumulate_team).
 static int contact_team(int32_t n, int forced) {
     if (forced == 1 || forced == 16 || forced == 64 || forced == CT_FLAT) return forced;
-    if (n <= 32768) return 64;
+    // the flat form: 32.2 -> 26.5 us per step at 4,096 particles, 334 -> 315 us at 32,768 (scripts/small_n_timing.py,
+    // profiles/r05_small_n.log)
+    if (n <= 32768) return CT_FLAT;
     if (n <= 262144) return 16;
     return 1;
 }

@@ -96,7 +96,7 @@ struct sph_ctx {
     int32_t keys_active = -1;
     // incremental re-sort (resort.hip): sorted keys of the current slot order, and scratch
     uint32_t *sk_cur = nullptr, *sk_next = nullptr;
-    uint32_t *mv_mi = nullptr, *mv_mk = nullptr, *mv_mo = nullptr, *mv_rank = nullptr, *mv_mx = nullptr, *mv_mos = nullptr;
+    uint32_t *mv_mi = nullptr, *mv_mk = nullptr, *mv_mo = nullptr, *mv_mx = nullptr, *mv_mos = nullptr;
     uint64_t* mv_ms = nullptr;
     uint32_t* mv_count = nullptr;   // [2] mover counters, ping-pong by step
     int mv_par = 0;                 // counter the next force pass appends into
@@ -106,13 +106,15 @@ struct sph_ctx {
     int resort_mode = 1;
     int ct_team = 0;                // env SPH_CT_TEAM: Model R lanes per target (0 = by size; tests)
     int small_mode = 1;             // env SPH_SMALL: Model S wave-per-target passes, 0 never, 1 up to SMALL_N (default), 2 always
-    // the tiled passes' y-band schedule (schedule.hip): env SPH_SCHED 0 off, 1 on (default); rebuilt every
-    // SCHED_EVERY steps and whenever the slot count or the grid changed (any table is a partition of [0, n))
-    int sched_mode = 1;
+    // the tiled passes' y-band schedule (schedule.hip): env SPH_SCHED 0 off (default: measured slower),
+    // 1 on; rebuilt every SCHED_EVERY steps and whenever the slot count or the grid changed (any table is a partition)
+    int sched_mode = 0;
     uint2* sched = nullptr;
     int32_t sched_cap = 0, sched_ent = 0, sched_n = -1;
     bool sched_valid = false;
-    uint32_t* mv_host = nullptr;    // pinned: the mover count of the latest step copied back
+    uint32_t* mv_host = nullptr;    // pinned, mapped: the mover count of a recent step (k_mv_rank writes it, mv_host_dev)
+    uint32_t* mv_host_dev = nullptr;
+    bool sorted_full = false;       // this step took the full radix sort (no k_mv_rank: the count is copied back)
     int64_t steps = 0;
     double sim_time = 0.0;
     sph_drag_input drag{-1, {0.f, 0.f, 0.f}, 0.f};

@@ -100,8 +100,10 @@ float forcing(const sph_ctx* ctx) {
 }
 
 ResortScratch resort_scratch(sph_ctx* ctx) {
-    return ResortScratch{ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_rank, ctx->mv_ms, ctx->mv_mx, ctx->mv_mos,
-                         (uint32_t)std::max(ctx->capacity, 1), 0};
+    ResortScratch w{ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_ms, ctx->mv_mx, ctx->mv_mos,
+                    (uint32_t)std::max(ctx->capacity, 1), 0};
+    w.host_count = ctx->mv_host_dev;
+    return w;
 }
 
 // The force pass appends movers for the next step's incremental re-sort.
@@ -136,11 +138,13 @@ int sort_wcsph(sph_ctx* ctx) {
                           ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, ctx->stream);
             ctx->mv_par = 1 - used;
         }
+        ctx->sorted_full = false;
         swap_sv(ctx);
         std::swap(ctx->id, ctx->id2);
         std::swap(ctx->sk_cur, ctx->sk_next);
         return SPH_OK;
     }
+    ctx->sorted_full = true;
     const uint32_t* sk = nullptr;
     int r = sort_and_reorder(ctx, 0, &sk);
     if (r != SPH_OK) return r;
@@ -174,9 +178,9 @@ int step_wcsph(sph_ctx* ctx, float dt) {
         KTimer t(ctx, "force_integrate", 76.0 * n, true);
         force_range(ctx, 0, n, dt, forcing(ctx), mv, sch);
     }
-    // this step's mover count, for the next steps' sort choice (no host wait); every 8th step, as the
-    // copy is a ~4 us blit and the count drifts slowly
-    if (mv.sk && (ctx->steps & 7) == 0)
+    // the mover count for the next steps' sort choice (no host wait): the next incremental re-sort's k_mv_rank stores
+    // it; after a full sort (no k_mv_rank) it is copied back every 8th step (a ~4 us blit; the count drifts slowly)
+    if (mv.sk && ctx->sorted_full && (ctx->steps & 7) == 0)
         HIPCHK(hipMemcpyAsync(ctx->mv_host, mv.count, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
     swap_sv(ctx);
     ctx->keys_valid = true;
@@ -250,6 +254,7 @@ int sort_contact(sph_ctx* ctx, int32_t act) {
                       ctx->mv_count + used, ctx->mv_count + (1 - used), resort_scratch(ctx), ctx->pos2, ctx->vel2,
                       ctx->id2, ctx->sk_next, ctx->stream, CsPick{{0}, 0, nullptr, nullptr}, ex);
         ctx->mv_par = 1 - used;
+        ctx->sorted_full = false;
         swap_sv(ctx);
         std::swap(ctx->id, ctx->id2);
         std::swap(ctx->omg, ctx->omg2);
@@ -259,6 +264,7 @@ int sort_contact(sph_ctx* ctx, int32_t act) {
         std::swap(ctx->sk_cur, ctx->sk_next);
         return SPH_OK;
     }
+    ctx->sorted_full = true;
     const uint32_t* sk = nullptr;
     int r = sort_and_reorder(ctx, act, &sk);
     if (r != SPH_OK) return r;
@@ -317,7 +323,7 @@ int step_contact(sph_ctx* ctx, float dt) {
                                   ctx->vel2, ctx->omg2, ctx->pos2, ctx->rot2, ctx->keys, mv, ctx->stream);
         }
     }
-    if (mv.sk && (ctx->steps & 7) == 0)   // the mover count for the next steps' sort choice (no wait)
+    if (mv.sk && ctx->sorted_full && (ctx->steps & 7) == 0)   // the mover count after a full sort (as step_wcsph)
         HIPCHK(hipMemcpyAsync(ctx->mv_host, mv.count, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
     swap_sv(ctx);
     std::swap(ctx->omg, ctx->omg2);

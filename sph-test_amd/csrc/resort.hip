@@ -116,22 +116,24 @@ static __device__ __forceinline__ uint32_t movers_before(bool mv, uint32_t block
     return off + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
 }
 
-// Mover ranks in O(m) per workgroup (replaces the all-pairs tile counts of r1-r4, whose work grew as m²: the C3
-// re-sort chain went from 27.7 us from rest to 41.5 us mid-collapse). Workgroup b of G owns the slots
-// [x0, x1) = [b·n/G, (b+1)·n/G) of the assembled old order and the new keys [kd0, kd1) = [sk(x0), sk(x1)) (the
-// old sorted keys at those slots, so every workgroup's key range holds about n/G particles and ~m/G movers; the
-// ranges partition all keys, sentinels included). It streams the whole mover list once (U per lane in flight):
-//   rk(x) = #{y : k_y < kd0} + #{y with k_y in [kd0, kd1) : (k_y, y) < (k_x, x)}   for its dest entries (k_x in range)
-//   ri(x) = #{y : y < x0} + #{y with slot in [x0, x1) : y < x}                    for its source entries (x in range)
-// the first terms counted while streaming, the second by comparisons among the entries staged in LDS (~m/G each).
-// It writes the sorted tables the merge reads, ms[rk] = (k, x), mx[ri] = x, mos[ri] = old key, and per mover rk and
-// its insertion slot q = clamp(x, cs_old[k], cs_old[k + 1]) (rank[r], rank[cap + r]) for the placement, so no kernel
-// after this one reads cs_old while the merge updates it in place. A range with more entries than LDS holds (a
-// state where most particles move, only under SPH_RESORT=2) counts them against the whole list instead: slow, same
-// result. Also zeroes the next step's mover counter.
+// Mover ranks and placement in O(m) per workgroup (replaces the all-pairs tile counts and the separate placement of
+// r1-r4, whose work grew as m²: the C3 re-sort chain went from 27.7 us from rest to 41.5 us mid-collapse). Workgroup
+// b of G owns the slots [x0, x1) = [b·n/G, (b+1)·n/G) of the assembled old order and the new keys
+// [kd0, kd1) = [sk(x0), sk(x1)) (the old sorted keys at those slots, so every workgroup's key range holds about n/G
+// particles and ~m/G movers; the ranges partition all keys, sentinels included). Its dest entries are the movers
+// with a new key in its range, its source entries those with a slot in its range. One stream over the whole mover
+// list (U per lane in flight) stages both in LDS and counts the movers below the ranges; then
+//   rk(x) = #{y : k_y < kd0} + #{dest entries : (k_y, y) < (k_x, x)}          -> ms[rk] = (k, x)
+//   ri(x) = #{y : y < x0} + #{source entries : y < x}                         -> mx[ri] = x, mos[ri] = old key
+// and for its dest entries the insertion slot q = clamp(x, cs_old[k], cs_old[k + 1]) and A(q) = #{y : y < q}: the
+// q sorted in LDS, a second stream over the movers' slots adds each slot to the count of the first q above it, a
+// prefix sum gives A(q). The mover is then scattered to dst = (q − A(q)) + rk here, so the merge that follows reads
+// only the tables (it updates cs_old in place). A range with more entries than LDS holds (a state where most
+// particles move, only under SPH_RESORT=2) counts them against the whole list instead: slow, same result. Also
+// zeroes the next step's mover counter.
 constexpr int MV_RANK_GRID = 256;                 // workgroups at most; one per CU
 constexpr int MV_RANK_U = 16;                     // movers per lane per streaming round
-constexpr int MV_RK_CAP = 4096, MV_RS_CAP = 4096;  // entries staged per workgroup (80 KB of LDS)
+constexpr int MV_RK_CAP = 2048, MV_RS_CAP = 4096;  // entries staged per workgroup (~104 KB of LDS)
 
 __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
 #pragma unroll
@@ -147,16 +149,24 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
 
 __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__ mtotal, uint32_t* __restrict__ next_count,
                                                     const uint32_t* __restrict__ cs_old, ResortScratch w, AsmSrc src,
-                                                    int32_t n) {
+                                                    int32_t n, float4* __restrict__ pos_o, float4* __restrict__ vel_o,
+                                                    int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o,
+                                                    ResortExtra ex) {
     __shared__ uint64_t dk[MV_RK_CAP];   // (new key, slot) of this workgroup's dest entries
     __shared__ uint32_t dr[MV_RK_CAP];   // their mover index
+    __shared__ uint32_t dq[MV_RK_CAP];   // their insertion slots q
+    __shared__ uint32_t qs[MV_RK_CAP];   // the q sorted
+    __shared__ uint32_t qc[MV_RK_CAP + 1];   // movers' slots counted at the first q above them, then A(q) by sorted q
     __shared__ uint32_t sx[MV_RS_CAP];   // slots of its source entries
     __shared__ uint32_t sr[MV_RS_CAP];
     __shared__ uint32_t cnt[2], red[MV_BLK / 64];
     resolve_sizes(src, w, n);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *next_count = 0u;
     if (threadIdx.x < 2) cnt[threadIdx.x] = 0u;
     const uint32_t m = *mtotal, G = gridDim.x, b = blockIdx.x;
+    if (b == 0 && threadIdx.x == 0) {
+        *next_count = 0u;
+        if (w.host_count) *w.host_count = m;   // for the host's next sort choices (no copy launch)
+    }
     const uint32_t x0 = (uint32_t)((uint64_t)(uint32_t)n * b / G), x1 = (uint32_t)((uint64_t)(uint32_t)n * (b + 1) / G);
     const uint32_t kd0 = b == 0 ? 0u : (x0 < (uint32_t)n ? asm_sk(src, (int32_t)x0) : 0xffffffffu);
     const uint32_t kd1 = b == G - 1 ? 0xffffffffu : (x1 < (uint32_t)n ? asm_sk(src, (int32_t)x1) : 0xffffffffu);
@@ -173,15 +183,15 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
 #pragma unroll
         for (int u = 0; u < MV_RANK_U; ++u) {
             const uint32_t r = base + u * MV_BLK + threadIdx.x;
-            if (r >= m) break;
+            const bool ok = r < m;
             const uint32_t x = mv_slot(w, xs[u]), k = ks[u];
-            below_k += k < kd0 ? 1u : 0u;
-            below_x += x < x0 ? 1u : 0u;
-            if (k >= kd0 && k < kd1) {
+            below_k += ok && k < kd0 ? 1u : 0u;
+            below_x += ok && x < x0 ? 1u : 0u;
+            if (ok && k >= kd0 && k < kd1) {
                 const uint32_t p = atomicAdd(&cnt[0], 1u);
                 if (p < MV_RK_CAP) { dk[p] = comp(k, x); dr[p] = r; }
             }
-            if (x >= x0 && x < x1) {
+            if (ok && x >= x0 && x < x1) {
                 const uint32_t p = atomicAdd(&cnt[1], 1u);
                 if (p < MV_RS_CAP) { sx[p] = x; sr[p] = r; }
             }
@@ -190,46 +200,16 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
     below_k = block_sum(below_k, red);   // (its barriers also publish the staged entries and counts)
     below_x = block_sum(below_x, red);
     const uint32_t nd = cnt[0], ns = cnt[1];
-    auto dest = [&](uint32_t r, uint64_t c, uint32_t lr) {
-        const uint32_t rk = below_k + lr, k = (uint32_t)(c >> 32), x = (uint32_t)c;
-        const uint32_t c0 = cs_old[k], c1 = cs_old[k + 1];
-        if (rk >= w.cap) {   // inconsistent tables: flag, never write past them
-            if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
-            return;
-        }
-        w.ms[rk] = c;
-        w.rank[r] = rk;
-        w.rank[w.cap + r] = x < c0 ? c0 : (x > c1 ? c1 : x);
-    };
+    // ---- source entries: their slot ranks, the tables by slot
     auto source = [&](uint32_t r, uint32_t x, uint32_t lr) {
         const uint32_t ri = below_x + lr;
-        if (ri >= w.cap) {
+        if (ri >= w.cap) {   // inconsistent tables: flag, never write past them
             if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
             return;
         }
         w.mx[ri] = x;
         w.mos[ri] = w.mo[r];   // old keys by slot: ascending
     };
-    if (nd <= MV_RK_CAP) {
-        for (uint32_t e = threadIdx.x; e < nd; e += MV_BLK) {
-            const uint64_t c = dk[e];
-            uint32_t lr = 0;
-            for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < c ? 1u : 0u;
-            dest(dr[e], c, lr);
-        }
-    } else {   // more dest entries than LDS holds: each one counted against the whole list
-        for (uint32_t r = threadIdx.x; r < m; r += MV_BLK) {
-            const uint32_t k = w.mk[r];
-            if (!(k >= kd0 && k < kd1)) continue;
-            const uint64_t c = comp(k, mv_slot(w, w.mi[r]));
-            uint32_t lr = 0;
-            for (uint32_t f = 0; f < m; ++f) {
-                const uint32_t kf = w.mk[f];
-                lr += (kf >= kd0 && kf < kd1 && comp(kf, mv_slot(w, w.mi[f])) < c) ? 1u : 0u;
-            }
-            dest(r, c, lr);
-        }
-    }
     if (ns <= MV_RS_CAP) {
         for (uint32_t e = threadIdx.x; e < ns; e += MV_BLK) {
             const uint32_t x = sx[e];
@@ -237,7 +217,7 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
             for (uint32_t f = 0; f < ns; ++f) lr += sx[f] < x ? 1u : 0u;
             source(sr[e], x, lr);
         }
-    } else {
+    } else {   // more source entries than LDS holds: each one counted against the whole list
         for (uint32_t r = threadIdx.x; r < m; r += MV_BLK) {
             const uint32_t x = mv_slot(w, w.mi[r]);
             if (!(x >= x0 && x < x1)) continue;
@@ -249,24 +229,15 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
             source(r, x, lr);
         }
     }
-}
-
-// The movers' scatter, as extra workgroups of k_mv_merge (after k_mv_rank): dst = (q − A(q)) + rk with A(q) =
-// #{movers with slot < q} from the slot-sorted table mx. It reads no cell start (q was taken by k_mv_rank), so it
-// runs beside the merge's in-place cell-start update.
-constexpr int MV_PLACE_BLOCKS = 64;
-static __device__ void mv_place(uint32_t m, const ResortScratch& w, const AsmSrc& src, float4* __restrict__ pos_o,
-                                float4* __restrict__ vel_o, int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o,
-                                const ResortExtra& ex, uint32_t blk) {
-    for (uint32_t r = blk * MV_BLK + threadIdx.x; r < m; r += MV_PLACE_BLOCKS * MV_BLK) {
-        const uint32_t x = mv_slot(w, w.mi[r]), k = w.mk[r];
-        const uint32_t rk = w.rank[r], q = w.rank[w.cap + r];
-        const uint32_t aq = lower_bound(w.mx, m, q);
+    // ---- dest entries: rank, insertion slot, A(q), placement
+    auto place = [&](uint32_t r, uint64_t c, uint32_t rk, uint32_t q, uint32_t aq) {
+        const uint32_t k = (uint32_t)(c >> 32), x = (uint32_t)c;
         const uint32_t dst = (q - aq) + rk;
-        if (dst >= w.cap || rk >= w.cap) {   // inconsistent tables: flag, never write past them
+        if (rk >= w.cap || dst >= w.cap) {   // inconsistent tables: flag, never write past them
             if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
-            continue;
+            return;
         }
+        w.ms[rk] = c;
         float4 p, v;
         int32_t pid;
         asm_load(src, (int32_t)x, p, v, pid);
@@ -275,6 +246,65 @@ static __device__ void mv_place(uint32_t m, const ResortScratch& w, const AsmSrc
         id_o[dst] = pid;
         sk_o[dst] = k;
         move_extra(ex, x, dst);
+    };
+    auto ins = [&](uint64_t c) {   // the insertion slot among the stayers
+        const uint32_t k = (uint32_t)(c >> 32), x = (uint32_t)c;
+        const uint32_t c0 = cs_old[k], c1 = cs_old[k + 1];
+        return x < c0 ? c0 : (x > c1 ? c1 : x);
+    };
+    if (nd <= MV_RK_CAP) {
+        for (uint32_t e = threadIdx.x; e < nd; e += MV_BLK) dq[e] = ins(dk[e]);
+        for (uint32_t e = threadIdx.x; e <= nd; e += MV_BLK) qc[e] = 0u;
+        __syncthreads();
+        for (uint32_t e = threadIdx.x; e < nd; e += MV_BLK) {   // the q sorted (ties by entry)
+            const uint32_t q = dq[e];
+            uint32_t p = 0;
+            for (uint32_t f = 0; f < nd; ++f) p += (dq[f] < q || (dq[f] == q && f < e)) ? 1u : 0u;
+            qs[p] = q;
+        }
+        __syncthreads();
+        // every mover's slot y counts at the first sorted q above it: A(qs[p]) = qc[0] + ... + qc[p]
+        for (uint32_t r = threadIdx.x; r < m && nd > 0; r += MV_BLK) {
+            const uint32_t y = mv_slot(w, w.mi[r]);
+            uint32_t lo = 0, hi = nd;   // first sorted q > y
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (qs[mid] <= y) lo = mid + 1;
+                else hi = mid;
+            }
+            atomicAdd(&qc[lo], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (uint32_t p = 1; p < nd; ++p) qc[p] += qc[p - 1];   // nd ~ m / G: a short serial prefix
+        __syncthreads();
+        for (uint32_t e = threadIdx.x; e < nd; e += MV_BLK) {
+            const uint64_t c = dk[e];
+            uint32_t lr = 0;
+            for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < c ? 1u : 0u;
+            const uint32_t q = dq[e];
+            uint32_t lo = 0, hi = nd;   // the first sorted position of q: A(q) counts the slots below q
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (qs[mid] < q) lo = mid + 1;
+                else hi = mid;
+            }
+            place(dr[e], c, below_k + lr, q, qc[lo]);
+        }
+    } else {   // more dest entries than LDS holds: each one counted against the whole list
+        for (uint32_t r = threadIdx.x; r < m; r += MV_BLK) {
+            const uint32_t k = w.mk[r];
+            if (!(k >= kd0 && k < kd1)) continue;
+            const uint64_t c = comp(k, mv_slot(w, w.mi[r]));
+            const uint32_t q = ins(c);
+            uint32_t lr = 0, aq = 0;
+            for (uint32_t f = 0; f < m; ++f) {
+                const uint32_t kf = w.mk[f], xf = mv_slot(w, w.mi[f]);
+                lr += (kf >= kd0 && kf < kd1 && comp(kf, xf) < c) ? 1u : 0u;
+                aq += xf < q ? 1u : 0u;
+            }
+            place(r, c, below_k + lr, q, aq);
+        }
     }
 }
 
@@ -339,15 +369,11 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
     __shared__ uint32_t b[4];
     __shared__ uint64_t lms[MV_LDS];
     __shared__ uint32_t lmo[MV_LDS];
-    if ((int32_t)blockIdx.x >= nb + MV_PLACE_BLOCKS) {   // the cell-start workgroups
-        mv_cell_start(cs, ncells, *mtotal, w, blockIdx.x - nb - MV_PLACE_BLOCKS, b, pick, lms, lmo);
+    if ((int32_t)blockIdx.x >= nb) {   // the cell-start workgroups
+        mv_cell_start(cs, ncells, *mtotal, w, blockIdx.x - nb, b, pick, lms, lmo);
         return;
     }
     resolve_sizes(src, w, n);          // device-sized slab step: nb is an upper bound
-    if ((int32_t)blockIdx.x >= nb) {   // the movers' scatter
-        mv_place(*mtotal, w, src, pos_o, vel_o, id_o, sk_o, ex, blockIdx.x - nb);
-        return;
-    }
     const int32_t i0 = xcd_block(blockIdx.x, nb) * MV_BLK;
     if (i0 >= n) return;               // whole workgroup, before any barrier
     const int32_t i = i0 + threadIdx.x;
@@ -531,11 +557,11 @@ void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const u
     if (n <= 0) return;
     const int32_t nb = (n + MV_BLK - 1) / MV_BLK;
     // n is an upper bound of the slots on device-sized steps: the rank kernel's ranges split the device count
-    SPH_LAUNCH(k_mv_rank, std::min(MV_RANK_GRID, nb), MV_BLK, 0, s, count, count_other, cs, w, src, n);
-    // the stayers' scatter, the movers' and the cell-start update (after k_mv_rank, the last reader of cs_old)
+    SPH_LAUNCH(k_mv_rank, std::min(MV_RANK_GRID, nb), MV_BLK, 0, s, count, count_other, cs, w, src, n, pos_o, vel_o, id_o,
+               sk_o, ex);
+    // the stayers' scatter and the cell-start update (after k_mv_rank, the last reader of cs_old)
     const int32_t ncs = (int32_t)((ncells + MV_CS_CELLS) / MV_CS_CELLS);
-    SPH_LAUNCH(k_mv_merge, nb + MV_PLACE_BLOCKS + ncs, MV_BLK, 0, s, src, n, count, w, pos_o, vel_o, id_o, sk_o, nb, cs,
-               ncells, pick, ex);
+    SPH_LAUNCH(k_mv_merge, nb + ncs, MV_BLK, 0, s, src, n, count, w, pos_o, vel_o, id_o, sk_o, nb, cs, ncells, pick, ex);
 }
 
 }  // namespace sph
