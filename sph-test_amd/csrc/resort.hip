@@ -122,18 +122,19 @@ static __device__ __forceinline__ uint32_t movers_before(bool mv, uint32_t block
 // [kd0, kd1) = [sk(x0), sk(x1)) (the old sorted keys at those slots, so every workgroup's key range holds about n/G
 // particles and ~m/G movers; the ranges partition all keys, sentinels included). Its dest entries are the movers
 // with a new key in its range, its source entries those with a slot in its range. One stream over the whole mover
-// list (U per lane in flight) stages both in LDS and counts the movers below the ranges; then
-//   rk(x) = #{y : k_y < kd0} + #{dest entries : (k_y, y) < (k_x, x)}          -> ms[rk] = (k, x)
-//   ri(x) = #{y : y < x0} + #{source entries : y < x}                         -> mx[ri] = x, mos[ri] = old key
+// list (U per lane in flight) stages both in LDS and counts the movers below the ranges; then, each set sorted in
+// LDS (bitonic: the movers crowd into a few ranges mid-collapse, where counting ranks pairwise cost O(entries²)),
+//   rk(x) = #{y : k_y < kd0} + (x's position among the sorted dest entries)   -> ms[rk] = (k, x)
+//   ri(x) = #{y : y < x0} + (x's position among the sorted source entries)    -> mx[ri] = x, mos[ri] = old key
 // and for its dest entries the insertion slot q = clamp(x, cs_old[k], cs_old[k + 1]) and A(q) = #{y : y < q}: the
-// q sorted in LDS, a second stream over the movers' slots adds each slot to the count of the first q above it, a
-// prefix sum gives A(q). The mover is then scattered to dst = (q − A(q)) + rk here, so the merge that follows reads
+// q sorted, a second stream over the movers' slots adds each slot to the count of the first q above it, a prefix
+// sum gives A(q). The mover is then scattered to dst = (q − A(q)) + rk here, so the merge that follows reads
 // only the tables (it updates cs_old in place). A range with more entries than LDS holds (a state where most
 // particles move, only under SPH_RESORT=2) counts them against the whole list instead: slow, same result. Also
 // zeroes the next step's mover counter.
-constexpr int MV_RANK_GRID = 256;                 // workgroups at most; one per CU
-constexpr int MV_RANK_U = 16;                     // movers per lane per streaming round
-constexpr int MV_RK_CAP = 2048, MV_RS_CAP = 4096;  // entries staged per workgroup (~104 KB of LDS)
+constexpr int MV_RANK_GRID = 256;   // workgroups at most; one per CU
+constexpr int MV_RANK_U = 16;       // movers per lane per streaming round
+constexpr int MV_RK_CAP = 4096;     // dest and source entries staged per workgroup (a power of two; ~144 KB of LDS)
 
 __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
 #pragma unroll
@@ -147,18 +148,71 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
     return t;
 }
 
+// Sorts a[0, len) ascending in LDS (bitonic over the next power of two, padded with ~0; the keys are distinct), with
+// the payload b (if any) moved along. Every thread of the workgroup calls it; it ends on a barrier.
+__device__ void lds_sort(uint64_t* a, uint32_t* b, uint32_t len) {
+    uint32_t P = 1;
+    while (P < len) P <<= 1;
+    for (uint32_t t = len + threadIdx.x; t < P; t += MV_BLK) a[t] = ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < P; t += MV_BLK) {
+                const uint32_t u = t ^ j;
+                if (u > t) {
+                    const uint64_t x = a[t], y = a[u];
+                    if ((x > y) == ((t & k) == 0)) {
+                        a[t] = y;
+                        a[u] = x;
+                        if (b) {
+                            const uint32_t bt = b[t];
+                            b[t] = b[u];
+                            b[u] = bt;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+// In-place inclusive prefix sum of v[0, len) in LDS by the workgroup (red: MV_BLK / 64 words); ends on a barrier.
+__device__ void lds_scan(uint32_t* v, uint32_t len, uint32_t* red) {
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < len; base += MV_BLK) {
+        const uint32_t t = base + threadIdx.x;
+        uint32_t inc = t < len ? v[t] : 0u;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
+            if (lane_id() >= (uint32_t)o) inc += u;
+        }
+        __syncthreads();
+        if (lane_id() == 63) red[threadIdx.x >> 6] = inc;
+        __syncthreads();
+        uint32_t pre = carry, tot = 0;
+#pragma unroll
+        for (int k = 0; k < MV_BLK / 64; ++k) {
+            pre += k < (int)(threadIdx.x >> 6) ? red[k] : 0u;
+            tot += red[k];
+        }
+        if (t < len) v[t] = pre + inc;
+        carry += tot;
+    }
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__ mtotal, uint32_t* __restrict__ next_count,
                                                     const uint32_t* __restrict__ cs_old, ResortScratch w, AsmSrc src,
                                                     int32_t n, float4* __restrict__ pos_o, float4* __restrict__ vel_o,
                                                     int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o,
                                                     ResortExtra ex) {
-    __shared__ uint64_t dk[MV_RK_CAP];   // (new key, slot) of this workgroup's dest entries
-    __shared__ uint32_t dr[MV_RK_CAP];   // their mover index
-    __shared__ uint32_t dq[MV_RK_CAP];   // their insertion slots q
-    __shared__ uint32_t qs[MV_RK_CAP];   // the q sorted
-    __shared__ uint32_t qc[MV_RK_CAP + 1];   // movers' slots counted at the first q above them, then A(q) by sorted q
-    __shared__ uint32_t sx[MV_RS_CAP];   // slots of its source entries
-    __shared__ uint32_t sr[MV_RS_CAP];
+    __shared__ uint64_t dk[MV_RK_CAP];       // dest entries (new key, slot), sorted in place
+    __shared__ uint32_t dr[MV_RK_CAP];       // their mover index (moves with the sort)
+    __shared__ uint32_t dq[MV_RK_CAP];       // their insertion slots q, by sorted dest position
+    __shared__ uint64_t qs[MV_RK_CAP];       // (q, position), sorted
+    __shared__ uint32_t qc[MV_RK_CAP + 1];   // movers' slots counted at the first sorted q above them; then prefixed
+    __shared__ uint64_t sxk[MV_RK_CAP];      // source entries (slot, mover index), sorted
     __shared__ uint32_t cnt[2], red[MV_BLK / 64];
     resolve_sizes(src, w, n);
     if (threadIdx.x < 2) cnt[threadIdx.x] = 0u;
@@ -193,7 +247,7 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
             }
             if (ok && x >= x0 && x < x1) {
                 const uint32_t p = atomicAdd(&cnt[1], 1u);
-                if (p < MV_RS_CAP) { sx[p] = x; sr[p] = r; }
+                if (p < MV_RK_CAP) sxk[p] = (uint64_t)x << 32 | r;
             }
         }
     }
@@ -201,8 +255,7 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
     below_x = block_sum(below_x, red);
     const uint32_t nd = cnt[0], ns = cnt[1];
     // ---- source entries: their slot ranks, the tables by slot
-    auto source = [&](uint32_t r, uint32_t x, uint32_t lr) {
-        const uint32_t ri = below_x + lr;
+    auto source = [&](uint32_t r, uint32_t x, uint32_t ri) {
         if (ri >= w.cap) {   // inconsistent tables: flag, never write past them
             if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
             return;
@@ -210,13 +263,9 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
         w.mx[ri] = x;
         w.mos[ri] = w.mo[r];   // old keys by slot: ascending
     };
-    if (ns <= MV_RS_CAP) {
-        for (uint32_t e = threadIdx.x; e < ns; e += MV_BLK) {
-            const uint32_t x = sx[e];
-            uint32_t lr = 0;
-            for (uint32_t f = 0; f < ns; ++f) lr += sx[f] < x ? 1u : 0u;
-            source(sr[e], x, lr);
-        }
+    if (ns <= MV_RK_CAP) {
+        lds_sort(sxk, nullptr, ns);
+        for (uint32_t e = threadIdx.x; e < ns; e += MV_BLK) source((uint32_t)sxk[e], (uint32_t)(sxk[e] >> 32), below_x + e);
     } else {   // more source entries than LDS holds: each one counted against the whole list
         for (uint32_t r = threadIdx.x; r < m; r += MV_BLK) {
             const uint32_t x = mv_slot(w, w.mi[r]);
@@ -226,7 +275,7 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
                 const uint32_t xf = mv_slot(w, w.mi[f]);
                 lr += (xf >= x0 && xf < x) ? 1u : 0u;
             }
-            source(r, x, lr);
+            source(r, x, below_x + lr);
         }
     }
     // ---- dest entries: rank, insertion slot, A(q), placement
@@ -253,43 +302,48 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
         return x < c0 ? c0 : (x > c1 ? c1 : x);
     };
     if (nd <= MV_RK_CAP) {
-        for (uint32_t e = threadIdx.x; e < nd; e += MV_BLK) dq[e] = ins(dk[e]);
-        for (uint32_t e = threadIdx.x; e <= nd; e += MV_BLK) qc[e] = 0u;
-        __syncthreads();
-        for (uint32_t e = threadIdx.x; e < nd; e += MV_BLK) {   // the q sorted (ties by entry)
-            const uint32_t q = dq[e];
-            uint32_t p = 0;
-            for (uint32_t f = 0; f < nd; ++f) p += (dq[f] < q || (dq[f] == q && f < e)) ? 1u : 0u;
-            qs[p] = q;
+        lds_sort(dk, dr, nd);   // position p: rank below_k + p
+        for (uint32_t e = threadIdx.x; e < nd; e += MV_BLK) {
+            const uint32_t q = ins(dk[e]);
+            dq[e] = q;
+            qs[e] = (uint64_t)q << 32 | e;
         }
-        __syncthreads();
-        // every mover's slot y counts at the first sorted q above it: A(qs[p]) = qc[0] + ... + qc[p]
+        for (uint32_t e = threadIdx.x; e <= nd; e += MV_BLK) qc[e] = 0u;
+        lds_sort(qs, nullptr, nd);
+        // every mover's slot y counts at the first sorted q above it: A(q) = qc[0] + ... + qc[lower_bound(q)]. Most
+        // movers lie below all of a workgroup's q (counted in a register: one LDS address would serialise them) or
+        // above all of them (never read).
+        uint32_t c0 = 0;
+        const uint32_t qlo = nd ? (uint32_t)(qs[0] >> 32) : 0u, qhi = nd ? (uint32_t)(qs[nd - 1] >> 32) : 0u;
         for (uint32_t r = threadIdx.x; r < m && nd > 0; r += MV_BLK) {
             const uint32_t y = mv_slot(w, w.mi[r]);
-            uint32_t lo = 0, hi = nd;   // first sorted q > y
+            if (y < qlo) {
+                ++c0;
+                continue;
+            }
+            if (y >= qhi) continue;
+            uint32_t lo = 0, hi = nd;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (qs[mid] <= y) lo = mid + 1;
+                if ((uint32_t)(qs[mid] >> 32) <= y) lo = mid + 1;
                 else hi = mid;
             }
             atomicAdd(&qc[lo], 1u);
         }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c0 += (uint32_t)__shfl_xor((int)c0, o, 64);
+        if (lane_id() == 0 && c0) atomicAdd(&qc[0], c0);
         __syncthreads();
-        if (threadIdx.x == 0)
-            for (uint32_t p = 1; p < nd; ++p) qc[p] += qc[p - 1];   // nd ~ m / G: a short serial prefix
-        __syncthreads();
+        lds_scan(qc, nd + 1, red);
         for (uint32_t e = threadIdx.x; e < nd; e += MV_BLK) {
-            const uint64_t c = dk[e];
-            uint32_t lr = 0;
-            for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < c ? 1u : 0u;
             const uint32_t q = dq[e];
-            uint32_t lo = 0, hi = nd;   // the first sorted position of q: A(q) counts the slots below q
+            uint32_t lo = 0, hi = nd;   // the first sorted position of q
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (qs[mid] < q) lo = mid + 1;
+                if ((uint32_t)(qs[mid] >> 32) < q) lo = mid + 1;
                 else hi = mid;
             }
-            place(dr[e], c, below_k + lr, q, qc[lo]);
+            place(dr[e], dk[e], below_k + e, q, qc[lo]);
         }
     } else {   // more dest entries than LDS holds: each one counted against the whole list
         for (uint32_t r = threadIdx.x; r < m; r += MV_BLK) {
