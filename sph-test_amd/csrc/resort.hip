@@ -122,19 +122,22 @@ static __device__ __forceinline__ uint32_t movers_before(bool mv, uint32_t block
 // [kd0, kd1) = [sk(x0), sk(x1)) (the old sorted keys at those slots, so every workgroup's key range holds about n/G
 // particles and ~m/G movers; the ranges partition all keys, sentinels included). Its dest entries are the movers
 // with a new key in its range, its source entries those with a slot in its range. One stream over the whole mover
-// list (U per lane in flight) stages both in LDS and counts the movers below the ranges; then, each set sorted in
+// list (U per lane in flight) stages both in LDS and counts the movers below the ranges (xa below); then, each set sorted in
 // LDS (bitonic: the movers crowd into a few ranges mid-collapse, where counting ranks pairwise cost O(entries²)),
 //   rk(x) = #{y : k_y < kd0} + (x's position among the sorted dest entries)   -> ms[rk] = (k, x)
-//   ri(x) = #{y : y < x0} + (x's position among the sorted source entries)    -> mx[ri] = x, mos[ri] = old key
-// and for its dest entries the insertion slot q = clamp(x, cs_old[k], cs_old[k + 1]) and A(q) = #{y : y < q}: the
-// q sorted, a second stream over the movers' slots adds each slot to the count of the first q above it, a prefix
-// sum gives A(q). The mover is then scattered to dst = (q − A(q)) + rk here, so the merge that follows reads
-// only the tables (it updates cs_old in place). A range with more entries than LDS holds (a state where most
-// particles move, only under SPH_RESORT=2) counts them against the whole list instead: slow, same result. Also
-// zeroes the next step's mover counter.
+//   ri(x) = #{y : y < xa} + (x's position among the sorted slot entries)      -> mx[ri] = x, mos[ri] = old key
+// and for its dest entries the insertion slot q = clamp(x, cs_old[k], cs_old[k + 1]) and A(q) = #{y : y < q}. Every
+// such q lies in [xa, x1] with xa = cs_old[kd0] <= x0 (the start of the cell holding slot x0), so the stream also
+// stages the movers with a slot in [xa, x1) (the source entries are their suffix from x0) and counts those below xa:
+// A(q) is that count plus a binary search in the sorted slots, with no second pass over the mover list (r5: a second
+// stream's dependent loads took the kernel from ~5 to ~32 us). The mover is then scattered to dst = (q − A(q)) + rk
+// here, so the merge that follows reads only the tables (it updates cs_old in place). A range with more entries than
+// LDS holds (a state where most particles move, only under SPH_RESORT=2) counts them against the whole list instead:
+// slow, same result. Also zeroes the next step's mover counter.
 constexpr int MV_RANK_GRID = 256;   // workgroups at most; one per CU
 constexpr int MV_RANK_U = 16;       // movers per lane per streaming round
-constexpr int MV_RK_CAP = 4096;     // dest and source entries staged per workgroup (a power of two; ~144 KB of LDS)
+constexpr int MV_RK_CAP = 4096;     // dest entries staged per workgroup (a power of two)
+constexpr int MV_RX_CAP = 8192;     // slot entries staged per workgroup (a power of two; 112 KB of LDS in all)
 
 __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
 #pragma unroll
@@ -207,12 +210,9 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
                                                     int32_t n, float4* __restrict__ pos_o, float4* __restrict__ vel_o,
                                                     int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o,
                                                     ResortExtra ex) {
-    __shared__ uint64_t dk[MV_RK_CAP];       // dest entries (new key, slot), sorted in place
-    __shared__ uint32_t dr[MV_RK_CAP];       // their mover index (moves with the sort)
-    __shared__ uint32_t dq[MV_RK_CAP];       // their insertion slots q, by sorted dest position
-    __shared__ uint64_t qs[MV_RK_CAP];       // (q, position), sorted
-    __shared__ uint32_t qc[MV_RK_CAP + 1];   // movers' slots counted at the first sorted q above them; then prefixed
-    __shared__ uint64_t sxk[MV_RK_CAP];      // source entries (slot, mover index), sorted
+    __shared__ uint64_t dk[MV_RK_CAP];   // dest entries (new key, slot), sorted in place
+    __shared__ uint32_t dr[MV_RK_CAP];   // their mover index (moves with the sort)
+    __shared__ uint64_t sxk[MV_RX_CAP];  // slot entries (slot, mover index) in [xa, x1), sorted
     __shared__ uint32_t cnt[2], red[MV_BLK / 64];
     resolve_sizes(src, w, n);
     if (threadIdx.x < 2) cnt[threadIdx.x] = 0u;
@@ -224,8 +224,10 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
     const uint32_t x0 = (uint32_t)((uint64_t)(uint32_t)n * b / G), x1 = (uint32_t)((uint64_t)(uint32_t)n * (b + 1) / G);
     const uint32_t kd0 = b == 0 ? 0u : (x0 < (uint32_t)n ? asm_sk(src, (int32_t)x0) : 0xffffffffu);
     const uint32_t kd1 = b == G - 1 ? 0xffffffffu : (x1 < (uint32_t)n ? asm_sk(src, (int32_t)x1) : 0xffffffffu);
+    // every insertion slot of a dest entry lies in [xa, x1]: q >= cs_old[kd0] = xa, q <= cs_old[kd1] <= x1
+    const uint32_t xa = b == 0 || kd0 == 0xffffffffu ? min(x0, 0u) : min(cs_old[kd0], x0);
     __syncthreads();
-    uint32_t below_k = 0, below_x = 0;
+    uint32_t below_k = 0, below_xa = 0;
     for (uint32_t base = 0; base < m; base += MV_BLK * MV_RANK_U) {
         uint32_t xs[MV_RANK_U], ks[MV_RANK_U];
 #pragma unroll
@@ -240,21 +242,36 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
             const bool ok = r < m;
             const uint32_t x = mv_slot(w, xs[u]), k = ks[u];
             below_k += ok && k < kd0 ? 1u : 0u;
-            below_x += ok && x < x0 ? 1u : 0u;
+            below_xa += ok && x < xa ? 1u : 0u;
             if (ok && k >= kd0 && k < kd1) {
                 const uint32_t p = atomicAdd(&cnt[0], 1u);
                 if (p < MV_RK_CAP) { dk[p] = comp(k, x); dr[p] = r; }
             }
-            if (ok && x >= x0 && x < x1) {
+            if (ok && x >= xa && x < x1) {
                 const uint32_t p = atomicAdd(&cnt[1], 1u);
-                if (p < MV_RK_CAP) sxk[p] = (uint64_t)x << 32 | r;
+                if (p < MV_RX_CAP) sxk[p] = (uint64_t)x << 32 | r;
             }
         }
     }
     below_k = block_sum(below_k, red);   // (its barriers also publish the staged entries and counts)
-    below_x = block_sum(below_x, red);
+    below_xa = block_sum(below_xa, red);
     const uint32_t nd = cnt[0], ns = cnt[1];
-    // ---- source entries: their slot ranks, the tables by slot
+    const bool slots_staged = ns <= MV_RX_CAP;   // block-uniform
+    auto slots_below = [&](uint32_t y) {   // #movers with slot in [xa, y), y in [xa, x1]: from the sorted slot entries
+        uint32_t lo = 0, hi = ns;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((uint32_t)(sxk[mid] >> 32) < y) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    };
+    auto count_below = [&](uint32_t y) {   // #movers with slot < y, against the whole list
+        uint32_t c = 0;
+        for (uint32_t f = 0; f < m; ++f) c += mv_slot(w, w.mi[f]) < y ? 1u : 0u;
+        return c;
+    };
+    // ---- source entries (slot in [x0, x1)): their slot ranks ri = #{y : y < x}, the tables by slot
     auto source = [&](uint32_t r, uint32_t x, uint32_t ri) {
         if (ri >= w.cap) {   // inconsistent tables: flag, never write past them
             if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
@@ -263,22 +280,18 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
         w.mx[ri] = x;
         w.mos[ri] = w.mo[r];   // old keys by slot: ascending
     };
-    if (ns <= MV_RK_CAP) {
+    if (slots_staged) {
         lds_sort(sxk, nullptr, ns);
-        for (uint32_t e = threadIdx.x; e < ns; e += MV_BLK) source((uint32_t)sxk[e], (uint32_t)(sxk[e] >> 32), below_x + e);
-    } else {   // more source entries than LDS holds: each one counted against the whole list
+        const uint32_t s0 = slots_below(x0);
+        for (uint32_t e = s0 + threadIdx.x; e < ns; e += MV_BLK)
+            source((uint32_t)sxk[e], (uint32_t)(sxk[e] >> 32), below_xa + e);
+    } else {   // more slot entries than LDS holds: each one counted against the whole list
         for (uint32_t r = threadIdx.x; r < m; r += MV_BLK) {
             const uint32_t x = mv_slot(w, w.mi[r]);
-            if (!(x >= x0 && x < x1)) continue;
-            uint32_t lr = 0;
-            for (uint32_t f = 0; f < m; ++f) {
-                const uint32_t xf = mv_slot(w, w.mi[f]);
-                lr += (xf >= x0 && xf < x) ? 1u : 0u;
-            }
-            source(r, x, below_x + lr);
+            if (x >= x0 && x < x1) source(r, x, count_below(x));
         }
     }
-    // ---- dest entries: rank, insertion slot, A(q), placement
+    // ---- dest entries: rank, insertion slot q, A(q) = #{y : y < q}, placement
     auto place = [&](uint32_t r, uint64_t c, uint32_t rk, uint32_t q, uint32_t aq) {
         const uint32_t k = (uint32_t)(c >> 32), x = (uint32_t)c;
         const uint32_t dst = (q - aq) + rk;
@@ -301,63 +314,25 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
         const uint32_t c0 = cs_old[k], c1 = cs_old[k + 1];
         return x < c0 ? c0 : (x > c1 ? c1 : x);
     };
+    auto aq_of = [&](uint32_t q) { return slots_staged ? below_xa + slots_below(max(q, xa)) : count_below(q); };
     if (nd <= MV_RK_CAP) {
-        lds_sort(dk, dr, nd);   // position p: rank below_k + p
+        lds_sort(dk, dr, nd);   // position e: rank below_k + e
         for (uint32_t e = threadIdx.x; e < nd; e += MV_BLK) {
             const uint32_t q = ins(dk[e]);
-            dq[e] = q;
-            qs[e] = (uint64_t)q << 32 | e;
-        }
-        for (uint32_t e = threadIdx.x; e <= nd; e += MV_BLK) qc[e] = 0u;
-        lds_sort(qs, nullptr, nd);
-        // every mover's slot y counts at the first sorted q above it: A(q) = qc[0] + ... + qc[lower_bound(q)]. Most
-        // movers lie below all of a workgroup's q (counted in a register: one LDS address would serialise them) or
-        // above all of them (never read).
-        uint32_t c0 = 0;
-        const uint32_t qlo = nd ? (uint32_t)(qs[0] >> 32) : 0u, qhi = nd ? (uint32_t)(qs[nd - 1] >> 32) : 0u;
-        for (uint32_t r = threadIdx.x; r < m && nd > 0; r += MV_BLK) {
-            const uint32_t y = mv_slot(w, w.mi[r]);
-            if (y < qlo) {
-                ++c0;
-                continue;
-            }
-            if (y >= qhi) continue;
-            uint32_t lo = 0, hi = nd;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if ((uint32_t)(qs[mid] >> 32) <= y) lo = mid + 1;
-                else hi = mid;
-            }
-            atomicAdd(&qc[lo], 1u);
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) c0 += (uint32_t)__shfl_xor((int)c0, o, 64);
-        if (lane_id() == 0 && c0) atomicAdd(&qc[0], c0);
-        __syncthreads();
-        lds_scan(qc, nd + 1, red);
-        for (uint32_t e = threadIdx.x; e < nd; e += MV_BLK) {
-            const uint32_t q = dq[e];
-            uint32_t lo = 0, hi = nd;   // the first sorted position of q
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if ((uint32_t)(qs[mid] >> 32) < q) lo = mid + 1;
-                else hi = mid;
-            }
-            place(dr[e], dk[e], below_k + e, q, qc[lo]);
+            place(dr[e], dk[e], below_k + e, q, aq_of(q));
         }
     } else {   // more dest entries than LDS holds: each one counted against the whole list
         for (uint32_t r = threadIdx.x; r < m; r += MV_BLK) {
             const uint32_t k = w.mk[r];
             if (!(k >= kd0 && k < kd1)) continue;
             const uint64_t c = comp(k, mv_slot(w, w.mi[r]));
-            const uint32_t q = ins(c);
-            uint32_t lr = 0, aq = 0;
+            uint32_t lr = 0;
             for (uint32_t f = 0; f < m; ++f) {
                 const uint32_t kf = w.mk[f], xf = mv_slot(w, w.mi[f]);
                 lr += (kf >= kd0 && kf < kd1 && comp(kf, xf) < c) ? 1u : 0u;
-                aq += xf < q ? 1u : 0u;
             }
-            place(r, c, below_k + lr, q, aq);
+            const uint32_t q = ins(c);
+            place(r, c, below_k + lr, q, aq_of(q));
         }
     }
 }

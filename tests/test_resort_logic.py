@@ -58,27 +58,37 @@ def test_resort_formulas_match_stable_sort(frac):
 def range_ranks(ks, newk, G):
     """resort.hip k_mv_rank restated: workgroup b owns the old slots [x0, x1) = [b·n/G, (b+1)·n/G) and the new keys
     [ks[x0], ks[x1]) (first range from 0, last to infinity); rk counts the movers below the key range plus those in
-    range with a smaller (key, slot), ri the movers below the slot range plus those in range with a smaller slot."""
+    range with a smaller (key, slot), ri the movers below the slot range plus those in range with a smaller slot.
+    A(q) for a dest entry counts the movers below xa = cs_old[kd0] plus the staged slots in [xa, q): every insertion
+    slot q of the range lies in [xa, x1]."""
     n = len(ks)
     movers = np.nonzero(newk != ks)[0]
     mk = newk[movers]
+    nc = int(max(ks.max(initial=0), newk.max(initial=0))) + 1
+    cs_old = np.concatenate([np.searchsorted(ks, np.arange(nc + 1), side="left"), [n]])
     rk = np.full(len(movers), -1, np.int64)
     ri = np.full(len(movers), -1, np.int64)
+    aq = np.full(len(movers), -1, np.int64)
     for b in range(G):
         x0, x1 = n * b // G, n * (b + 1) // G
         kd0 = 0 if b == 0 else (ks[x0] if x0 < n else np.iinfo(np.int64).max)
         kd1 = np.iinfo(np.int64).max if b == G - 1 else (ks[x1] if x1 < n else np.iinfo(np.int64).max)
+        xa = 0 if b == 0 else min(int(cs_old[kd0]), x0)
         ind = (mk >= kd0) & (mk < kd1)
         ins = (movers >= x0) & (movers < x1)
-        below_k, below_x = int((mk < kd0).sum()), int((movers < x0).sum())
+        staged = np.sort(movers[(movers >= xa) & (movers < x1)])
+        below_k, below_xa = int((mk < kd0).sum()), int((movers < xa).sum())
         c = _comp(mk, movers)
         for e in np.nonzero(ind)[0]:
             assert rk[e] < 0, "a mover in two key ranges"
             rk[e] = below_k + int((c[ind] < c[e]).sum())
+            q = min(max(int(movers[e]), int(cs_old[mk[e]])), int(cs_old[mk[e] + 1]))
+            assert xa <= q <= x1
+            aq[e] = below_xa + int(np.searchsorted(staged, q, side="left"))
         for e in np.nonzero(ins)[0]:
             assert ri[e] < 0, "a mover in two slot ranges"
-            ri[e] = below_x + int((movers[ins] < movers[e]).sum())
-    return movers, mk, rk, ri
+            ri[e] = below_xa + int(np.searchsorted(staged, movers[e], side="left"))
+    return movers, mk, rk, ri, aq, cs_old
 
 
 @pytest.mark.parametrize("frac", [0.0, 0.01, 0.3, 1.0])
@@ -92,7 +102,9 @@ def test_range_ranks_equal_global_ranks(frac, G):
         newk = ks.copy()
         mv = rng.random(n) < frac
         newk[mv] = rng.integers(0, nc + 1, int(mv.sum()))    # nc: the sentinel key (inactive / left the window)
-        movers, mk, rk, ri = range_ranks(ks, newk, min(G, max(n // 256, 1)) if G == 256 else G)
+        movers, mk, rk, ri, aq, cs_old = range_ranks(ks, newk, min(G, max(n // 256, 1)) if G == 256 else G)
         c = _comp(mk, movers)
         assert np.array_equal(rk, np.argsort(np.argsort(c, kind="stable"), kind="stable"))
         assert np.array_equal(ri, np.arange(len(movers)))
+        q = np.minimum(np.maximum(movers, cs_old[mk]), cs_old[mk + 1])
+        assert np.array_equal(aq, np.searchsorted(movers, q, side="left"))
