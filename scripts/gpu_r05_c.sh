@@ -4,7 +4,7 @@ cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r05c; mkdir -p $O; export TMPDIR=/tmp
 ( while true; do date >> $O/heartbeat; sleep 50; done ) & HB=$!
 trap "kill $HB" EXIT
 python -c "import torch; print(torch.__version__, flush=True)"
-timeout -k 10 600 python -u -m pytest -x -v -s -m gpu --timeout 300 --timeout-method thread tests/test_gpu_resort.py tests/test_gpu_small.py > $O/pytest.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest -x -v -s -m gpu --timeout 300 --timeout-method thread tests/ > $O/pytest.log 2>&1; rc=$?
 echo "pytest rc=$rc"; grep -E " passed| failed|FAILED|ERROR" $O/pytest.log | tail -15
 [ $rc -ne 0 ] && { grep -B5 -A40 "Error\|FAILED\|assert" $O/pytest.log | tail -80; exit $rc; }
 timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench.log 2>&1; rc=$?; echo "bench rc=$rc"; tail -c 700 $O/bench.log; [ $rc -ne 0 ] && exit $rc

@@ -44,6 +44,19 @@ static __device__ __forceinline__ void move_extra(const ResortExtra& ex, uint32_
     ex.aux_o[dst] = ex.aux[x];
     ex.mode_o[dst] = ex.mode[x];
 }
+struct ExtraVals { float4 omg, rot, aux; int32_t mode; };
+static __device__ __forceinline__ ExtraVals load_extra(const ResortExtra& ex, uint32_t x) {
+    ExtraVals e{};
+    if (ex.omg) e = ExtraVals{ex.omg[x], ex.rot[x], ex.aux[x], ex.mode[x]};
+    return e;
+}
+static __device__ __forceinline__ void store_extra(const ResortExtra& ex, const ExtraVals& e, uint32_t dst) {
+    if (!ex.omg) return;
+    ex.omg_o[dst] = e.omg;
+    ex.rot_o[dst] = e.rot;
+    ex.aux_o[dst] = e.aux;
+    ex.mode_o[dst] = e.mode;
+}
 
 static __device__ __forceinline__ uint32_t asm_sk(const AsmSrc& a, int32_t x) {
     return asm_rec(a, x) ? a.skr[x] : a.sk[x + a.o_off];
@@ -105,17 +118,6 @@ static __device__ uint32_t wave_lower_bound(const T* __restrict__ a, uint32_t n,
     return base + (uint32_t)__popcll(__ballot(lt));
 }
 
-// A(i) for the calling lane: movers with index < i (block offset + earlier waves + earlier lanes)
-static __device__ __forceinline__ uint32_t movers_before(bool mv, uint32_t block_off, uint32_t* wc) {
-    const uint64_t b = __ballot(mv);
-    const int w = threadIdx.x >> 6;
-    if (lane_id() == 0) wc[w] = (uint32_t)__popcll(b);
-    __syncthreads();
-    uint32_t off = block_off;
-    for (int k = 0; k < w; ++k) off += wc[k];
-    return off + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-}
-
 // Mover ranks and placement in O(m) per workgroup (replaces the all-pairs tile counts and the separate placement of
 // r1-r4, whose work grew as m²: the C3 re-sort chain went from 27.7 us from rest to 41.5 us mid-collapse). Workgroup
 // b of G owns the slots [x0, x1) = [b·n/G, (b+1)·n/G) of the assembled old order and the new keys
@@ -151,9 +153,42 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
     return t;
 }
 
+static __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int j) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, j, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), j, 64);
+    return (uint64_t)hi << 32 | lo;
+}
+
 // Sorts a[0, len) ascending in LDS (bitonic over the next power of two, padded with ~0; the keys are distinct), with
-// the payload b (if any) moved along. Every thread of the workgroup calls it; it ends on a barrier.
+// the payload b (if any) moved along. Every thread of the workgroup calls it; it ends on a barrier. Up to 64 entries
+// (a workgroup's usual share of the movers) wave 0 sorts them in registers, exchanging by shuffles: no workgroup
+// barrier per stage.
 __device__ void lds_sort(uint64_t* a, uint32_t* b, uint32_t len) {
+    if (len <= 64) {   // block-uniform
+        if (threadIdx.x < 64) {
+            const uint32_t l = threadIdx.x;
+            uint64_t v = l < len ? a[l] : ~0ull;
+            uint32_t pb = (b && l < len) ? b[l] : 0u;
+#pragma unroll
+            for (uint32_t k = 2; k <= 64; k <<= 1)
+#pragma unroll
+                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                    const uint64_t o = shfl_xor64(v, (int)j);
+                    const uint32_t ob = (uint32_t)__shfl_xor((int)pb, (int)j, 64);
+                    // the pair's lower lane keeps the smaller key in an ascending block, the larger in a descending one
+                    const bool take = ((l & j) == 0) == ((l & k) == 0) ? o < v : o > v;
+                    if (take) {
+                        v = o;
+                        pb = ob;
+                    }
+                }
+            if (l < len) {
+                a[l] = v;
+                if (b) b[l] = pb;
+            }
+        }
+        __syncthreads();
+        return;
+    }
     uint32_t P = 1;
     while (P < len) P <<= 1;
     for (uint32_t t = len + threadIdx.x; t < P; t += MV_BLK) a[t] = ~0ull;
@@ -222,20 +257,31 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
         if (w.host_count) *w.host_count = m;   // for the host's next sort choices (no copy launch)
     }
     const uint32_t x0 = (uint32_t)((uint64_t)(uint32_t)n * b / G), x1 = (uint32_t)((uint64_t)(uint32_t)n * (b + 1) / G);
-    const uint32_t kd0 = b == 0 ? 0u : (x0 < (uint32_t)n ? asm_sk(src, (int32_t)x0) : 0xffffffffu);
-    const uint32_t kd1 = b == G - 1 ? 0xffffffffu : (x1 < (uint32_t)n ? asm_sk(src, (int32_t)x1) : 0xffffffffu);
-    // every insertion slot of a dest entry lies in [xa, x1]: q >= cs_old[kd0] = xa, q <= cs_old[kd1] <= x1
-    const uint32_t xa = b == 0 || kd0 == 0xffffffffu ? min(x0, 0u) : min(cs_old[kd0], x0);
-    __syncthreads();
-    uint32_t below_k = 0, below_xa = 0;
-    for (uint32_t base = 0; base < m; base += MV_BLK * MV_RANK_U) {
-        uint32_t xs[MV_RANK_U], ks[MV_RANK_U];
+    // both range keys in one round trip (pointer selects, unconditional loads)
+    auto sk_ptr = [&](uint32_t x) {
+        const int32_t xi = (int32_t)min(x, (uint32_t)max(n - 1, 0));
+        return asm_rec(src, xi) ? src.skr + xi : src.sk + (xi + src.o_off);
+    };
+    const uint32_t sk0 = *sk_ptr(x0), sk1 = *sk_ptr(x1);
+    const uint32_t kd0 = b == 0 ? 0u : (x0 < (uint32_t)n ? sk0 : 0xffffffffu);
+    const uint32_t kd1 = b == G - 1 ? 0xffffffffu : (x1 < (uint32_t)n ? sk1 : 0xffffffffu);
+    // The kernel is a chain of dependent memory round trips (~1-2 us each at this occupancy): the code keeps them few.
+    // Round 0 of the mover stream issues together with the load of xa.
+    uint32_t xs[MV_RANK_U], ks[MV_RANK_U];
+    auto load_round = [&](uint32_t base) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < MV_RANK_U; ++u) {   // every load of the round issues before any is used
             const uint32_t r = min(base + u * MV_BLK + threadIdx.x, m - 1u);
             xs[u] = w.mi[r];
             ks[u] = w.mk[r];
         }
+    };
+    if (m) load_round(0);
+    // every insertion slot of a dest entry lies in [xa, x1]: q >= cs_old[kd0] = xa, q <= cs_old[kd1] <= x1
+    const uint32_t xa = b == 0 || kd0 == 0xffffffffu ? 0u : min(cs_old[kd0], x0);
+    __syncthreads();
+    uint32_t below_k = 0, below_xa = 0;
+    for (uint32_t base = 0; base < m; base += MV_BLK * MV_RANK_U) {
 #pragma unroll
         for (int u = 0; u < MV_RANK_U; ++u) {
             const uint32_t r = base + u * MV_BLK + threadIdx.x;
@@ -252,11 +298,12 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
                 if (p < MV_RX_CAP) sxk[p] = (uint64_t)x << 32 | r;
             }
         }
+        if (base + MV_BLK * MV_RANK_U < m) load_round(base + MV_BLK * MV_RANK_U);
     }
     below_k = block_sum(below_k, red);   // (its barriers also publish the staged entries and counts)
     below_xa = block_sum(below_xa, red);
     const uint32_t nd = cnt[0], ns = cnt[1];
-    const bool slots_staged = ns <= MV_RX_CAP;   // block-uniform
+    const bool slots_staged = ns <= MV_RX_CAP, dest_staged = nd <= MV_RK_CAP;   // block-uniform
     auto slots_below = [&](uint32_t y) {   // #movers with slot in [xa, y), y in [xa, x1]: from the sorted slot entries
         uint32_t lo = 0, hi = ns;
         while (lo < hi) {
@@ -271,57 +318,83 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
         for (uint32_t f = 0; f < m; ++f) c += mv_slot(w, w.mi[f]) < y ? 1u : 0u;
         return c;
     };
-    // ---- source entries (slot in [x0, x1)): their slot ranks ri = #{y : y < x}, the tables by slot
-    auto source = [&](uint32_t r, uint32_t x, uint32_t ri) {
+    auto aq_of = [&](uint32_t q) { return slots_staged ? below_xa + slots_below(max(q, xa)) : count_below(q); };
+    // source entries (slot in [x0, x1)): ri = #{y : y < x} -> mx[ri] = x, mos[ri] = old key (ascending by slot)
+    auto source = [&](uint32_t x, uint32_t ri, uint32_t mo) {
         if (ri >= w.cap) {   // inconsistent tables: flag, never write past them
             if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
             return;
         }
         w.mx[ri] = x;
-        w.mos[ri] = w.mo[r];   // old keys by slot: ascending
+        w.mos[ri] = mo;
     };
-    if (slots_staged) {
-        lds_sort(sxk, nullptr, ns);
-        const uint32_t s0 = slots_below(x0);
-        for (uint32_t e = s0 + threadIdx.x; e < ns; e += MV_BLK)
-            source((uint32_t)sxk[e], (uint32_t)(sxk[e] >> 32), below_xa + e);
-    } else {   // more slot entries than LDS holds: each one counted against the whole list
-        for (uint32_t r = threadIdx.x; r < m; r += MV_BLK) {
-            const uint32_t x = mv_slot(w, w.mi[r]);
-            if (x >= x0 && x < x1) source(r, x, count_below(x));
-        }
-    }
-    // ---- dest entries: rank, insertion slot q, A(q) = #{y : y < q}, placement
-    auto place = [&](uint32_t r, uint64_t c, uint32_t rk, uint32_t q, uint32_t aq) {
-        const uint32_t k = (uint32_t)(c >> 32), x = (uint32_t)c;
+    // dest entries: rank rk, insertion slot q among the stayers, A(q) = #{y : y < q}, placement at (q − A(q)) + rk
+    auto place = [&](uint64_t c, uint32_t rk, uint32_t q, uint32_t aq, float4 p, float4 v, int32_t pid,
+                     const ExtraVals& e) {
+        const uint32_t k = (uint32_t)(c >> 32);
         const uint32_t dst = (q - aq) + rk;
         if (rk >= w.cap || dst >= w.cap) {   // inconsistent tables: flag, never write past them
             if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
             return;
         }
         w.ms[rk] = c;
-        float4 p, v;
-        int32_t pid;
-        asm_load(src, (int32_t)x, p, v, pid);
         pos_o[dst] = p;
         vel_o[dst] = v;
         id_o[dst] = pid;
         sk_o[dst] = k;
-        move_extra(ex, x, dst);
+        store_extra(ex, e, dst);
     };
-    auto ins = [&](uint64_t c) {   // the insertion slot among the stayers
-        const uint32_t k = (uint32_t)(c >> 32), x = (uint32_t)c;
-        const uint32_t c0 = cs_old[k], c1 = cs_old[k + 1];
-        return x < c0 ? c0 : (x > c1 ? c1 : x);
-    };
-    auto aq_of = [&](uint32_t q) { return slots_staged ? below_xa + slots_below(max(q, xa)) : count_below(q); };
-    if (nd <= MV_RK_CAP) {
-        lds_sort(dk, dr, nd);   // position e: rank below_k + e
-        for (uint32_t e = threadIdx.x; e < nd; e += MV_BLK) {
-            const uint32_t q = ins(dk[e]);
-            place(dr[e], dk[e], below_k + e, q, aq_of(q));
+    auto ins = [&](uint32_t k, uint32_t x, uint32_t c0, uint32_t c1) { return x < c0 ? c0 : (x > c1 ? c1 : x); };
+    if (slots_staged) lds_sort(sxk, nullptr, ns);
+    if (dest_staged) lds_sort(dk, dr, nd);   // position e: rank below_k + e
+    if (slots_staged && dest_staged) {
+        // one pass over both kinds of entry, every global load of an entry issued before its stores
+        const uint32_t s0 = slots_below(x0), nsrc = ns - s0;
+        for (uint32_t t = threadIdx.x; t < max(nsrc, nd); t += MV_BLK) {
+            const bool hs = t < nsrc, hd = t < nd;
+            const uint64_t se = hs ? sxk[s0 + t] : 0ull;
+            const uint64_t c = hd ? dk[t] : 0ull;
+            const uint32_t k = (uint32_t)(c >> 32), x = (uint32_t)c;
+            const uint32_t mo = hs ? w.mo[(uint32_t)se] : 0u;
+            const uint32_t c0 = hd ? cs_old[k] : 0u, c1 = hd ? cs_old[k + 1] : 0u;
+            float4 p = make_float4(0.f, 0.f, 0.f, 0.f), v = p;
+            int32_t pid = 0;
+            ExtraVals e{};
+            if (hd) {
+                asm_load(src, (int32_t)x, p, v, pid);
+                e = load_extra(ex, x);
+            }
+            if (hs) source((uint32_t)(se >> 32), below_xa + s0 + t, mo);
+            if (hd) {
+                const uint32_t q = ins(k, x, c0, c1);
+                place(c, below_k + t, q, aq_of(q), p, v, pid, e);
+            }
         }
-    } else {   // more dest entries than LDS holds: each one counted against the whole list
+        return;
+    }
+    // more entries than LDS holds (a state where most particles move, only under SPH_RESORT=2): the overflowing kind
+    // counted against the whole list instead, slow, same result
+    if (slots_staged) {
+        const uint32_t s0 = slots_below(x0);
+        for (uint32_t e = s0 + threadIdx.x; e < ns; e += MV_BLK)
+            source((uint32_t)(sxk[e] >> 32), below_xa + e, w.mo[(uint32_t)sxk[e]]);
+    } else {
+        for (uint32_t r = threadIdx.x; r < m; r += MV_BLK) {
+            const uint32_t x = mv_slot(w, w.mi[r]);
+            if (x >= x0 && x < x1) source(x, count_below(x), w.mo[r]);
+        }
+    }
+    auto place_entry = [&](uint64_t c, uint32_t rk) {
+        const uint32_t k = (uint32_t)(c >> 32), x = (uint32_t)c;
+        float4 p, v;
+        int32_t pid;
+        asm_load(src, (int32_t)x, p, v, pid);
+        const uint32_t q = ins(k, x, cs_old[k], cs_old[k + 1]);
+        place(c, rk, q, aq_of(q), p, v, pid, load_extra(ex, x));
+    };
+    if (dest_staged) {
+        for (uint32_t e = threadIdx.x; e < nd; e += MV_BLK) place_entry(dk[e], below_k + e);
+    } else {
         for (uint32_t r = threadIdx.x; r < m; r += MV_BLK) {
             const uint32_t k = w.mk[r];
             if (!(k >= kd0 && k < kd1)) continue;
@@ -331,19 +404,16 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
                 const uint32_t kf = w.mk[f], xf = mv_slot(w, w.mi[f]);
                 lr += (kf >= kd0 && kf < kd1 && comp(kf, xf) < c) ? 1u : 0u;
             }
-            const uint32_t q = ins(c);
-            place(r, c, below_k + lr, q, aq_of(q));
+            place_entry(c, below_k + lr);
         }
     }
 }
 
-// cs[k] += #{movers: new key < k} − #{movers: old key < k}, for k in [0, ncells]; 1024 cells per
+// cs[k] += #{movers: new key < k} − #{movers: old key < k}, for k in [0, ncells]; 4096 cells per
 // workgroup. A workgroup whose counts agree at its start and that holds no mover key leaves its cells.
 // Runs as extra workgroups of k_mv_merge (it needs only k_mv_rank's tables), beside the scatter.
-constexpr int MV_CS_CELLS = 4 * MV_BLK;
-#ifndef SPH_MERGE_PREFETCH
-#define SPH_MERGE_PREFETCH 1
-#endif
+constexpr int MV_CS_PER = 16;
+constexpr int MV_CS_CELLS = MV_CS_PER * MV_BLK;
 // movers staged in LDS for the merge's binary searches (a workgroup's cells or slots rarely hold more)
 constexpr uint32_t MV_LDS = 1024;
 
@@ -366,8 +436,8 @@ static __device__ void mv_cell_start(uint32_t* __restrict__ cs, uint32_t ncells,
             for (uint32_t t = threadIdx.x; t < no; t += MV_BLK) lmo[t] = w.mos[olo + t];
             __syncthreads();
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
+#pragma unroll 4
+        for (int j = 0; j < MV_CS_PER; ++j) {
             const uint32_t k = k0 + j * MV_BLK + threadIdx.x;
             if (k > ncells) break;
             const uint32_t cn = nlo + (staged ? lower_bound(lms, nn, comp(k, 0u)) : lower_bound(w.ms + nlo, nn, comp(k, 0u)));
@@ -388,13 +458,19 @@ static __device__ void mv_cell_start(uint32_t* __restrict__ cs, uint32_t ncells,
     }
 }
 
+// Slots per merge workgroup: MV_MERGE_PER per thread. The merge is a chain of dependent round trips (the searches,
+// the staging, the scatter) more than a stream: a workgroup of 4 x 256 slots pays the chain once for 4x the slots, and
+// its 1024 workgroups at C3 are resident at once (256-slot workgroups ran the chain twice over: 22.6 us mid-collapse).
+constexpr int MV_MERGE_PER = 4;
+constexpr int MV_MERGE_SLOTS = MV_BLK * MV_MERGE_PER;
+
 __global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
                                                      const uint32_t* __restrict__ mtotal, ResortScratch w,
                                                      float4* __restrict__ pos_o,
                                                      float4* __restrict__ vel_o, int32_t* __restrict__ id_o,
                                                      uint32_t* __restrict__ sk_o, int32_t nb, uint32_t* __restrict__ cs,
                                                      uint32_t ncells, CsPick pick, ResortExtra ex) {
-    __shared__ uint32_t wc[MV_BLK / 64];
+    __shared__ uint32_t wc[MV_MERGE_PER][MV_BLK / 64];
     __shared__ uint32_t b[4];
     __shared__ uint64_t lms[MV_LDS];
     __shared__ uint32_t lmo[MV_LDS];
@@ -403,10 +479,9 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
         return;
     }
     resolve_sizes(src, w, n);          // device-sized slab step: nb is an upper bound
-    const int32_t i0 = xcd_block(blockIdx.x, nb) * MV_BLK;
+    const int32_t i0 = xcd_block(blockIdx.x, nb) * MV_MERGE_SLOTS;
     if (i0 >= n) return;               // whole workgroup, before any barrier
-    const int32_t i = i0 + threadIdx.x;
-    const int32_t ilast = min(i0 + MV_BLK, n) - 1;
+    const int32_t ilast = min(i0 + MV_MERGE_SLOTS, n) - 1;
     const uint32_t m = *mtotal;
     const int wv = threadIdx.x >> 6;
     // movers below this block's first slot, and the movers whose (key, index) falls inside its
@@ -419,40 +494,61 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
         const uint32_t p = wave_lower_bound(w.ms, m, v);
         if (lane_id() == 0) b[wv] = p;
     }
-    const uint32_t ko = i < n ? asm_sk(src, i) : 0u;
-    const bool stay = i < n && asm_key(src, i) == ko;
-#if SPH_MERGE_PREFETCH
-    // the slot's particle loads issue before the searches' dependent loads and the barrier (a mover's are unused)
-    float4 p = make_float4(0.f, 0.f, 0.f, 0.f), v = p;
-    int32_t pid = 0;
-    if (i < n) asm_load(src, i, p, v, pid);
-#endif
+    // slot j of this thread: i0 + j·256 + t; its particle loads issue before the searches' dependent loads and the
+    // barrier (a mover's are unused)
+    uint32_t ko[MV_MERGE_PER];
+    bool stay[MV_MERGE_PER];
+    float4 p[MV_MERGE_PER], v[MV_MERGE_PER];
+    int32_t pid[MV_MERGE_PER];
+#pragma unroll
+    for (int j = 0; j < MV_MERGE_PER; ++j) {
+        const int32_t i = i0 + j * MV_BLK + (int32_t)threadIdx.x;
+        ko[j] = i < n ? asm_sk(src, i) : 0u;
+        stay[j] = i < n && asm_key(src, i) == ko[j];
+        p[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        v[j] = p[j];
+        pid[j] = 0;
+        if (i < n) asm_load(src, i, p[j], v[j], pid[j]);
+    }
+    // A(i) = movers below the block + in its earlier chunks + in earlier waves of this chunk + earlier lanes
+    uint64_t bal[MV_MERGE_PER];
+#pragma unroll
+    for (int j = 0; j < MV_MERGE_PER; ++j) {
+        const int32_t i = i0 + j * MV_BLK + (int32_t)threadIdx.x;
+        bal[j] = __ballot(i < n && !stay[j]);
+        if (lane_id() == 0) wc[j][wv] = (uint32_t)__popcll(bal[j]);
+    }
     __syncthreads();
-    const uint32_t a = movers_before(i < n && !stay, b[0], wc);
     const uint32_t lo = b[1], hi = b[2];
     const bool staged = hi - lo <= MV_LDS;   // block-uniform
     if (staged) {
         for (uint32_t t = threadIdx.x; t < hi - lo; t += MV_BLK) lms[t] = w.ms[lo + t];
         __syncthreads();
     }
-    if (!stay) return;
-    const uint64_t kv = comp(ko, (uint32_t)i);
-    const uint32_t below = lo + (staged ? lower_bound(lms, hi - lo, kv) : lower_bound(w.ms + lo, hi - lo, kv));
-    const uint32_t dst = ((uint32_t)i - a) + below;
-    if (dst >= w.cap) {
-        if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
-        return;
+    uint32_t a = b[0];
+#pragma unroll
+    for (int j = 0; j < MV_MERGE_PER; ++j) {
+        uint32_t aj = a;
+        for (int k = 0; k < MV_BLK / 64; ++k) {
+            aj += k < wv ? wc[j][k] : 0u;
+            a += wc[j][k];
+        }
+        aj += __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[j], 0u));
+        if (!stay[j]) continue;
+        const uint32_t i = (uint32_t)(i0 + j * MV_BLK) + threadIdx.x;
+        const uint64_t kv = comp(ko[j], i);
+        const uint32_t below = lo + (staged ? lower_bound(lms, hi - lo, kv) : lower_bound(w.ms + lo, hi - lo, kv));
+        const uint32_t dst = (i - aj) + below;
+        if (dst >= w.cap) {
+            if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
+            continue;
+        }
+        pos_o[dst] = p[j];
+        vel_o[dst] = v[j];
+        id_o[dst] = pid[j];
+        sk_o[dst] = ko[j];
+        move_extra(ex, i, dst);
     }
-#if !SPH_MERGE_PREFETCH
-    float4 p, v;
-    int32_t pid;
-    asm_load(src, i, p, v, pid);
-#endif
-    pos_o[dst] = p;
-    vel_o[dst] = v;
-    id_o[dst] = pid;
-    sk_o[dst] = ko;
-    move_extra(ex, (uint32_t)i, dst);
 }
 
 // The slab step's halo records: new keys (window sentinel, as k_keys) and old keys moved into this
@@ -584,9 +680,10 @@ void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const u
                    uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,
                    uint32_t* sk_o, hipStream_t s, CsPick pick, ResortExtra ex) {
     if (n <= 0) return;
-    const int32_t nb = (n + MV_BLK - 1) / MV_BLK;
+    const int32_t nb = (n + MV_MERGE_SLOTS - 1) / MV_MERGE_SLOTS;
+    const int32_t nb_rank = (n + MV_BLK - 1) / MV_BLK;
     // n is an upper bound of the slots on device-sized steps: the rank kernel's ranges split the device count
-    SPH_LAUNCH(k_mv_rank, std::min(MV_RANK_GRID, nb), MV_BLK, 0, s, count, count_other, cs, w, src, n, pos_o, vel_o, id_o,
+    SPH_LAUNCH(k_mv_rank, std::min(MV_RANK_GRID, nb_rank), MV_BLK, 0, s, count, count_other, cs, w, src, n, pos_o, vel_o, id_o,
                sk_o, ex);
     // the stayers' scatter and the cell-start update (after k_mv_rank, the last reader of cs_old)
     const int32_t ncs = (int32_t)((ncells + MV_CS_CELLS) / MV_CS_CELLS);
