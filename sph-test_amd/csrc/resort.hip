@@ -137,10 +137,11 @@ static __device__ uint32_t wave_lower_bound(const T* __restrict__ a, uint32_t n,
 // LDS holds (a state where most particles move, only under SPH_RESORT=2) counts them against the whole list instead:
 // slow, same result. Also zeroes the next step's mover counter.
 constexpr int MV_RANK_GRID = 256;   // workgroups at most; one per CU
-constexpr int MV_RANK_U = 16;       // movers per lane per streaming round
+constexpr int RK_U = 8;             // movers per lane per streaming round
 constexpr int MV_RK_CAP = 4096;     // dest entries staged per workgroup (a power of two)
 constexpr int MV_RX_CAP = 8192;     // slot entries staged per workgroup (a power of two; 112 KB of LDS in all)
 
+template <int BLK>
 __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
@@ -149,7 +150,7 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
     __syncthreads();
     uint32_t t = 0;
 #pragma unroll
-    for (int k = 0; k < MV_BLK / 64; ++k) t += red[k];
+    for (int k = 0; k < BLK / 64; ++k) t += red[k];
     return t;
 }
 
@@ -158,89 +159,75 @@ static __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int j) {
     return (uint64_t)hi << 32 | lo;
 }
 
-// Sorts a[0, len) ascending in LDS (bitonic over the next power of two, padded with ~0; the keys are distinct), with
-// the payload b (if any) moved along. Every thread of the workgroup calls it; it ends on a barrier. Up to 64 entries
-// (a workgroup's usual share of the movers) wave 0 sorts them in registers, exchanging by shuffles: no workgroup
-// barrier per stage.
-__device__ void lds_sort(uint64_t* a, uint32_t* b, uint32_t len) {
-    if (len <= 64) {   // block-uniform
-        if (threadIdx.x < 64) {
-            const uint32_t l = threadIdx.x;
-            uint64_t v = l < len ? a[l] : ~0ull;
-            uint32_t pb = (b && l < len) ? b[l] : 0u;
-#pragma unroll
-            for (uint32_t k = 2; k <= 64; k <<= 1)
-#pragma unroll
-                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                    const uint64_t o = shfl_xor64(v, (int)j);
-                    const uint32_t ob = (uint32_t)__shfl_xor((int)pb, (int)j, 64);
-                    // the pair's lower lane keeps the smaller key in an ascending block, the larger in a descending one
-                    const bool take = ((l & j) == 0) == ((l & k) == 0) ? o < v : o > v;
-                    if (take) {
-                        v = o;
-                        pb = ob;
-                    }
+// The rank kernel's workgroup: 16 waves, so a crowded range's sorts and entries spread over 1024 lanes.
+constexpr int RK_BLK = 1024;
+
+// Bitonic steps (k, j) for k = k0 .. k1 and j = min(k / 2, 32) .. 1, i.e. the ones whose partners lie in the same
+// 64-entry block, in registers: each wave takes whole blocks and exchanges by shuffles.
+__device__ void bitonic_regs(uint64_t* a, uint32_t* b, uint32_t P, uint32_t k0, uint32_t k1) {
+    const uint32_t l = lane_id();
+    for (uint32_t base = (threadIdx.x >> 6) * 64; base < P; base += RK_BLK) {
+        const uint32_t i = base + l;
+        uint64_t v = a[i];
+        uint32_t pb = b ? b[i] : 0u;
+        for (uint32_t k = k0; k <= k1; k <<= 1)
+            for (uint32_t j = min(k >> 1, 32u); j > 0; j >>= 1) {
+                const uint64_t o = shfl_xor64(v, (int)j);
+                const uint32_t ob = (uint32_t)__shfl_xor((int)pb, (int)j, 64);
+                // the pair's lower entry keeps the smaller key in an ascending run, the larger in a descending one
+                const bool take = ((i & j) == 0) == ((i & k) == 0) ? o < v : o > v;
+                if (take) {
+                    v = o;
+                    pb = ob;
                 }
-            if (l < len) {
-                a[l] = v;
-                if (b) b[l] = pb;
             }
-        }
+        a[i] = v;
+        if (b) b[i] = pb;
+    }
+}
+
+// Sorts a[0, len) ascending in LDS, the payload b (if any) moved along; the keys are distinct; the arrays hold the
+// next power of two >= max(len, 64) entries. Bitonic: the steps with partners 64 or more entries apart go through LDS
+// (one pair per lane, a barrier each), all shorter ones in registers (bitonic_regs), so a sort of 2048 entries takes
+// 26 barriers instead of 66 (a crowded range mid-collapse holds ~1,600 entries: r5 measured 20 us for the kernel with
+// the plain LDS form at 256 lanes). Every thread of the workgroup calls it; it ends on a barrier.
+__device__ void lds_sort(uint64_t* a, uint32_t* b, uint32_t len) {
+    if (len <= 1) {
         __syncthreads();
         return;
     }
-    uint32_t P = 1;
+    uint32_t P = 64;
     while (P < len) P <<= 1;
-    for (uint32_t t = len + threadIdx.x; t < P; t += MV_BLK) a[t] = ~0ull;
+    for (uint32_t t = len + threadIdx.x; t < P; t += RK_BLK) {
+        a[t] = ~0ull;
+        if (b) b[t] = 0u;
+    }
     __syncthreads();
-    for (uint32_t k = 2; k <= P; k <<= 1)
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t t = threadIdx.x; t < P; t += MV_BLK) {
-                const uint32_t u = t ^ j;
-                if (u > t) {
-                    const uint64_t x = a[t], y = a[u];
-                    if ((x > y) == ((t & k) == 0)) {
-                        a[t] = y;
-                        a[u] = x;
-                        if (b) {
-                            const uint32_t bt = b[t];
-                            b[t] = b[u];
-                            b[u] = bt;
-                        }
+    bitonic_regs(a, b, P, 2, 64);
+    __syncthreads();
+    for (uint32_t k = 128; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j >= 64; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < P / 2; t += RK_BLK) {
+                const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), u = i | j;   // pair t: i < u = i + j
+                const uint64_t x = a[i], y = a[u];
+                if ((x > y) == ((i & k) == 0)) {
+                    a[i] = y;
+                    a[u] = x;
+                    if (b) {
+                        const uint32_t bi = b[i];
+                        b[i] = b[u];
+                        b[u] = bi;
                     }
                 }
             }
             __syncthreads();
         }
-}
-
-// In-place inclusive prefix sum of v[0, len) in LDS by the workgroup (red: MV_BLK / 64 words); ends on a barrier.
-__device__ void lds_scan(uint32_t* v, uint32_t len, uint32_t* red) {
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < len; base += MV_BLK) {
-        const uint32_t t = base + threadIdx.x;
-        uint32_t inc = t < len ? v[t] : 0u;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
-            if (lane_id() >= (uint32_t)o) inc += u;
-        }
+        bitonic_regs(a, b, P, k, k);
         __syncthreads();
-        if (lane_id() == 63) red[threadIdx.x >> 6] = inc;
-        __syncthreads();
-        uint32_t pre = carry, tot = 0;
-#pragma unroll
-        for (int k = 0; k < MV_BLK / 64; ++k) {
-            pre += k < (int)(threadIdx.x >> 6) ? red[k] : 0u;
-            tot += red[k];
-        }
-        if (t < len) v[t] = pre + inc;
-        carry += tot;
     }
-    __syncthreads();
 }
 
-__global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__ mtotal, uint32_t* __restrict__ next_count,
+__global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__ mtotal, uint32_t* __restrict__ next_count,
                                                     const uint32_t* __restrict__ cs_old, ResortScratch w, AsmSrc src,
                                                     int32_t n, float4* __restrict__ pos_o, float4* __restrict__ vel_o,
                                                     int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o,
@@ -248,7 +235,7 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
     __shared__ uint64_t dk[MV_RK_CAP];   // dest entries (new key, slot), sorted in place
     __shared__ uint32_t dr[MV_RK_CAP];   // their mover index (moves with the sort)
     __shared__ uint64_t sxk[MV_RX_CAP];  // slot entries (slot, mover index) in [xa, x1), sorted
-    __shared__ uint32_t cnt[2], red[MV_BLK / 64];
+    __shared__ uint32_t cnt[2], red[RK_BLK / 64];
     resolve_sizes(src, w, n);
     if (threadIdx.x < 2) cnt[threadIdx.x] = 0u;
     const uint32_t m = *mtotal, G = gridDim.x, b = blockIdx.x;
@@ -267,11 +254,11 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
     const uint32_t kd1 = b == G - 1 ? 0xffffffffu : (x1 < (uint32_t)n ? sk1 : 0xffffffffu);
     // The kernel is a chain of dependent memory round trips (~1-2 us each at this occupancy): the code keeps them few.
     // Round 0 of the mover stream issues together with the load of xa.
-    uint32_t xs[MV_RANK_U], ks[MV_RANK_U];
+    uint32_t xs[RK_U], ks[RK_U];
     auto load_round = [&](uint32_t base) __attribute__((always_inline)) {
 #pragma unroll
-        for (int u = 0; u < MV_RANK_U; ++u) {   // every load of the round issues before any is used
-            const uint32_t r = min(base + u * MV_BLK + threadIdx.x, m - 1u);
+        for (int u = 0; u < RK_U; ++u) {   // every load of the round issues before any is used
+            const uint32_t r = min(base + u * RK_BLK + threadIdx.x, m - 1u);
             xs[u] = w.mi[r];
             ks[u] = w.mk[r];
         }
@@ -281,10 +268,10 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
     const uint32_t xa = b == 0 || kd0 == 0xffffffffu ? 0u : min(cs_old[kd0], x0);
     __syncthreads();
     uint32_t below_k = 0, below_xa = 0;
-    for (uint32_t base = 0; base < m; base += MV_BLK * MV_RANK_U) {
+    for (uint32_t base = 0; base < m; base += RK_BLK * RK_U) {
 #pragma unroll
-        for (int u = 0; u < MV_RANK_U; ++u) {
-            const uint32_t r = base + u * MV_BLK + threadIdx.x;
+        for (int u = 0; u < RK_U; ++u) {
+            const uint32_t r = base + u * RK_BLK + threadIdx.x;
             const bool ok = r < m;
             const uint32_t x = mv_slot(w, xs[u]), k = ks[u];
             below_k += ok && k < kd0 ? 1u : 0u;
@@ -298,10 +285,10 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
                 if (p < MV_RX_CAP) sxk[p] = (uint64_t)x << 32 | r;
             }
         }
-        if (base + MV_BLK * MV_RANK_U < m) load_round(base + MV_BLK * MV_RANK_U);
+        if (base + RK_BLK * RK_U < m) load_round(base + RK_BLK * RK_U);
     }
-    below_k = block_sum(below_k, red);   // (its barriers also publish the staged entries and counts)
-    below_xa = block_sum(below_xa, red);
+    below_k = block_sum<RK_BLK>(below_k, red);   // (its barriers also publish the staged entries and counts)
+    below_xa = block_sum<RK_BLK>(below_xa, red);
     const uint32_t nd = cnt[0], ns = cnt[1];
     const bool slots_staged = ns <= MV_RX_CAP, dest_staged = nd <= MV_RK_CAP;   // block-uniform
     auto slots_below = [&](uint32_t y) {   // #movers with slot in [xa, y), y in [xa, x1]: from the sorted slot entries
@@ -350,7 +337,7 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
     if (slots_staged && dest_staged) {
         // one pass over both kinds of entry, every global load of an entry issued before its stores
         const uint32_t s0 = slots_below(x0), nsrc = ns - s0;
-        for (uint32_t t = threadIdx.x; t < max(nsrc, nd); t += MV_BLK) {
+        for (uint32_t t = threadIdx.x; t < max(nsrc, nd); t += RK_BLK) {
             const bool hs = t < nsrc, hd = t < nd;
             const uint64_t se = hs ? sxk[s0 + t] : 0ull;
             const uint64_t c = hd ? dk[t] : 0ull;
@@ -376,10 +363,10 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
     // counted against the whole list instead, slow, same result
     if (slots_staged) {
         const uint32_t s0 = slots_below(x0);
-        for (uint32_t e = s0 + threadIdx.x; e < ns; e += MV_BLK)
+        for (uint32_t e = s0 + threadIdx.x; e < ns; e += RK_BLK)
             source((uint32_t)(sxk[e] >> 32), below_xa + e, w.mo[(uint32_t)sxk[e]]);
     } else {
-        for (uint32_t r = threadIdx.x; r < m; r += MV_BLK) {
+        for (uint32_t r = threadIdx.x; r < m; r += RK_BLK) {
             const uint32_t x = mv_slot(w, w.mi[r]);
             if (x >= x0 && x < x1) source(x, count_below(x), w.mo[r]);
         }
@@ -393,9 +380,9 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
         place(c, rk, q, aq_of(q), p, v, pid, load_extra(ex, x));
     };
     if (dest_staged) {
-        for (uint32_t e = threadIdx.x; e < nd; e += MV_BLK) place_entry(dk[e], below_k + e);
+        for (uint32_t e = threadIdx.x; e < nd; e += RK_BLK) place_entry(dk[e], below_k + e);
     } else {
-        for (uint32_t r = threadIdx.x; r < m; r += MV_BLK) {
+        for (uint32_t r = threadIdx.x; r < m; r += RK_BLK) {
             const uint32_t k = w.mk[r];
             if (!(k >= kd0 && k < kd1)) continue;
             const uint64_t c = comp(k, mv_slot(w, w.mi[r]));
@@ -409,10 +396,10 @@ __global__ __launch_bounds__(MV_BLK) void k_mv_rank(const uint32_t* __restrict__
     }
 }
 
-// cs[k] += #{movers: new key < k} − #{movers: old key < k}, for k in [0, ncells]; 4096 cells per
+// cs[k] += #{movers: new key < k} − #{movers: old key < k}, for k in [0, ncells]; 1024 cells per
 // workgroup. A workgroup whose counts agree at its start and that holds no mover key leaves its cells.
 // Runs as extra workgroups of k_mv_merge (it needs only k_mv_rank's tables), beside the scatter.
-constexpr int MV_CS_PER = 16;
+constexpr int MV_CS_PER = 4;
 constexpr int MV_CS_CELLS = MV_CS_PER * MV_BLK;
 // movers staged in LDS for the merge's binary searches (a workgroup's cells or slots rarely hold more)
 constexpr uint32_t MV_LDS = 1024;
@@ -458,10 +445,8 @@ static __device__ void mv_cell_start(uint32_t* __restrict__ cs, uint32_t ncells,
     }
 }
 
-// Slots per merge workgroup: MV_MERGE_PER per thread. The merge is a chain of dependent round trips (the searches,
-// the staging, the scatter) more than a stream: a workgroup of 4 x 256 slots pays the chain once for 4x the slots, and
-// its 1024 workgroups at C3 are resident at once (256-slot workgroups ran the chain twice over: 22.6 us mid-collapse).
-constexpr int MV_MERGE_PER = 4;
+// Slots per merge workgroup: MV_MERGE_PER per thread (4 per thread: 30.7 us mid-collapse against 22.6 for 1, r5).
+constexpr int MV_MERGE_PER = 1;
 constexpr int MV_MERGE_SLOTS = MV_BLK * MV_MERGE_PER;
 
 __global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
@@ -683,7 +668,7 @@ void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const u
     const int32_t nb = (n + MV_MERGE_SLOTS - 1) / MV_MERGE_SLOTS;
     const int32_t nb_rank = (n + MV_BLK - 1) / MV_BLK;
     // n is an upper bound of the slots on device-sized steps: the rank kernel's ranges split the device count
-    SPH_LAUNCH(k_mv_rank, std::min(MV_RANK_GRID, nb_rank), MV_BLK, 0, s, count, count_other, cs, w, src, n, pos_o, vel_o, id_o,
+    SPH_LAUNCH(k_mv_rank, std::min(MV_RANK_GRID, nb_rank), RK_BLK, 0, s, count, count_other, cs, w, src, n, pos_o, vel_o, id_o,
                sk_o, ex);
     // the stayers' scatter and the cell-start update (after k_mv_rank, the last reader of cs_old)
     const int32_t ncs = (int32_t)((ncells + MV_CS_CELLS) / MV_CS_CELLS);
