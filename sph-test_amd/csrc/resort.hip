@@ -131,15 +131,17 @@ static __device__ uint32_t wave_lower_bound(const T* __restrict__ a, uint32_t n,
 // and for its dest entries the insertion slot q = clamp(x, cs_old[k], cs_old[k + 1]) and A(q) = #{y : y < q}. Every
 // such q lies in [xa, x1] with xa = cs_old[kd0] <= x0 (the start of the cell holding slot x0), so the stream also
 // stages the movers with a slot in [xa, x1) (the source entries are their suffix from x0) and counts those below xa:
-// A(q) is that count plus a binary search in the sorted slots, with no second pass over the mover list (r5: a second
-// stream's dependent loads took the kernel from ~5 to ~32 us). The mover is then scattered to dst = (q − A(q)) + rk
+// A(q) is that count plus the rank of q among the staged slots, read from a presence bitmap of [xa, x1) and its word
+// prefix (the slots are distinct, so they need no sort; ranges too long for the bitmap sort them instead), with no
+// second pass over the mover list (r5: a second stream's dependent loads took the kernel from ~5 to ~32 us). The mover is then scattered to dst = (q − A(q)) + rk
 // here, so the merge that follows reads only the tables (it updates cs_old in place). A range with more entries than
 // LDS holds (a state where most particles move, only under SPH_RESORT=2) counts them against the whole list instead:
 // slow, same result. Also zeroes the next step's mover counter.
 constexpr int MV_RANK_GRID = 256;   // workgroups at most; one per CU
 constexpr int RK_U = 8;             // movers per lane per streaming round
 constexpr int MV_RK_CAP = 4096;     // dest entries staged per workgroup (a power of two)
-constexpr int MV_RX_CAP = 8192;     // slot entries staged per workgroup (a power of two; 112 KB of LDS in all)
+constexpr int MV_RX_CAP = 4096;     // slot entries staged per workgroup (a power of two)
+constexpr int RK_BM_WORDS = 2048;   // slot-presence bitmap over [xa, x1): ranges up to 65,536 slots (~100 KB of LDS in all)
 
 template <int BLK>
 __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
@@ -234,10 +236,12 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
                                                     ResortExtra ex) {
     __shared__ uint64_t dk[MV_RK_CAP];   // dest entries (new key, slot), sorted in place
     __shared__ uint32_t dr[MV_RK_CAP];   // their mover index (moves with the sort)
-    __shared__ uint64_t sxk[MV_RX_CAP];  // slot entries (slot, mover index) in [xa, x1), sorted
+    __shared__ uint64_t sxk[MV_RX_CAP];  // slot entries (slot, mover index) in [xa, x1)
+    __shared__ uint32_t bm[RK_BM_WORDS + 1], bpre[RK_BM_WORDS + 1];   // their slots' presence bits, word prefix
     __shared__ uint32_t cnt[2], red[RK_BLK / 64];
     resolve_sizes(src, w, n);
     if (threadIdx.x < 2) cnt[threadIdx.x] = 0u;
+    for (uint32_t t = threadIdx.x; t <= (uint32_t)RK_BM_WORDS; t += RK_BLK) bm[t] = 0u;
     const uint32_t m = *mtotal, G = gridDim.x, b = blockIdx.x;
     if (b == 0 && threadIdx.x == 0) {
         *next_count = 0u;
@@ -283,6 +287,7 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
             if (ok && x >= xa && x < x1) {
                 const uint32_t p = atomicAdd(&cnt[1], 1u);
                 if (p < MV_RX_CAP) sxk[p] = (uint64_t)x << 32 | r;
+                if (x - xa < 32u * RK_BM_WORDS) atomicOr(&bm[(x - xa) >> 5], 1u << ((x - xa) & 31u));
             }
         }
         if (base + RK_BLK * RK_U < m) load_round(base + RK_BLK * RK_U);
@@ -291,8 +296,34 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
     below_xa = block_sum<RK_BLK>(below_xa, red);
     const uint32_t nd = cnt[0], ns = cnt[1];
     const bool slots_staged = ns <= MV_RX_CAP, dest_staged = nd <= MV_RK_CAP;   // block-uniform
-    auto slots_below = [&](uint32_t y) {   // #movers with slot in [xa, y), y in [xa, x1]: from the sorted slot entries
-        uint32_t lo = 0, hi = ns;
+    // slot ranks by the presence bitmap (the slots are distinct): rank(y) = #{staged slots < y}, y in [xa, x1]
+    const bool bitmap = slots_staged && x1 - xa <= 32u * RK_BM_WORDS;
+    if (bitmap) {
+        const uint32_t nw = (x1 - xa + 31u) >> 5, w0 = 2 * threadIdx.x;   // two words per lane
+        const uint32_t c0 = w0 < nw ? (uint32_t)__popc(bm[w0]) : 0u, c1 = w0 + 1 < nw ? (uint32_t)__popc(bm[w0 + 1]) : 0u;
+        uint32_t inc = c0 + c1;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
+            if (lane_id() >= (uint32_t)o) inc += u;
+        }
+        __syncthreads();   // block_sum's last reads of red
+        if (lane_id() == 63) red[threadIdx.x >> 6] = inc;
+        __syncthreads();
+        uint32_t pre = 0;
+        for (uint32_t k = 0; k < (threadIdx.x >> 6); ++k) pre += red[k];
+        const uint32_t ex0 = pre + inc - c0 - c1;
+        if (w0 <= nw) bpre[w0] = ex0;
+        if (w0 + 1 <= nw) bpre[w0 + 1] = ex0 + c0;
+        if (nw == (uint32_t)RK_BM_WORDS && threadIdx.x == RK_BLK - 1) bpre[RK_BM_WORDS] = pre + inc;
+        __syncthreads();
+    }
+    auto slots_below = [&](uint32_t y) {   // #movers with slot in [xa, y), y in [xa, x1]
+        if (bitmap) {
+            const uint32_t d = min(y, x1) - xa, wd = d >> 5;
+            return bpre[wd] + (uint32_t)__popc(bm[wd] & ((1u << (d & 31u)) - 1u));
+        }
+        uint32_t lo = 0, hi = ns;   // the sorted slot entries
         while (lo < hi) {
             const uint32_t mid = (lo + hi) >> 1;
             if ((uint32_t)(sxk[mid] >> 32) < y) lo = mid + 1;
@@ -332,14 +363,16 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
         store_extra(ex, e, dst);
     };
     auto ins = [&](uint32_t k, uint32_t x, uint32_t c0, uint32_t c1) { return x < c0 ? c0 : (x > c1 ? c1 : x); };
-    if (slots_staged) lds_sort(sxk, nullptr, ns);
+    if (slots_staged && !bitmap) lds_sort(sxk, nullptr, ns);
     if (dest_staged) lds_sort(dk, dr, nd);   // position e: rank below_k + e
     if (slots_staged && dest_staged) {
-        // one pass over both kinds of entry, every global load of an entry issued before its stores
-        const uint32_t s0 = slots_below(x0), nsrc = ns - s0;
+        // one pass over both kinds of entry, every global load of an entry issued before its stores; the source
+        // entries are the slot entries from x0 on (staged order with the bitmap, sorted without)
+        const uint32_t s0 = bitmap ? 0u : slots_below(x0), nsrc = ns - s0;
         for (uint32_t t = threadIdx.x; t < max(nsrc, nd); t += RK_BLK) {
-            const bool hs = t < nsrc, hd = t < nd;
-            const uint64_t se = hs ? sxk[s0 + t] : 0ull;
+            const uint64_t se0 = t < nsrc ? sxk[s0 + t] : 0ull;
+            const bool hs = t < nsrc && (uint32_t)(se0 >> 32) >= x0, hd = t < nd;
+            const uint64_t se = hs ? se0 : 0ull;
             const uint64_t c = hd ? dk[t] : 0ull;
             const uint32_t k = (uint32_t)(c >> 32), x = (uint32_t)c;
             const uint32_t mo = hs ? w.mo[(uint32_t)se] : 0u;
@@ -351,7 +384,7 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
                 asm_load(src, (int32_t)x, p, v, pid);
                 e = load_extra(ex, x);
             }
-            if (hs) source((uint32_t)(se >> 32), below_xa + s0 + t, mo);
+            if (hs) source((uint32_t)(se >> 32), below_xa + (bitmap ? slots_below((uint32_t)(se >> 32)) : s0 + t), mo);
             if (hd) {
                 const uint32_t q = ins(k, x, c0, c1);
                 place(c, below_k + t, q, aq_of(q), p, v, pid, e);
@@ -362,9 +395,11 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
     // more entries than LDS holds (a state where most particles move, only under SPH_RESORT=2): the overflowing kind
     // counted against the whole list instead, slow, same result
     if (slots_staged) {
-        const uint32_t s0 = slots_below(x0);
-        for (uint32_t e = s0 + threadIdx.x; e < ns; e += RK_BLK)
-            source((uint32_t)(sxk[e] >> 32), below_xa + e, w.mo[(uint32_t)sxk[e]]);
+        const uint32_t s0 = bitmap ? 0u : slots_below(x0);
+        for (uint32_t e = s0 + threadIdx.x; e < ns; e += RK_BLK) {
+            const uint32_t x = (uint32_t)(sxk[e] >> 32);
+            if (x >= x0) source(x, below_xa + (bitmap ? slots_below(x) : e), w.mo[(uint32_t)sxk[e]]);
+        }
     } else {
         for (uint32_t r = threadIdx.x; r < m; r += RK_BLK) {
             const uint32_t x = mv_slot(w, w.mi[r]);
