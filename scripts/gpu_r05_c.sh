@@ -12,4 +12,5 @@ timeout -k 10 200 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$O/mid" -o run -
 echo "mid trace rc=$rc"; grep -v amdgpu.ids $O/mid.log; [ $rc -ne 0 ] && exit $rc
 f=$(find $O/mid -name "*kernel_trace.csv" | head -1)
 python3 scripts/trace_window.py "$f" 200 k_density_tiled
+timeout -k 10 300 python scripts/rank_probe.py --steps 4 > $O/probe.log 2>&1; echo "probe rc=$?"; grep -v amdgpu.ids $O/probe.log | cut -c1-400
 exit 0

@@ -124,24 +124,42 @@ static __device__ uint32_t wave_lower_bound(const T* __restrict__ a, uint32_t n,
 // [kd0, kd1) = [sk(x0), sk(x1)) (the old sorted keys at those slots, so every workgroup's key range holds about n/G
 // particles and ~m/G movers; the ranges partition all keys, sentinels included). Its dest entries are the movers
 // with a new key in its range, its source entries those with a slot in its range. One stream over the whole mover
-// list (U per lane in flight) stages both in LDS and counts the movers below the ranges (xa below); then, each set sorted in
-// LDS (bitonic: the movers crowd into a few ranges mid-collapse, where counting ranks pairwise cost O(entries²)),
-//   rk(x) = #{y : k_y < kd0} + (x's position among the sorted dest entries)   -> ms[rk] = (k, x)
-//   ri(x) = #{y : y < xa} + (x's position among the sorted slot entries)      -> mx[ri] = x, mos[ri] = old key
+// list (U per lane in flight) stages both in LDS and counts the movers below the ranges; then
+//   rk(x) = #{y : k_y < kd0} + #{dest entries (k', y) < (k, x)}               -> ms[rk] = (k, x)
+//   ri(x) = #{y : y < x}                                                      -> mx[ri] = x, mos[ri] = old key
 // and for its dest entries the insertion slot q = clamp(x, cs_old[k], cs_old[k + 1]) and A(q) = #{y : y < q}. Every
-// such q lies in [xa, x1] with xa = cs_old[kd0] <= x0 (the start of the cell holding slot x0), so the stream also
-// stages the movers with a slot in [xa, x1) (the source entries are their suffix from x0) and counts those below xa:
-// A(q) is that count plus the rank of q among the staged slots, read from a presence bitmap of [xa, x1) and its word
-// prefix (the slots are distinct, so they need no sort; ranges too long for the bitmap sort them instead), with no
-// second pass over the mover list (r5: a second stream's dependent loads took the kernel from ~5 to ~32 us). The mover is then scattered to dst = (q − A(q)) + rk
-// here, so the merge that follows reads only the tables (it updates cs_old in place). A range with more entries than
-// LDS holds (a state where most particles move, only under SPH_RESORT=2) counts them against the whole list instead:
-// slow, same result. Also zeroes the next step's mover counter.
+// such q lies in [cs_old[kd0], x1], and cs_old[kd0] (the start of the cell holding slot x0) lies within RK_WIN below
+// x0 but in cells of more than RK_WIN particles, so the stream also stages the movers with a slot in
+// [xw, x1) = [x0 − RK_WIN, x1) into a presence bitmap and counts those below x0: a slot rank or A(q) is that count
+// plus (or minus) the staged slots between x0 and the slot, read from the bitmap's word prefix (the slots are
+// distinct, so they need no sort), with no second pass over the mover list (r5: a second stream's dependent loads
+// took the kernel from ~5 to ~32 us). The dest entries are ranked by counting (LDS broadcast reads) up to RK_COUNT of
+// them, by sorting beyond. The mover is then scattered to dst = (q − A(q)) + rk here, so the merge that follows
+// reads only the tables (it updates cs_old in place). A range with more entries than LDS holds (a state where most
+// particles move, only under SPH_RESORT=2) counts them against the whole list instead: slow, same result. Also zeroes
+// the next step's mover counter. Per workgroup the kernel is a chain of memory round trips (~1.5 us each; the probe
+// build, scripts/rank_probe.py): one before the stream (count, range keys and the first movers together), one for
+// the entries' loads.
 constexpr int MV_RANK_GRID = 256;   // workgroups at most; one per CU
 constexpr int RK_U = 8;             // movers per lane per streaming round
 constexpr int MV_RK_CAP = 4096;     // dest entries staged per workgroup (a power of two)
 constexpr int MV_RX_CAP = 4096;     // slot entries staged per workgroup (a power of two)
-constexpr int RK_BM_WORDS = 2048;   // slot-presence bitmap over [xa, x1): ranges up to 65,536 slots (~100 KB of LDS in all)
+constexpr int RK_BM_WORDS = 2048;   // slot-presence bitmap over [xw, x1): ranges up to 65,536 slots (~100 KB of LDS in all)
+constexpr int RK_WIN = 2048;        // slot entries staged below x0 (covers the cell holding x0)
+constexpr int RK_COUNT = 256;       // dest entries ranked by counting, more by sorting
+// Test-only timing probe (scripts/rank_probe.py, a -DSPH_RANK_PROBE build): per workgroup the wall clock at its start,
+// after the mover stream, after the sorts and at its end, with its entry counts.
+#ifdef SPH_RANK_PROBE
+__device__ uint64_t g_rank_probe[MV_RANK_GRID * 8];
+#define RK_PROBE(slot, val)                                                          \
+    do {                                                                             \
+        if (threadIdx.x == 0) g_rank_probe[blockIdx.x * 8 + (slot)] = (uint64_t)(val); \
+    } while (0)
+#else
+#define RK_PROBE(slot, val) \
+    do {                    \
+    } while (0)
+#endif
 
 template <int BLK>
 __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
@@ -234,44 +252,48 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
                                                     int32_t n, float4* __restrict__ pos_o, float4* __restrict__ vel_o,
                                                     int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o,
                                                     ResortExtra ex) {
-    __shared__ uint64_t dk[MV_RK_CAP];   // dest entries (new key, slot), sorted in place
-    __shared__ uint32_t dr[MV_RK_CAP];   // their mover index (moves with the sort)
-    __shared__ uint64_t sxk[MV_RX_CAP];  // slot entries (slot, mover index) in [xa, x1)
+    __shared__ uint64_t dk[MV_RK_CAP];   // dest entries (new key, slot)
+    __shared__ uint32_t dr[MV_RK_CAP];   // their mover index
+    __shared__ uint64_t sxk[MV_RX_CAP];  // slot entries (slot, mover index) in [xw, x1)
     __shared__ uint32_t bm[RK_BM_WORDS + 1], bpre[RK_BM_WORDS + 1];   // their slots' presence bits, word prefix
     __shared__ uint32_t cnt[2], red[RK_BLK / 64];
+    RK_PROBE(0, wall_clock64());
     resolve_sizes(src, w, n);
     if (threadIdx.x < 2) cnt[threadIdx.x] = 0u;
     for (uint32_t t = threadIdx.x; t <= (uint32_t)RK_BM_WORDS; t += RK_BLK) bm[t] = 0u;
-    const uint32_t m = *mtotal, G = gridDim.x, b = blockIdx.x;
-    if (b == 0 && threadIdx.x == 0) {
-        *next_count = 0u;
-        if (w.host_count) *w.host_count = m;   // for the host's next sort choices (no copy launch)
-    }
+    const uint32_t G = gridDim.x, b = blockIdx.x;
     const uint32_t x0 = (uint32_t)((uint64_t)(uint32_t)n * b / G), x1 = (uint32_t)((uint64_t)(uint32_t)n * (b + 1) / G);
-    // both range keys in one round trip (pointer selects, unconditional loads)
+    // Everything the stream needs in one round trip (the kernel is a chain of dependent round trips of ~1.5 us each,
+    // r5 probe): the mover count, both range keys (pointer selects) and the first round of movers, whose loads are
+    // clamped to the lists' capacity rather than to the count they would otherwise wait for.
     auto sk_ptr = [&](uint32_t x) {
         const int32_t xi = (int32_t)min(x, (uint32_t)max(n - 1, 0));
         return asm_rec(src, xi) ? src.skr + xi : src.sk + (xi + src.o_off);
     };
-    const uint32_t sk0 = *sk_ptr(x0), sk1 = *sk_ptr(x1);
-    const uint32_t kd0 = b == 0 ? 0u : (x0 < (uint32_t)n ? sk0 : 0xffffffffu);
-    const uint32_t kd1 = b == G - 1 ? 0xffffffffu : (x1 < (uint32_t)n ? sk1 : 0xffffffffu);
-    // The kernel is a chain of dependent memory round trips (~1-2 us each at this occupancy): the code keeps them few.
-    // Round 0 of the mover stream issues together with the load of xa.
     uint32_t xs[RK_U], ks[RK_U];
-    auto load_round = [&](uint32_t base) __attribute__((always_inline)) {
+    auto load_round = [&](uint32_t base, uint32_t last) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < RK_U; ++u) {   // every load of the round issues before any is used
-            const uint32_t r = min(base + u * RK_BLK + threadIdx.x, m - 1u);
+            const uint32_t r = min(base + u * RK_BLK + threadIdx.x, last);
             xs[u] = w.mi[r];
             ks[u] = w.mk[r];
         }
     };
-    if (m) load_round(0);
-    // every insertion slot of a dest entry lies in [xa, x1]: q >= cs_old[kd0] = xa, q <= cs_old[kd1] <= x1
-    const uint32_t xa = b == 0 || kd0 == 0xffffffffu ? 0u : min(cs_old[kd0], x0);
+    load_round(0, w.cap - 1u);
+    const uint32_t m = *mtotal;
+    const uint32_t sk0 = *sk_ptr(x0), sk1 = *sk_ptr(x1);
+    if (b == 0 && threadIdx.x == 0) {
+        *next_count = 0u;
+        if (w.host_count) *w.host_count = m;   // for the host's next sort choices (no copy launch)
+    }
+    const uint32_t kd0 = b == 0 ? 0u : (x0 < (uint32_t)n ? sk0 : 0xffffffffu);
+    const uint32_t kd1 = b == G - 1 ? 0xffffffffu : (x1 < (uint32_t)n ? sk1 : 0xffffffffu);
+    // Slot entries are staged from xw = x0 − RK_WIN: every insertion slot q of a dest entry lies in [cs_old[kd0], x1],
+    // and cs_old[kd0] (the start of the cell holding slot x0) is at most RK_WIN below x0 except in cells of more than
+    // RK_WIN particles; such an entry counts its A(q) against the whole list instead.
+    const uint32_t xw = x0 > (uint32_t)RK_WIN ? x0 - (uint32_t)RK_WIN : 0u;
     __syncthreads();
-    uint32_t below_k = 0, below_xa = 0;
+    uint32_t below_k = 0, below_x0 = 0;
     for (uint32_t base = 0; base < m; base += RK_BLK * RK_U) {
 #pragma unroll
         for (int u = 0; u < RK_U; ++u) {
@@ -279,27 +301,30 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
             const bool ok = r < m;
             const uint32_t x = mv_slot(w, xs[u]), k = ks[u];
             below_k += ok && k < kd0 ? 1u : 0u;
-            below_xa += ok && x < xa ? 1u : 0u;
+            below_x0 += ok && x < x0 ? 1u : 0u;
             if (ok && k >= kd0 && k < kd1) {
                 const uint32_t p = atomicAdd(&cnt[0], 1u);
                 if (p < MV_RK_CAP) { dk[p] = comp(k, x); dr[p] = r; }
             }
-            if (ok && x >= xa && x < x1) {
+            if (ok && x >= xw && x < x1) {
                 const uint32_t p = atomicAdd(&cnt[1], 1u);
                 if (p < MV_RX_CAP) sxk[p] = (uint64_t)x << 32 | r;
-                if (x - xa < 32u * RK_BM_WORDS) atomicOr(&bm[(x - xa) >> 5], 1u << ((x - xa) & 31u));
+                if (x - xw < 32u * RK_BM_WORDS) atomicOr(&bm[(x - xw) >> 5], 1u << ((x - xw) & 31u));
             }
         }
-        if (base + RK_BLK * RK_U < m) load_round(base + RK_BLK * RK_U);
+        if (base + RK_BLK * RK_U < m) load_round(base + RK_BLK * RK_U, m - 1u);
     }
     below_k = block_sum<RK_BLK>(below_k, red);   // (its barriers also publish the staged entries and counts)
-    below_xa = block_sum<RK_BLK>(below_xa, red);
+    below_x0 = block_sum<RK_BLK>(below_x0, red);
     const uint32_t nd = cnt[0], ns = cnt[1];
-    const bool slots_staged = ns <= MV_RX_CAP, dest_staged = nd <= MV_RK_CAP;   // block-uniform
-    // slot ranks by the presence bitmap (the slots are distinct): rank(y) = #{staged slots < y}, y in [xa, x1]
-    const bool bitmap = slots_staged && x1 - xa <= 32u * RK_BM_WORDS;
-    if (bitmap) {
-        const uint32_t nw = (x1 - xa + 31u) >> 5, w0 = 2 * threadIdx.x;   // two words per lane
+    // block-uniform: the slot entries fit the list and the bitmap; the dest entries fit the list
+    const bool slots_ok = ns <= MV_RX_CAP && x1 - xw <= 32u * RK_BM_WORDS, dest_staged = nd <= MV_RK_CAP;
+    RK_PROBE(1, wall_clock64());
+    RK_PROBE(4, nd);
+    RK_PROBE(5, ns);
+    RK_PROBE(6, m);
+    if (slots_ok) {   // the bitmap's word prefix
+        const uint32_t nw = (x1 - xw + 31u) >> 5, w0 = 2 * threadIdx.x;   // two words per lane
         const uint32_t c0 = w0 < nw ? (uint32_t)__popc(bm[w0]) : 0u, c1 = w0 + 1 < nw ? (uint32_t)__popc(bm[w0 + 1]) : 0u;
         uint32_t inc = c0 + c1;
 #pragma unroll
@@ -318,25 +343,18 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
         if (nw == (uint32_t)RK_BM_WORDS && threadIdx.x == RK_BLK - 1) bpre[RK_BM_WORDS] = pre + inc;
         __syncthreads();
     }
-    auto slots_below = [&](uint32_t y) {   // #movers with slot in [xa, y), y in [xa, x1]
-        if (bitmap) {
-            const uint32_t d = min(y, x1) - xa, wd = d >> 5;
-            return bpre[wd] + (uint32_t)__popc(bm[wd] & ((1u << (d & 31u)) - 1u));
-        }
-        uint32_t lo = 0, hi = ns;   // the sorted slot entries
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if ((uint32_t)(sxk[mid] >> 32) < y) lo = mid + 1;
-            else hi = mid;
-        }
-        return lo;
+    auto rank_of = [&](uint32_t y) {   // #staged slots in [xw, y), y in [xw, x1]
+        const uint32_t d = min(y, x1) - xw, wd = d >> 5;
+        return bpre[wd] + (uint32_t)__popc(bm[wd] & ((1u << (d & 31u)) - 1u));
     };
     auto count_below = [&](uint32_t y) {   // #movers with slot < y, against the whole list
         uint32_t c = 0;
         for (uint32_t f = 0; f < m; ++f) c += mv_slot(w, w.mi[f]) < y ? 1u : 0u;
         return c;
     };
-    auto aq_of = [&](uint32_t q) { return slots_staged ? below_xa + slots_below(max(q, xa)) : count_below(q); };
+    // #movers with slot < y: below x0 plus the staged slots in [x0, y), or below x0 minus those in [y, x0)
+    const uint32_t r0 = slots_ok ? rank_of(x0) : 0u;
+    auto slots_below = [&](uint32_t y) { return slots_ok && y >= xw ? below_x0 + rank_of(y) - r0 : count_below(y); };
     // source entries (slot in [x0, x1)): ri = #{y : y < x} -> mx[ri] = x, mos[ri] = old key (ascending by slot)
     auto source = [&](uint32_t x, uint32_t ri, uint32_t mo) {
         if (ri >= w.cap) {   // inconsistent tables: flag, never write past them
@@ -347,10 +365,9 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
         w.mos[ri] = mo;
     };
     // dest entries: rank rk, insertion slot q among the stayers, A(q) = #{y : y < q}, placement at (q − A(q)) + rk
-    auto place = [&](uint64_t c, uint32_t rk, uint32_t q, uint32_t aq, float4 p, float4 v, int32_t pid,
-                     const ExtraVals& e) {
+    auto place = [&](uint64_t c, uint32_t rk, uint32_t q, float4 p, float4 v, int32_t pid, const ExtraVals& e) {
         const uint32_t k = (uint32_t)(c >> 32);
-        const uint32_t dst = (q - aq) + rk;
+        const uint32_t dst = (q - slots_below(q)) + rk;
         if (rk >= w.cap || dst >= w.cap) {   // inconsistent tables: flag, never write past them
             if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
             return;
@@ -362,20 +379,21 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
         sk_o[dst] = k;
         store_extra(ex, e, dst);
     };
-    auto ins = [&](uint32_t k, uint32_t x, uint32_t c0, uint32_t c1) { return x < c0 ? c0 : (x > c1 ? c1 : x); };
-    if (slots_staged && !bitmap) lds_sort(sxk, nullptr, ns);
-    if (dest_staged) lds_sort(dk, dr, nd);   // position e: rank below_k + e
-    if (slots_staged && dest_staged) {
-        // one pass over both kinds of entry, every global load of an entry issued before its stores; the source
-        // entries are the slot entries from x0 on (staged order with the bitmap, sorted without)
-        const uint32_t s0 = bitmap ? 0u : slots_below(x0), nsrc = ns - s0;
-        for (uint32_t t = threadIdx.x; t < max(nsrc, nd); t += RK_BLK) {
-            const uint64_t se0 = t < nsrc ? sxk[s0 + t] : 0ull;
-            const bool hs = t < nsrc && (uint32_t)(se0 >> 32) >= x0, hd = t < nd;
-            const uint64_t se = hs ? se0 : 0ull;
+    auto ins = [&](uint32_t x, uint32_t c0, uint32_t c1) { return x < c0 ? c0 : (x > c1 ? c1 : x); };
+    // dest ranks: up to RK_COUNT entries each lane counts the smaller ones (LDS broadcast reads, no barrier stages);
+    // more are sorted (lds_sort) and ranked by position
+    const bool counted = nd <= (uint32_t)RK_COUNT;
+    if (dest_staged && !counted) lds_sort(dk, dr, nd);
+    RK_PROBE(2, wall_clock64());
+    RK_PROBE(7, slots_ok ? 1 : 0);
+    if (slots_ok && dest_staged) {
+        // one pass over both kinds of entry, every global load of an entry issued before its stores
+        for (uint32_t t = threadIdx.x; t < max(ns, nd); t += RK_BLK) {
+            const uint64_t se0 = t < ns ? sxk[t] : 0ull;
+            const bool hs = t < ns && (uint32_t)(se0 >> 32) >= x0, hd = t < nd;
             const uint64_t c = hd ? dk[t] : 0ull;
             const uint32_t k = (uint32_t)(c >> 32), x = (uint32_t)c;
-            const uint32_t mo = hs ? w.mo[(uint32_t)se] : 0u;
+            const uint32_t mo = hs ? w.mo[(uint32_t)se0] : 0u;
             const uint32_t c0 = hd ? cs_old[k] : 0u, c1 = hd ? cs_old[k + 1] : 0u;
             float4 p = make_float4(0.f, 0.f, 0.f, 0.f), v = p;
             int32_t pid = 0;
@@ -384,21 +402,29 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
                 asm_load(src, (int32_t)x, p, v, pid);
                 e = load_extra(ex, x);
             }
-            if (hs) source((uint32_t)(se >> 32), below_xa + (bitmap ? slots_below((uint32_t)(se >> 32)) : s0 + t), mo);
-            if (hd) {
-                const uint32_t q = ins(k, x, c0, c1);
-                place(c, below_k + t, q, aq_of(q), p, v, pid, e);
+            uint32_t lr = t;
+            if (hd && counted) {
+                lr = 0;
+                for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < c ? 1u : 0u;
             }
+            if (hs) {
+                const uint32_t xs0 = (uint32_t)(se0 >> 32);
+                source(xs0, below_x0 + rank_of(xs0) - r0, mo);
+            }
+            if (hd) place(c, below_k + lr, ins(x, c0, c1), p, v, pid, e);
         }
+#ifdef SPH_RANK_PROBE
+        __syncthreads();
+        RK_PROBE(3, wall_clock64());
+#endif
         return;
     }
     // more entries than LDS holds (a state where most particles move, only under SPH_RESORT=2): the overflowing kind
     // counted against the whole list instead, slow, same result
-    if (slots_staged) {
-        const uint32_t s0 = bitmap ? 0u : slots_below(x0);
-        for (uint32_t e = s0 + threadIdx.x; e < ns; e += RK_BLK) {
+    if (slots_ok) {
+        for (uint32_t e = threadIdx.x; e < ns; e += RK_BLK) {
             const uint32_t x = (uint32_t)(sxk[e] >> 32);
-            if (x >= x0) source(x, below_xa + (bitmap ? slots_below(x) : e), w.mo[(uint32_t)sxk[e]]);
+            if (x >= x0) source(x, below_x0 + rank_of(x) - r0, w.mo[(uint32_t)sxk[e]]);
         }
     } else {
         for (uint32_t r = threadIdx.x; r < m; r += RK_BLK) {
@@ -411,11 +437,17 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
         float4 p, v;
         int32_t pid;
         asm_load(src, (int32_t)x, p, v, pid);
-        const uint32_t q = ins(k, x, cs_old[k], cs_old[k + 1]);
-        place(c, rk, q, aq_of(q), p, v, pid, load_extra(ex, x));
+        place(c, rk, ins(x, cs_old[k], cs_old[k + 1]), p, v, pid, load_extra(ex, x));
     };
     if (dest_staged) {
-        for (uint32_t e = threadIdx.x; e < nd; e += RK_BLK) place_entry(dk[e], below_k + e);
+        for (uint32_t e = threadIdx.x; e < nd; e += RK_BLK) {
+            uint32_t lr = e;
+            if (counted) {
+                lr = 0;
+                for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < dk[e] ? 1u : 0u;
+            }
+            place_entry(dk[e], below_k + lr);
+        }
     } else {
         for (uint32_t r = threadIdx.x; r < m; r += RK_BLK) {
             const uint32_t k = w.mk[r];
@@ -695,6 +727,12 @@ void launch_slab_rec(AsmSrc src, int32_t n, GridDesc g, uint32_t key_base, uint3
         k_slab_rec<<<nb_rec + nb_cs, MV_BLK, 0, s>>>(src, n, g, key_base, keyr, skr, sink, sizes ? *sizes : SizesIn{},
                                                      sizes ? 1 : 0, nb_cs ? cs : CsOld{}, nb_rec);
 }
+
+#ifdef SPH_RANK_PROBE
+extern "C" int sph_debug_rank_probe(uint64_t* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rank_probe), sizeof(g_rank_probe)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* count,
                    uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,

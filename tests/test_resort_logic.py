@@ -55,12 +55,12 @@ def test_resort_formulas_match_stable_sort(frac):
         assert np.array_equal(cs_new, np.searchsorted(newk[ref], np.arange(nc + 1), side="left"))
 
 
-def range_ranks(ks, newk, G):
+def range_ranks(ks, newk, G, win=2048):
     """resort.hip k_mv_rank restated: workgroup b owns the old slots [x0, x1) = [b·n/G, (b+1)·n/G) and the new keys
     [ks[x0], ks[x1]) (first range from 0, last to infinity); rk counts the movers below the key range plus those in
-    range with a smaller (key, slot), ri the movers below the slot range plus those in range with a smaller slot.
-    A(q) for a dest entry counts the movers below xa = cs_old[kd0] plus the staged slots in [xa, q): every insertion
-    slot q of the range lies in [xa, x1]."""
+    range with a smaller (key, slot). The slots staged are those in [xw, x1), xw = x0 − win: a source entry's rank is
+    the movers below x0 plus the staged slots in [x0, x); A(q) for a dest entry likewise from x0 (minus the staged
+    slots in [q, x0) when q < x0), or counted against the whole list when q < xw (a cell of more than win slots)."""
     n = len(ks)
     movers = np.nonzero(newk != ks)[0]
     mk = newk[movers]
@@ -73,21 +73,25 @@ def range_ranks(ks, newk, G):
         x0, x1 = n * b // G, n * (b + 1) // G
         kd0 = 0 if b == 0 else (ks[x0] if x0 < n else np.iinfo(np.int64).max)
         kd1 = np.iinfo(np.int64).max if b == G - 1 else (ks[x1] if x1 < n else np.iinfo(np.int64).max)
-        xa = 0 if b == 0 else min(int(cs_old[kd0]), x0)
+        xw = max(x0 - win, 0)
         ind = (mk >= kd0) & (mk < kd1)
         ins = (movers >= x0) & (movers < x1)
-        staged = np.sort(movers[(movers >= xa) & (movers < x1)])
-        below_k, below_xa = int((mk < kd0).sum()), int((movers < xa).sum())
+        staged = np.sort(movers[(movers >= xw) & (movers < x1)])
+        below_k, below_x0 = int((mk < kd0).sum()), int((movers < x0).sum())
+        r0 = int(np.searchsorted(staged, x0, side="left"))
         c = _comp(mk, movers)
         for e in np.nonzero(ind)[0]:
             assert rk[e] < 0, "a mover in two key ranges"
             rk[e] = below_k + int((c[ind] < c[e]).sum())
             q = min(max(int(movers[e]), int(cs_old[mk[e]])), int(cs_old[mk[e] + 1]))
-            assert xa <= q <= x1
-            aq[e] = below_xa + int(np.searchsorted(staged, q, side="left"))
+            assert int(cs_old[kd0]) <= q <= x1
+            if q >= xw:
+                aq[e] = below_x0 + int(np.searchsorted(staged, q, side="left")) - r0
+            else:
+                aq[e] = int((movers < q).sum())
         for e in np.nonzero(ins)[0]:
             assert ri[e] < 0, "a mover in two slot ranges"
-            ri[e] = below_xa + int(np.searchsorted(staged, movers[e], side="left"))
+            ri[e] = below_x0 + int(np.searchsorted(staged, movers[e], side="left")) - r0
     return movers, mk, rk, ri, aq, cs_old
 
 
@@ -102,7 +106,8 @@ def test_range_ranks_equal_global_ranks(frac, G):
         newk = ks.copy()
         mv = rng.random(n) < frac
         newk[mv] = rng.integers(0, nc + 1, int(mv.sum()))    # nc: the sentinel key (inactive / left the window)
-        movers, mk, rk, ri, aq, cs_old = range_ranks(ks, newk, min(G, max(n // 256, 1)) if G == 256 else G)
+        win = int(rng.integers(1, 64)) if rng.random() < 0.5 else 2048   # small windows: the counted fallback
+        movers, mk, rk, ri, aq, cs_old = range_ranks(ks, newk, min(G, max(n // 256, 1)) if G == 256 else G, win)
         c = _comp(mk, movers)
         assert np.array_equal(rk, np.argsort(np.argsort(c, kind="stable"), kind="stable"))
         assert np.array_equal(ri, np.arange(len(movers)))
