@@ -20,11 +20,10 @@
 // for bit with the full sort.
 //
 // Kernels:
-//   k_mv_rank        per mover its (key, index) rank and insertion slot q, and the tables by (key, index) and by
-//                    index, each workgroup over its own range of slots and of new keys: O(m) per workgroup
-//   k_mv_merge       stayers: scatter of (pos, vel, id, key); extra workgroups place the movers (A(q) from the
-//                    table by index) and update the cell starts in place:
-//                    cs[k] += #{movers: new key < k} − #{movers: old key < k}
+//   k_mv_rank        per workgroup a range of old slots and the new keys it holds: the movers' ranks, insertion
+//                    slots and placement, the stayers' scatter of (pos, vel, id, key), and the tables by
+//                    (key, index) and by index: O(m) per workgroup plus its slots
+//   k_mv_cells       the cell starts, in place from the tables: cs[k] += #{movers: new key < k} − #{movers: old key < k}
 // The scatters replace the permutation gather, and the update the cell-start rebuild, of the full path.
 #include "common.h"
 
@@ -142,11 +141,13 @@ static __device__ uint32_t wave_lower_bound(const T* __restrict__ a, uint32_t n,
 // the entries' loads.
 constexpr int MV_RANK_GRID = 256;   // workgroups at most; one per CU
 constexpr int RK_U = 8;             // movers per lane per streaming round
-constexpr int MV_RK_CAP = 4096;     // dest entries staged per workgroup (a power of two)
+constexpr int MV_RK_CAP = 2048;     // dest entries staged per workgroup (a power of two)
 constexpr int MV_RX_CAP = 4096;     // slot entries staged per workgroup (a power of two)
 constexpr int RK_BM_WORDS = 2048;   // slot-presence bitmap over [xw, x1): ranges up to 65,536 slots (~100 KB of LDS in all)
 constexpr int RK_WIN = 2048;        // slot entries staged below x0 (covers the cell holding x0)
 constexpr int RK_COUNT = 256;       // dest entries ranked by counting, more by sorting
+constexpr int RK_KD1_CAP = 1024;    // movers into the cell a range ends in, staged
+constexpr int RK_SU = 4;            // stayer slots per lane in flight
 // Test-only timing probe (scripts/rank_probe.py, a -DSPH_RANK_PROBE build): per workgroup the wall clock at its start,
 // after the mover stream, after the sorts and at its end, with its entry counts.
 #ifdef SPH_RANK_PROBE
@@ -254,15 +255,20 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
                                                     ResortExtra ex) {
     __shared__ uint64_t dk[MV_RK_CAP];   // dest entries (new key, slot)
     __shared__ uint32_t dr[MV_RK_CAP];   // their mover index
+    __shared__ uint64_t ds[MV_RK_CAP];   // the dest entries in (key, slot) order (the stayers' searches)
+    __shared__ uint32_t kx1[RK_KD1_CAP]; // slots of the movers whose new key is kd1 (the cell the range ends in)
     __shared__ uint64_t sxk[MV_RX_CAP];  // slot entries (slot, mover index) in [xw, x1)
     __shared__ uint32_t bm[RK_BM_WORDS + 1], bpre[RK_BM_WORDS + 1];   // their slots' presence bits, word prefix
-    __shared__ uint32_t cnt[2], red[RK_BLK / 64];
+    __shared__ uint32_t cnt[3], red[RK_BLK / 64];
     RK_PROBE(0, wall_clock64());
     resolve_sizes(src, w, n);
-    if (threadIdx.x < 2) cnt[threadIdx.x] = 0u;
+    if (threadIdx.x < 3) cnt[threadIdx.x] = 0u;
     for (uint32_t t = threadIdx.x; t <= (uint32_t)RK_BM_WORDS; t += RK_BLK) bm[t] = 0u;
     const uint32_t G = gridDim.x, b = blockIdx.x;
-    const uint32_t x0 = (uint32_t)((uint64_t)(uint32_t)n * b / G), x1 = (uint32_t)((uint64_t)(uint32_t)n * (b + 1) / G);
+    // the ranges are whole blocks of 256 slots (the stayers' scatter below reads no key past its range's)
+    const uint32_t nbk = ((uint32_t)n + 255u) / 256u;
+    const uint32_t x0 = min((uint32_t)((uint64_t)nbk * b / G) * 256u, (uint32_t)n);
+    const uint32_t x1 = min((uint32_t)((uint64_t)nbk * (b + 1) / G) * 256u, (uint32_t)n);
     // Everything the stream needs in one round trip (the kernel is a chain of dependent round trips of ~1.5 us each,
     // r5 probe): the mover count, both range keys (pointer selects) and the first round of movers, whose loads are
     // clamped to the lists' capacity rather than to the count they would otherwise wait for.
@@ -306,6 +312,10 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
                 const uint32_t p = atomicAdd(&cnt[0], 1u);
                 if (p < MV_RK_CAP) { dk[p] = comp(k, x); dr[p] = r; }
             }
+            if (ok && k == kd1) {
+                const uint32_t p = atomicAdd(&cnt[2], 1u);
+                if (p < RK_KD1_CAP) kx1[p] = x;
+            }
             if (ok && x >= xw && x < x1) {
                 const uint32_t p = atomicAdd(&cnt[1], 1u);
                 if (p < MV_RX_CAP) sxk[p] = (uint64_t)x << 32 | r;
@@ -316,7 +326,7 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
     }
     below_k = block_sum<RK_BLK>(below_k, red);   // (its barriers also publish the staged entries and counts)
     below_x0 = block_sum<RK_BLK>(below_x0, red);
-    const uint32_t nd = cnt[0], ns = cnt[1];
+    const uint32_t nd = cnt[0], ns = cnt[1], n1 = cnt[2];
     // block-uniform: the slot entries fit the list and the bitmap; the dest entries fit the list
     const bool slots_ok = ns <= MV_RX_CAP && x1 - xw <= 32u * RK_BM_WORDS, dest_staged = nd <= MV_RK_CAP;
     RK_PROBE(1, wall_clock64());
@@ -380,6 +390,48 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
         store_extra(ex, e, dst);
     };
     auto ins = [&](uint32_t x, uint32_t c0, uint32_t c1) { return x < c0 ? c0 : (x > c1 ? c1 : x); };
+    // The stayers of [x0, x1): dst = (i − A(i)) + #{movers (k, y) < (k_i, i)}. k_i lies in [kd0, kd1]: below kd1
+    // the movers before it are the ones below the key range and the dest entries before it (sorted: ordered), at kd1
+    // all of those plus the kd1 movers with a smaller slot. Every load of a round of slots issues before its stores.
+    auto stayers = [&](const uint64_t* sd) {
+        for (uint32_t base = x0; base < x1; base += RK_BLK * RK_SU) {
+            uint32_t ko[RK_SU], kn[RK_SU];
+            float4 p[RK_SU], v[RK_SU];
+            int32_t pid[RK_SU];
+#pragma unroll
+            for (int u = 0; u < RK_SU; ++u) {
+                const uint32_t i = min(base + u * RK_BLK + threadIdx.x, x1 - 1u);
+                ko[u] = asm_sk(src, (int32_t)i);
+                kn[u] = asm_key(src, (int32_t)i);
+                asm_load(src, (int32_t)i, p[u], v[u], pid[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < RK_SU; ++u) {
+                const uint32_t i = base + u * RK_BLK + threadIdx.x;
+                if (i >= x1 || kn[u] != ko[u]) continue;
+                uint32_t below;
+                if (ko[u] < kd1) {
+                    below = below_k + lower_bound(sd, nd, comp(ko[u], i));
+                } else if (n1 <= (uint32_t)RK_KD1_CAP) {
+                    below = below_k + nd;
+                    for (uint32_t f = 0; f < n1; ++f) below += kx1[f] < i ? 1u : 0u;
+                } else {   // more kd1 movers than LDS holds: counted against the whole list
+                    below = 0;
+                    for (uint32_t f = 0; f < m; ++f) below += comp(w.mk[f], mv_slot(w, w.mi[f])) < comp(ko[u], i) ? 1u : 0u;
+                }
+                const uint32_t dst = (i - slots_below(i)) + below;
+                if (dst >= w.cap) {
+                    if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
+                    continue;
+                }
+                pos_o[dst] = p[u];
+                vel_o[dst] = v[u];
+                id_o[dst] = pid[u];
+                sk_o[dst] = ko[u];
+                move_extra(ex, i, dst);   // Model R's further arrays (the reference's scale: not prefetched)
+            }
+        }
+    };
     // dest ranks: up to RK_COUNT entries each lane counts the smaller ones (LDS broadcast reads, no barrier stages);
     // more are sorted (lds_sort) and ranked by position
     const bool counted = nd <= (uint32_t)RK_COUNT;
@@ -412,7 +464,10 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
                 source(xs0, below_x0 + rank_of(xs0) - r0, mo);
             }
             if (hd) place(c, below_k + lr, ins(x, c0, c1), p, v, pid, e);
+            if (hd && counted) ds[lr] = c;
         }
+        __syncthreads();
+        stayers(counted ? ds : dk);
 #ifdef SPH_RANK_PROBE
         __syncthreads();
         RK_PROBE(3, wall_clock64());
@@ -461,11 +516,42 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
             place_entry(c, below_k + lr);
         }
     }
+    if (dest_staged) {   // the dest entries in order for the stayers' searches
+        if (counted) {
+            for (uint32_t e = threadIdx.x; e < nd; e += RK_BLK) {
+                uint32_t lr = 0;
+                for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < dk[e] ? 1u : 0u;
+                ds[lr] = dk[e];
+            }
+        }
+        __syncthreads();
+        stayers(counted ? ds : dk);
+    } else {   // more dest entries than LDS holds: the stayers count theirs against the whole list
+        for (uint32_t i = x0 + threadIdx.x; i < x1; i += RK_BLK) {
+            const uint32_t ko = asm_sk(src, (int32_t)i);
+            if (asm_key(src, (int32_t)i) != ko) continue;
+            uint32_t below = 0;
+            for (uint32_t f = 0; f < m; ++f) below += comp(w.mk[f], mv_slot(w, w.mi[f])) < comp(ko, i) ? 1u : 0u;
+            const uint32_t dst = (i - slots_below(i)) + below;
+            if (dst >= w.cap) {
+                if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
+                continue;
+            }
+            float4 p, v;
+            int32_t pid;
+            asm_load(src, (int32_t)i, p, v, pid);
+            pos_o[dst] = p;
+            vel_o[dst] = v;
+            id_o[dst] = pid;
+            sk_o[dst] = ko;
+            move_extra(ex, i, dst);
+        }
+    }
 }
 
 // cs[k] += #{movers: new key < k} − #{movers: old key < k}, for k in [0, ncells]; 1024 cells per
 // workgroup. A workgroup whose counts agree at its start and that holds no mover key leaves its cells.
-// Runs as extra workgroups of k_mv_merge (it needs only k_mv_rank's tables), beside the scatter.
+// Its own launch after k_mv_rank (it needs only k_mv_rank's tables).
 constexpr int MV_CS_PER = 4;
 constexpr int MV_CS_CELLS = MV_CS_PER * MV_BLK;
 // movers staged in LDS for the merge's binary searches (a workgroup's cells or slots rarely hold more)
@@ -512,95 +598,13 @@ static __device__ void mv_cell_start(uint32_t* __restrict__ cs, uint32_t ncells,
     }
 }
 
-// Slots per merge workgroup: MV_MERGE_PER per thread (4 per thread: 30.7 us mid-collapse against 22.6 for 1, r5).
-constexpr int MV_MERGE_PER = 1;
-constexpr int MV_MERGE_SLOTS = MV_BLK * MV_MERGE_PER;
-
-__global__ __launch_bounds__(MV_BLK) void k_mv_merge(AsmSrc src, int32_t n,
-                                                     const uint32_t* __restrict__ mtotal, ResortScratch w,
-                                                     float4* __restrict__ pos_o,
-                                                     float4* __restrict__ vel_o, int32_t* __restrict__ id_o,
-                                                     uint32_t* __restrict__ sk_o, int32_t nb, uint32_t* __restrict__ cs,
-                                                     uint32_t ncells, CsPick pick, ResortExtra ex) {
-    __shared__ uint32_t wc[MV_MERGE_PER][MV_BLK / 64];
+// The cell-start update (after k_mv_rank, the last reader of cs_old, and from its tables).
+__global__ __launch_bounds__(MV_BLK) void k_mv_cells(const uint32_t* __restrict__ mtotal, ResortScratch w,
+                                                     uint32_t* __restrict__ cs, uint32_t ncells, CsPick pick) {
     __shared__ uint32_t b[4];
     __shared__ uint64_t lms[MV_LDS];
     __shared__ uint32_t lmo[MV_LDS];
-    if ((int32_t)blockIdx.x >= nb) {   // the cell-start workgroups
-        mv_cell_start(cs, ncells, *mtotal, w, blockIdx.x - nb, b, pick, lms, lmo);
-        return;
-    }
-    resolve_sizes(src, w, n);          // device-sized slab step: nb is an upper bound
-    const int32_t i0 = xcd_block(blockIdx.x, nb) * MV_MERGE_SLOTS;
-    if (i0 >= n) return;               // whole workgroup, before any barrier
-    const int32_t ilast = min(i0 + MV_MERGE_SLOTS, n) - 1;
-    const uint32_t m = *mtotal;
-    const int wv = threadIdx.x >> 6;
-    // movers below this block's first slot, and the movers whose (key, index) falls inside its
-    // stayers' range: ms[b1, b2)
-    if (wv == 0) {
-        const uint32_t p = wave_lower_bound(w.mx, m, (uint32_t)i0);
-        if (lane_id() == 0) b[0] = p;
-    } else if (wv < 3) {
-        const uint64_t v = wv == 1 ? comp(asm_sk(src, i0), (uint32_t)i0) : comp(asm_sk(src, ilast), (uint32_t)ilast) + 1;
-        const uint32_t p = wave_lower_bound(w.ms, m, v);
-        if (lane_id() == 0) b[wv] = p;
-    }
-    // slot j of this thread: i0 + j·256 + t; its particle loads issue before the searches' dependent loads and the
-    // barrier (a mover's are unused)
-    uint32_t ko[MV_MERGE_PER];
-    bool stay[MV_MERGE_PER];
-    float4 p[MV_MERGE_PER], v[MV_MERGE_PER];
-    int32_t pid[MV_MERGE_PER];
-#pragma unroll
-    for (int j = 0; j < MV_MERGE_PER; ++j) {
-        const int32_t i = i0 + j * MV_BLK + (int32_t)threadIdx.x;
-        ko[j] = i < n ? asm_sk(src, i) : 0u;
-        stay[j] = i < n && asm_key(src, i) == ko[j];
-        p[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        v[j] = p[j];
-        pid[j] = 0;
-        if (i < n) asm_load(src, i, p[j], v[j], pid[j]);
-    }
-    // A(i) = movers below the block + in its earlier chunks + in earlier waves of this chunk + earlier lanes
-    uint64_t bal[MV_MERGE_PER];
-#pragma unroll
-    for (int j = 0; j < MV_MERGE_PER; ++j) {
-        const int32_t i = i0 + j * MV_BLK + (int32_t)threadIdx.x;
-        bal[j] = __ballot(i < n && !stay[j]);
-        if (lane_id() == 0) wc[j][wv] = (uint32_t)__popcll(bal[j]);
-    }
-    __syncthreads();
-    const uint32_t lo = b[1], hi = b[2];
-    const bool staged = hi - lo <= MV_LDS;   // block-uniform
-    if (staged) {
-        for (uint32_t t = threadIdx.x; t < hi - lo; t += MV_BLK) lms[t] = w.ms[lo + t];
-        __syncthreads();
-    }
-    uint32_t a = b[0];
-#pragma unroll
-    for (int j = 0; j < MV_MERGE_PER; ++j) {
-        uint32_t aj = a;
-        for (int k = 0; k < MV_BLK / 64; ++k) {
-            aj += k < wv ? wc[j][k] : 0u;
-            a += wc[j][k];
-        }
-        aj += __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[j], 0u));
-        if (!stay[j]) continue;
-        const uint32_t i = (uint32_t)(i0 + j * MV_BLK) + threadIdx.x;
-        const uint64_t kv = comp(ko[j], i);
-        const uint32_t below = lo + (staged ? lower_bound(lms, hi - lo, kv) : lower_bound(w.ms + lo, hi - lo, kv));
-        const uint32_t dst = (i - aj) + below;
-        if (dst >= w.cap) {
-            if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
-            continue;
-        }
-        pos_o[dst] = p[j];
-        vel_o[dst] = v[j];
-        id_o[dst] = pid[j];
-        sk_o[dst] = ko[j];
-        move_extra(ex, i, dst);
-    }
+    mv_cell_start(cs, ncells, *mtotal, w, blockIdx.x, b, pick, lms, lmo);
 }
 
 // The slab step's halo records: new keys (window sentinel, as k_keys) and old keys moved into this
@@ -738,14 +742,12 @@ void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const u
                    uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,
                    uint32_t* sk_o, hipStream_t s, CsPick pick, ResortExtra ex) {
     if (n <= 0) return;
-    const int32_t nb = (n + MV_MERGE_SLOTS - 1) / MV_MERGE_SLOTS;
-    const int32_t nb_rank = (n + MV_BLK - 1) / MV_BLK;
+    const int32_t nbk = (n + MV_BLK - 1) / MV_BLK;
     // n is an upper bound of the slots on device-sized steps: the rank kernel's ranges split the device count
-    SPH_LAUNCH(k_mv_rank, std::min(MV_RANK_GRID, nb_rank), RK_BLK, 0, s, count, count_other, cs, w, src, n, pos_o, vel_o, id_o,
+    SPH_LAUNCH(k_mv_rank, std::min(MV_RANK_GRID, nbk), RK_BLK, 0, s, count, count_other, cs, w, src, n, pos_o, vel_o, id_o,
                sk_o, ex);
-    // the stayers' scatter and the cell-start update (after k_mv_rank, the last reader of cs_old)
     const int32_t ncs = (int32_t)((ncells + MV_CS_CELLS) / MV_CS_CELLS);
-    SPH_LAUNCH(k_mv_merge, nb + ncs, MV_BLK, 0, s, src, n, count, w, pos_o, vel_o, id_o, sk_o, nb, cs, ncells, pick, ex);
+    SPH_LAUNCH(k_mv_cells, ncs, MV_BLK, 0, s, count, w, cs, ncells, pick);
 }
 
 }  // namespace sph
