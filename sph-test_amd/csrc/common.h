@@ -356,6 +356,7 @@ struct ResortScratch {
     const SlabSizes* dz = nullptr;   // non-null: mi_off = nl - o0 from the device sizes
     uint32_t* err = nullptr;         // SZ_OVF_MOVERS if a destination would pass cap (never written)
     uint32_t* host_count = nullptr;  // mapped host memory: k_mv_rank stores the mover count there (the host's sort choice)
+    uint32_t* bnd = nullptr;         // [2 * 256]: the rank ranges' first cells and their new starts (k_mv_bounds)
 };
 // a mover entry whose mi has this bit holds a slot of the assembled array (a halo record's);
 // without it, mi is the force pass's slot and the assembled slot is mi + mi_off

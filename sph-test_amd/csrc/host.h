@@ -98,6 +98,7 @@ struct sph_ctx {
     uint32_t *sk_cur = nullptr, *sk_next = nullptr;
     uint32_t *mv_mi = nullptr, *mv_mk = nullptr, *mv_mo = nullptr, *mv_mx = nullptr, *mv_mos = nullptr;
     uint64_t* mv_ms = nullptr;
+    uint32_t* mv_bnd = nullptr;     // the re-sort's boundary-cell table (ResortScratch.bnd)
     uint32_t* mv_count = nullptr;   // [2] mover counters, ping-pong by step
     int mv_par = 0;                 // counter the next force pass appends into
     bool sk_valid = false;       // sk_cur matches the slot order and cs (set by a Model S sort)

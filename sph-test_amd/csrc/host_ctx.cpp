@@ -15,7 +15,7 @@ void free_all(sph_ctx* c) {
     dfree(c->sblk); dfree(c->sdev); dfree(c->paths); dfree(c->hmask);
     dfree(c->sk_cur); dfree(c->sk_next);
     dfree(c->mv_mi); dfree(c->mv_mk); dfree(c->mv_mo); dfree(c->mv_mx); dfree(c->mv_mos);
-    dfree(c->mv_ms); dfree(c->mv_count);
+    dfree(c->mv_ms); dfree(c->mv_count); dfree(c->mv_bnd);
     dfree(c->sched);
     c->sched_cap = 0;
     c->sched_valid = false;
@@ -56,7 +56,7 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
     // incremental re-sort (both models)
     AL(sk_cur, n); AL(sk_next, n);
     AL(mv_mi, n); AL(mv_mk, n); AL(mv_mo, n); AL(mv_mx, n); AL(mv_mos, n); AL(mv_ms, n);
-    AL(mv_count, 2);
+    AL(mv_count, 2); AL(mv_bnd, 512);
     HIPCHK(hipMemset(ctx->mv_count, 0, 2 * sizeof(uint32_t)));
 #undef AL
     ctx->staging_bytes = n * 84;

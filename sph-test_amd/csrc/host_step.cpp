@@ -103,6 +103,7 @@ ResortScratch resort_scratch(sph_ctx* ctx) {
     ResortScratch w{ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_ms, ctx->mv_mx, ctx->mv_mos,
                     (uint32_t)std::max(ctx->capacity, 1), 0};
     w.host_count = ctx->mv_host_dev;
+    w.bnd = ctx->mv_bnd;
     return w;
 }
 

@@ -97,26 +97,6 @@ static __device__ __forceinline__ uint32_t lower_bound(const T* __restrict__ a, 
     return lo;
 }
 
-// lower_bound by one wave: 64 probes per level, so a few dependent loads for any n (wave-uniform).
-template <typename T>
-static __device__ uint32_t wave_lower_bound(const T* __restrict__ a, uint32_t n, T v) {
-    const uint32_t lane = lane_id();
-    uint32_t base = 0, len = n;
-    while (len > 64) {
-        const uint32_t step = (len + 63) / 64;
-        const uint32_t idx = base + lane * step;
-        const bool lt = idx < base + len && a[idx] < v;
-        const uint32_t k = (uint32_t)__popcll(__ballot(lt));   // probes below v form a prefix
-        if (k == 0) return base;
-        const uint32_t nb = base + (k - 1) * step + 1;
-        const uint32_t end = k * step < len ? base + k * step : base + len;   // a[end] >= v (or end of range)
-        base = nb;
-        len = end - nb;
-    }
-    const bool lt = lane < len && a[base + lane] < v;
-    return base + (uint32_t)__popcll(__ballot(lt));
-}
-
 // Mover ranks and placement in O(m) per workgroup (replaces the all-pairs tile counts and the separate placement of
 // r1-r4, whose work grew as m²: the C3 re-sort chain went from 27.7 us from rest to 41.5 us mid-collapse). Workgroup
 // b of G owns the slots [x0, x1) = [b·n/G, (b+1)·n/G) of the assembled old order and the new keys
@@ -142,12 +122,12 @@ static __device__ uint32_t wave_lower_bound(const T* __restrict__ a, uint32_t n,
 constexpr int MV_RANK_GRID = 256;   // workgroups at most; one per CU
 constexpr int RK_U = 8;             // movers per lane per streaming round
 constexpr int MV_RK_CAP = 2048;     // dest entries staged per workgroup (a power of two)
-constexpr int MV_RX_CAP = 4096;     // slot entries staged per workgroup (a power of two)
 constexpr int RK_BM_WORDS = 2048;   // slot-presence bitmap over [xw, x1): ranges up to 65,536 slots (~100 KB of LDS in all)
 constexpr int RK_WIN = 2048;        // slot entries staged below x0 (covers the cell holding x0)
 constexpr int RK_COUNT = 256;       // dest entries ranked by counting, more by sorting
 constexpr int RK_KD1_CAP = 1024;    // movers into the cell a range ends in, staged
 constexpr int RK_SU = 4;            // stayer slots per lane in flight
+constexpr int RK_OK_CAP = 2048;     // movers' old keys in the key range, staged
 // Test-only timing probe (scripts/rank_probe.py, a -DSPH_RANK_PROBE build): per workgroup the wall clock at its start,
 // after the mover stream, after the sorts and at its end, with its entry counts.
 #ifdef SPH_RANK_PROBE
@@ -249,23 +229,24 @@ __device__ void lds_sort(uint64_t* a, uint32_t* b, uint32_t len) {
 }
 
 __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__ mtotal, uint32_t* __restrict__ next_count,
-                                                    const uint32_t* __restrict__ cs_old, ResortScratch w, AsmSrc src,
-                                                    int32_t n, float4* __restrict__ pos_o, float4* __restrict__ vel_o,
-                                                    int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o,
-                                                    ResortExtra ex) {
+                                                    uint32_t* __restrict__ cs, uint32_t ncells, ResortScratch w,
+                                                    AsmSrc src, int32_t n, float4* __restrict__ pos_o,
+                                                    float4* __restrict__ vel_o, int32_t* __restrict__ id_o,
+                                                    uint32_t* __restrict__ sk_o, ResortExtra ex) {
     __shared__ uint64_t dk[MV_RK_CAP];   // dest entries (new key, slot)
     __shared__ uint32_t dr[MV_RK_CAP];   // their mover index
-    __shared__ uint64_t ds[MV_RK_CAP];   // the dest entries in (key, slot) order (the stayers' searches)
+    __shared__ uint64_t ds[MV_RK_CAP];   // the dest entries in (key, slot) order
+    __shared__ uint64_t ok[RK_OK_CAP];   // old keys in [kd0, kd1) (old key, mover index)
+    __shared__ uint64_t oks[RK_OK_CAP];  // the same in order
     __shared__ uint32_t kx1[RK_KD1_CAP]; // slots of the movers whose new key is kd1 (the cell the range ends in)
-    __shared__ uint64_t sxk[MV_RX_CAP];  // slot entries (slot, mover index) in [xw, x1)
-    __shared__ uint32_t bm[RK_BM_WORDS + 1], bpre[RK_BM_WORDS + 1];   // their slots' presence bits, word prefix
-    __shared__ uint32_t cnt[3], red[RK_BLK / 64];
+    __shared__ uint32_t bm[RK_BM_WORDS + 1], bpre[RK_BM_WORDS + 1];   // movers' slots in [xw, x1): bits, word prefix
+    __shared__ uint32_t cnt[4], red[RK_BLK / 64];
     RK_PROBE(0, wall_clock64());
     resolve_sizes(src, w, n);
-    if (threadIdx.x < 3) cnt[threadIdx.x] = 0u;
+    if (threadIdx.x < 4) cnt[threadIdx.x] = 0u;
     for (uint32_t t = threadIdx.x; t <= (uint32_t)RK_BM_WORDS; t += RK_BLK) bm[t] = 0u;
     const uint32_t G = gridDim.x, b = blockIdx.x;
-    // the ranges are whole blocks of 256 slots (the stayers' scatter below reads no key past its range's)
+    // the ranges are whole blocks of 256 slots
     const uint32_t nbk = ((uint32_t)n + 255u) / 256u;
     const uint32_t x0 = min((uint32_t)((uint64_t)nbk * b / G) * 256u, (uint32_t)n);
     const uint32_t x1 = min((uint32_t)((uint64_t)nbk * (b + 1) / G) * 256u, (uint32_t)n);
@@ -276,13 +257,14 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
         const int32_t xi = (int32_t)min(x, (uint32_t)max(n - 1, 0));
         return asm_rec(src, xi) ? src.skr + xi : src.sk + (xi + src.o_off);
     };
-    uint32_t xs[RK_U], ks[RK_U];
+    uint32_t xs[RK_U], ks[RK_U], os[RK_U];
     auto load_round = [&](uint32_t base, uint32_t last) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < RK_U; ++u) {   // every load of the round issues before any is used
             const uint32_t r = min(base + u * RK_BLK + threadIdx.x, last);
             xs[u] = w.mi[r];
             ks[u] = w.mk[r];
+            os[u] = w.mo[r];
         }
     };
     load_round(0, w.cap - 1u);
@@ -294,46 +276,51 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
     }
     const uint32_t kd0 = b == 0 ? 0u : (x0 < (uint32_t)n ? sk0 : 0xffffffffu);
     const uint32_t kd1 = b == G - 1 ? 0xffffffffu : (x1 < (uint32_t)n ? sk1 : 0xffffffffu);
-    // Slot entries are staged from xw = x0 − RK_WIN: every insertion slot q of a dest entry lies in [cs_old[kd0], x1],
-    // and cs_old[kd0] (the start of the cell holding slot x0) is at most RK_WIN below x0 except in cells of more than
-    // RK_WIN particles; such an entry counts its A(q) against the whole list instead.
+    // Movers' slots are staged from xw = x0 − RK_WIN: every insertion slot q of a dest entry lies in
+    // [cs_old[kd0], x1], and cs_old[kd0] (the start of the cell holding slot x0) is at most RK_WIN below x0 except
+    // in cells of more than RK_WIN particles; such an entry counts its A(q) against the whole list instead.
     const uint32_t xw = x0 > (uint32_t)RK_WIN ? x0 - (uint32_t)RK_WIN : 0u;
+    const bool bits_ok = x1 - xw <= 32u * RK_BM_WORDS;   // block-uniform
     __syncthreads();
-    uint32_t below_k = 0, below_x0 = 0;
+    uint32_t below_k = 0, below_x0 = 0, below_ko = 0;
     for (uint32_t base = 0; base < m; base += RK_BLK * RK_U) {
 #pragma unroll
         for (int u = 0; u < RK_U; ++u) {
             const uint32_t r = base + u * RK_BLK + threadIdx.x;
-            const bool ok = r < m;
-            const uint32_t x = mv_slot(w, xs[u]), k = ks[u];
-            below_k += ok && k < kd0 ? 1u : 0u;
-            below_x0 += ok && x < x0 ? 1u : 0u;
-            if (ok && k >= kd0 && k < kd1) {
+            const bool okr = r < m;
+            const uint32_t x = mv_slot(w, xs[u]), k = ks[u], o = os[u];
+            below_k += okr && k < kd0 ? 1u : 0u;
+            below_x0 += okr && x < x0 ? 1u : 0u;
+            below_ko += okr && o < kd0 ? 1u : 0u;
+            if (okr && k >= kd0 && k < kd1) {
                 const uint32_t p = atomicAdd(&cnt[0], 1u);
                 if (p < MV_RK_CAP) { dk[p] = comp(k, x); dr[p] = r; }
             }
-            if (ok && k == kd1) {
+            if (okr && k == kd1) {
                 const uint32_t p = atomicAdd(&cnt[2], 1u);
                 if (p < RK_KD1_CAP) kx1[p] = x;
             }
-            if (ok && x >= xw && x < x1) {
-                const uint32_t p = atomicAdd(&cnt[1], 1u);
-                if (p < MV_RX_CAP) sxk[p] = (uint64_t)x << 32 | r;
-                if (x - xw < 32u * RK_BM_WORDS) atomicOr(&bm[(x - xw) >> 5], 1u << ((x - xw) & 31u));
+            if (okr && o >= kd0 && o < kd1) {
+                const uint32_t p = atomicAdd(&cnt[3], 1u);
+                if (p < RK_OK_CAP) ok[p] = comp(o, r);
+            }
+            if (okr && bits_ok && x >= xw && x < x1) {
+                atomicAdd(&cnt[1], 1u);
+                atomicOr(&bm[(x - xw) >> 5], 1u << ((x - xw) & 31u));
             }
         }
         if (base + RK_BLK * RK_U < m) load_round(base + RK_BLK * RK_U, m - 1u);
     }
     below_k = block_sum<RK_BLK>(below_k, red);   // (its barriers also publish the staged entries and counts)
     below_x0 = block_sum<RK_BLK>(below_x0, red);
-    const uint32_t nd = cnt[0], ns = cnt[1], n1 = cnt[2];
-    // block-uniform: the slot entries fit the list and the bitmap; the dest entries fit the list
-    const bool slots_ok = ns <= MV_RX_CAP && x1 - xw <= 32u * RK_BM_WORDS, dest_staged = nd <= MV_RK_CAP;
+    below_ko = block_sum<RK_BLK>(below_ko, red);
+    const uint32_t nd = cnt[0], n1 = cnt[2], no = cnt[3];
+    const bool dest_staged = nd <= MV_RK_CAP, old_staged = no <= RK_OK_CAP;   // block-uniform
     RK_PROBE(1, wall_clock64());
     RK_PROBE(4, nd);
-    RK_PROBE(5, ns);
+    RK_PROBE(5, cnt[1]);
     RK_PROBE(6, m);
-    if (slots_ok) {   // the bitmap's word prefix
+    if (bits_ok) {   // the bitmap's word prefix
         const uint32_t nw = (x1 - xw + 31u) >> 5, w0 = 2 * threadIdx.x;   // two words per lane
         const uint32_t c0 = w0 < nw ? (uint32_t)__popc(bm[w0]) : 0u, c1 = w0 + 1 < nw ? (uint32_t)__popc(bm[w0 + 1]) : 0u;
         uint32_t inc = c0 + c1;
@@ -351,260 +338,165 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
         if (w0 <= nw) bpre[w0] = ex0;
         if (w0 + 1 <= nw) bpre[w0 + 1] = ex0 + c0;
         if (nw == (uint32_t)RK_BM_WORDS && threadIdx.x == RK_BLK - 1) bpre[RK_BM_WORDS] = pre + inc;
-        __syncthreads();
     }
-    auto rank_of = [&](uint32_t y) {   // #staged slots in [xw, y), y in [xw, x1]
-        const uint32_t d = min(y, x1) - xw, wd = d >> 5;
-        return bpre[wd] + (uint32_t)__popc(bm[wd] & ((1u << (d & 31u)) - 1u));
-    };
-    auto count_below = [&](uint32_t y) {   // #movers with slot < y, against the whole list
+    // the dest entries and the old keys in order: up to RK_COUNT of them each lane counts the smaller ones (LDS
+    // broadcast reads, no barrier stages), more are sorted (lds_sort)
+    const bool dcount = nd <= (uint32_t)RK_COUNT, ocount = no <= (uint32_t)RK_COUNT;
+    if (dest_staged && dcount)
+        for (uint32_t e = threadIdx.x; e < nd; e += RK_BLK) {
+            uint32_t lr = 0;
+            for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < dk[e] ? 1u : 0u;
+            ds[lr] = dk[e];
+        }
+    if (old_staged && ocount)
+        for (uint32_t e = threadIdx.x; e < no; e += RK_BLK) {
+            uint32_t lr = 0;
+            for (uint32_t f = 0; f < no; ++f) lr += ok[f] < ok[e] ? 1u : 0u;
+            oks[lr] = ok[e];
+        }
+    if (dest_staged && !dcount) lds_sort(dk, nullptr, nd);
+    if (old_staged && !ocount) lds_sort(ok, nullptr, no);
+    __syncthreads();
+    const uint64_t* sd = dcount ? ds : dk;   // sorted dest entries (dest_staged)
+    const uint64_t* so = ocount ? oks : ok;  // sorted old keys (old_staged)
+    RK_PROBE(2, wall_clock64());
+    RK_PROBE(7, bits_ok ? 1 : 0);
+    // ---- counts against the whole list (ranges holding more than LDS does: a state where most particles move)
+    auto count_slots = [&](uint32_t y) {   // #movers with slot < y
         uint32_t c = 0;
         for (uint32_t f = 0; f < m; ++f) c += mv_slot(w, w.mi[f]) < y ? 1u : 0u;
         return c;
     };
-    // #movers with slot < y: below x0 plus the staged slots in [x0, y), or below x0 minus those in [y, x0)
-    const uint32_t r0 = slots_ok ? rank_of(x0) : 0u;
-    auto slots_below = [&](uint32_t y) { return slots_ok && y >= xw ? below_x0 + rank_of(y) - r0 : count_below(y); };
-    // source entries (slot in [x0, x1)): ri = #{y : y < x} -> mx[ri] = x, mos[ri] = old key (ascending by slot)
-    auto source = [&](uint32_t x, uint32_t ri, uint32_t mo) {
-        if (ri >= w.cap) {   // inconsistent tables: flag, never write past them
-            if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
-            return;
-        }
-        w.mx[ri] = x;
-        w.mos[ri] = mo;
+    auto count_dest = [&](uint64_t v) {    // #movers with (new key, slot) < v
+        uint32_t c = 0;
+        for (uint32_t f = 0; f < m; ++f) c += comp(w.mk[f], mv_slot(w, w.mi[f])) < v ? 1u : 0u;
+        return c;
     };
-    // dest entries: rank rk, insertion slot q among the stayers, A(q) = #{y : y < q}, placement at (q − A(q)) + rk
-    auto place = [&](uint64_t c, uint32_t rk, uint32_t q, float4 p, float4 v, int32_t pid, const ExtraVals& e) {
-        const uint32_t k = (uint32_t)(c >> 32);
-        const uint32_t dst = (q - slots_below(q)) + rk;
-        if (rk >= w.cap || dst >= w.cap) {   // inconsistent tables: flag, never write past them
+    auto count_old = [&](uint32_t k) {     // #movers with old key < k
+        uint32_t c = 0;
+        for (uint32_t f = 0; f < m; ++f) c += w.mo[f] < k ? 1u : 0u;
+        return c;
+    };
+    // #movers with slot < y: below x0 plus (minus) the staged slots between x0 and y
+    auto rank_of = [&](uint32_t y) {   // #staged slots in [xw, y), y in [xw, x1]
+        const uint32_t d = min(y, x1) - xw, wd = d >> 5;
+        return bpre[wd] + (uint32_t)__popc(bm[wd] & ((1u << (d & 31u)) - 1u));
+    };
+    const uint32_t r0 = bits_ok ? rank_of(x0) : 0u;
+    auto slots_below = [&](uint32_t y) { return bits_ok && y >= xw ? below_x0 + rank_of(y) - r0 : count_slots(y); };
+    // #movers with (new key, slot) < (k, i) for k in [kd0, kd1]: below the key range plus the dest entries before it;
+    // at kd1 all of those plus the kd1 movers with a smaller slot
+    auto dest_below = [&](uint32_t k, uint32_t i) {
+        if (!dest_staged) return count_dest(comp(k, i));
+        if (k < kd1) return below_k + lower_bound(sd, nd, comp(k, i));
+        if (n1 > (uint32_t)RK_KD1_CAP) return count_dest(comp(k, i));
+        uint32_t c = below_k + nd;
+        for (uint32_t f = 0; f < n1; ++f) c += kx1[f] < i ? 1u : 0u;
+        return c;
+    };
+    // ---- the movers of this key range: rank rk = #{(k', y) < (k, x)}, insertion slot q among the stayers,
+    // A(q) = #{y : y < q}; placed at (q − A(q)) + rk. Loads first.
+    auto place = [&](uint64_t c) {
+        const uint32_t k = (uint32_t)(c >> 32), x = (uint32_t)c;
+        const uint32_t c0 = cs[k], c1 = cs[k + 1];   // not yet updated: this workgroup's cells change after a barrier
+        float4 p, v;
+        int32_t pid;
+        asm_load(src, (int32_t)x, p, v, pid);
+        const ExtraVals e = load_extra(ex, x);
+        const uint32_t q = x < c0 ? c0 : (x > c1 ? c1 : x);
+        const uint32_t dst = (q - slots_below(q)) + dest_below(k, x);
+        if (dst >= w.cap) {   // inconsistent tables: flag, never write past them
             if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
             return;
         }
-        w.ms[rk] = c;
         pos_o[dst] = p;
         vel_o[dst] = v;
         id_o[dst] = pid;
         sk_o[dst] = k;
         store_extra(ex, e, dst);
     };
-    auto ins = [&](uint32_t x, uint32_t c0, uint32_t c1) { return x < c0 ? c0 : (x > c1 ? c1 : x); };
-    // The stayers of [x0, x1): dst = (i − A(i)) + #{movers (k, y) < (k_i, i)}. k_i lies in [kd0, kd1]: below kd1
-    // the movers before it are the ones below the key range and the dest entries before it (sorted: ordered), at kd1
-    // all of those plus the kd1 movers with a smaller slot. Every load of a round of slots issues before its stores.
-    auto stayers = [&](const uint64_t* sd) {
-        for (uint32_t base = x0; base < x1; base += RK_BLK * RK_SU) {
-            uint32_t ko[RK_SU], kn[RK_SU];
-            float4 p[RK_SU], v[RK_SU];
-            int32_t pid[RK_SU];
-#pragma unroll
-            for (int u = 0; u < RK_SU; ++u) {
-                const uint32_t i = min(base + u * RK_BLK + threadIdx.x, x1 - 1u);
-                ko[u] = asm_sk(src, (int32_t)i);
-                kn[u] = asm_key(src, (int32_t)i);
-                asm_load(src, (int32_t)i, p[u], v[u], pid[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < RK_SU; ++u) {
-                const uint32_t i = base + u * RK_BLK + threadIdx.x;
-                if (i >= x1 || kn[u] != ko[u]) continue;
-                uint32_t below;
-                if (ko[u] < kd1) {
-                    below = below_k + lower_bound(sd, nd, comp(ko[u], i));
-                } else if (n1 <= (uint32_t)RK_KD1_CAP) {
-                    below = below_k + nd;
-                    for (uint32_t f = 0; f < n1; ++f) below += kx1[f] < i ? 1u : 0u;
-                } else {   // more kd1 movers than LDS holds: counted against the whole list
-                    below = 0;
-                    for (uint32_t f = 0; f < m; ++f) below += comp(w.mk[f], mv_slot(w, w.mi[f])) < comp(ko[u], i) ? 1u : 0u;
-                }
-                const uint32_t dst = (i - slots_below(i)) + below;
-                if (dst >= w.cap) {
-                    if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
-                    continue;
-                }
-                pos_o[dst] = p[u];
-                vel_o[dst] = v[u];
-                id_o[dst] = pid[u];
-                sk_o[dst] = ko[u];
-                move_extra(ex, i, dst);   // Model R's further arrays (the reference's scale: not prefetched)
-            }
-        }
-    };
-    // dest ranks: up to RK_COUNT entries each lane counts the smaller ones (LDS broadcast reads, no barrier stages);
-    // more are sorted (lds_sort) and ranked by position
-    const bool counted = nd <= (uint32_t)RK_COUNT;
-    if (dest_staged && !counted) lds_sort(dk, dr, nd);
-    RK_PROBE(2, wall_clock64());
-    RK_PROBE(7, slots_ok ? 1 : 0);
-    if (slots_ok && dest_staged) {
-        // one pass over both kinds of entry, every global load of an entry issued before its stores
-        for (uint32_t t = threadIdx.x; t < max(ns, nd); t += RK_BLK) {
-            const uint64_t se0 = t < ns ? sxk[t] : 0ull;
-            const bool hs = t < ns && (uint32_t)(se0 >> 32) >= x0, hd = t < nd;
-            const uint64_t c = hd ? dk[t] : 0ull;
-            const uint32_t k = (uint32_t)(c >> 32), x = (uint32_t)c;
-            const uint32_t mo = hs ? w.mo[(uint32_t)se0] : 0u;
-            const uint32_t c0 = hd ? cs_old[k] : 0u, c1 = hd ? cs_old[k + 1] : 0u;
-            float4 p = make_float4(0.f, 0.f, 0.f, 0.f), v = p;
-            int32_t pid = 0;
-            ExtraVals e{};
-            if (hd) {
-                asm_load(src, (int32_t)x, p, v, pid);
-                e = load_extra(ex, x);
-            }
-            uint32_t lr = t;
-            if (hd && counted) {
-                lr = 0;
-                for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < c ? 1u : 0u;
-            }
-            if (hs) {
-                const uint32_t xs0 = (uint32_t)(se0 >> 32);
-                source(xs0, below_x0 + rank_of(xs0) - r0, mo);
-            }
-            if (hd) place(c, below_k + lr, ins(x, c0, c1), p, v, pid, e);
-            if (hd && counted) ds[lr] = c;
-        }
-        __syncthreads();
-        stayers(counted ? ds : dk);
-#ifdef SPH_RANK_PROBE
-        __syncthreads();
-        RK_PROBE(3, wall_clock64());
-#endif
-        return;
-    }
-    // more entries than LDS holds (a state where most particles move, only under SPH_RESORT=2): the overflowing kind
-    // counted against the whole list instead, slow, same result
-    if (slots_ok) {
-        for (uint32_t e = threadIdx.x; e < ns; e += RK_BLK) {
-            const uint32_t x = (uint32_t)(sxk[e] >> 32);
-            if (x >= x0) source(x, below_x0 + rank_of(x) - r0, w.mo[(uint32_t)sxk[e]]);
-        }
-    } else {
-        for (uint32_t r = threadIdx.x; r < m; r += RK_BLK) {
-            const uint32_t x = mv_slot(w, w.mi[r]);
-            if (x >= x0 && x < x1) source(x, count_below(x), w.mo[r]);
-        }
-    }
-    auto place_entry = [&](uint64_t c, uint32_t rk) {
-        const uint32_t k = (uint32_t)(c >> 32), x = (uint32_t)c;
-        float4 p, v;
-        int32_t pid;
-        asm_load(src, (int32_t)x, p, v, pid);
-        place(c, rk, ins(x, cs_old[k], cs_old[k + 1]), p, v, pid, load_extra(ex, x));
-    };
     if (dest_staged) {
-        for (uint32_t e = threadIdx.x; e < nd; e += RK_BLK) {
-            uint32_t lr = e;
-            if (counted) {
-                lr = 0;
-                for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < dk[e] ? 1u : 0u;
-            }
-            place_entry(dk[e], below_k + lr);
-        }
+        for (uint32_t t = threadIdx.x; t < nd; t += RK_BLK) place(dk[t]);
     } else {
         for (uint32_t r = threadIdx.x; r < m; r += RK_BLK) {
             const uint32_t k = w.mk[r];
-            if (!(k >= kd0 && k < kd1)) continue;
-            const uint64_t c = comp(k, mv_slot(w, w.mi[r]));
-            uint32_t lr = 0;
-            for (uint32_t f = 0; f < m; ++f) {
-                const uint32_t kf = w.mk[f], xf = mv_slot(w, w.mi[f]);
-                lr += (kf >= kd0 && kf < kd1 && comp(kf, xf) < c) ? 1u : 0u;
-            }
-            place_entry(c, below_k + lr);
+            if (k >= kd0 && k < kd1) place(comp(k, mv_slot(w, w.mi[r])));
         }
     }
-    if (dest_staged) {   // the dest entries in order for the stayers' searches
-        if (counted) {
-            for (uint32_t e = threadIdx.x; e < nd; e += RK_BLK) {
-                uint32_t lr = 0;
-                for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < dk[e] ? 1u : 0u;
-                ds[lr] = dk[e];
-            }
+    // ---- the stayers of [x0, x1): dst = (i − A(i)) + #{movers (k, y) < (k_i, i)}, k_i in [kd0, kd1]. Every load
+    // of a round of slots issues before its stores.
+    for (uint32_t base = x0; base < x1; base += RK_BLK * RK_SU) {
+        uint32_t ko[RK_SU], kn[RK_SU];
+        float4 p[RK_SU], v[RK_SU];
+        int32_t pid[RK_SU];
+#pragma unroll
+        for (int u = 0; u < RK_SU; ++u) {
+            const uint32_t i = min(base + u * RK_BLK + threadIdx.x, x1 - 1u);
+            ko[u] = asm_sk(src, (int32_t)i);
+            kn[u] = asm_key(src, (int32_t)i);
+            asm_load(src, (int32_t)i, p[u], v[u], pid[u]);
         }
-        __syncthreads();
-        stayers(counted ? ds : dk);
-    } else {   // more dest entries than LDS holds: the stayers count theirs against the whole list
-        for (uint32_t i = x0 + threadIdx.x; i < x1; i += RK_BLK) {
-            const uint32_t ko = asm_sk(src, (int32_t)i);
-            if (asm_key(src, (int32_t)i) != ko) continue;
-            uint32_t below = 0;
-            for (uint32_t f = 0; f < m; ++f) below += comp(w.mk[f], mv_slot(w, w.mi[f])) < comp(ko, i) ? 1u : 0u;
-            const uint32_t dst = (i - slots_below(i)) + below;
+#pragma unroll
+        for (int u = 0; u < RK_SU; ++u) {
+            const uint32_t i = base + u * RK_BLK + threadIdx.x;
+            if (i >= x1 || kn[u] != ko[u]) continue;
+            const uint32_t dst = (i - slots_below(i)) + dest_below(ko[u], i);
             if (dst >= w.cap) {
                 if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
                 continue;
             }
-            float4 p, v;
-            int32_t pid;
-            asm_load(src, (int32_t)i, p, v, pid);
-            pos_o[dst] = p;
-            vel_o[dst] = v;
-            id_o[dst] = pid;
-            sk_o[dst] = ko;
-            move_extra(ex, i, dst);
+            pos_o[dst] = p[u];
+            vel_o[dst] = v[u];
+            id_o[dst] = pid[u];
+            sk_o[dst] = ko[u];
+            move_extra(ex, i, dst);   // Model R's further arrays (the reference's scale: not prefetched)
         }
     }
+    // ---- the cell starts of this key range, in place: cs[k] += #{movers: new key < k} − #{movers: old key < k} for
+    // the cells kd0 < k < kd1 (kd1 = ncells + 1 for the last range). Only this workgroup reads them (its movers'
+    // insertion slots, above); every cell kd0 is read by two workgroups, so its new value goes to the boundary table
+    // and k_mv_bounds writes it after the launch.
+    __syncthreads();
+    if (kd0 != 0xffffffffu) {
+        const uint32_t khi = min(kd1, ncells + 1u);
+        const int32_t base_d = (int32_t)below_k - (int32_t)below_ko;
+        for (uint32_t k = kd0 + 1u + threadIdx.x; k < khi; k += RK_BLK) {
+            const uint32_t cn = dest_staged ? lower_bound(sd, nd, comp(k, 0u)) : count_dest(comp(k, 0u)) - below_k;
+            const uint32_t co = old_staged ? lower_bound(so, no, comp(k, 0u)) : count_old(k) - below_ko;
+            const int32_t dlt = base_d + (int32_t)cn - (int32_t)co;
+            if (dlt != 0) cs[k] = (uint32_t)((int32_t)cs[k] + dlt);
+        }
+        if (threadIdx.x == 0) {
+            w.bnd[b] = kd0;
+            w.bnd[G + b] = (uint32_t)((int32_t)cs[kd0] + base_d);
+        }
+    } else if (threadIdx.x == 0) {
+        w.bnd[b] = 0xffffffffu;
+    }
+#ifdef SPH_RANK_PROBE
+    __syncthreads();
+    RK_PROBE(3, wall_clock64());
+#endif
 }
 
-// cs[k] += #{movers: new key < k} − #{movers: old key < k}, for k in [0, ncells]; 1024 cells per
-// workgroup. A workgroup whose counts agree at its start and that holds no mover key leaves its cells.
-// Its own launch after k_mv_rank (it needs only k_mv_rank's tables).
-constexpr int MV_CS_PER = 4;
-constexpr int MV_CS_CELLS = MV_CS_PER * MV_BLK;
-// movers staged in LDS for the merge's binary searches (a workgroup's cells or slots rarely hold more)
-constexpr uint32_t MV_LDS = 1024;
-
-// Picks falling in this workgroup's cells are read back once its cells are final.
-static __device__ void mv_cell_start(uint32_t* __restrict__ cs, uint32_t ncells, uint32_t m, const ResortScratch& w,
-                                     uint32_t blk, uint32_t* b, const CsPick& pick, uint64_t* lms, uint32_t* lmo) {
-    const uint32_t k0 = blk * MV_CS_CELLS, k1 = k0 + MV_CS_CELLS;
-    const int wv = threadIdx.x >> 6;
-    const uint32_t p = wv < 2 ? wave_lower_bound(w.ms, m, comp(wv == 0 ? k0 : k1, 0u))
-                              : wave_lower_bound(w.mos, m, wv == 2 ? k0 : k1);
-    if (lane_id() == 0) b[wv] = p;
-    __syncthreads();
-    const uint32_t nlo = b[0], nhi = b[1], olo = b[2], ohi = b[3];
-    if (!(nlo == olo && nhi == nlo && ohi == olo)) {
-        // the movers' new and old keys in this workgroup's cell range, staged in LDS (block-uniform test)
-        const uint32_t nn = nhi - nlo, no = ohi - olo;
-        const bool staged = nn <= MV_LDS && no <= MV_LDS;
-        if (staged) {
-            for (uint32_t t = threadIdx.x; t < nn; t += MV_BLK) lms[t] = w.ms[nlo + t];
-            for (uint32_t t = threadIdx.x; t < no; t += MV_BLK) lmo[t] = w.mos[olo + t];
-            __syncthreads();
-        }
-#pragma unroll 4
-        for (int j = 0; j < MV_CS_PER; ++j) {
-            const uint32_t k = k0 + j * MV_BLK + threadIdx.x;
-            if (k > ncells) break;
-            const uint32_t cn = nlo + (staged ? lower_bound(lms, nn, comp(k, 0u)) : lower_bound(w.ms + nlo, nn, comp(k, 0u)));
-            const uint32_t co = olo + (staged ? lower_bound(lmo, no, k) : lower_bound(w.mos + olo, no, k));
-            cs[k] += cn - co;
-        }
+// The cells every rank range starts at (read by two workgroups of k_mv_rank, so written here), then the picks.
+__global__ __launch_bounds__(MV_BLK) void k_mv_bounds(const ResortScratch w, uint32_t G, uint32_t* __restrict__ cs,
+                                                      uint32_t ncells, CsPick pick) {
+    for (uint32_t b = threadIdx.x; b < G; b += MV_BLK) {
+        const uint32_t k = w.bnd[b];
+        if (k <= ncells) cs[k] = w.bnd[G + b];
     }
     if (pick.m == 0) return;
-    __syncthreads();   // this workgroup's cell updates are visible to all its lanes
+    __syncthreads();
     const int t = threadIdx.x;
     if (t < pick.m) {
         const uint32_t k = (uint32_t)pick.idx[t];
-        if (k >= k0 && k < k1 && k <= ncells) {
+        if (k <= ncells) {
             const uint32_t v = cs[k];
             pick.out[t] = v;
             if (pick.out_host) pick.out_host[t] = v;
         }
     }
-}
-
-// The cell-start update (after k_mv_rank, the last reader of cs_old, and from its tables).
-__global__ __launch_bounds__(MV_BLK) void k_mv_cells(const uint32_t* __restrict__ mtotal, ResortScratch w,
-                                                     uint32_t* __restrict__ cs, uint32_t ncells, CsPick pick) {
-    __shared__ uint32_t b[4];
-    __shared__ uint64_t lms[MV_LDS];
-    __shared__ uint32_t lmo[MV_LDS];
-    mv_cell_start(cs, ncells, *mtotal, w, blockIdx.x, b, pick, lms, lmo);
 }
 
 // The slab step's halo records: new keys (window sentinel, as k_keys) and old keys moved into this
@@ -744,10 +636,9 @@ void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const u
     if (n <= 0) return;
     const int32_t nbk = (n + MV_BLK - 1) / MV_BLK;
     // n is an upper bound of the slots on device-sized steps: the rank kernel's ranges split the device count
-    SPH_LAUNCH(k_mv_rank, std::min(MV_RANK_GRID, nbk), RK_BLK, 0, s, count, count_other, cs, w, src, n, pos_o, vel_o, id_o,
-               sk_o, ex);
-    const int32_t ncs = (int32_t)((ncells + MV_CS_CELLS) / MV_CS_CELLS);
-    SPH_LAUNCH(k_mv_cells, ncs, MV_BLK, 0, s, count, w, cs, ncells, pick);
+    const uint32_t G = (uint32_t)std::min(MV_RANK_GRID, nbk);
+    SPH_LAUNCH(k_mv_rank, G, RK_BLK, 0, s, count, count_other, cs, ncells, w, src, n, pos_o, vel_o, id_o, sk_o, ex);
+    SPH_LAUNCH(k_mv_bounds, 1, MV_BLK, 0, s, w, G, cs, ncells, pick);
 }
 
 }  // namespace sph

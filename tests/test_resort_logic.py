@@ -55,7 +55,7 @@ def test_resort_formulas_match_stable_sort(frac):
         assert np.array_equal(cs_new, np.searchsorted(newk[ref], np.arange(nc + 1), side="left"))
 
 
-def range_ranks(ks, newk, G, win=2048):
+def range_ranks(ks, newk, G, win=2048, blocks=False):
     """resort.hip k_mv_rank restated: workgroup b owns the old slots [x0, x1) = [b·n/G, (b+1)·n/G) and the new keys
     [ks[x0], ks[x1]) (first range from 0, last to infinity); rk counts the movers below the key range plus those in
     range with a smaller (key, slot). The slots staged are those in [xw, x1), xw = x0 − win: a source entry's rank is
@@ -69,8 +69,11 @@ def range_ranks(ks, newk, G, win=2048):
     rk = np.full(len(movers), -1, np.int64)
     ri = np.full(len(movers), -1, np.int64)
     aq = np.full(len(movers), -1, np.int64)
+    cs_new = np.full(nc + 1, -1, np.int64)
+    bnd = []
+    nbk = (n + 255) // 256 if blocks else n
     for b in range(G):
-        x0, x1 = n * b // G, n * (b + 1) // G
+        x0, x1 = min(nbk * b // G * (256 if blocks else 1), n), min(nbk * (b + 1) // G * (256 if blocks else 1), n)
         kd0 = 0 if b == 0 else (ks[x0] if x0 < n else np.iinfo(np.int64).max)
         kd1 = np.iinfo(np.int64).max if b == G - 1 else (ks[x1] if x1 < n else np.iinfo(np.int64).max)
         xw = max(x0 - win, 0)
@@ -92,7 +95,19 @@ def range_ranks(ks, newk, G, win=2048):
         for e in np.nonzero(ins)[0]:
             assert ri[e] < 0, "a mover in two slot ranges"
             ri[e] = below_x0 + int(np.searchsorted(staged, movers[e], side="left")) - r0
-    return movers, mk, rk, ri, aq, cs_old
+        # the range's cells kd0 < k < kd1 in place, its first cell kd0 through the boundary table
+        if x0 < n or b == 0:
+            mo = ks[movers]
+            below_ko = int((mo < kd0).sum())
+            dkeys = np.sort(mk[ind])
+            okeys = np.sort(mo[(mo >= kd0) & (mo < kd1)])
+            for k in range(int(kd0) + 1, int(min(kd1, nc + 1))):
+                d = below_k - below_ko + int(np.searchsorted(dkeys, k)) - int(np.searchsorted(okeys, k))
+                cs_new[k] = cs_old[k] + d
+            bnd.append((int(kd0), int(cs_old[kd0]) + below_k - below_ko))
+    for k, v in bnd:
+        cs_new[k] = v
+    return movers, mk, rk, ri, aq, cs_old, cs_new
 
 
 @pytest.mark.parametrize("frac", [0.0, 0.01, 0.3, 1.0])
@@ -107,9 +122,13 @@ def test_range_ranks_equal_global_ranks(frac, G):
         mv = rng.random(n) < frac
         newk[mv] = rng.integers(0, nc + 1, int(mv.sum()))    # nc: the sentinel key (inactive / left the window)
         win = int(rng.integers(1, 64)) if rng.random() < 0.5 else 2048   # small windows: the counted fallback
-        movers, mk, rk, ri, aq, cs_old = range_ranks(ks, newk, min(G, max(n // 256, 1)) if G == 256 else G, win)
+        blocks = bool(rng.random() < 0.5)   # ranges of whole 256-slot blocks (the kernel) or of n/G slots
+        movers, mk, rk, ri, aq, cs_old, cs_new = range_ranks(ks, newk, min(G, max(n // 256, 1)) if G == 256 else G,
+                                                             win, blocks)
         c = _comp(mk, movers)
         assert np.array_equal(rk, np.argsort(np.argsort(c, kind="stable"), kind="stable"))
         assert np.array_equal(ri, np.arange(len(movers)))
         q = np.minimum(np.maximum(movers, cs_old[mk]), cs_old[mk + 1])
         assert np.array_equal(aq, np.searchsorted(movers, q, side="left"))
+        ref = np.sort(newk, kind="stable")
+        assert np.array_equal(cs_new, np.searchsorted(ref, np.arange(len(cs_new)), side="left"))
