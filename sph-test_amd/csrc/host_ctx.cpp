@@ -56,7 +56,7 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
     // incremental re-sort (both models)
     AL(sk_cur, n); AL(sk_next, n);
     AL(mv_mi, n); AL(mv_mk, n); AL(mv_mo, n); AL(mv_mx, n); AL(mv_mos, n); AL(mv_ms, n);
-    AL(mv_count, 2); AL(mv_bnd, 512);
+    AL(mv_count, 2); AL(mv_bnd, 2 * (size_t)resort_ranges((int32_t)n));
     HIPCHK(hipMemset(ctx->mv_count, 0, 2 * sizeof(uint32_t)));
 #undef AL
     ctx->staging_bytes = n * 84;

@@ -122,8 +122,11 @@ static __device__ __forceinline__ uint32_t lower_bound(const T* __restrict__ a, 
 constexpr int MV_RANK_GRID = 256;   // workgroups at most; one per CU
 constexpr int RK_U = 8;             // movers per lane per streaming round
 constexpr int MV_RK_CAP = 2048;     // dest entries staged per workgroup (a power of two)
-constexpr int RK_BM_WORDS = 2048;   // slot-presence bitmap over [xw, x1): ranges up to 65,536 slots (~100 KB of LDS in all)
+constexpr int RK_BM_WORDS = 4096;   // slot-presence bitmap over [xw, x1): up to 131,072 slots (~100 KB of LDS in all)
 constexpr int RK_WIN = 2048;        // slot entries staged below x0 (covers the cell holding x0)
+// the longest range the bitmap covers with its window and the 256-slot rounding: the grid grows past MV_RANK_GRID
+// workgroups above 256 such ranges (C5 single-context, 16.8M particles: 129 ranges fit in 256)
+constexpr uint32_t RK_MAX_RANGE = 32u * RK_BM_WORDS - RK_WIN - 256u;
 constexpr int RK_COUNT = 256;       // dest entries ranked by counting, more by sorting
 constexpr int RK_KD1_CAP = 1024;    // movers into the cell a range ends in, staged
 constexpr int RK_SU = 4;            // stayer slots per lane in flight
@@ -132,9 +135,9 @@ constexpr int RK_OK_CAP = 2048;     // movers' old keys in the key range, staged
 // after the mover stream, after the sorts and at its end, with its entry counts.
 #ifdef SPH_RANK_PROBE
 __device__ uint64_t g_rank_probe[MV_RANK_GRID * 8];
-#define RK_PROBE(slot, val)                                                          \
-    do {                                                                             \
-        if (threadIdx.x == 0) g_rank_probe[blockIdx.x * 8 + (slot)] = (uint64_t)(val); \
+#define RK_PROBE(slot, val)                                                                            \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < MV_RANK_GRID) g_rank_probe[blockIdx.x * 8 + (slot)] = (uint64_t)(val); \
     } while (0)
 #else
 #define RK_PROBE(slot, val) \
@@ -630,13 +633,18 @@ extern "C" int sph_debug_rank_probe(uint64_t* out) {
 }
 #endif
 
+uint32_t resort_ranges(int32_t n) {
+    const uint32_t nbk = ((uint32_t)std::max(n, 1) + 255u) / 256u;
+    const uint32_t need = ((uint32_t)std::max(n, 1) + RK_MAX_RANGE - 1u) / RK_MAX_RANGE;
+    return std::min(nbk, std::max((uint32_t)MV_RANK_GRID, need + 1u));
+}
+
 void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* count,
                    uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,
                    uint32_t* sk_o, hipStream_t s, CsPick pick, ResortExtra ex) {
     if (n <= 0) return;
-    const int32_t nbk = (n + MV_BLK - 1) / MV_BLK;
     // n is an upper bound of the slots on device-sized steps: the rank kernel's ranges split the device count
-    const uint32_t G = (uint32_t)std::min(MV_RANK_GRID, nbk);
+    const uint32_t G = resort_ranges(n);
     SPH_LAUNCH(k_mv_rank, G, RK_BLK, 0, s, count, count_other, cs, ncells, w, src, n, pos_o, vel_o, id_o, sk_o, ex);
     SPH_LAUNCH(k_mv_bounds, 1, MV_BLK, 0, s, w, G, cs, ncells, pick);
 }
