@@ -323,10 +323,17 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
     RK_PROBE(4, nd);
     RK_PROBE(5, cnt[1]);
     RK_PROBE(6, m);
-    if (bits_ok) {   // the bitmap's word prefix
-        const uint32_t nw = (x1 - xw + 31u) >> 5, w0 = 2 * threadIdx.x;   // two words per lane
-        const uint32_t c0 = w0 < nw ? (uint32_t)__popc(bm[w0]) : 0u, c1 = w0 + 1 < nw ? (uint32_t)__popc(bm[w0 + 1]) : 0u;
-        uint32_t inc = c0 + c1;
+    if (bits_ok) {   // the bitmap's word prefix: RK_BM_WORDS / RK_BLK consecutive words per lane
+        constexpr uint32_t WPL = RK_BM_WORDS / RK_BLK;
+        static_assert(WPL * RK_BLK == RK_BM_WORDS, "bitmap words per lane");
+        const uint32_t nw = (x1 - xw + 31u) >> 5, w0 = WPL * threadIdx.x;
+        uint32_t c[WPL], inc = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < WPL; ++j) {
+            c[j] = w0 + j < nw ? (uint32_t)__popc(bm[w0 + j]) : 0u;
+            inc += c[j];
+        }
+        const uint32_t mine = inc;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
@@ -337,10 +344,13 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
         __syncthreads();
         uint32_t pre = 0;
         for (uint32_t k = 0; k < (threadIdx.x >> 6); ++k) pre += red[k];
-        const uint32_t ex0 = pre + inc - c0 - c1;
-        if (w0 <= nw) bpre[w0] = ex0;
-        if (w0 + 1 <= nw) bpre[w0 + 1] = ex0 + c0;
-        if (nw == (uint32_t)RK_BM_WORDS && threadIdx.x == RK_BLK - 1) bpre[RK_BM_WORDS] = pre + inc;
+        uint32_t run = pre + inc - mine;   // words before w0
+#pragma unroll
+        for (uint32_t j = 0; j < WPL; ++j) {
+            if (w0 + j <= nw) bpre[w0 + j] = run;
+            run += c[j];
+        }
+        if (nw == (uint32_t)RK_BM_WORDS && threadIdx.x == RK_BLK - 1) bpre[RK_BM_WORDS] = run;
     }
     // the dest entries and the old keys in order: up to RK_COUNT of them each lane counts the smaller ones (LDS
     // broadcast reads, no barrier stages), more are sorted (lds_sort)
