@@ -29,5 +29,5 @@ for s in range(0, a.steps, a.sample):
     sim.step(k)
     ms.append(sim.ctx.mover_count())
 print({"config": a.config, "advance": a.advance, "steps": a.steps, "movers_sampled": ms,
-       "movers_mean": round(sum(ms) / len(ms), 1), "resort_limit": max(4096, int(12 * sim.n ** 0.5))}, flush=True)
+       "movers_mean": round(sum(ms) / len(ms), 1), "resort_limit": max(4096, min(sim.n // 16, 262144))}, flush=True)
 sim.close()

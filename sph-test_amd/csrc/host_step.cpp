@@ -116,12 +116,11 @@ MoverSink mover_sink(sph_ctx* ctx) {
 
 // Bring the slots into stable (key, index) order: the incremental re-sort when the previous
 // step's sorted keys and cell starts describe the current slot order, else the full radix sort.
-// Movers above which the full radix sort is taken instead of the incremental re-sort. Until r4 k_mv_rank counted
-// all pairs of movers (m², crossing the full sort's cost at ~12k movers at C3, the limit was 12·√n); its ranges are
-// O(m) per workgroup now, and the re-sort's cost is the stayers' scatter (n) plus a few passes over the movers, so the
-// full sort (three 8-bit passes, a gather and the cell starts over n) pays only when a large share moves.
+// Movers above which the full radix sort is taken instead of the incremental re-sort. k_mv_rank's work is O(m) per
+// workgroup plus its slots (every workgroup streams the mover list), so the full sort (three 8-bit passes, a gather
+// and the cell starts over n) pays only when a large share moves; capped so that a range's entries stay within LDS.
 uint32_t resort_limit(int32_t n) {
-    return std::max<uint32_t>(4096u, (uint32_t)std::max(n, 0) / 16u);
+    return std::max<uint32_t>(4096u, std::min<uint32_t>((uint32_t)std::max(n, 0) / 16u, 262144u));
 }
 
 int sort_wcsph(sph_ctx* ctx) {

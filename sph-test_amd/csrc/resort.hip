@@ -122,11 +122,13 @@ static __device__ __forceinline__ uint32_t lower_bound(const T* __restrict__ a, 
 constexpr int MV_RANK_GRID = 256;   // workgroups at most; one per CU
 constexpr int RK_U = 8;             // movers per lane per streaming round
 constexpr int MV_RK_CAP = 2048;     // dest entries staged per workgroup (a power of two)
-constexpr int RK_BM_WORDS = 4096;   // slot-presence bitmap over [xw, x1): up to 131,072 slots (~100 KB of LDS in all)
+constexpr int RK_BM_WORDS = 1024;   // slot-presence bitmap over [xw, x1): up to 32,768 slots
 constexpr int RK_WIN = 2048;        // slot entries staged below x0 (covers the cell holding x0)
-// the longest range the bitmap covers with its window and the 256-slot rounding: the grid grows past MV_RANK_GRID
-// workgroups above 256 such ranges (C5 single-context, 16.8M particles: 129 ranges fit in 256)
-constexpr uint32_t RK_MAX_RANGE = 32u * RK_BM_WORDS - RK_WIN - 256u;
+// Slots per range at most: the grid grows past MV_RANK_GRID workgroups for n > 2M (C5 single-context: 2,048 ranges;
+// every workgroup streams the whole mover list, so that costs ~G·m, small against such a step), which keeps a range's
+// entries within LDS (a C5 range of 65,536 slots held more old keys than RK_OK_CAP mid-run, r5).
+constexpr uint32_t RK_MAX_RANGE = 8192;
+static_assert(RK_MAX_RANGE + RK_WIN + 512u <= 32u * RK_BM_WORDS, "a range and its window fit the bitmap");
 constexpr int RK_COUNT = 256;       // dest entries ranked by counting, more by sorting
 constexpr int RK_KD1_CAP = 1024;    // movers into the cell a range ends in, staged
 constexpr int RK_SU = 4;            // stayer slots per lane in flight
@@ -237,7 +239,6 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
                                                     float4* __restrict__ vel_o, int32_t* __restrict__ id_o,
                                                     uint32_t* __restrict__ sk_o, ResortExtra ex) {
     __shared__ uint64_t dk[MV_RK_CAP];   // dest entries (new key, slot)
-    __shared__ uint32_t dr[MV_RK_CAP];   // their mover index
     __shared__ uint64_t ds[MV_RK_CAP];   // the dest entries in (key, slot) order
     __shared__ uint64_t ok[RK_OK_CAP];   // old keys in [kd0, kd1) (old key, mover index)
     __shared__ uint64_t oks[RK_OK_CAP];  // the same in order
@@ -297,7 +298,7 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
             below_ko += okr && o < kd0 ? 1u : 0u;
             if (okr && k >= kd0 && k < kd1) {
                 const uint32_t p = atomicAdd(&cnt[0], 1u);
-                if (p < MV_RK_CAP) { dk[p] = comp(k, x); dr[p] = r; }
+                if (p < MV_RK_CAP) dk[p] = comp(k, x);
             }
             if (okr && k == kd1) {
                 const uint32_t p = atomicAdd(&cnt[2], 1u);
@@ -385,11 +386,6 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
         for (uint32_t f = 0; f < m; ++f) c += comp(w.mk[f], mv_slot(w, w.mi[f])) < v ? 1u : 0u;
         return c;
     };
-    auto count_old = [&](uint32_t k) {     // #movers with old key < k
-        uint32_t c = 0;
-        for (uint32_t f = 0; f < m; ++f) c += w.mo[f] < k ? 1u : 0u;
-        return c;
-    };
     // #movers with slot < y: below x0 plus (minus) the staged slots between x0 and y
     auto rank_of = [&](uint32_t y) {   // #staged slots in [xw, y), y in [xw, x1]
         const uint32_t d = min(y, x1) - xw, wd = d >> 5;
@@ -475,9 +471,14 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
         const int32_t base_d = (int32_t)below_k - (int32_t)below_ko;
         for (uint32_t k = kd0 + 1u + threadIdx.x; k < khi; k += RK_BLK) {
             const uint32_t cn = dest_staged ? lower_bound(sd, nd, comp(k, 0u)) : count_dest(comp(k, 0u)) - below_k;
-            const uint32_t co = old_staged ? lower_bound(so, no, comp(k, 0u)) : count_old(k) - below_ko;
-            const int32_t dlt = base_d + (int32_t)cn - (int32_t)co;
-            if (dlt != 0) cs[k] = (uint32_t)((int32_t)cs[k] + dlt);
+            if (old_staged) {
+                const uint32_t co = lower_bound(so, no, comp(k, 0u));
+                const int32_t dlt = base_d + (int32_t)cn - (int32_t)co;
+                if (dlt != 0) cs[k] = (uint32_t)((int32_t)cs[k] + dlt);
+            } else {   // more old keys than LDS holds: #movers with old key < k = #movers with slot < cs_old[k]
+                const uint32_t c = cs[k];
+                cs[k] = c + (below_k + cn) - slots_below(c);
+            }
         }
         if (threadIdx.x == 0) {
             w.bnd[b] = kd0;
@@ -646,7 +647,7 @@ extern "C" int sph_debug_rank_probe(uint64_t* out) {
 uint32_t resort_ranges(int32_t n) {
     const uint32_t nbk = ((uint32_t)std::max(n, 1) + 255u) / 256u;
     const uint32_t need = ((uint32_t)std::max(n, 1) + RK_MAX_RANGE - 1u) / RK_MAX_RANGE;
-    return std::min(nbk, std::max((uint32_t)MV_RANK_GRID, need + 1u));
+    return std::min(nbk, std::max((uint32_t)MV_RANK_GRID, need + 1u));   // (+1: the ranges are whole 256-slot blocks)
 }
 
 void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* count,
