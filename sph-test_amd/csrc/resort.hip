@@ -133,6 +133,7 @@ constexpr int RK_COUNT = 256;       // dest entries ranked by counting, more by 
 constexpr int RK_KD1_CAP = 1024;    // movers into the cell a range ends in, staged
 constexpr int RK_SU = 4;            // stayer slots per lane in flight
 constexpr int RK_OK_CAP = 2048;     // movers' old keys in the key range, staged
+constexpr int RK_EV_CAP = 2048;     // cell events (dest + old keys) of a range handled by segments
 // Test-only timing probe (scripts/rank_probe.py, a -DSPH_RANK_PROBE build): per workgroup the wall clock at its start,
 // after the mover stream, after the sorts and at its end, with its entry counts.
 #ifdef SPH_RANK_PROBE
@@ -244,6 +245,10 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
     __shared__ uint64_t oks[RK_OK_CAP];  // the same in order
     __shared__ uint32_t kx1[RK_KD1_CAP]; // slots of the movers whose new key is kd1 (the cell the range ends in)
     __shared__ uint32_t bm[RK_BM_WORDS + 1], bpre[RK_BM_WORDS + 1];   // movers' slots in [xw, x1): bits, word prefix
+    __shared__ uint32_t ev[RK_EV_CAP];   // the cell events: keys (dest then old at equal keys), and their ±1
+    __shared__ int32_t evd[RK_EV_CAP];
+    __shared__ int32_t sgd[RK_EV_CAP + 1];   // segments between events: Δ and first written cell
+    __shared__ uint32_t sgl[RK_EV_CAP + 1];
     __shared__ uint32_t cnt[4], red[RK_BLK / 64];
     RK_PROBE(0, wall_clock64());
     resolve_sizes(src, w, n);
@@ -467,17 +472,116 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
     // and k_mv_bounds writes it after the launch.
     __syncthreads();
     if (kd0 != 0xffffffffu) {
-        const uint32_t khi = min(kd1, ncells + 1u);
+        const uint32_t klo = kd0 + 1u, khi = max(min(kd1, ncells + 1u), klo);
         const int32_t base_d = (int32_t)below_k - (int32_t)below_ko;
-        for (uint32_t k = kd0 + 1u + threadIdx.x; k < khi; k += RK_BLK) {
-            const uint32_t cn = dest_staged ? lower_bound(sd, nd, comp(k, 0u)) : count_dest(comp(k, 0u)) - below_k;
-            if (old_staged) {
-                const uint32_t co = lower_bound(so, no, comp(k, 0u));
-                const int32_t dlt = base_d + (int32_t)cn - (int32_t)co;
-                if (dlt != 0) cs[k] = (uint32_t)((int32_t)cs[k] + dlt);
-            } else {   // more old keys than LDS holds: #movers with old key < k = #movers with slot < cs_old[k]
-                const uint32_t c = cs[k];
-                cs[k] = c + (below_k + cn) - slots_below(c);
+        const uint32_t E = nd + no;
+        if (dest_staged && old_staged && E <= (uint32_t)RK_EV_CAP) {
+            // Δ(k) = base + #{dest keys < k} − #{old keys < k} is constant between the entries' keys: merge the two
+            // sorted key lists into events (+1 / −1 at key + 1), then write only the cells of the segments where
+            // Δ != 0, spread evenly over the lanes (a range can hold long runs of empty cells, where Δ is often 0).
+            for (uint32_t t = threadIdx.x; t < nd; t += RK_BLK) {
+                const uint32_t key = (uint32_t)(sd[t] >> 32);
+                uint32_t lo = 0, hi = no;   // old keys < key (dest events first at equal keys)
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if ((uint32_t)(so[mid] >> 32) < key) lo = mid + 1;
+                    else hi = mid;
+                }
+                ev[t + lo] = key;
+                evd[t + lo] = 1;
+            }
+            for (uint32_t t = threadIdx.x; t < no; t += RK_BLK) {
+                const uint32_t key = (uint32_t)(so[t] >> 32);
+                uint32_t lo = 0, hi = nd;   // dest keys <= key
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if ((uint32_t)(sd[mid] >> 32) <= key) lo = mid + 1;
+                    else hi = mid;
+                }
+                ev[t + lo] = key;
+                evd[t + lo] = -1;
+            }
+            __syncthreads();
+            // segment j in [0, E]: cells [start_j, end_j), Δ_j = base + Σ_{i<j} evd[i]; lengths of the Δ != 0 ones
+            constexpr uint32_t SPL = (RK_EV_CAP + RK_BLK) / RK_BLK;   // segments per lane
+            const uint32_t j0 = SPL * threadIdx.x;
+            int32_t dsum = 0;
+            for (uint32_t j = j0; j < min(j0 + SPL, E); ++j) dsum += evd[j];
+            uint32_t lsum = 0;
+            // the lane's Δ before j0: a block scan of the event sums
+            int32_t inc = dsum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t u = __shfl_up(inc, o, 64);
+                if (lane_id() >= (uint32_t)o) inc += u;
+            }
+            if (lane_id() == 63) red[threadIdx.x >> 6] = (uint32_t)inc;
+            __syncthreads();
+            int32_t dpre = base_d;
+            for (uint32_t k = 0; k < (threadIdx.x >> 6); ++k) dpre += (int32_t)red[k];
+            dpre += inc - dsum;
+            auto seg = [&](uint32_t j, uint32_t& st, uint32_t& en) {
+                st = j == 0 ? klo : max(ev[j - 1] + 1u, klo);
+                en = j == E ? khi : min(ev[j] + 1u, khi);
+                if (en < st) en = st;
+            };
+            {
+                int32_t dj = dpre;
+                for (uint32_t j = j0; j < min(j0 + SPL, E + 1u); ++j) {
+                    uint32_t st, en;
+                    seg(j, st, en);
+                    const uint32_t len = dj != 0 ? en - st : 0u;
+                    sgd[j] = dj;
+                    sgl[j] = len;
+                    lsum += len;
+                    if (j < E) dj += evd[j];
+                }
+            }
+            __syncthreads();   // red reused
+            uint32_t linc = lsum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = (uint32_t)__shfl_up((int)linc, o, 64);
+                if (lane_id() >= (uint32_t)o) linc += u;
+            }
+            if (lane_id() == 63) red[threadIdx.x >> 6] = linc;
+            __syncthreads();
+            uint32_t lpre = 0, T = 0;
+            for (uint32_t k = 0; k < RK_BLK / 64; ++k) {
+                lpre += k < (threadIdx.x >> 6) ? red[k] : 0u;
+                T += red[k];
+            }
+            lpre += linc - lsum;
+            for (uint32_t j = j0; j < min(j0 + SPL, E + 1u); ++j) {   // segment j's first cell in the written order
+                const uint32_t len = sgl[j];
+                sgl[j] = lpre;
+                lpre += len;
+            }
+            __syncthreads();
+            for (uint32_t t = threadIdx.x; t < T; t += RK_BLK) {
+                uint32_t lo = 0, hi = E + 1u;   // the last segment whose first written cell is <= t
+                while (hi - lo > 1u) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (sgl[mid] <= t) lo = mid;
+                    else hi = mid;
+                }
+                while (lo < E && sgl[lo + 1] <= t) ++lo;   // skip empty segments that share the offset
+                uint32_t st, en;
+                seg(lo, st, en);
+                const uint32_t k = st + (t - sgl[lo]);
+                cs[k] = (uint32_t)((int32_t)cs[k] + sgd[lo]);
+            }
+        } else {   // entries past LDS: cell by cell
+            for (uint32_t k = klo + threadIdx.x; k < khi; k += RK_BLK) {
+                const uint32_t cn = dest_staged ? lower_bound(sd, nd, comp(k, 0u)) : count_dest(comp(k, 0u)) - below_k;
+                if (old_staged) {
+                    const uint32_t co = lower_bound(so, no, comp(k, 0u));
+                    const int32_t dlt = base_d + (int32_t)cn - (int32_t)co;
+                    if (dlt != 0) cs[k] = (uint32_t)((int32_t)cs[k] + dlt);
+                } else {   // more old keys than LDS holds: #movers with old key < k = #movers with slot < cs_old[k]
+                    const uint32_t c = cs[k];
+                    cs[k] = c + (below_k + cn) - slots_below(c);
+                }
             }
         }
         if (threadIdx.x == 0) {

@@ -101,9 +101,22 @@ def range_ranks(ks, newk, G, win=2048, blocks=False):
             below_ko = int((mo < kd0).sum())
             dkeys = np.sort(mk[ind])
             okeys = np.sort(mo[(mo >= kd0) & (mo < kd1)])
-            for k in range(int(kd0) + 1, int(min(kd1, nc + 1))):
+            klo, khi = int(kd0) + 1, max(int(min(kd1, nc + 1)), int(kd0) + 1)
+            for k in range(klo, khi):
                 d = below_k - below_ko + int(np.searchsorted(dkeys, k)) - int(np.searchsorted(okeys, k))
                 cs_new[k] = cs_old[k] + d
+            # the kernel's segment form: events +1 (dest key) / −1 (old key) merged, Δ constant between them
+            ev = sorted([(int(k), 0, 1) for k in dkeys] + [(int(k), 1, -1) for k in okeys])
+            seg_cs = {}
+            dlt = below_k - below_ko
+            for j in range(len(ev) + 1):
+                st = klo if j == 0 else max(ev[j - 1][0] + 1, klo)
+                en = khi if j == len(ev) else min(ev[j][0] + 1, khi)
+                for k in range(st, max(en, st)):
+                    seg_cs[k] = cs_old[k] + dlt
+                if j < len(ev):
+                    dlt += ev[j][2]
+            assert all(seg_cs.get(k, cs_old[k]) == cs_new[k] for k in range(klo, khi))
             bnd.append((int(kd0), int(cs_old[kd0]) + below_k - below_ko))
     for k, v in bnd:
         cs_new[k] = v
