@@ -702,8 +702,9 @@ int phase_assemble(RankState& R, bool exact) {
         ResortScratch w = resort_scratch(ctx);
         w.dz = R.dz;
         w.err = &R.dz->flags;
-        launch_resort(src, ctx->cs, ctx->grid.ncells, n_ub, ctx->mv_count + used, ctx->mv_count + (1 - used), w,
-                      ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, s, pick);
+        launch_resort(src, ctx->cs, ctx->cs2, ctx->grid.ncells, n_ub, ctx->mv_count + used, ctx->mv_count + (1 - used),
+                      w, ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, s, pick);
+        swap_cs(ctx);
         CKPT(R, "resort");   // (k_mv_rank stored the mover count for the host)
         ctx->mv_par = 1 - used;
         swap_sv(ctx);

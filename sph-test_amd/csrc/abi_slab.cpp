@@ -284,8 +284,9 @@ int sph::slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const voi
         for (int k = 0; k < 8; ++k) pick.idx[k] = idx[k];
         ResortScratch w = resort_scratch(ctx);
         w.mi_off = nl - ctx->o0;   // own movers were appended by slot in the previous order
-        launch_resort(src, ctx->cs, ctx->grid.ncells, (int32_t)n, ctx->mv_count + used, ctx->mv_count + (1 - used), w,
-                      ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, s, pick);
+        launch_resort(src, ctx->cs, ctx->cs2, ctx->grid.ncells, (int32_t)n, ctx->mv_count + used,
+                      ctx->mv_count + (1 - used), w, ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, s, pick);
+        swap_cs(ctx);
         ctx->mv_par = 1 - used;   // (k_mv_rank stored the mover count for the host)
         swap_sv(ctx);
         std::swap(ctx->id, ctx->id2);

@@ -356,7 +356,6 @@ struct ResortScratch {
     const SlabSizes* dz = nullptr;   // non-null: mi_off = nl - o0 from the device sizes
     uint32_t* err = nullptr;         // SZ_OVF_MOVERS if a destination would pass cap (never written)
     uint32_t* host_count = nullptr;  // mapped host memory: k_mv_rank stores the mover count there (the host's sort choice)
-    uint32_t* bnd = nullptr;         // [2 * resort_ranges(n)]: the ranges' first cells and their new starts (k_mv_bounds)
 };
 // a mover entry whose mi has this bit holds a slot of the assembled array (a halo record's);
 // without it, mi is the force pass's slot and the assembled slot is mi + mi_off
@@ -519,7 +518,8 @@ struct ResortExtra {
 };
 // k_mv_rank's workgroups (key/slot ranges) for n slots
 uint32_t resort_ranges(int32_t n);
-void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* count,
+// cs: the old cell-start table (read), cs_new: the new one (every entry written)
+void launch_resort(AsmSrc src, uint32_t* cs, uint32_t* cs_new, uint32_t ncells, int32_t n, const uint32_t* count,
                    uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,
                    uint32_t* sk_o, hipStream_t s, CsPick pick = CsPick{{0}, 0, nullptr, nullptr},
                    ResortExtra ex = ResortExtra{});

@@ -87,6 +87,8 @@ struct sph_ctx {
     uint32_t *hist = nullptr, *bin_total = nullptr;
     uint32_t* cs = nullptr;
     uint32_t cs_cap = 0;
+    uint32_t* cs2 = nullptr;   // the incremental re-sort's new cell-start table (swapped with cs)
+    uint32_t cs2_cap = 0;
     uint4* gaps = nullptr;       // cell-start long-gap queue
     uint32_t gaps_cap = 0;
     void* staging = nullptr;
@@ -98,7 +100,6 @@ struct sph_ctx {
     uint32_t *sk_cur = nullptr, *sk_next = nullptr;
     uint32_t *mv_mi = nullptr, *mv_mk = nullptr, *mv_mo = nullptr, *mv_mx = nullptr, *mv_mos = nullptr;
     uint64_t* mv_ms = nullptr;
-    uint32_t* mv_bnd = nullptr;     // the re-sort's boundary-cell table (ResortScratch.bnd)
     uint32_t* mv_count = nullptr;   // [2] mover counters, ping-pong by step
     int mv_par = 0;                 // counter the next force pass appends into
     bool sk_valid = false;       // sk_cur matches the slot order and cs (set by a Model S sort)
@@ -262,6 +263,7 @@ struct KTimer {
 
 // per-step launch sequences (host_step.cpp)
 void swap_sv(sph_ctx* c);
+void swap_cs(sph_ctx* c);
 int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id, const uint32_t** sorted_keys = nullptr);
 // Model S pass 1 -> pass 2 (common.h): the density pass writes the mask (and marks it valid for the
 // current slot order); the force pass reads it only while valid, else scans by distance. Every change

@@ -10,12 +10,12 @@ void free_all(sph_ctx* c) {
     dfree(c->id); dfree(c->id2); dfree(c->mode); dfree(c->mode2);
     dfree(c->rp); dfree(c->torque); dfree(c->slot_of);
     dfree(c->keys); dfree(c->keys2); dfree(c->vals); dfree(c->vals2); dfree(c->hist); dfree(c->bin_total);
-    dfree(c->cs); dfree(c->gaps);
+    dfree(c->cs); dfree(c->cs2); dfree(c->gaps);
     c->gaps_cap = 0;
     dfree(c->sblk); dfree(c->sdev); dfree(c->paths); dfree(c->hmask);
     dfree(c->sk_cur); dfree(c->sk_next);
     dfree(c->mv_mi); dfree(c->mv_mk); dfree(c->mv_mo); dfree(c->mv_mx); dfree(c->mv_mos);
-    dfree(c->mv_ms); dfree(c->mv_count); dfree(c->mv_bnd);
+    dfree(c->mv_ms); dfree(c->mv_count);
     dfree(c->sched);
     c->sched_cap = 0;
     c->sched_valid = false;
@@ -56,7 +56,7 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
     // incremental re-sort (both models)
     AL(sk_cur, n); AL(sk_next, n);
     AL(mv_mi, n); AL(mv_mk, n); AL(mv_mo, n); AL(mv_mx, n); AL(mv_mos, n); AL(mv_ms, n);
-    AL(mv_count, 2); AL(mv_bnd, 2 * (size_t)resort_ranges((int32_t)n));
+    AL(mv_count, 2);
     HIPCHK(hipMemset(ctx->mv_count, 0, 2 * sizeof(uint32_t)));
 #undef AL
     ctx->staging_bytes = n * 84;
@@ -71,6 +71,11 @@ int ensure_cells(sph_ctx* ctx) {
         int r = dalloc(ctx, &ctx->cs, need);
         if (r != SPH_OK) return r;
         ctx->cs_cap = need;
+    }
+    if (need > ctx->cs2_cap) {
+        int r = dalloc(ctx, &ctx->cs2, need);
+        if (r != SPH_OK) return r;
+        ctx->cs2_cap = need;
     }
     // queued chunks: one per long gap (> 32 cells, so at most (ncells+1)/33) plus one per
     // 8192 cells of gap length

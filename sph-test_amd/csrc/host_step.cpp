@@ -8,6 +8,12 @@ void swap_sv(sph_ctx* c) {
     std::swap(c->vel, c->vel2);
 }
 
+// the incremental re-sort wrote the new cell-start table into cs2
+void swap_cs(sph_ctx* c) {
+    std::swap(c->cs, c->cs2);
+    std::swap(c->cs_cap, c->cs2_cap);
+}
+
 int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id, const uint32_t** sorted_keys) {
     const int32_t n = ctx->n;
     if (!ctx->keys_valid || ctx->keys_active != n_active_id) {
@@ -103,7 +109,6 @@ ResortScratch resort_scratch(sph_ctx* ctx) {
     ResortScratch w{ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_ms, ctx->mv_mx, ctx->mv_mos,
                     (uint32_t)std::max(ctx->capacity, 1), 0};
     w.host_count = ctx->mv_host_dev;
-    w.bnd = ctx->mv_bnd;
     return w;
 }
 
@@ -133,11 +138,12 @@ int sort_wcsph(sph_ctx* ctx) {
         {
             KTimer t(ctx, "resort", (double)n * (2 * 4 + 2 * 36), true);
             const int used = ctx->mv_par;
-            launch_resort(asm_plain(ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->keys, n), ctx->cs,
+            launch_resort(asm_plain(ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->keys, n), ctx->cs, ctx->cs2,
                           ctx->grid.ncells, n, ctx->mv_count + used, ctx->mv_count + (1 - used), resort_scratch(ctx),
                           ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, ctx->stream);
             ctx->mv_par = 1 - used;
         }
+        swap_cs(ctx);
         ctx->sorted_full = false;
         swap_sv(ctx);
         std::swap(ctx->id, ctx->id2);
@@ -250,10 +256,11 @@ int sort_contact(sph_ctx* ctx, int32_t act) {
         KTimer t(ctx, "resort", (double)n * (2 * 4 + 2 * 88));
         const int used = ctx->mv_par;
         const ResortExtra ex{ctx->omg, ctx->rot, ctx->aux, ctx->mode, ctx->omg2, ctx->rot2, ctx->aux2, ctx->mode2};
-        launch_resort(asm_plain(ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->keys, n), ctx->cs, ctx->grid.ncells, n,
+        launch_resort(asm_plain(ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->keys, n), ctx->cs, ctx->cs2, ctx->grid.ncells, n,
                       ctx->mv_count + used, ctx->mv_count + (1 - used), resort_scratch(ctx), ctx->pos2, ctx->vel2,
                       ctx->id2, ctx->sk_next, ctx->stream, CsPick{{0}, 0, nullptr, nullptr}, ex);
         ctx->mv_par = 1 - used;
+        swap_cs(ctx);
         ctx->sorted_full = false;
         swap_sv(ctx);
         std::swap(ctx->id, ctx->id2);

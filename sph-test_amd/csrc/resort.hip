@@ -132,8 +132,8 @@ static_assert(RK_MAX_RANGE + RK_WIN + 512u <= 32u * RK_BM_WORDS, "a range and it
 constexpr int RK_COUNT = 256;       // dest entries ranked by counting, more by sorting
 constexpr int RK_KD1_CAP = 1024;    // movers into the cell a range ends in, staged
 constexpr int RK_SU = 4;            // stayer slots per lane in flight
-constexpr int RK_OK_CAP = 2048;     // movers' old keys in the key range, staged
-constexpr int RK_EV_CAP = 2048;     // cell events (dest + old keys) of a range handled by segments
+constexpr int RK_EV_CAP = 2048;     // movers' new / old keys in a cell chunk, staged
+constexpr int RK_CU = 4;            // cells per lane in flight
 // Test-only timing probe (scripts/rank_probe.py, a -DSPH_RANK_PROBE build): per workgroup the wall clock at its start,
 // after the mover stream, after the sorts and at its end, with its entry counts.
 #ifdef SPH_RANK_PROBE
@@ -235,30 +235,29 @@ __device__ void lds_sort(uint64_t* a, uint32_t* b, uint32_t len) {
 }
 
 __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__ mtotal, uint32_t* __restrict__ next_count,
-                                                    uint32_t* __restrict__ cs, uint32_t ncells, ResortScratch w,
-                                                    AsmSrc src, int32_t n, float4* __restrict__ pos_o,
-                                                    float4* __restrict__ vel_o, int32_t* __restrict__ id_o,
-                                                    uint32_t* __restrict__ sk_o, ResortExtra ex) {
+                                                    const uint32_t* __restrict__ cs, uint32_t* __restrict__ cs_new,
+                                                    uint32_t ncells, CsPick pick, ResortScratch w, AsmSrc src, int32_t n,
+                                                    float4* __restrict__ pos_o, float4* __restrict__ vel_o,
+                                                    int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o,
+                                                    ResortExtra ex) {
     __shared__ uint64_t dk[MV_RK_CAP];   // dest entries (new key, slot)
     __shared__ uint64_t ds[MV_RK_CAP];   // the dest entries in (key, slot) order
-    __shared__ uint64_t ok[RK_OK_CAP];   // old keys in [kd0, kd1) (old key, mover index)
-    __shared__ uint64_t oks[RK_OK_CAP];  // the same in order
+    __shared__ uint64_t en[RK_EV_CAP];   // movers' new keys in this workgroup's cell chunk [c0, c1) (key, index)
+    __shared__ uint64_t eo[RK_EV_CAP];   // their old keys in it
     __shared__ uint32_t kx1[RK_KD1_CAP]; // slots of the movers whose new key is kd1 (the cell the range ends in)
     __shared__ uint32_t bm[RK_BM_WORDS + 1], bpre[RK_BM_WORDS + 1];   // movers' slots in [xw, x1): bits, word prefix
-    __shared__ uint32_t ev[RK_EV_CAP];   // the cell events: keys (dest then old at equal keys), and their ±1
-    __shared__ int32_t evd[RK_EV_CAP];
-    __shared__ int32_t sgd[RK_EV_CAP + 1];   // segments between events: Δ and first written cell
-    __shared__ uint32_t sgl[RK_EV_CAP + 1];
-    __shared__ uint32_t cnt[4], red[RK_BLK / 64];
+    __shared__ uint32_t cnt[5], red[RK_BLK / 64];
     RK_PROBE(0, wall_clock64());
     resolve_sizes(src, w, n);
-    if (threadIdx.x < 4) cnt[threadIdx.x] = 0u;
+    if (threadIdx.x < 5) cnt[threadIdx.x] = 0u;
     for (uint32_t t = threadIdx.x; t <= (uint32_t)RK_BM_WORDS; t += RK_BLK) bm[t] = 0u;
     const uint32_t G = gridDim.x, b = blockIdx.x;
     // the ranges are whole blocks of 256 slots
     const uint32_t nbk = ((uint32_t)n + 255u) / 256u;
     const uint32_t x0 = min((uint32_t)((uint64_t)nbk * b / G) * 256u, (uint32_t)n);
     const uint32_t x1 = min((uint32_t)((uint64_t)nbk * (b + 1) / G) * 256u, (uint32_t)n);
+    // and an equal share of the cells [0, ncells]: cs_new[k] = cs[k] + #{movers: new key < k} − #{movers: old key < k}
+    const uint32_t c0 = (uint32_t)((uint64_t)(ncells + 1u) * b / G), c1 = (uint32_t)((uint64_t)(ncells + 1u) * (b + 1) / G);
     // Everything the stream needs in one round trip (the kernel is a chain of dependent round trips of ~1.5 us each,
     // r5 probe): the mover count, both range keys (pointer selects) and the first round of movers, whose loads are
     // clamped to the lists' capacity rather than to the count they would otherwise wait for.
@@ -291,7 +290,7 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
     const uint32_t xw = x0 > (uint32_t)RK_WIN ? x0 - (uint32_t)RK_WIN : 0u;
     const bool bits_ok = x1 - xw <= 32u * RK_BM_WORDS;   // block-uniform
     __syncthreads();
-    uint32_t below_k = 0, below_x0 = 0, below_ko = 0;
+    uint32_t below_k = 0, below_x0 = 0, bn_c = 0, bo_c = 0;
     for (uint32_t base = 0; base < m; base += RK_BLK * RK_U) {
 #pragma unroll
         for (int u = 0; u < RK_U; ++u) {
@@ -300,7 +299,8 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
             const uint32_t x = mv_slot(w, xs[u]), k = ks[u], o = os[u];
             below_k += okr && k < kd0 ? 1u : 0u;
             below_x0 += okr && x < x0 ? 1u : 0u;
-            below_ko += okr && o < kd0 ? 1u : 0u;
+            bn_c += okr && k < c0 ? 1u : 0u;
+            bo_c += okr && o < c0 ? 1u : 0u;
             if (okr && k >= kd0 && k < kd1) {
                 const uint32_t p = atomicAdd(&cnt[0], 1u);
                 if (p < MV_RK_CAP) dk[p] = comp(k, x);
@@ -309,9 +309,13 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
                 const uint32_t p = atomicAdd(&cnt[2], 1u);
                 if (p < RK_KD1_CAP) kx1[p] = x;
             }
-            if (okr && o >= kd0 && o < kd1) {
+            if (okr && k >= c0 && k < c1) {
                 const uint32_t p = atomicAdd(&cnt[3], 1u);
-                if (p < RK_OK_CAP) ok[p] = comp(o, r);
+                if (p < RK_EV_CAP) en[p] = comp(k, r);
+            }
+            if (okr && o >= c0 && o < c1) {
+                const uint32_t p = atomicAdd(&cnt[4], 1u);
+                if (p < RK_EV_CAP) eo[p] = comp(o, r);
             }
             if (okr && bits_ok && x >= xw && x < x1) {
                 atomicAdd(&cnt[1], 1u);
@@ -322,9 +326,10 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
     }
     below_k = block_sum<RK_BLK>(below_k, red);   // (its barriers also publish the staged entries and counts)
     below_x0 = block_sum<RK_BLK>(below_x0, red);
-    below_ko = block_sum<RK_BLK>(below_ko, red);
-    const uint32_t nd = cnt[0], n1 = cnt[2], no = cnt[3];
-    const bool dest_staged = nd <= MV_RK_CAP, old_staged = no <= RK_OK_CAP;   // block-uniform
+    bn_c = block_sum<RK_BLK>(bn_c, red);
+    bo_c = block_sum<RK_BLK>(bo_c, red);
+    const uint32_t nd = cnt[0], n1 = cnt[2], nen = cnt[3], neo = cnt[4];
+    const bool dest_staged = nd <= MV_RK_CAP, ev_staged = nen <= RK_EV_CAP && neo <= RK_EV_CAP;   // block-uniform
     RK_PROBE(1, wall_clock64());
     RK_PROBE(4, nd);
     RK_PROBE(5, cnt[1]);
@@ -360,24 +365,21 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
     }
     // the dest entries and the old keys in order: up to RK_COUNT of them each lane counts the smaller ones (LDS
     // broadcast reads, no barrier stages), more are sorted (lds_sort)
-    const bool dcount = nd <= (uint32_t)RK_COUNT, ocount = no <= (uint32_t)RK_COUNT;
+    const bool dcount = nd <= (uint32_t)RK_COUNT;
     if (dest_staged && dcount)
         for (uint32_t e = threadIdx.x; e < nd; e += RK_BLK) {
             uint32_t lr = 0;
             for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < dk[e] ? 1u : 0u;
             ds[lr] = dk[e];
         }
-    if (old_staged && ocount)
-        for (uint32_t e = threadIdx.x; e < no; e += RK_BLK) {
-            uint32_t lr = 0;
-            for (uint32_t f = 0; f < no; ++f) lr += ok[f] < ok[e] ? 1u : 0u;
-            oks[lr] = ok[e];
-        }
+    const bool ecount = nen <= (uint32_t)RK_COUNT && neo <= (uint32_t)RK_COUNT;
     if (dest_staged && !dcount) lds_sort(dk, nullptr, nd);
-    if (old_staged && !ocount) lds_sort(ok, nullptr, no);
+    if (ev_staged && !ecount) {
+        lds_sort(en, nullptr, nen);
+        lds_sort(eo, nullptr, neo);
+    }
     __syncthreads();
     const uint64_t* sd = dcount ? ds : dk;   // sorted dest entries (dest_staged)
-    const uint64_t* so = ocount ? oks : ok;  // sorted old keys (old_staged)
     RK_PROBE(2, wall_clock64());
     RK_PROBE(7, bits_ok ? 1 : 0);
     // ---- counts against the whole list (ranges holding more than LDS does: a state where most particles move)
@@ -466,155 +468,63 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
             move_extra(ex, i, dst);   // Model R's further arrays (the reference's scale: not prefetched)
         }
     }
-    // ---- the cell starts of this key range, in place: cs[k] += #{movers: new key < k} − #{movers: old key < k} for
-    // the cells kd0 < k < kd1 (kd1 = ncells + 1 for the last range). Only this workgroup reads them (its movers'
-    // insertion slots, above); every cell kd0 is read by two workgroups, so its new value goes to the boundary table
-    // and k_mv_bounds writes it after the launch.
-    __syncthreads();
-    if (kd0 != 0xffffffffu) {
-        const uint32_t klo = kd0 + 1u, khi = max(min(kd1, ncells + 1u), klo);
-        const int32_t base_d = (int32_t)below_k - (int32_t)below_ko;
-        const uint32_t E = nd + no;
-        if (dest_staged && old_staged && E <= (uint32_t)RK_EV_CAP) {
-            // Δ(k) = base + #{dest keys < k} − #{old keys < k} is constant between the entries' keys: merge the two
-            // sorted key lists into events (+1 / −1 at key + 1), then write only the cells of the segments where
-            // Δ != 0, spread evenly over the lanes (a range can hold long runs of empty cells, where Δ is often 0).
-            for (uint32_t t = threadIdx.x; t < nd; t += RK_BLK) {
-                const uint32_t key = (uint32_t)(sd[t] >> 32);
-                uint32_t lo = 0, hi = no;   // old keys < key (dest events first at equal keys)
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if ((uint32_t)(so[mid] >> 32) < key) lo = mid + 1;
-                    else hi = mid;
-                }
-                ev[t + lo] = key;
-                evd[t + lo] = 1;
+    // ---- the cell starts of this workgroup's chunk [c0, c1) into the new table (the old one is only read here).
+    // Counts of the movers' keys below each cell: below the chunk (stream) plus the chunk's keys before it (sorted).
+    {
+        uint64_t* snn = en;   // sorted new / old keys in the chunk (ev_staged)
+        uint64_t* soo = eo;
+        if (ev_staged && ecount) {   // rank by counting into the dest / slot scratch (done with them above)
+            __syncthreads();
+            for (uint32_t e = threadIdx.x; e < nen; e += RK_BLK) {
+                uint32_t lr = 0;
+                for (uint32_t f = 0; f < nen; ++f) lr += en[f] < en[e] ? 1u : 0u;
+                ds[lr] = en[e];
             }
-            for (uint32_t t = threadIdx.x; t < no; t += RK_BLK) {
-                const uint32_t key = (uint32_t)(so[t] >> 32);
-                uint32_t lo = 0, hi = nd;   // dest keys <= key
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if ((uint32_t)(sd[mid] >> 32) <= key) lo = mid + 1;
-                    else hi = mid;
-                }
-                ev[t + lo] = key;
-                evd[t + lo] = -1;
+            for (uint32_t e = threadIdx.x; e < neo; e += RK_BLK) {
+                uint32_t lr = 0;
+                for (uint32_t f = 0; f < neo; ++f) lr += eo[f] < eo[e] ? 1u : 0u;
+                dk[lr] = eo[e];
             }
             __syncthreads();
-            // segment j in [0, E]: cells [start_j, end_j), Δ_j = base + Σ_{i<j} evd[i]; lengths of the Δ != 0 ones
-            constexpr uint32_t SPL = (RK_EV_CAP + RK_BLK) / RK_BLK;   // segments per lane
-            const uint32_t j0 = SPL * threadIdx.x;
-            int32_t dsum = 0;
-            for (uint32_t j = j0; j < min(j0 + SPL, E); ++j) dsum += evd[j];
-            uint32_t lsum = 0;
-            // the lane's Δ before j0: a block scan of the event sums
-            int32_t inc = dsum;
+            snn = ds;
+            soo = dk;
+        }
+        const int32_t base_d = (int32_t)bn_c - (int32_t)bo_c;
+        auto new_start = [&](uint32_t k, uint32_t c) {
+            if (ev_staged)
+                return (uint32_t)((int32_t)c + base_d + (int32_t)lower_bound(snn, nen, comp(k, 0u)) -
+                                  (int32_t)lower_bound(soo, neo, comp(k, 0u)));
+            uint32_t cn = 0, co = 0;   // more keys in the chunk than LDS holds: counted against the whole list
+            for (uint32_t f = 0; f < m; ++f) {
+                cn += w.mk[f] < k ? 1u : 0u;
+                co += w.mo[f] < k ? 1u : 0u;
+            }
+            return c + cn - co;
+        };
+        for (uint32_t base = c0; base < c1; base += RK_BLK * RK_CU) {
+            uint32_t cv[RK_CU];
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int32_t u = __shfl_up(inc, o, 64);
-                if (lane_id() >= (uint32_t)o) inc += u;
-            }
-            if (lane_id() == 63) red[threadIdx.x >> 6] = (uint32_t)inc;
-            __syncthreads();
-            int32_t dpre = base_d;
-            for (uint32_t k = 0; k < (threadIdx.x >> 6); ++k) dpre += (int32_t)red[k];
-            dpre += inc - dsum;
-            auto seg = [&](uint32_t j, uint32_t& st, uint32_t& en) {
-                st = j == 0 ? klo : max(ev[j - 1] + 1u, klo);
-                en = j == E ? khi : min(ev[j] + 1u, khi);
-                if (en < st) en = st;
-            };
-            {
-                int32_t dj = dpre;
-                for (uint32_t j = j0; j < min(j0 + SPL, E + 1u); ++j) {
-                    uint32_t st, en;
-                    seg(j, st, en);
-                    const uint32_t len = dj != 0 ? en - st : 0u;
-                    sgd[j] = dj;
-                    sgl[j] = len;
-                    lsum += len;
-                    if (j < E) dj += evd[j];
-                }
-            }
-            __syncthreads();   // red reused
-            uint32_t linc = lsum;
+            for (int u = 0; u < RK_CU; ++u) cv[u] = cs[min(base + u * RK_BLK + threadIdx.x, c1 - 1u)];
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t u = (uint32_t)__shfl_up((int)linc, o, 64);
-                if (lane_id() >= (uint32_t)o) linc += u;
-            }
-            if (lane_id() == 63) red[threadIdx.x >> 6] = linc;
-            __syncthreads();
-            uint32_t lpre = 0, T = 0;
-            for (uint32_t k = 0; k < RK_BLK / 64; ++k) {
-                lpre += k < (threadIdx.x >> 6) ? red[k] : 0u;
-                T += red[k];
-            }
-            lpre += linc - lsum;
-            for (uint32_t j = j0; j < min(j0 + SPL, E + 1u); ++j) {   // segment j's first cell in the written order
-                const uint32_t len = sgl[j];
-                sgl[j] = lpre;
-                lpre += len;
-            }
-            __syncthreads();
-            for (uint32_t t = threadIdx.x; t < T; t += RK_BLK) {
-                uint32_t lo = 0, hi = E + 1u;   // the last segment whose first written cell is <= t
-                while (hi - lo > 1u) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (sgl[mid] <= t) lo = mid;
-                    else hi = mid;
-                }
-                while (lo < E && sgl[lo + 1] <= t) ++lo;   // skip empty segments that share the offset
-                uint32_t st, en;
-                seg(lo, st, en);
-                const uint32_t k = st + (t - sgl[lo]);
-                cs[k] = (uint32_t)((int32_t)cs[k] + sgd[lo]);
-            }
-        } else {   // entries past LDS: cell by cell
-            for (uint32_t k = klo + threadIdx.x; k < khi; k += RK_BLK) {
-                const uint32_t cn = dest_staged ? lower_bound(sd, nd, comp(k, 0u)) : count_dest(comp(k, 0u)) - below_k;
-                if (old_staged) {
-                    const uint32_t co = lower_bound(so, no, comp(k, 0u));
-                    const int32_t dlt = base_d + (int32_t)cn - (int32_t)co;
-                    if (dlt != 0) cs[k] = (uint32_t)((int32_t)cs[k] + dlt);
-                } else {   // more old keys than LDS holds: #movers with old key < k = #movers with slot < cs_old[k]
-                    const uint32_t c = cs[k];
-                    cs[k] = c + (below_k + cn) - slots_below(c);
-                }
+            for (int u = 0; u < RK_CU; ++u) {
+                const uint32_t k = base + u * RK_BLK + threadIdx.x;
+                if (k < c1) cs_new[k] = new_start(k, cv[u]);
             }
         }
-        if (threadIdx.x == 0) {
-            w.bnd[b] = kd0;
-            w.bnd[G + b] = (uint32_t)((int32_t)cs[kd0] + base_d);
+        if (c1 == ncells + 1u && threadIdx.x == 0) cs_new[ncells + 1u] = cs[ncells + 1u];
+        if ((int32_t)threadIdx.x < pick.m) {   // cell starts read back: the ones in this chunk
+            const uint32_t k = (uint32_t)pick.idx[threadIdx.x];
+            if (k >= c0 && k < c1) {
+                const uint32_t v = new_start(k, cs[k]);
+                pick.out[threadIdx.x] = v;
+                if (pick.out_host) pick.out_host[threadIdx.x] = v;
+            }
         }
-    } else if (threadIdx.x == 0) {
-        w.bnd[b] = 0xffffffffu;
     }
 #ifdef SPH_RANK_PROBE
     __syncthreads();
     RK_PROBE(3, wall_clock64());
 #endif
-}
-
-// The cells every rank range starts at (read by two workgroups of k_mv_rank, so written here), then the picks.
-__global__ __launch_bounds__(MV_BLK) void k_mv_bounds(const ResortScratch w, uint32_t G, uint32_t* __restrict__ cs,
-                                                      uint32_t ncells, CsPick pick) {
-    for (uint32_t b = threadIdx.x; b < G; b += MV_BLK) {
-        const uint32_t k = w.bnd[b];
-        if (k <= ncells) cs[k] = w.bnd[G + b];
-    }
-    if (pick.m == 0) return;
-    __syncthreads();
-    const int t = threadIdx.x;
-    if (t < pick.m) {
-        const uint32_t k = (uint32_t)pick.idx[t];
-        if (k <= ncells) {
-            const uint32_t v = cs[k];
-            pick.out[t] = v;
-            if (pick.out_host) pick.out_host[t] = v;
-        }
-    }
 }
 
 // The slab step's halo records: new keys (window sentinel, as k_keys) and old keys moved into this
@@ -754,14 +664,14 @@ uint32_t resort_ranges(int32_t n) {
     return std::min(nbk, std::max((uint32_t)MV_RANK_GRID, need + 1u));   // (+1: the ranges are whole 256-slot blocks)
 }
 
-void launch_resort(AsmSrc src, uint32_t* cs, uint32_t ncells, int32_t n, const uint32_t* count,
+void launch_resort(AsmSrc src, uint32_t* cs, uint32_t* cs_new, uint32_t ncells, int32_t n, const uint32_t* count,
                    uint32_t* count_other, ResortScratch w, float4* pos_o, float4* vel_o, int32_t* id_o,
                    uint32_t* sk_o, hipStream_t s, CsPick pick, ResortExtra ex) {
     if (n <= 0) return;
     // n is an upper bound of the slots on device-sized steps: the rank kernel's ranges split the device count
     const uint32_t G = resort_ranges(n);
-    SPH_LAUNCH(k_mv_rank, G, RK_BLK, 0, s, count, count_other, cs, ncells, w, src, n, pos_o, vel_o, id_o, sk_o, ex);
-    SPH_LAUNCH(k_mv_bounds, 1, MV_BLK, 0, s, w, G, cs, ncells, pick);
+    SPH_LAUNCH(k_mv_rank, G, RK_BLK, 0, s, count, count_other, cs, cs_new, ncells, pick, w, src, n, pos_o, vel_o, id_o,
+               sk_o, ex);
 }
 
 }  // namespace sph
