@@ -24,6 +24,7 @@ void free_all(sph_ctx* c) {
     c->staging = nullptr;
     c->staging_bytes = 0;
     c->cs_cap = 0;
+    c->cs2_cap = 0;
     c->device_bytes = 0;
 }
 
