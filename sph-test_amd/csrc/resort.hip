@@ -19,12 +19,11 @@
 // tests/test_resort_logic.py restates the formulas; tests/test_gpu_resort.py compares runs bit
 // for bit with the full sort.
 //
-// Kernels:
-//   k_mv_rank        per workgroup a range of old slots and the new keys it holds: the movers' ranks, insertion
-//                    slots and placement, the stayers' scatter of (pos, vel, id, key), and the tables by
-//                    (key, index) and by index: O(m) per workgroup plus its slots
-//   k_mv_cells       the cell starts, in place from the tables: cs[k] += #{movers: new key < k} − #{movers: old key < k}
-// The scatters replace the permutation gather, and the update the cell-start rebuild, of the full path.
+// One launch (k_mv_rank): workgroup b takes a range of old slots and the new keys they hold, and an equal share of the
+// cells. Per range: the movers' ranks, insertion slots and placement, and the stayers' scatter of (pos, vel, id, key);
+// per share of cells: the new cell-start table, cs_new[k] = cs[k] + #{movers: new key < k} − #{movers: old key < k},
+// with the mover keys in the share staged from the same stream over the mover list. The scatters replace the
+// permutation gather, and the table update the cell-start rebuild, of the full path.
 #include "common.h"
 
 namespace sph {
@@ -113,13 +112,14 @@ static __device__ __forceinline__ uint32_t lower_bound(const T* __restrict__ a, 
 // plus (or minus) the staged slots between x0 and the slot, read from the bitmap's word prefix (the slots are
 // distinct, so they need no sort), with no second pass over the mover list (r5: a second stream's dependent loads
 // took the kernel from ~5 to ~32 us). The dest entries are ranked by counting (LDS broadcast reads) up to RK_COUNT of
-// them, by sorting beyond. The mover is then scattered to dst = (q − A(q)) + rk here, so the merge that follows
-// reads only the tables (it updates cs_old in place). A range with more entries than LDS holds (a state where most
-// particles move, only under SPH_RESORT=2) counts them against the whole list instead: slow, same result. Also zeroes
-// the next step's mover counter. Per workgroup the kernel is a chain of memory round trips (~1.5 us each; the probe
-// build, scripts/rank_probe.py): one before the stream (count, range keys and the first movers together), one for
-// the entries' loads.
-constexpr int MV_RANK_GRID = 256;   // workgroups at most; one per CU
+// them, by sorting beyond. The mover is placed at dst = (q − A(q)) + rk, every stayer of the slot range at
+// (i − A(i)) + #{movers (k, y) < (k_i, i)} (k_i in [kd0, kd1]; at kd1 the kd1 movers staged apart), and the share of
+// cells written from its staged keys. A range with more entries than LDS holds (a state where most particles move,
+// only under SPH_RESORT=2) counts them against the whole list instead: slow, same result. Also zeroes the next step's
+// mover counter. Per workgroup the kernel is a chain of memory round trips (~1.5 us each; the probe build,
+// scripts/rank_probe.py): one before the stream (count, range keys and the first movers together), one for the
+// entries' and stayers' loads, one for the cells.
+constexpr int MV_RANK_GRID = 256;   // workgroups at least (one per CU); more above 2M slots
 constexpr int RK_U = 8;             // movers per lane per streaming round
 constexpr int MV_RK_CAP = 2048;     // dest entries staged per workgroup (a power of two)
 constexpr int RK_BM_WORDS = 1024;   // slot-presence bitmap over [xw, x1): up to 32,768 slots
@@ -234,9 +234,109 @@ __device__ void lds_sort(uint64_t* a, uint32_t* b, uint32_t len) {
     }
 }
 
+// A share of the cells [c0, c1) of [0, ncells] (workgroups G.. of k_mv_rank): cs_new[k] = cs[k] + #{movers: new key
+// < k} − #{movers: old key < k}. One stream over the movers' keys counts those below c0 and stages those in [c0, c1);
+// sorted, they give the counts below every cell of the share. The old table is only read (every workgroup's movers
+// read their insertion cells from it), the new one written whole; the cell starts read back (picks) come from here.
+__device__ void mv_cells(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ mtotal, const uint32_t* __restrict__ cs,
+                         uint32_t* __restrict__ cs_new, uint32_t ncells, const CsPick& pick, const ResortScratch& w,
+                         uint64_t* en, uint64_t* eo, uint64_t* sa, uint64_t* sb, uint32_t* red, uint32_t* cnt) {
+    const uint32_t c0 = (uint32_t)((uint64_t)(ncells + 1u) * cb / Gc), c1 = (uint32_t)((uint64_t)(ncells + 1u) * (cb + 1) / Gc);
+    uint32_t ks[RK_U], os[RK_U];
+    auto load_round = [&](uint32_t base, uint32_t last) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < RK_U; ++u) {
+            const uint32_t r = min(base + u * RK_BLK + threadIdx.x, last);
+            ks[u] = w.mk[r];
+            os[u] = w.mo[r];
+        }
+    };
+    load_round(0, w.cap - 1u);
+    const uint32_t m = *mtotal;
+    __syncthreads();   // cnt zeroed
+    uint32_t bn_c = 0, bo_c = 0;
+    for (uint32_t base = 0; base < m; base += RK_BLK * RK_U) {
+#pragma unroll
+        for (int u = 0; u < RK_U; ++u) {
+            const uint32_t r = base + u * RK_BLK + threadIdx.x;
+            const bool okr = r < m;
+            const uint32_t k = ks[u], o = os[u];
+            bn_c += okr && k < c0 ? 1u : 0u;
+            bo_c += okr && o < c0 ? 1u : 0u;
+            if (okr && k >= c0 && k < c1) {
+                const uint32_t p = atomicAdd(&cnt[3], 1u);
+                if (p < RK_EV_CAP) en[p] = comp(k, r);
+            }
+            if (okr && o >= c0 && o < c1) {
+                const uint32_t p = atomicAdd(&cnt[4], 1u);
+                if (p < RK_EV_CAP) eo[p] = comp(o, r);
+            }
+        }
+        if (base + RK_BLK * RK_U < m) load_round(base + RK_BLK * RK_U, m - 1u);
+    }
+    bn_c = block_sum<RK_BLK>(bn_c, red);
+    bo_c = block_sum<RK_BLK>(bo_c, red);
+    const uint32_t nen = cnt[3], neo = cnt[4];
+    const bool ev_staged = nen <= RK_EV_CAP && neo <= RK_EV_CAP;   // block-uniform
+    uint64_t* snn = en;
+    uint64_t* soo = eo;
+    if (ev_staged) {
+        if (nen <= (uint32_t)RK_COUNT && neo <= (uint32_t)RK_COUNT) {   // rank by counting into the scratch lists
+            for (uint32_t e = threadIdx.x; e < nen; e += RK_BLK) {
+                uint32_t lr = 0;
+                for (uint32_t f = 0; f < nen; ++f) lr += en[f] < en[e] ? 1u : 0u;
+                sa[lr] = en[e];
+            }
+            for (uint32_t e = threadIdx.x; e < neo; e += RK_BLK) {
+                uint32_t lr = 0;
+                for (uint32_t f = 0; f < neo; ++f) lr += eo[f] < eo[e] ? 1u : 0u;
+                sb[lr] = eo[e];
+            }
+            snn = sa;
+            soo = sb;
+        } else {
+            lds_sort(en, nullptr, nen);
+            lds_sort(eo, nullptr, neo);
+        }
+        __syncthreads();
+    }
+    const int32_t base_d = (int32_t)bn_c - (int32_t)bo_c;
+    auto new_start = [&](uint32_t k, uint32_t c) {
+        if (ev_staged)
+            return (uint32_t)((int32_t)c + base_d + (int32_t)lower_bound(snn, nen, comp(k, 0u)) -
+                              (int32_t)lower_bound(soo, neo, comp(k, 0u)));
+        uint32_t cn = 0, co = 0;   // more keys in the share than LDS holds: counted against the whole list
+        for (uint32_t f = 0; f < m; ++f) {
+            cn += w.mk[f] < k ? 1u : 0u;
+            co += w.mo[f] < k ? 1u : 0u;
+        }
+        return c + cn - co;
+    };
+    for (uint32_t base = c0; base < c1; base += RK_BLK * RK_CU) {
+        uint32_t cv[RK_CU];
+#pragma unroll
+        for (int u = 0; u < RK_CU; ++u) cv[u] = cs[min(base + u * RK_BLK + threadIdx.x, c1 - 1u)];
+#pragma unroll
+        for (int u = 0; u < RK_CU; ++u) {
+            const uint32_t k = base + u * RK_BLK + threadIdx.x;
+            if (k < c1) cs_new[k] = new_start(k, cv[u]);
+        }
+    }
+    if (c1 == ncells + 1u && threadIdx.x == 0) cs_new[ncells + 1u] = cs[ncells + 1u];
+    if ((int32_t)threadIdx.x < pick.m) {   // cell starts read back: the ones in this share
+        const uint32_t k = (uint32_t)pick.idx[threadIdx.x];
+        if (k >= c0 && k < c1) {
+            const uint32_t v = new_start(k, cs[k]);
+            pick.out[threadIdx.x] = v;
+            if (pick.out_host) pick.out_host[threadIdx.x] = v;
+        }
+    }
+}
+
 __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__ mtotal, uint32_t* __restrict__ next_count,
                                                     const uint32_t* __restrict__ cs, uint32_t* __restrict__ cs_new,
-                                                    uint32_t ncells, CsPick pick, ResortScratch w, AsmSrc src, int32_t n,
+                                                    uint32_t ncells, CsPick pick, uint32_t G, ResortScratch w,
+                                                    AsmSrc src, int32_t n,
                                                     float4* __restrict__ pos_o, float4* __restrict__ vel_o,
                                                     int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o,
                                                     ResortExtra ex) {
@@ -251,13 +351,15 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
     resolve_sizes(src, w, n);
     if (threadIdx.x < 5) cnt[threadIdx.x] = 0u;
     for (uint32_t t = threadIdx.x; t <= (uint32_t)RK_BM_WORDS; t += RK_BLK) bm[t] = 0u;
-    const uint32_t G = gridDim.x, b = blockIdx.x;
+    if (blockIdx.x >= G) {   // a share of the cells: its own workgroup, beside the ranges
+        mv_cells(blockIdx.x - G, gridDim.x - G, mtotal, cs, cs_new, ncells, pick, w, en, eo, dk, ds, red, cnt);
+        return;
+    }
+    const uint32_t b = blockIdx.x;
     // the ranges are whole blocks of 256 slots
     const uint32_t nbk = ((uint32_t)n + 255u) / 256u;
     const uint32_t x0 = min((uint32_t)((uint64_t)nbk * b / G) * 256u, (uint32_t)n);
     const uint32_t x1 = min((uint32_t)((uint64_t)nbk * (b + 1) / G) * 256u, (uint32_t)n);
-    // and an equal share of the cells [0, ncells]: cs_new[k] = cs[k] + #{movers: new key < k} − #{movers: old key < k}
-    const uint32_t c0 = (uint32_t)((uint64_t)(ncells + 1u) * b / G), c1 = (uint32_t)((uint64_t)(ncells + 1u) * (b + 1) / G);
     // Everything the stream needs in one round trip (the kernel is a chain of dependent round trips of ~1.5 us each,
     // r5 probe): the mover count, both range keys (pointer selects) and the first round of movers, whose loads are
     // clamped to the lists' capacity rather than to the count they would otherwise wait for.
@@ -265,14 +367,13 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
         const int32_t xi = (int32_t)min(x, (uint32_t)max(n - 1, 0));
         return asm_rec(src, xi) ? src.skr + xi : src.sk + (xi + src.o_off);
     };
-    uint32_t xs[RK_U], ks[RK_U], os[RK_U];
+    uint32_t xs[RK_U], ks[RK_U];
     auto load_round = [&](uint32_t base, uint32_t last) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < RK_U; ++u) {   // every load of the round issues before any is used
             const uint32_t r = min(base + u * RK_BLK + threadIdx.x, last);
             xs[u] = w.mi[r];
             ks[u] = w.mk[r];
-            os[u] = w.mo[r];
         }
     };
     load_round(0, w.cap - 1u);
@@ -290,17 +391,15 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
     const uint32_t xw = x0 > (uint32_t)RK_WIN ? x0 - (uint32_t)RK_WIN : 0u;
     const bool bits_ok = x1 - xw <= 32u * RK_BM_WORDS;   // block-uniform
     __syncthreads();
-    uint32_t below_k = 0, below_x0 = 0, bn_c = 0, bo_c = 0;
+    uint32_t below_k = 0, below_x0 = 0;
     for (uint32_t base = 0; base < m; base += RK_BLK * RK_U) {
 #pragma unroll
         for (int u = 0; u < RK_U; ++u) {
             const uint32_t r = base + u * RK_BLK + threadIdx.x;
             const bool okr = r < m;
-            const uint32_t x = mv_slot(w, xs[u]), k = ks[u], o = os[u];
+            const uint32_t x = mv_slot(w, xs[u]), k = ks[u];
             below_k += okr && k < kd0 ? 1u : 0u;
             below_x0 += okr && x < x0 ? 1u : 0u;
-            bn_c += okr && k < c0 ? 1u : 0u;
-            bo_c += okr && o < c0 ? 1u : 0u;
             if (okr && k >= kd0 && k < kd1) {
                 const uint32_t p = atomicAdd(&cnt[0], 1u);
                 if (p < MV_RK_CAP) dk[p] = comp(k, x);
@@ -308,14 +407,6 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
             if (okr && k == kd1) {
                 const uint32_t p = atomicAdd(&cnt[2], 1u);
                 if (p < RK_KD1_CAP) kx1[p] = x;
-            }
-            if (okr && k >= c0 && k < c1) {
-                const uint32_t p = atomicAdd(&cnt[3], 1u);
-                if (p < RK_EV_CAP) en[p] = comp(k, r);
-            }
-            if (okr && o >= c0 && o < c1) {
-                const uint32_t p = atomicAdd(&cnt[4], 1u);
-                if (p < RK_EV_CAP) eo[p] = comp(o, r);
             }
             if (okr && bits_ok && x >= xw && x < x1) {
                 atomicAdd(&cnt[1], 1u);
@@ -326,10 +417,8 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
     }
     below_k = block_sum<RK_BLK>(below_k, red);   // (its barriers also publish the staged entries and counts)
     below_x0 = block_sum<RK_BLK>(below_x0, red);
-    bn_c = block_sum<RK_BLK>(bn_c, red);
-    bo_c = block_sum<RK_BLK>(bo_c, red);
-    const uint32_t nd = cnt[0], n1 = cnt[2], nen = cnt[3], neo = cnt[4];
-    const bool dest_staged = nd <= MV_RK_CAP, ev_staged = nen <= RK_EV_CAP && neo <= RK_EV_CAP;   // block-uniform
+    const uint32_t nd = cnt[0], n1 = cnt[2];
+    const bool dest_staged = nd <= MV_RK_CAP;   // block-uniform
     RK_PROBE(1, wall_clock64());
     RK_PROBE(4, nd);
     RK_PROBE(5, cnt[1]);
@@ -372,12 +461,7 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
             for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < dk[e] ? 1u : 0u;
             ds[lr] = dk[e];
         }
-    const bool ecount = nen <= (uint32_t)RK_COUNT && neo <= (uint32_t)RK_COUNT;
     if (dest_staged && !dcount) lds_sort(dk, nullptr, nd);
-    if (ev_staged && !ecount) {
-        lds_sort(en, nullptr, nen);
-        lds_sort(eo, nullptr, neo);
-    }
     __syncthreads();
     const uint64_t* sd = dcount ? ds : dk;   // sorted dest entries (dest_staged)
     RK_PROBE(2, wall_clock64());
@@ -466,59 +550,6 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
             id_o[dst] = pid[u];
             sk_o[dst] = ko[u];
             move_extra(ex, i, dst);   // Model R's further arrays (the reference's scale: not prefetched)
-        }
-    }
-    // ---- the cell starts of this workgroup's chunk [c0, c1) into the new table (the old one is only read here).
-    // Counts of the movers' keys below each cell: below the chunk (stream) plus the chunk's keys before it (sorted).
-    {
-        uint64_t* snn = en;   // sorted new / old keys in the chunk (ev_staged)
-        uint64_t* soo = eo;
-        if (ev_staged && ecount) {   // rank by counting into the dest / slot scratch (done with them above)
-            __syncthreads();
-            for (uint32_t e = threadIdx.x; e < nen; e += RK_BLK) {
-                uint32_t lr = 0;
-                for (uint32_t f = 0; f < nen; ++f) lr += en[f] < en[e] ? 1u : 0u;
-                ds[lr] = en[e];
-            }
-            for (uint32_t e = threadIdx.x; e < neo; e += RK_BLK) {
-                uint32_t lr = 0;
-                for (uint32_t f = 0; f < neo; ++f) lr += eo[f] < eo[e] ? 1u : 0u;
-                dk[lr] = eo[e];
-            }
-            __syncthreads();
-            snn = ds;
-            soo = dk;
-        }
-        const int32_t base_d = (int32_t)bn_c - (int32_t)bo_c;
-        auto new_start = [&](uint32_t k, uint32_t c) {
-            if (ev_staged)
-                return (uint32_t)((int32_t)c + base_d + (int32_t)lower_bound(snn, nen, comp(k, 0u)) -
-                                  (int32_t)lower_bound(soo, neo, comp(k, 0u)));
-            uint32_t cn = 0, co = 0;   // more keys in the chunk than LDS holds: counted against the whole list
-            for (uint32_t f = 0; f < m; ++f) {
-                cn += w.mk[f] < k ? 1u : 0u;
-                co += w.mo[f] < k ? 1u : 0u;
-            }
-            return c + cn - co;
-        };
-        for (uint32_t base = c0; base < c1; base += RK_BLK * RK_CU) {
-            uint32_t cv[RK_CU];
-#pragma unroll
-            for (int u = 0; u < RK_CU; ++u) cv[u] = cs[min(base + u * RK_BLK + threadIdx.x, c1 - 1u)];
-#pragma unroll
-            for (int u = 0; u < RK_CU; ++u) {
-                const uint32_t k = base + u * RK_BLK + threadIdx.x;
-                if (k < c1) cs_new[k] = new_start(k, cv[u]);
-            }
-        }
-        if (c1 == ncells + 1u && threadIdx.x == 0) cs_new[ncells + 1u] = cs[ncells + 1u];
-        if ((int32_t)threadIdx.x < pick.m) {   // cell starts read back: the ones in this chunk
-            const uint32_t k = (uint32_t)pick.idx[threadIdx.x];
-            if (k >= c0 && k < c1) {
-                const uint32_t v = new_start(k, cs[k]);
-                pick.out[threadIdx.x] = v;
-                if (pick.out_host) pick.out_host[threadIdx.x] = v;
-            }
         }
     }
 #ifdef SPH_RANK_PROBE
@@ -670,8 +701,10 @@ void launch_resort(AsmSrc src, uint32_t* cs, uint32_t* cs_new, uint32_t ncells, 
     if (n <= 0) return;
     // n is an upper bound of the slots on device-sized steps: the rank kernel's ranges split the device count
     const uint32_t G = resort_ranges(n);
-    SPH_LAUNCH(k_mv_rank, G, RK_BLK, 0, s, count, count_other, cs, cs_new, ncells, pick, w, src, n, pos_o, vel_o, id_o,
-               sk_o, ex);
+    // the cell shares: as many workgroups, at least one per 16,384 cells (C3: 224 of 256)
+    const uint32_t Gc = std::max(G, (ncells + 16384u) / 16384u);
+    SPH_LAUNCH(k_mv_rank, G + Gc, RK_BLK, 0, s, count, count_other, cs, cs_new, ncells, pick, G, w, src, n, pos_o, vel_o,
+               id_o, sk_o, ex);
 }
 
 }  // namespace sph
