@@ -132,8 +132,10 @@ static_assert(RK_MAX_RANGE + RK_WIN + 512u <= 32u * RK_BM_WORDS, "a range and it
 constexpr int RK_COUNT = 256;       // dest entries ranked by counting, more by sorting
 constexpr int RK_KD1_CAP = 1024;    // movers into the cell a range ends in, staged
 constexpr int RK_SU = 4;            // stayer slots per lane in flight
-constexpr int RK_EV_CAP = 2048;     // movers' new / old keys in a cell chunk, staged
+constexpr uint32_t RK_CELLS = 16384; // cells per share at most (k_mv_rank's cell workgroups)
+constexpr int RK_POOL_U64 = RK_CELLS / 2;   // the LDS pool: a share's differences, or a range's entries and bitmap
 constexpr int RK_CU = 4;            // cells per lane in flight
+static_assert(2 * MV_RK_CAP * 8 + 4 * (RK_KD1_CAP + 2 * (RK_BM_WORDS + 1)) <= RK_POOL_U64 * 8, "a range's LDS fits the pool");
 // Test-only timing probe (scripts/rank_probe.py, a -DSPH_RANK_PROBE build): per workgroup the wall clock at its start,
 // after the mover stream, after the sorts and at its end, with its entry counts.
 #ifdef SPH_RANK_PROBE
@@ -235,13 +237,15 @@ __device__ void lds_sort(uint64_t* a, uint32_t* b, uint32_t len) {
 }
 
 // A share of the cells [c0, c1) of [0, ncells] (workgroups G.. of k_mv_rank): cs_new[k] = cs[k] + #{movers: new key
-// < k} − #{movers: old key < k}. One stream over the movers' keys counts those below c0 and stages those in [c0, c1);
-// sorted, they give the counts below every cell of the share. The old table is only read (every workgroup's movers
-// read their insertion cells from it), the new one written whole; the cell starts read back (picks) come from here.
+// < k} − #{movers: old key < k}. One stream over the movers' keys counts those below c0 and adds +1 (new key) / −1 (old
+// key) at key + 1 into a difference array over the share; its prefix sum is each cell's change. The old table is only
+// read (every workgroup's movers read their insertion cells from it), the new one written whole; the cell starts read
+// back (picks) come from here.
 __device__ void mv_cells(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ mtotal, const uint32_t* __restrict__ cs,
                          uint32_t* __restrict__ cs_new, uint32_t ncells, const CsPick& pick, const ResortScratch& w,
-                         uint64_t* en, uint64_t* eo, uint64_t* sa, uint64_t* sb, uint32_t* red, uint32_t* cnt) {
+                         int32_t* diff, uint32_t* red) {
     const uint32_t c0 = (uint32_t)((uint64_t)(ncells + 1u) * cb / Gc), c1 = (uint32_t)((uint64_t)(ncells + 1u) * (cb + 1) / Gc);
+    const uint32_t L = c1 - c0;   // <= RK_CELLS (the launcher's share count)
     uint32_t ks[RK_U], os[RK_U];
     auto load_round = [&](uint32_t base, uint32_t last) __attribute__((always_inline)) {
 #pragma unroll
@@ -253,7 +257,8 @@ __device__ void mv_cells(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ 
     };
     load_round(0, w.cap - 1u);
     const uint32_t m = *mtotal;
-    __syncthreads();   // cnt zeroed
+    for (uint32_t t = threadIdx.x; t < L; t += RK_BLK) diff[t] = 0;
+    __syncthreads();
     uint32_t bn_c = 0, bo_c = 0;
     for (uint32_t base = 0; base < m; base += RK_BLK * RK_U) {
 #pragma unroll
@@ -263,70 +268,52 @@ __device__ void mv_cells(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ 
             const uint32_t k = ks[u], o = os[u];
             bn_c += okr && k < c0 ? 1u : 0u;
             bo_c += okr && o < c0 ? 1u : 0u;
-            if (okr && k >= c0 && k < c1) {
-                const uint32_t p = atomicAdd(&cnt[3], 1u);
-                if (p < RK_EV_CAP) en[p] = comp(k, r);
-            }
-            if (okr && o >= c0 && o < c1) {
-                const uint32_t p = atomicAdd(&cnt[4], 1u);
-                if (p < RK_EV_CAP) eo[p] = comp(o, r);
-            }
+            if (okr && k >= c0 && k + 1u < c1) atomicAdd(&diff[k + 1u - c0], 1);
+            if (okr && o >= c0 && o + 1u < c1) atomicAdd(&diff[o + 1u - c0], -1);
         }
         if (base + RK_BLK * RK_U < m) load_round(base + RK_BLK * RK_U, m - 1u);
     }
-    bn_c = block_sum<RK_BLK>(bn_c, red);
+    bn_c = block_sum<RK_BLK>(bn_c, red);   // (its barriers also publish the differences)
     bo_c = block_sum<RK_BLK>(bo_c, red);
-    const uint32_t nen = cnt[3], neo = cnt[4];
-    const bool ev_staged = nen <= RK_EV_CAP && neo <= RK_EV_CAP;   // block-uniform
-    uint64_t* snn = en;
-    uint64_t* soo = eo;
-    if (ev_staged) {
-        if (nen <= (uint32_t)RK_COUNT && neo <= (uint32_t)RK_COUNT) {   // rank by counting into the scratch lists
-            for (uint32_t e = threadIdx.x; e < nen; e += RK_BLK) {
-                uint32_t lr = 0;
-                for (uint32_t f = 0; f < nen; ++f) lr += en[f] < en[e] ? 1u : 0u;
-                sa[lr] = en[e];
-            }
-            for (uint32_t e = threadIdx.x; e < neo; e += RK_BLK) {
-                uint32_t lr = 0;
-                for (uint32_t f = 0; f < neo; ++f) lr += eo[f] < eo[e] ? 1u : 0u;
-                sb[lr] = eo[e];
-            }
-            snn = sa;
-            soo = sb;
-        } else {
-            lds_sort(en, nullptr, nen);
-            lds_sort(eo, nullptr, neo);
-        }
-        __syncthreads();
+    // inclusive prefix of diff[0, L): RK_CELLS / RK_BLK consecutive entries per lane
+    constexpr uint32_t EPL = RK_CELLS / RK_BLK;
+    const uint32_t e0 = EPL * threadIdx.x;
+    int32_t loc[EPL], tot = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < EPL; ++j) {
+        tot += e0 + j < L ? diff[e0 + j] : 0;
+        loc[j] = tot;
     }
-    const int32_t base_d = (int32_t)bn_c - (int32_t)bo_c;
-    auto new_start = [&](uint32_t k, uint32_t c) {
-        if (ev_staged)
-            return (uint32_t)((int32_t)c + base_d + (int32_t)lower_bound(snn, nen, comp(k, 0u)) -
-                              (int32_t)lower_bound(soo, neo, comp(k, 0u)));
-        uint32_t cn = 0, co = 0;   // more keys in the share than LDS holds: counted against the whole list
-        for (uint32_t f = 0; f < m; ++f) {
-            cn += w.mk[f] < k ? 1u : 0u;
-            co += w.mo[f] < k ? 1u : 0u;
-        }
-        return c + cn - co;
-    };
-    for (uint32_t base = c0; base < c1; base += RK_BLK * RK_CU) {
+    int32_t inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t u = __shfl_up(inc, o, 64);
+        if (lane_id() >= (uint32_t)o) inc += u;
+    }
+    __syncthreads();   // block_sum's last reads of red
+    if (lane_id() == 63) red[threadIdx.x >> 6] = (uint32_t)inc;
+    __syncthreads();
+    int32_t pre = (int32_t)bn_c - (int32_t)bo_c + inc - tot;
+    for (uint32_t k = 0; k < (threadIdx.x >> 6); ++k) pre += (int32_t)red[k];
+#pragma unroll
+    for (uint32_t j = 0; j < EPL; ++j)
+        if (e0 + j < L) diff[e0 + j] = pre + loc[j];   // now the change of cell c0 + e0 + j
+    __syncthreads();
+    for (uint32_t base = 0; base < L; base += RK_BLK * RK_CU) {
         uint32_t cv[RK_CU];
 #pragma unroll
-        for (int u = 0; u < RK_CU; ++u) cv[u] = cs[min(base + u * RK_BLK + threadIdx.x, c1 - 1u)];
+        for (int u = 0; u < RK_CU; ++u) cv[u] = cs[c0 + min(base + u * RK_BLK + threadIdx.x, L - 1u)];
 #pragma unroll
         for (int u = 0; u < RK_CU; ++u) {
-            const uint32_t k = base + u * RK_BLK + threadIdx.x;
-            if (k < c1) cs_new[k] = new_start(k, cv[u]);
+            const uint32_t t = base + u * RK_BLK + threadIdx.x;
+            if (t < L) cs_new[c0 + t] = (uint32_t)((int32_t)cv[u] + diff[t]);
         }
     }
     if (c1 == ncells + 1u && threadIdx.x == 0) cs_new[ncells + 1u] = cs[ncells + 1u];
     if ((int32_t)threadIdx.x < pick.m) {   // cell starts read back: the ones in this share
         const uint32_t k = (uint32_t)pick.idx[threadIdx.x];
         if (k >= c0 && k < c1) {
-            const uint32_t v = new_start(k, cs[k]);
+            const uint32_t v = (uint32_t)((int32_t)cs[k] + diff[k - c0]);
             pick.out[threadIdx.x] = v;
             if (pick.out_host) pick.out_host[threadIdx.x] = v;
         }
@@ -340,21 +327,22 @@ __global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__
                                                     float4* __restrict__ pos_o, float4* __restrict__ vel_o,
                                                     int32_t* __restrict__ id_o, uint32_t* __restrict__ sk_o,
                                                     ResortExtra ex) {
-    __shared__ uint64_t dk[MV_RK_CAP];   // dest entries (new key, slot)
-    __shared__ uint64_t ds[MV_RK_CAP];   // the dest entries in (key, slot) order
-    __shared__ uint64_t en[RK_EV_CAP];   // movers' new keys in this workgroup's cell chunk [c0, c1) (key, index)
-    __shared__ uint64_t eo[RK_EV_CAP];   // their old keys in it
-    __shared__ uint32_t kx1[RK_KD1_CAP]; // slots of the movers whose new key is kd1 (the cell the range ends in)
-    __shared__ uint32_t bm[RK_BM_WORDS + 1], bpre[RK_BM_WORDS + 1];   // movers' slots in [xw, x1): bits, word prefix
+    // one LDS pool, laid out per role: a range's entries and slot bitmap, or a cell share's count differences
+    __shared__ uint64_t pool[RK_POOL_U64];
     __shared__ uint32_t cnt[5], red[RK_BLK / 64];
+    uint64_t* dk = pool;                                    // dest entries (new key, slot)
+    uint64_t* ds = pool + MV_RK_CAP;                        // the dest entries in (key, slot) order
+    uint32_t* kx1 = (uint32_t*)(pool + 2 * MV_RK_CAP);      // slots of the movers whose new key is kd1
+    uint32_t* bm = kx1 + RK_KD1_CAP;                        // movers' slots in [xw, x1): bits
+    uint32_t* bpre = bm + (RK_BM_WORDS + 1);                // and the words' prefix
     RK_PROBE(0, wall_clock64());
     resolve_sizes(src, w, n);
     if (threadIdx.x < 5) cnt[threadIdx.x] = 0u;
-    for (uint32_t t = threadIdx.x; t <= (uint32_t)RK_BM_WORDS; t += RK_BLK) bm[t] = 0u;
     if (blockIdx.x >= G) {   // a share of the cells: its own workgroup, beside the ranges
-        mv_cells(blockIdx.x - G, gridDim.x - G, mtotal, cs, cs_new, ncells, pick, w, en, eo, dk, ds, red, cnt);
+        mv_cells(blockIdx.x - G, gridDim.x - G, mtotal, cs, cs_new, ncells, pick, w, (int32_t*)pool, red);
         return;
     }
+    for (uint32_t t = threadIdx.x; t <= (uint32_t)RK_BM_WORDS; t += RK_BLK) bm[t] = 0u;
     const uint32_t b = blockIdx.x;
     // the ranges are whole blocks of 256 slots
     const uint32_t nbk = ((uint32_t)n + 255u) / 256u;
@@ -701,8 +689,8 @@ void launch_resort(AsmSrc src, uint32_t* cs, uint32_t* cs_new, uint32_t ncells, 
     if (n <= 0) return;
     // n is an upper bound of the slots on device-sized steps: the rank kernel's ranges split the device count
     const uint32_t G = resort_ranges(n);
-    // the cell shares: as many workgroups, at least one per 16,384 cells (C3: 224 of 256)
-    const uint32_t Gc = std::max(G, (ncells + 16384u) / 16384u);
+    // the cell shares: as many workgroups, and at most RK_CELLS cells each (C3: 224 would do)
+    const uint32_t Gc = std::max(G, (ncells + RK_CELLS) / RK_CELLS);
     SPH_LAUNCH(k_mv_rank, G + Gc, RK_BLK, 0, s, count, count_other, cs, cs_new, ncells, pick, G, w, src, n, pos_o, vel_o,
                id_o, sk_o, ex);
 }
