@@ -131,7 +131,7 @@ constexpr uint32_t RK_MAX_RANGE = 8192;
 static_assert(RK_MAX_RANGE + RK_WIN + 512u <= 32u * RK_BM_WORDS, "a range and its window fit the bitmap");
 constexpr int RK_COUNT = 256;       // dest entries ranked by counting, more by sorting
 constexpr int RK_KD1_CAP = 1024;    // movers into the cell a range ends in, staged
-constexpr int RK_SU = 4;            // stayer slots per lane in flight
+constexpr int RK_SU = 2;            // stayer slots per lane in flight
 constexpr uint32_t RK_CELLS = 16384; // cells per share at most (k_mv_rank's cell workgroups)
 constexpr int RK_POOL_U64 = RK_CELLS / 2;   // the LDS pool: a share's differences, or a range's entries and bitmap
 constexpr int RK_CU = 4;            // cells per lane in flight
@@ -278,12 +278,9 @@ __device__ void mv_cells(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ 
     // inclusive prefix of diff[0, L): RK_CELLS / RK_BLK consecutive entries per lane
     constexpr uint32_t EPL = RK_CELLS / RK_BLK;
     const uint32_t e0 = EPL * threadIdx.x;
-    int32_t loc[EPL], tot = 0;
+    int32_t tot = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < EPL; ++j) {
-        tot += e0 + j < L ? diff[e0 + j] : 0;
-        loc[j] = tot;
-    }
+    for (uint32_t j = 0; j < EPL; ++j) tot += e0 + j < L ? diff[e0 + j] : 0;
     int32_t inc = tot;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -296,8 +293,11 @@ __device__ void mv_cells(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ 
     int32_t pre = (int32_t)bn_c - (int32_t)bo_c + inc - tot;
     for (uint32_t k = 0; k < (threadIdx.x >> 6); ++k) pre += (int32_t)red[k];
 #pragma unroll
-    for (uint32_t j = 0; j < EPL; ++j)
-        if (e0 + j < L) diff[e0 + j] = pre + loc[j];   // now the change of cell c0 + e0 + j
+    for (uint32_t j = 0; j < EPL; ++j)   // now the change of cell c0 + e0 + j (each lane rewrites only its own entries)
+        if (e0 + j < L) {
+            pre += diff[e0 + j];
+            diff[e0 + j] = pre;
+        }
     __syncthreads();
     for (uint32_t base = 0; base < L; base += RK_BLK * RK_CU) {
         uint32_t cv[RK_CU];
@@ -320,7 +320,7 @@ __device__ void mv_cells(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ 
     }
 }
 
-__global__ __launch_bounds__(RK_BLK) void k_mv_rank(const uint32_t* __restrict__ mtotal, uint32_t* __restrict__ next_count,
+__global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restrict__ mtotal, uint32_t* __restrict__ next_count,
                                                     const uint32_t* __restrict__ cs, uint32_t* __restrict__ cs_new,
                                                     uint32_t ncells, CsPick pick, uint32_t G, ResortScratch w,
                                                     AsmSrc src, int32_t n,
