@@ -1,10 +1,11 @@
 # PMC passes over the force pass at the per-rank shape of BASELINE's 8-GPU configuration (C5 on 8 GPUs: a rank holds
 # ~2M particles of C5's 256 x 512 cross-section, ~7 columns): one context of C5's cross-section 16 lattice layers
-# deep in x, against C3 (DESIGN.md §4, round-5 verdict item 3). --kernel-trace only; one counter group per run.
+# deep in x, with the y-band schedule (schedule.hip) and without, against C3 (DESIGN.md §4, round-5 verdict item 3). --kernel-trace only; one counter group per run.
 set +e
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
-for case in "slab8:--scenario 0,3,16,256,512,64,512,512" "C3:--config C3"; do
+for case in "slab8:--scenario 0,3,16,256,512,64,512,512" "slab8sched:--scenario 0,3,16,256,512,64,512,512" "C3:--config C3"; do
   name=${case%%:*}; args=${case#*:}
+  if [ "$name" = slab8sched ]; then export SPH_SCHED=1; else unset SPH_SCHED; fi
   mkdir -p gpurun_out/pmc_$name
   i=0
   for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU" "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
