@@ -30,6 +30,7 @@ int sph_create(const sph_config* cfg, int32_t device, sph_ctx** out) {
     if (const char* v = std::getenv("SPH_RESORT")) ctx->resort_mode = std::atoi(v);
     if (const char* v = std::getenv("SPH_CT_TEAM")) ctx->ct_team = std::atoi(v);
     if (const char* v = std::getenv("SPH_SMALL")) ctx->small_mode = std::atoi(v);
+    if (const char* v = std::getenv("SPH_FUSED")) ctx->fused_mode = std::atoi(v);
     if (const char* v = std::getenv("SPH_SCHED")) ctx->sched_mode = std::atoi(v);   // default off
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&ctx->mv_host, sizeof(uint32_t), hipHostMallocMapped) != hipSuccess ||

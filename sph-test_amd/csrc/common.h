@@ -713,6 +713,22 @@ void launch_set_range(const void* aos, const int32_t* slot_of, int32_t first, in
 
 // Model R (contact.hip). team: lanes per target (0 = by size, else 1, 16 or 64; any choice gives
 // bit-identical results).
+// The one-launch Model R step at the reference's scale (contact.hip k_contact_fused): re-sort + contact + drag +
+// motion + rotation for n <= contact_fused_max(), reading the previous step's arrays through this step's permutation.
+struct FusedIO {
+    const float4 *pos, *vel, *omg, *rot, *aux;
+    const int32_t *id, *mode;
+    const uint32_t *sk, *cs;
+    const uint32_t *mi, *mk;
+    const uint32_t* count;
+    float4 *pos_o, *vel_o, *omg_o, *rot_o, *aux_o;
+    int32_t *id_o, *mode_o, *torque_o;
+    uint32_t *sk_o, *keys_o, *cs_o;
+    uint32_t *mi_o, *mk_o, *mo_o, *count_o, *count_zero, *host_count;
+    uint32_t cap;
+};
+int32_t contact_fused_max();
+void launch_contact_fused(const FusedIO& io, int32_t n_active, int32_t n, GridDesc g, ContactConst c, hipStream_t s);
 void launch_contact_step(const float4* pos, const float4* vel, const float4* omg, const float4* rot,
                          const float4* aux, const int32_t* id, const uint32_t* cs, int32_t n_active,
                          int32_t n, GridDesc g, ContactConst c, float4* pos_o, float4* vel_o,

@@ -211,8 +211,17 @@ __device__ __forceinline__ void contact_accumulate_team(const float4* __restrict
 // one at a time instead: same order, same sums.
 constexpr int CT_FLAT = 65;
 constexpr int CF_CHUNKS = 8, CF_SLOTS = 3;
+// The slot arrays as the contact pass reads them: cell starts and the slot holding sorted position j. DirectMap: the
+// arrays are in sorted order (after the re-sort); FusedMap (below): the previous step's order, read through this
+// step's permutation (the one-launch step at the reference's scale).
+struct DirectMap {
+    const uint32_t* cs;
+    __device__ __forceinline__ uint32_t start(uint32_t k) const { return cs[k]; }
+    __device__ __forceinline__ uint32_t old(uint32_t j) const { return j; }
+};
+template <class Map>
 __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict__ pos, const float4* __restrict__ vel,
-                                                        const float4* __restrict__ omg, const uint32_t* __restrict__ cs,
+                                                        const float4* __restrict__ omg, const Map& M,
                                                         const GridDesc& g, const ContactConst& c, int32_t a, float4 pa,
                                                         float4 va, float4 wa, f3& v, f3& w, uint32_t tq[3]) {
     const int lane = (int)(threadIdx.x & 63u);
@@ -229,8 +238,8 @@ __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict
         const int32_t xx = cx + lane / 3 - 1, yy = cy + lane % 3 - 1;
         if (xx >= 0 && xx < g.gx && yy >= 0 && yy < g.gy) {
             const uint32_t rowk = ((uint32_t)xx * (uint32_t)g.gy + (uint32_t)yy) * (uint32_t)g.gz;
-            rj0 = cs[rowk + (uint32_t)z0];
-            rlen = cs[rowk + (uint32_t)z1 + 1u] - rj0;
+            rj0 = M.start(rowk + (uint32_t)z0);
+            rlen = M.start(rowk + (uint32_t)z1 + 1u) - rj0;
         }
     }
     uint32_t incl = rlen;   // inclusive prefix over lanes 0..8 (lanes >= 9 hold 0)
@@ -255,7 +264,8 @@ __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict
     };
     // the hit's F and TA (TA = 0 for a repulsion-only contact) and the int torque b scatters into a (:291)
     auto body = [&](uint32_t j, f3& F, f3& TA) __attribute__((always_inline)) {
-        const float4 pb = pos[j], vb = vel[j], wb = omg[j];
+        const uint32_t o = M.old(j);
+        const float4 pb = pos[o], vb = vel[o], wb = omg[o];
         const Body B{xyz(pb), xyz(vb), xyz(wb), pb.w};
         f3 TB;
         const int h = contact_pair(c, A, B, F, TA, TB);
@@ -283,7 +293,7 @@ __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict
         for (int ch = 0; ch < CF_CHUNKS; ++ch) {   // every position load of the round in flight together
             const uint32_t f = round + (uint32_t)(ch * 64 + lane);
             jj[ch] = slot_of(min(f, total - 1u));
-            pb[ch] = pos[jj[ch]];
+            pb[ch] = pos[M.old(jj[ch])];
         }
         uint32_t touch = 0u;   // bit ch: candidate (round, ch, lane) touches a (:240, :253)
 #pragma unroll
@@ -350,7 +360,7 @@ __device__ __forceinline__ void contact_accumulate_lanes(const float4* __restric
                                                          const GridDesc& g, const ContactConst& c, int32_t a, float4 pa,
                                                          float4 va, float4 wa, f3& v, f3& w, uint32_t tq[3]) {
     if constexpr (T == CT_FLAT)
-        contact_accumulate_flat(pos, vel, omg, cs, g, c, a, pa, va, wa, v, w, tq);
+        contact_accumulate_flat(pos, vel, omg, DirectMap{cs}, g, c, a, pa, va, wa, v, w, tq);
     else
         contact_accumulate_team<T>(pos, vel, omg, cs, g, c, a, pa, va, wa, v, w, tq);
 }
@@ -556,6 +566,208 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_finish(
     rot_o[a] = q;
     keys_o[a] = cell_key(g, p.x, p.y, p.z);
     append_mover(mv, a, keys_o[a]);
+}
+
+// ---------------------------------------------------------------- the one-launch step at the reference's scale
+// Model R at N <= FZ_N (the reference runs 4-10,000 particles, ParticleSystemController.cs:12): the re-sort, ApplySPHForces,
+// drag, motion and rotation of a step in ONE launch, with no grid barrier. Every workgroup rebuilds, in LDS, the step's
+// permutation from the previous step's mover list (m <= N <= FZ_N movers fit whole): the movers sorted by (new key,
+// slot), their new slots dst_r = (q − A(q)) + r (resort.hip's formulas, q the insertion slot, A the movers below a slot
+// from a slot bitmap), so that any sorted position j maps to the slot of the previous order that holds it
+// (FusedMap::old) and any cell start follows from the old table (FusedMap::start). The contact pass then reads the
+// previous step's arrays through that map and writes its targets at their sorted positions: the outputs are the
+// re-sorted arrays, bit-identical to re-sort + contact (tests/test_gpu_small.py). Each workgroup also writes an equal
+// share of the new cell-start table. Movers of this step go to the other list; the counters rotate over three (the one
+// this step appends to was zeroed by the step before).
+constexpr int32_t FZ_N = 4096;
+constexpr int FZ_BLK = 1024;   // 16 targets (one per wave) per workgroup: the permutation is built once per 16
+constexpr int FZ_WORDS = FZ_N / 32 + 1;
+
+struct FusedMap {
+    const uint32_t* cs;    // the previous step's cell-start table
+    const uint64_t* ms;    // LDS: movers by (new key, old slot)
+    const uint32_t* dst;   // LDS: their sorted positions, ascending
+    const uint32_t* bm;    // LDS: the movers' old slots as bits, and the words' exclusive prefix
+    const uint32_t* bpre;
+    uint32_t m;
+    __device__ __forceinline__ uint32_t A(uint32_t y) const {   // movers with an old slot < y
+        const uint32_t wd = y >> 5;
+        return bpre[wd] + (uint32_t)__popc(bm[wd] & ((1u << (y & 31u)) - 1u));
+    }
+    __device__ __forceinline__ uint32_t start(uint32_t k) const {   // cs_new[k]
+        const uint32_t c = cs[k];
+        if (m == 0) return c;
+        uint32_t lo = 0, hi = m;   // movers with new key < k
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((uint32_t)(ms[mid] >> 32) < k) lo = mid + 1;
+            else hi = mid;
+        }
+        return c + lo - A(c);   // old keys follow the old slots: movers with an old key < k = A(cs[k])
+    }
+    // the previous order's slot of sorted position j; mv: it is a mover (its new key in key)
+    __device__ __forceinline__ uint32_t old_of(uint32_t j, bool& mv, uint32_t& key) const {
+        mv = false;
+        if (m == 0) return j;
+        uint32_t lo = 0, hi = m;   // movers placed below j
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (dst[mid] < j) lo = mid + 1;
+            else hi = mid;
+        }
+        if (lo < m && dst[lo] == j) {
+            mv = true;
+            key = (uint32_t)(ms[lo] >> 32);
+            return (uint32_t)ms[lo];
+        }
+        const uint32_t s = j - lo;   // the s-th stayer: the smallest i with (i + 1) − A(i + 1) > s, i in [s, s + m]
+        uint32_t a = s, b = s + m;
+        while (a < b) {
+            const uint32_t mid = (a + b) >> 1;
+            if (mid + 1u - A(mid + 1u) > s) b = mid;
+            else a = mid + 1;
+        }
+        return a;
+    }
+    __device__ __forceinline__ uint32_t old(uint32_t j) const {
+        bool mv;
+        uint32_t key;
+        return old_of(j, mv, key);
+    }
+};
+
+__global__ __launch_bounds__(FZ_BLK) void k_contact_fused(FusedIO io, int32_t n_active, int32_t n, GridDesc g,
+                                                          ContactConst c) {
+    __shared__ uint64_t ms[FZ_N];
+    __shared__ uint32_t dst[FZ_N];
+    __shared__ uint32_t bm[FZ_WORDS], bpre[FZ_WORDS];
+    const uint32_t m = min(*io.count, (uint32_t)n);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *io.count_zero = 0u;   // the counter the step after next appends to (read by the step before this one)
+        if (io.host_count) *io.host_count = m;
+    }
+    const uint32_t nw = ((uint32_t)n >> 5) + 1u;
+    for (uint32_t t = threadIdx.x; t < nw; t += FZ_BLK) bm[t] = 0u;
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < m; r += FZ_BLK) {
+        const uint32_t x = io.mi[r], k = io.mk[r];
+        ms[r] = (uint64_t)k << 32 | x;
+        atomicOr(&bm[x >> 5], 1u << (x & 31u));
+    }
+    __syncthreads();
+    // the movers in (new key, slot) order: up to FZ_BLK by counting, more by a bitonic sort
+    if (m <= (uint32_t)FZ_BLK) {
+        uint64_t e = 0;
+        uint32_t rk = 0;
+        if (threadIdx.x < m) {
+            e = ms[threadIdx.x];
+            for (uint32_t f = 0; f < m; ++f) rk += ms[f] < e ? 1u : 0u;
+        }
+        __syncthreads();
+        if (threadIdx.x < m) ms[rk] = e;
+    } else {
+        uint32_t P = 1;
+        while (P < m) P <<= 1;
+        for (uint32_t t = m + threadIdx.x; t < P; t += FZ_BLK) ms[t] = ~0ull;
+        __syncthreads();
+        for (uint32_t k = 2; k <= P; k <<= 1)
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t t = threadIdx.x; t < P / 2; t += FZ_BLK) {
+                    const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), u = i | j;
+                    const uint64_t x = ms[i], y = ms[u];
+                    if ((x > y) == ((i & k) == 0)) {
+                        ms[i] = y;
+                        ms[u] = x;
+                    }
+                }
+                __syncthreads();
+            }
+    }
+    // the bitmap's word prefix (nw <= 129 words: one pass)
+    if (threadIdx.x < 64) {
+        uint32_t carry = 0;
+        for (uint32_t base = 0; base < nw; base += 64) {
+            const uint32_t t = base + threadIdx.x;
+            const uint32_t v = t < nw ? (uint32_t)__popc(bm[t]) : 0u;
+            uint32_t inc = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
+                if (lane_id() >= (uint32_t)o) inc += u;
+            }
+            if (t < nw) bpre[t] = carry + inc - v;
+            carry += (uint32_t)__shfl((int)inc, 63, 64);
+        }
+    }
+    __syncthreads();
+    FusedMap M{io.cs, ms, dst, bm, bpre, m};
+    for (uint32_t r = threadIdx.x; r < m; r += FZ_BLK) {   // the movers' sorted positions
+        const uint32_t k = (uint32_t)(ms[r] >> 32), x = (uint32_t)ms[r];
+        const uint32_t c0 = io.cs[k], c1 = io.cs[k + 1];
+        const uint32_t q = x < c0 ? c0 : (x > c1 ? c1 : x);
+        dst[r] = (q - M.A(q)) + r;
+    }
+    __syncthreads();
+    // this workgroup's share of the new cell-start table
+    {
+        const uint32_t tot = g.ncells + 2u, G = gridDim.x;
+        const uint32_t k0 = (uint32_t)((uint64_t)tot * blockIdx.x / G), k1 = (uint32_t)((uint64_t)tot * (blockIdx.x + 1) / G);
+        for (uint32_t k = k0 + threadIdx.x; k < k1; k += FZ_BLK)
+            io.cs_o[k] = k <= g.ncells ? M.start(k) : io.cs[k];   // (entry ncells + 1: the slot count, unchanged)
+    }
+    // one target per wave: sorted position a, read from the previous order's slot o
+    const int32_t a = blockIdx.x * (FZ_BLK / 64) + (int32_t)(threadIdx.x >> 6);
+    const bool lead = (threadIdx.x & 63u) == 0;
+    if (a >= n) return;   // wave-uniform
+    bool mv;
+    uint32_t key_a;
+    const uint32_t o = M.old_of((uint32_t)a, mv, key_a);
+    if (!mv) key_a = io.sk[o];
+    const float4 pa = io.pos[o], va = io.vel[o], wa = io.omg[o];
+    uint32_t key_n;
+    f3 p, v, w;
+    float4 q;
+    uint32_t tq[3] = {0u, 0u, 0u};
+    if (a >= n_active) {   // inactive slots (id >= activeParticleCount): drag only
+        if (!lead) return;
+        v = apply_drag(c, io.id[o], xyz(pa), xyz(va), va.w);
+        p = xyz(pa);
+        w = xyz(wa);
+        q = io.rot[o];
+        key_n = g.ncells;
+    } else {
+        contact_accumulate_flat(io.pos, io.vel, io.omg, M, g, c, a, pa, va, wa, v, w, tq);
+        if (!lead) return;
+        contact_finish(c, io.id[o], pa, v, w, va.w, wa.w, io.aux[o].x, io.rot[o], tq, p, v, w, q);
+        key_n = cell_key(g, p.x, p.y, p.z);
+    }
+    io.pos_o[a] = a >= n_active ? pa : make_float4(p.x, p.y, p.z, pa.w);
+    io.vel_o[a] = make_float4(v.x, v.y, v.z, va.w);
+    io.omg_o[a] = a >= n_active ? wa : make_float4(w.x, w.y, w.z, wa.w);
+    io.rot_o[a] = q;
+    io.aux_o[a] = io.aux[o];
+    io.id_o[a] = io.id[o];
+    io.mode_o[a] = io.mode[o];
+    if (io.torque_o) {
+        io.torque_o[3 * a] = (int32_t)tq[0]; io.torque_o[3 * a + 1] = (int32_t)tq[1]; io.torque_o[3 * a + 2] = (int32_t)tq[2];
+    }
+    io.sk_o[a] = key_a;
+    io.keys_o[a] = key_n;
+    if (key_n != key_a) {   // a mover of the next step's re-sort
+        const uint32_t r = atomicAdd(io.count_o, 1u);
+        if (r < io.cap) {
+            io.mi_o[r] = (uint32_t)a;
+            io.mk_o[r] = key_n;
+            io.mo_o[r] = key_a;
+        }
+    }
+}
+
+int32_t contact_fused_max() { return FZ_N; }
+
+void launch_contact_fused(const FusedIO& io, int32_t n_active, int32_t n, GridDesc g, ContactConst c, hipStream_t s) {
+    if (n <= 0 || n > FZ_N) return;
+    SPH_LAUNCH(k_contact_fused, (n + FZ_BLK / 64 - 1) / (FZ_BLK / 64), FZ_BLK, 0, s, io, n_active, n, g, c);
 }
 
 // Lanes per target: enough teams to fill the chip (256 CUs × 8 waves × 64 lanes ≈ 131k lanes) without

@@ -100,8 +100,11 @@ struct sph_ctx {
     uint32_t *sk_cur = nullptr, *sk_next = nullptr;
     uint32_t *mv_mi = nullptr, *mv_mk = nullptr, *mv_mo = nullptr, *mv_mx = nullptr, *mv_mos = nullptr;
     uint64_t* mv_ms = nullptr;
-    uint32_t* mv_count = nullptr;   // [2] mover counters, ping-pong by step
+    uint32_t* mv_count = nullptr;   // [3] mover counters: Model S and slabs ping-pong over two; Model R cycles three
     int mv_par = 0;                 // counter the next force pass appends into
+    uint32_t *mv_mi2 = nullptr, *mv_mk2 = nullptr, *mv_mo2 = nullptr;   // Model R's second mover list (one-launch step)
+    bool fz_ready = false;          // the one-launch step's append counter is known to be zero
+    int fused_mode = 1;             // env SPH_FUSED: Model R one-launch step, 0 never, 1 up to contact_fused_max()
     bool sk_valid = false;       // sk_cur matches the slot order and cs (set by a Model S sort)
     // env SPH_RESORT: 0 full radix sort every step, 1 (default) incremental re-sort unless the last
     // seen mover count exceeds resort_limit(n), 2 incremental whenever possible (tests)

@@ -15,7 +15,8 @@ void free_all(sph_ctx* c) {
     dfree(c->sblk); dfree(c->sdev); dfree(c->paths); dfree(c->hmask);
     dfree(c->sk_cur); dfree(c->sk_next);
     dfree(c->mv_mi); dfree(c->mv_mk); dfree(c->mv_mo); dfree(c->mv_mx); dfree(c->mv_mos);
-    dfree(c->mv_ms); dfree(c->mv_count);
+    dfree(c->mv_ms); dfree(c->mv_count); dfree(c->mv_mi2); dfree(c->mv_mk2); dfree(c->mv_mo2);
+    c->fz_ready = false;
     dfree(c->sched);
     c->sched_cap = 0;
     c->sched_valid = false;
@@ -57,8 +58,9 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
     // incremental re-sort (both models)
     AL(sk_cur, n); AL(sk_next, n);
     AL(mv_mi, n); AL(mv_mk, n); AL(mv_mo, n); AL(mv_mx, n); AL(mv_mos, n); AL(mv_ms, n);
-    AL(mv_count, 2);
-    HIPCHK(hipMemset(ctx->mv_count, 0, 2 * sizeof(uint32_t)));
+    AL(mv_count, 3);
+    HIPCHK(hipMemset(ctx->mv_count, 0, 3 * sizeof(uint32_t)));
+    if (is_contact(ctx)) { AL(mv_mi2, n); AL(mv_mk2, n); AL(mv_mo2, n); }
 #undef AL
     ctx->staging_bytes = n * 84;
     HIPCHK(hipMalloc(&ctx->staging, ctx->staging_bytes));

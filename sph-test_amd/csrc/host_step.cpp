@@ -254,12 +254,13 @@ int sort_contact(sph_ctx* ctx, int32_t act) {
     const bool many = ctx->resort_mode == 1 && *(volatile uint32_t*)ctx->mv_host > resort_limit(n);
     if (ctx->resort_mode != 0 && !many && ctx->keys_valid && ctx->keys_active == act && ctx->sk_valid && n > 0) {
         KTimer t(ctx, "resort", (double)n * (2 * 4 + 2 * 88));
-        const int used = ctx->mv_par;
+        const int used = ctx->mv_par, next = (used + 1) % 3;   // Model R cycles three counters (the one-launch step)
         const ResortExtra ex{ctx->omg, ctx->rot, ctx->aux, ctx->mode, ctx->omg2, ctx->rot2, ctx->aux2, ctx->mode2};
         launch_resort(asm_plain(ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->keys, n), ctx->cs, ctx->cs2, ctx->grid.ncells, n,
-                      ctx->mv_count + used, ctx->mv_count + (1 - used), resort_scratch(ctx), ctx->pos2, ctx->vel2,
+                      ctx->mv_count + used, ctx->mv_count + next, resort_scratch(ctx), ctx->pos2, ctx->vel2,
                       ctx->id2, ctx->sk_next, ctx->stream, CsPick{{0}, 0, nullptr, nullptr}, ex);
-        ctx->mv_par = 1 - used;
+        ctx->mv_par = next;
+        ctx->fz_ready = false;
         swap_cs(ctx);
         ctx->sorted_full = false;
         swap_sv(ctx);
@@ -277,19 +278,82 @@ int sort_contact(sph_ctx* ctx, int32_t act) {
     if (r != SPH_OK) return r;
     if (ctx->resort_mode != 0 && n > 0) {
         HIPCHK(hipMemcpyAsync(ctx->sk_cur, sk, (size_t)n * 4, hipMemcpyDeviceToDevice, ctx->stream));
-        HIPCHK(hipMemsetAsync(ctx->mv_count, 0, 2 * sizeof(uint32_t), ctx->stream));
+        HIPCHK(hipMemsetAsync(ctx->mv_count, 0, 3 * sizeof(uint32_t), ctx->stream));
     }
+    ctx->fz_ready = false;
     ctx->sk_valid = ctx->resort_mode != 0;
+    return SPH_OK;
+}
+
+ContactConst contact_const(const sph_ctx* ctx, float dt) {
+    const sph_params& p = ctx->prm;
+    ContactConst c{};
+    c.dt = dt;
+    c.spawn_radius = p.spawn_radius;
+    c.global_drag = p.global_drag_multiplier;
+    c.torque_factor = p.torque_factor;
+    c.torque_damping = p.torque_damping;
+    c.boundary_friction = p.boundary_friction;
+    c.roll_mult = p.rolling_contact_radius_multiplier;
+    c.repulsion_strength = p.repulsion_strength;
+    c.drag_id = ctx->drag.selected_id;
+    c.drag_tx = ctx->drag.target[0];
+    c.drag_ty = ctx->drag.target[1];
+    c.drag_tz = ctx->drag.target[2];
+    c.drag_strength = ctx->drag.strength;
+    return c;
+}
+
+// The one-launch step (contact.hip k_contact_fused) while the previous step's order, movers and cell starts hold:
+// at the reference's scale, no bonds. Same results as sort_contact + the contact pass.
+bool fused_step_ok(const sph_ctx* ctx, int32_t act) {
+    return ctx->fused_mode != 0 && ctx->n > 0 && ctx->n <= contact_fused_max() && ctx->nbonds == 0 &&
+           ctx->resort_mode != 0 && ctx->keys_valid && ctx->keys_active == act && ctx->sk_valid;
+}
+
+int step_contact_fused(sph_ctx* ctx, float dt, int32_t act) {
+    const int32_t n = ctx->n;
+    const int cur = ctx->mv_par, nxt = (cur + 1) % 3, zro = (cur + 2) % 3;
+    if (!ctx->fz_ready) HIPCHK(hipMemsetAsync(ctx->mv_count + nxt, 0, sizeof(uint32_t), ctx->stream));
+    const FusedIO io{ctx->pos, ctx->vel, ctx->omg, ctx->rot, ctx->aux, ctx->id, ctx->mode, ctx->sk_cur, ctx->cs,
+                     ctx->mv_mi, ctx->mv_mk, ctx->mv_count + cur,
+                     ctx->pos2, ctx->vel2, ctx->omg2, ctx->rot2, ctx->aux2, ctx->id2, ctx->mode2, ctx->torque,
+                     ctx->sk_next, ctx->keys2, ctx->cs2,
+                     ctx->mv_mi2, ctx->mv_mk2, ctx->mv_mo2, ctx->mv_count + nxt, ctx->mv_count + zro, ctx->mv_host_dev,
+                     (uint32_t)std::max(ctx->capacity, 1)};
+    {
+        KTimer t(ctx, "contact_fused", (double)n * (2 * 88 + 2 * 64 + 4 + 12 + 4), true);
+        launch_contact_fused(io, act, n, ctx->grid, contact_const(ctx, dt), ctx->stream);
+    }
+    swap_sv(ctx);
+    std::swap(ctx->omg, ctx->omg2);
+    std::swap(ctx->rot, ctx->rot2);
+    std::swap(ctx->aux, ctx->aux2);
+    std::swap(ctx->id, ctx->id2);
+    std::swap(ctx->mode, ctx->mode2);
+    std::swap(ctx->sk_cur, ctx->sk_next);
+    std::swap(ctx->keys, ctx->keys2);
+    swap_cs(ctx);
+    std::swap(ctx->mv_mi, ctx->mv_mi2);
+    std::swap(ctx->mv_mk, ctx->mv_mk2);
+    std::swap(ctx->mv_mo, ctx->mv_mo2);
+    ctx->mv_par = nxt;
+    ctx->fz_ready = true;
+    ctx->sorted_full = false;
+    ctx->keys_valid = true;
+    ctx->keys_active = act;
     return SPH_OK;
 }
 
 int step_contact(sph_ctx* ctx, float dt) {
     const int32_t n = ctx->n;
     const int32_t act = contact_active(ctx);
+    if (fused_step_ok(ctx, act)) return step_contact_fused(ctx, dt, act);
     int r = sort_contact(ctx, act);
     if (r != SPH_OK) return r;
     const MoverSink mv = mover_sink(ctx);
     const sph_params& p = ctx->prm;
+    (void)p;
     ContactConst c{};
     c.dt = dt;
     c.spawn_radius = p.spawn_radius;
