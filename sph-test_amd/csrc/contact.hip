@@ -629,11 +629,8 @@ struct FusedMap {
         }
         return a;
     }
-    __device__ __forceinline__ uint32_t old(uint32_t j) const {
-        bool mv;
-        uint32_t key;
-        return old_of(j, mv, key);
-    }
+    const uint16_t* pm;    // LDS: old_of for every sorted position (filled once per workgroup)
+    __device__ __forceinline__ uint32_t old(uint32_t j) const { return m == 0 ? j : (uint32_t)pm[j]; }
 };
 
 __global__ __launch_bounds__(FZ_BLK) void k_contact_fused(FusedIO io, int32_t n_active, int32_t n, GridDesc g,
@@ -641,6 +638,7 @@ __global__ __launch_bounds__(FZ_BLK) void k_contact_fused(FusedIO io, int32_t n_
     __shared__ uint64_t ms[FZ_N];
     __shared__ uint32_t dst[FZ_N];
     __shared__ uint32_t bm[FZ_WORDS], bpre[FZ_WORDS];
+    __shared__ uint16_t pm[FZ_N];
     const uint32_t m = min(*io.count, (uint32_t)n);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         *io.count_zero = 0u;   // the counter the step after next appends to (read by the step before this one)
@@ -700,7 +698,7 @@ __global__ __launch_bounds__(FZ_BLK) void k_contact_fused(FusedIO io, int32_t n_
         }
     }
     __syncthreads();
-    FusedMap M{io.cs, ms, dst, bm, bpre, m};
+    FusedMap M{io.cs, ms, dst, bm, bpre, m, pm};
     for (uint32_t r = threadIdx.x; r < m; r += FZ_BLK) {   // the movers' sorted positions
         const uint32_t k = (uint32_t)(ms[r] >> 32), x = (uint32_t)ms[r];
         const uint32_t c0 = io.cs[k], c1 = io.cs[k + 1];
@@ -708,6 +706,14 @@ __global__ __launch_bounds__(FZ_BLK) void k_contact_fused(FusedIO io, int32_t n_
         dst[r] = (q - M.A(q)) + r;
     }
     __syncthreads();
+    if (m) {   // the whole permutation in LDS: the contact pass's candidate lookups are one read each
+        for (uint32_t j = threadIdx.x; j < (uint32_t)n; j += FZ_BLK) {
+            bool mv;
+            uint32_t key;
+            pm[j] = (uint16_t)M.old_of(j, mv, key);
+        }
+        __syncthreads();
+    }
     // this workgroup's share of the new cell-start table
     {
         const uint32_t tot = g.ncells + 2u, G = gridDim.x;
