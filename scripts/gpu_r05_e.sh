@@ -10,4 +10,6 @@ echo "pytest rc=$rc"; grep -E " passed| failed|FAILED|ERROR" $O/pytest.log | tai
 timeout -k 10 200 python -u scripts/small_n_timing.py 500 > $O/small_n.log 2>&1; echo "small-N rc=$?"; grep -v amdgpu.ids $O/small_n.log
 timeout -k 10 200 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$O/r4096" -o run --output-format csv -- python3 scripts/run_steps.py --model-r 4096 --steps 300 > $O/r4096.log 2>&1; echo "R trace rc=$?"
 f=$(find $O/r4096 -name "*kernel_trace.csv" | head -1); python3 scripts/trace_window.py "$f" 300 k_contact_fused
+timeout -k 10 200 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$O/c1" -o run --output-format csv -- python3 scripts/run_steps.py --config C1 --steps 300 > $O/c1.log 2>&1; echo "C1 trace rc=$?"
+f=$(find $O/c1 -name "*kernel_trace.csv" | head -1); python3 scripts/trace_window.py "$f" 300 k_density_fused
 exit 0

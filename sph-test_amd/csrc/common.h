@@ -728,6 +728,21 @@ struct FusedIO {
     uint32_t cap;
 };
 int32_t contact_fused_max();
+// Model S's counterpart (wcsph_tiled.hip k_density_fused): re-sort + pass 1 in one launch, then k_force_small
+struct FusedIOS {
+    const float4 *pos, *vel;
+    const int32_t* id;
+    const uint32_t *sk, *cs;
+    const uint32_t *mi, *mk;
+    const uint32_t* count;
+    float4 *pos_o, *vel_o;
+    int32_t* id_o;
+    uint32_t *sk_o, *cs_o;
+    float2* rp_o;
+    uint32_t *count_zero, *host_count;
+};
+int32_t density_fused_max();
+void launch_density_fused(const FusedIOS& io, int32_t n, GridDesc g, SphConst c, hipStream_t s);
 void launch_contact_fused(const FusedIO& io, int32_t n_active, int32_t n, GridDesc g, ContactConst c, hipStream_t s);
 void launch_contact_step(const float4* pos, const float4* vel, const float4* omg, const float4* rot,
                          const float4* aux, const int32_t* id, const uint32_t* cs, int32_t n_active,

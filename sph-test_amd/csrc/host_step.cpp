@@ -160,8 +160,45 @@ int sort_wcsph(sph_ctx* ctx) {
     return SPH_OK;
 }
 
+// Model S's two-launch step at the reference's scale: re-sort + pass 1 in one launch (wcsph_tiled.hip
+// k_density_fused), then pass 2 on the sorted arrays it wrote; while the incremental re-sort's state holds.
+bool fused_s_ok(const sph_ctx* ctx) {
+    const int32_t n = ctx->n;
+    return ctx->fused_mode != 0 && n > 0 && n <= density_fused_max() && (ctx->small_mode == 2 || (ctx->small_mode == 1 && n <= SMALL_N)) &&
+           ctx->resort_mode != 0 && ctx->keys_valid && ctx->keys_active == 0 && ctx->sk_valid;
+}
+
+int step_wcsph_fused(sph_ctx* ctx, float dt) {
+    const int32_t n = ctx->n;
+    const int cur = ctx->mv_par, nxt = 1 - cur;
+    ctx->hm_valid = false;
+    const FusedIOS io{ctx->pos, ctx->vel, ctx->id, ctx->sk_cur, ctx->cs, ctx->mv_mi, ctx->mv_mk, ctx->mv_count + cur,
+                      ctx->pos2, ctx->vel2, ctx->id2, ctx->sk_next, ctx->cs2, ctx->rp, ctx->mv_count + nxt,
+                      ctx->mv_host_dev};
+    {
+        KTimer t(ctx, "density_fused", (double)n * (2 * 36 + 24), true);
+        launch_density_fused(io, n, ctx->grid, ctx->sc, ctx->stream);
+    }
+    swap_cs(ctx);
+    std::swap(ctx->id, ctx->id2);
+    std::swap(ctx->sk_cur, ctx->sk_next);
+    ctx->mv_par = nxt;
+    ctx->sorted_full = false;
+    // the sorted arrays are pos2 / vel2 now; pass 2 integrates them back into pos / vel
+    const MoverSink mv = mover_sink(ctx);
+    {
+        KTimer t(ctx, "force_integrate", 56.0 * n, true);
+        launch_force_small(ctx->pos2, ctx->vel2, ctx->rp, ctx->cs, n, ctx->grid, ctx->sc, dt, forcing(ctx), ctx->pos,
+                           ctx->vel, ctx->keys, mv, ctx->stream);
+    }
+    ctx->keys_valid = true;
+    ctx->keys_active = 0;
+    return SPH_OK;
+}
+
 int step_wcsph(sph_ctx* ctx, float dt) {
     const int32_t n = ctx->n;
+    if (fused_s_ok(ctx)) return step_wcsph_fused(ctx, dt);
     int r = sort_wcsph(ctx);
     if (r != SPH_OK) return r;
     const MoverSink mv = mover_sink(ctx);

@@ -21,6 +21,7 @@
 // offset by offset in chunks, and an offset beyond the fallback length is gathered directly from
 // global memory.
 #include "common.h"
+#include "fused_perm.h"
 
 namespace sph {
 
@@ -964,6 +965,29 @@ struct SmallRows {
             rj0 = (uint32_t)r0;
             len = (uint32_t)(r1 - r0);
         }
+        prefix(len, lane);
+    }
+    // the same rows from a permutation's cell starts (fused_perm.h: the one-launch steps)
+    __device__ __forceinline__ SmallRows(const GridDesc& g, const FusedMap& M, float4 pi, int lane) {
+        BlockRows b;
+        b.cx = cell_cxs<XS>(g, pi.x);
+        b.cy = cell_coord(pi.y, g.oy, g.inv_cell, g.gy);
+        cell_fracs<XS>(g, pi.x, pi.y, pi.z, b.cx, b.cy, b.fx, b.fy, b.gzf);
+        uint32_t len = 0u;
+        if (lane < NR) {
+            const int32_t dxk = lane / 3 - XS, dyk = lane % 3 - 1;
+            const int32_t xx = b.cx + dxk, yy = b.cy + dyk;
+            int32_t zlo, zhi;
+            if (xx >= 0 && xx < g.gx * XS && yy >= 0 && yy < g.gy &&
+                row_window<XS>(g, b.fx, b.fy, b.gzf, dxk, dyk, zlo, zhi)) {
+                const uint32_t rowk = ((uint32_t)xx * (uint32_t)g.gy + (uint32_t)yy) * (uint32_t)g.gz;
+                rj0 = M.start(rowk + (uint32_t)zlo);
+                len = M.start(rowk + (uint32_t)zhi + 1u) - rj0;
+            }
+        }
+        prefix(len, lane);
+    }
+    __device__ __forceinline__ void prefix(uint32_t len, int lane) {
         uint32_t incl = len;
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
@@ -1045,6 +1069,55 @@ __global__ __launch_bounds__(256) void k_force_small(const float4* __restrict__ 
     if (lane != 0) return;
     const uint32_t key = integrate_target<XS>(acc, pk, c, g, pi, vi, dt, fext_x, i, pos_o, vel_o, keys_o);
     append_mover(mv, i, key);   // one lane: window_key = cell_key in a single domain
+}
+
+// The one-launch re-sort + pass 1 at the reference's scale (n <= FZ_N, fused_perm.h): each workgroup rebuilds the
+// step's permutation from the previous step's movers, every wave takes one target at its sorted position, reads the
+// previous order through the permutation, sums pass 1 exactly as k_density_small and writes the target's (x, v, id,
+// sorted key) at its sorted position, so pass 2 (k_force_small) runs on the sorted arrays as after the re-sort. Two
+// launches per step instead of three, bit-identical (tests/test_gpu_small.py).
+constexpr int FZS_BLK = 1024;
+template <int XS>
+__global__ __launch_bounds__(FZS_BLK) void k_density_fused(FusedIOS io, int32_t n, GridDesc g, SphConst c) {
+    __shared__ FusedLds L;
+    const FusedMap M = fused_build<FZS_BLK>(L, io.count, io.mi, io.mk, io.cs, io.cs_o, g.ncells, n, io.count_zero,
+                                            io.host_count);
+    const int lane = (int)lane_id();
+    const int32_t i = (int32_t)blockIdx.x * (FZS_BLK / 64) + (int32_t)(threadIdx.x >> 6);
+    if (i >= n) return;   // wave-uniform
+    bool mv;
+    uint32_t key;
+    const uint32_t o = M.old_of((uint32_t)i, mv, key);
+    if (!mv) key = io.sk[o];
+    const float4 pi = io.pos[o];
+    const SmallRows<XS> R(g, M, pi, lane);
+    float s = 0.0f;
+#pragma unroll 1
+    for (uint32_t base = 0; base < R.total; base += 64u) {
+        const uint32_t f = base + (uint32_t)lane;
+        float v;
+        const float w4 = spline_w4(c, dist2(pi, io.pos[M.old(R.slot(min(f, R.total - 1u)))]), v);
+        const float w = f < R.total ? w4 : 0.0f;
+#pragma unroll
+        for (int t = 0; t < 64; ++t) s += lanef(w, (uint32_t)t);   // visit order; past the end +0
+    }
+    if (lane != 0) return;
+    io.rp_o[i] = density_eos(c, s);
+    io.pos_o[i] = pi;
+    io.vel_o[i] = io.vel[o];
+    io.id_o[i] = io.id[o];
+    io.sk_o[i] = key;
+}
+
+int32_t density_fused_max() { return FZ_N; }
+
+void launch_density_fused(const FusedIOS& io, int32_t n, GridDesc g, SphConst c, hipStream_t s) {
+    if (n <= 0 || n > FZ_N) return;
+    const int32_t grid = (n + FZS_BLK / 64 - 1) / (FZS_BLK / 64);
+    if (g.xsub == 2)
+        SPH_LAUNCH(k_density_fused<2>, grid, FZS_BLK, 0, s, io, n, g, c);
+    else
+        SPH_LAUNCH(k_density_fused<1>, grid, FZS_BLK, 0, s, io, n, g, c);
 }
 
 void launch_density_small(const float4* pos, const uint32_t* cs, int32_t n, GridDesc g, SphConst c, float2* rp,

@@ -54,3 +54,33 @@ def test_small_form_bit_identical_to_tiled(pkg, monkeypatch, case):
     finally:
         tiled.close()
         small.close()
+
+
+@pytest.mark.parametrize("case", ["C1", "3d", "violent"])
+def test_two_launch_step_bit_identical(pkg, monkeypatch, case):
+    """Model S at n <= 4,096: the re-sort fused into pass 1 (wcsph_tiled.hip k_density_fused, then k_force_small on
+    the sorted arrays it wrote; two launches per step) against the re-sort kernel + the small form (SPH_FUSED=0)."""
+    def make(flag):
+        monkeypatch.setenv("SPH_FUSED", flag)
+        if case == "C1":
+            s = pkg.SPHSim.from_config("C1")
+        else:
+            sc = pkg.make_scenario(pkg.SPH_SCENARIO_DAMBREAK, 3, 16, 16, 16, 32, 32, 32, dx=0.01, seed=9)
+            s = pkg.SPHSim(sc, capacity=4096)
+            if case == "violent":
+                rng = np.random.default_rng(13)
+                x = s.positions()
+                v = rng.uniform(-1.0, 1.0, x.shape).astype(np.float32) * (2 * s.params.h / 6 / s.dt)
+                s.ctx.upload_state(x, v)
+        monkeypatch.delenv("SPH_FUSED")
+        return s
+
+    three, two = make("0"), make("1")
+    try:
+        for k in (1, 2, 7, 40):
+            three.step(k)
+            two.step(k)
+            _same(three.ctx, two.ctx, f"{case}, after {k} more steps")
+    finally:
+        three.close()
+        two.close()
