@@ -86,7 +86,9 @@ def test_resort_after_state_changes(pkg, monkeypatch):
             s.step(3)
         _assert_same(full.ctx, inc.ctx, "after state changes")
         ks = inc.ctx.kernel_stats()
-        assert ks["radix_sort"]["launches"] == 4 and ks["resort"]["launches"] == 10
+        # C1 is within the two-launch step's size: there the re-sort runs inside k_density_fused
+        incremental = sum(ks.get(k, {}).get("launches", 0) for k in ("resort", "density_fused"))
+        assert ks["radix_sort"]["launches"] == 4 and incremental == 10, ks
     finally:
         full.close()
         inc.close()
