@@ -203,7 +203,7 @@ def _timed_cpu(step, budget_s):
     return steps, time.perf_counter() - t0
 
 
-def rate_table(budget_s: float, gpu_steps: int = 50):
+def rate_table(budget_s: float, gpu_steps: int = 500):
     """SURVEY.md §8d CPU-baseline table: GPU, 1-thread and all-thread oracle rates (particle-steps/s) at
     C1, C2, C3 (Model S) and Model R at N = 4,096 / 32,768 (positions in the R = 15 sphere, the
     test_gpu_parity recipe). Rank 0, N = 1; the oracle runs only here, as the timed CPU reference."""
@@ -281,6 +281,25 @@ def rate_table(budget_s: float, gpu_steps: int = 50):
             row[f"cpu_{th}t_steps"] = k
         rows.append(row)
         print(json.dumps(row), flush=True)
+    # the controller's own scene (InitParticles, ParticleSystemController.cs:12's 4,096 particles) at its 1/144 s frame
+    n, dt = 4096, 1.0 / 144.0
+    ctl = pkg.ParticleSystemController(particleCount=n)
+    ctl.Start()
+    parts = ctl.GetParticles().copy()
+    g = gpu_rate(lambda k: ctl.context.step(dt, k), n)
+    ctl.OnDestroy()
+    row = {"model": "R", "config": f"controller InitParticles, N={n}, dt=1/144", "particles": n, "gpu": g}
+    cp = O.contact_params(dt)
+    for th in (1, allc):
+        st = {"p": parts.view(O.PARTICLE84).copy()}
+
+        def one(st=st, th=th):
+            st["p"], _ = O.contact_step(cp, st["p"], nthreads=th)
+        k, el = _timed_cpu(one, budget_s)
+        row[f"cpu_{th}t"] = n * k / el
+        row[f"cpu_{th}t_steps"] = k
+    rows.append(row)
+    print(json.dumps(row), flush=True)
     return {"unit": "particle-steps/s", "threads_all": allc, "budget_s_per_cpu_cell": budget_s,
             "gpu_steps": gpu_steps, "rows": rows}
 
