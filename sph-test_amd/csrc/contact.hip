@@ -9,13 +9,19 @@
 // (adhesion.hip), k_contact_finish.
 // Jacobi semantics: all reads come from the start-of-step arrays, all writes go to the
 // *_o arrays. The reaction torque the reference scatters with three InterlockedAdds per
-// contact (compute:291-294) is gathered instead: particle a evaluates each contact pair a
-// second time from b's side and sums the same truncated int3 terms. int32 addition is
-// associative, so the sum is bit-identical to the atomic one, with no atomics and no
-// ordering dependence.
+// contact (compute:291-294) is gathered instead: particle a sums the truncated int3 terms b's
+// thread would scatter into it. int32 addition is associative, so the sum is bit-identical to the
+// atomic one, with no atomics and no ordering dependence. b's term needs no second evaluation of the
+// pair body from b's side: that evaluation's torqueB equals a's own torqueA bit for bit up to the
+// sign of zero components (below, reaction_equals_own), which the truncation to int removes.
 // Every rounding is the one written (no fused multiply-adds), as in the oracle: with the double-evaluated
 // intrinsics (vec3.h) the Model R step is bit-identical to oracle/contact_oracle.c.
 #pragma clang fp contract(off)
+#ifdef SPH_CONTACT_PROBE
+namespace sph { extern __device__ uint64_t g_ct_probe[]; }
+#define FZ_PROBE(slot) \
+    do { if (threadIdx.x == 0 && blockIdx.x < 256) sph::g_ct_probe[blockIdx.x * 24 + (slot)] = wall_clock64(); } while (0)
+#endif
 #include "bonds.h"
 #include "common.h"
 #include "fused_perm.h"
@@ -61,6 +67,15 @@ __device__ __forceinline__ int contact_pair(const ContactConst& c, const Body& A
     torqueB = cross(dir * effectiveRadiusTorqueB, frictionDir * frictionMag);
     return 2;
 }
+// reaction_equals_own: b's thread evaluates contact_pair(c, B, A) and scatters its torqueB into a (compute:291-294).
+// Every quantity of that evaluation is the one of contact_pair(c, A, B), exactly or negated exactly, because IEEE
+// subtraction, multiplication, division and sqrt are sign-symmetric and + is commutative, with no contraction
+// (fp contract off): delta' = -delta, dist' = dist, the same overlap, falloffs and contact points, dir' = -dir,
+// relSurfaceVel' = -relSurfaceVel, dot(rel', dir') = dot(rel, dir), tangentVel' = -tangentVel, the same slipSpeed
+// (so the same hit code), frictionDir' = -frictionDir, the same frictionMag, and effectiveRadiusTorqueB' is the
+// expression of effectiveRadiusTorqueA. So torqueB' = cross(-dir * eRTA, -frictionDir * frictionMag) = torqueA, with
+// at most the sign of a zero component differing (b - a = +0 where -(a - b) = -0), and ftoi(+-0) = 0. The oracle
+// evaluates both sides; the Model R bit-exact tests compare the int torque sums.
 
 // ApplySPHForces' neighbour loop (compute:228-300) for slot a, then its integration
 // (:302-306): v1 = v + F/m·dt, w1 = ω + T/I·dt, and the int reaction torque sums.
@@ -95,10 +110,9 @@ __device__ __forceinline__ void contact_accumulate(const float4* __restrict__ po
             const int hit = contact_pair(c, A, B, F, TA, TB);
             if (hit == 0) continue;
             totalForce = add_exact(totalForce, F);                           // :261
-            if (hit == 2) totalTorque = add_exact(totalTorque, TA);          // :289
-            f3 F2, TA2, TB2;
-            if (contact_pair(c, B, A, F2, TA2, TB2) == 2) {                  // b's scatter into a
-                const f3 sc = TB2 * dt * TORQUE_SCALE;                       // :291
+            if (hit == 2) {
+                totalTorque = add_exact(totalTorque, TA);                    // :289
+                const f3 sc = TA * dt * TORQUE_SCALE;                        // b's scatter into a, :291
                 tq[0] += (uint32_t)ftoi(sc.x);
                 tq[1] += (uint32_t)ftoi(sc.y);
                 tq[2] += (uint32_t)ftoi(sc.z);
@@ -165,17 +179,14 @@ __device__ __forceinline__ void contact_accumulate_team(const float4* __restrict
                     f3 TB;
                     const int h = contact_pair(c, A, B, F, TA, TB);
                     hit = h != 0;
+                    if (h == 2) {                                               // b's scatter into a, :291
+                        const f3 sc = TA * dt * TORQUE_SCALE;
+                        q0 += (uint32_t)ftoi(sc.x);
+                        q1 += (uint32_t)ftoi(sc.y);
+                        q2 += (uint32_t)ftoi(sc.z);
+                    }
                     if (h != 2) TA = mk(0, 0, 0);
                     if (h == 0) F = mk(0, 0, 0);
-                    if (hit) {
-                        f3 F2, TA2, TB2;
-                        if (contact_pair(c, B, A, F2, TA2, TB2) == 2) {         // b's scatter into a
-                            const f3 sc = TB2 * dt * TORQUE_SCALE;              // :291
-                            q0 += (uint32_t)ftoi(sc.x);
-                            q1 += (uint32_t)ftoi(sc.y);
-                            q2 += (uint32_t)ftoi(sc.z);
-                        }
-                    }
                 }
             }
             // this team's hits, lowest lane (= lowest j) first
@@ -270,17 +281,14 @@ __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict
         const Body B{xyz(pb), xyz(vb), xyz(wb), pb.w};
         f3 TB;
         const int h = contact_pair(c, A, B, F, TA, TB);
+        if (h == 2) {   // b's scatter into a (:291)
+            const f3 sc = TA * dt * TORQUE_SCALE;
+            q0 += (uint32_t)ftoi(sc.x);
+            q1 += (uint32_t)ftoi(sc.y);
+            q2 += (uint32_t)ftoi(sc.z);
+        }
         if (h != 2) TA = mk(0, 0, 0);
         if (h == 0) F = mk(0, 0, 0);
-        if (h != 0) {
-            f3 F2, TA2, TB2;
-            if (contact_pair(c, B, A, F2, TA2, TB2) == 2) {
-                const f3 sc = TB2 * dt * TORQUE_SCALE;
-                q0 += (uint32_t)ftoi(sc.x);
-                q1 += (uint32_t)ftoi(sc.y);
-                q2 += (uint32_t)ftoi(sc.z);
-            }
-        }
     };
     auto add_hit = [&](const f3& F, const f3& TA, int src) __attribute__((always_inline)) {
         totalForce = add_exact(totalForce, mk(__shfl(F.x, src, 64), __shfl(F.y, src, 64), __shfl(F.z, src, 64)));
@@ -288,21 +296,32 @@ __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict
     };
 #pragma unroll 1
     for (uint32_t round = 0; round < total; round += 64u * CF_CHUNKS) {
+        // chunks holding candidates (wave-uniform): a round past the last candidate scans nothing (the reference's
+        // R = 15 sphere: ~350 candidates, 6 of 8 chunks)
+        const uint32_t nch = min((total - round + 63u) >> 6, (uint32_t)CF_CHUNKS);
         uint32_t jj[CF_CHUNKS];
         float4 pb[CF_CHUNKS];
 #pragma unroll
         for (int ch = 0; ch < CF_CHUNKS; ++ch) {   // every position load of the round in flight together
+            if ((uint32_t)ch >= nch) break;
             const uint32_t f = round + (uint32_t)(ch * 64 + lane);
             jj[ch] = slot_of(min(f, total - 1u));
             pb[ch] = pos[M.old(jj[ch])];
         }
-        uint32_t touch = 0u;   // bit ch: candidate (round, ch, lane) touches a (:240, :253)
+        // bit ch: candidate (round, ch, lane) may touch a (:240, :253). A superset of the reference's test
+        // reff − |d| > 0.001 without the square root: |d|² < t² with t = reff − 0.0009 + 1e-5·reff, whose margin
+        // (1e-4 + 1e-5·reff) exceeds the few-ulp rounding of |d| and t for every reff; contact_pair's own first test
+        // is that same reference test, and a candidate it rejects adds F = TA = +0 (no change to the sums, which
+        // are never −0) and no torque.
+        uint32_t touch = 0u;
 #pragma unroll
         for (int ch = 0; ch < CF_CHUNKS; ++ch) {
+            if ((uint32_t)ch >= nch) break;
             const uint32_t f = round + (uint32_t)(ch * 64 + lane);
             const f3 d = A.pos - xyz(pb[ch]);
             const float reff = A.r * 0.5f + pb[ch].w * 0.5f;
-            if (f < total && (int32_t)jj[ch] != a && reff - len(d) > 0.001f) touch |= 1u << ch;
+            const float t = (reff - 0.0009f) + reff * 1e-5f;
+            if (f < total && (int32_t)jj[ch] != a && t > 0.0f && dot(d, d) < t * t) touch |= 1u << ch;
         }
         if (__any(__popc(touch) > CF_SLOTS)) {   // wave-uniform: chunk by chunk
 #pragma unroll
@@ -581,47 +600,104 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_finish(
 // share of the new cell-start table. Movers of this step go to the other list; the counters rotate over three (the one
 // this step appends to was zeroed by the step before).
 constexpr int FZ_BLK = 1024;   // 16 targets (one per wave) per workgroup: the permutation is built once per 16
+constexpr int FZ_T = FZ_BLK / 64;
+
+// Test-only timing probe (scripts/contact_probe.py, a -DSPH_CONTACT_PROBE build): per workgroup the wall clock (100 MHz)
+// at its start, after the permutation build, after the barrier and at its end, and each wave's end of its neighbour sums.
+#ifdef SPH_CONTACT_PROBE
+constexpr int CT_PROBE_W = 24;
+__device__ uint64_t g_ct_probe[256 * 24];
+static_assert(CT_PROBE_W == 24, "FZ_PROBE's stride");
+#define CT_PROBE(cond, slot)                                                                               \
+    do {                                                                                                   \
+        if ((cond) && blockIdx.x < 256) g_ct_probe[blockIdx.x * CT_PROBE_W + (slot)] = wall_clock64();    \
+    } while (0)
+extern "C" int sph_debug_contact_probe(uint64_t* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ct_probe), sizeof(g_ct_probe)) == hipSuccess ? 0 : -1;
+}
+#else
+#define CT_PROBE(cond, slot) \
+    do {                     \
+    } while (0)
+#endif
+
+// A target's neighbour sums, handed from its wave to the lane that finishes it
+struct FusedFin {
+    float4 pa, va, wa, rot, aux;
+    f3 v, w;
+    uint32_t tq[3];
+    uint32_t key_a;
+    int32_t id, mode;
+};
 
 __global__ __launch_bounds__(FZ_BLK) void k_contact_fused(FusedIO io, int32_t n_active, int32_t n, GridDesc g,
                                                           ContactConst c) {
     __shared__ FusedLds L;
-    const FusedMap M = fused_build<FZ_BLK>(L, io.count, io.mi, io.mk, io.cs, io.cs_o, g.ncells, n, io.count_zero,
-                                           io.host_count);
-    // one target per wave: sorted position a, read from the previous order's slot o
-    const int32_t a = blockIdx.x * (FZ_BLK / 64) + (int32_t)(threadIdx.x >> 6);
-    const bool lead = (threadIdx.x & 63u) == 0;
-    if (a >= n) return;   // wave-uniform
-    bool mv;
-    uint32_t key_a;
-    const uint32_t o = M.old_of((uint32_t)a, mv, key_a);
-    if (!mv) key_a = io.sk[o];
-    const float4 pa = io.pos[o], va = io.vel[o], wa = io.omg[o];
+    __shared__ FusedFin fin[FZ_T];
+    CT_PROBE(threadIdx.x == 0, 0);
+    const FusedMap M = fused_build<FZ_BLK>(L, io.count, io.mi, io.mk, io.cs, n, io.count_zero, io.host_count);
+    CT_PROBE(threadIdx.x == 0, 1);
+    {   // one target per wave: sorted position a, read from the previous order's slot o
+        const int32_t a = blockIdx.x * FZ_T + (int32_t)(threadIdx.x >> 6);
+        if (a < n) {   // wave-uniform
+            bool mv;
+            uint32_t key_a;
+            const uint32_t o = M.old_at((uint32_t)a, mv, key_a);
+            if (!mv) key_a = io.sk[o];
+            const float4 pa = io.pos[o], va = io.vel[o], wa = io.omg[o];
+            // the finishing lane's inputs, loaded under the neighbour sums
+            const float4 rot = io.rot[o], aux = io.aux[o];
+            const int32_t id = io.id[o], mode = io.mode[o];
+            f3 v = xyz(va), w = xyz(wa);
+            uint32_t tq[3] = {0u, 0u, 0u};
+            if (a < n_active) contact_accumulate_flat(io.pos, io.vel, io.omg, M, g, c, a, pa, va, wa, v, w, tq);
+            if ((threadIdx.x & 63u) == 0) {
+                FusedFin& f = fin[threadIdx.x >> 6];
+                f.pa = pa; f.va = va; f.wa = wa; f.v = v; f.w = w;
+                f.tq[0] = tq[0]; f.tq[1] = tq[1]; f.tq[2] = tq[2];
+                f.rot = rot; f.aux = aux;
+                f.key_a = key_a; f.id = id; f.mode = mode;
+            }
+        }
+        CT_PROBE((threadIdx.x & 63u) == 0, 8 + (threadIdx.x >> 6));
+    }
+    __syncthreads();
+    CT_PROBE(threadIdx.x == 0, 2);
+    // drag, motion and rotation of the workgroup's 16 targets on 16 lanes of wave 0: the per-target tail (double-
+    // evaluated exp, sin, cos) costs one wave's issue instead of sixteen. Waves 1-15 meanwhile write the workgroup's
+    // share of the new cell-start table.
+    if (threadIdx.x >= 64u) {
+        fused_cs_share(M, io.cs_o, g.ncells, threadIdx.x - 64u, FZ_BLK - 64u);
+        return;
+    }
+    const int32_t a = blockIdx.x * FZ_T + (int32_t)threadIdx.x;
+    if (threadIdx.x >= (uint32_t)FZ_T || a >= n) return;
+    const FusedFin& f = fin[threadIdx.x];
+    const uint32_t key_a = f.key_a;
+    const float4 pa = f.pa, va = f.va, wa = f.wa;
     uint32_t key_n;
     f3 p, v, w;
     float4 q;
-    uint32_t tq[3] = {0u, 0u, 0u};
     if (a >= n_active) {   // inactive slots (id >= activeParticleCount): drag only
-        if (!lead) return;
-        v = apply_drag(c, io.id[o], xyz(pa), xyz(va), va.w);
+        v = apply_drag(c, f.id, xyz(pa), xyz(va), va.w);
         p = xyz(pa);
         w = xyz(wa);
-        q = io.rot[o];
+        q = f.rot;
         key_n = g.ncells;
     } else {
-        contact_accumulate_flat(io.pos, io.vel, io.omg, M, g, c, a, pa, va, wa, v, w, tq);
-        if (!lead) return;
-        contact_finish(c, io.id[o], pa, v, w, va.w, wa.w, io.aux[o].x, io.rot[o], tq, p, v, w, q);
+        contact_finish(c, f.id, pa, f.v, f.w, va.w, wa.w, f.aux.x, f.rot, f.tq, p, v, w, q);
         key_n = cell_key(g, p.x, p.y, p.z);
     }
     io.pos_o[a] = a >= n_active ? pa : make_float4(p.x, p.y, p.z, pa.w);
     io.vel_o[a] = make_float4(v.x, v.y, v.z, va.w);
     io.omg_o[a] = a >= n_active ? wa : make_float4(w.x, w.y, w.z, wa.w);
     io.rot_o[a] = q;
-    io.aux_o[a] = io.aux[o];
-    io.id_o[a] = io.id[o];
-    io.mode_o[a] = io.mode[o];
+    io.aux_o[a] = f.aux;
+    io.id_o[a] = f.id;
+    io.mode_o[a] = f.mode;
     if (io.torque_o) {
-        io.torque_o[3 * a] = (int32_t)tq[0]; io.torque_o[3 * a + 1] = (int32_t)tq[1]; io.torque_o[3 * a + 2] = (int32_t)tq[2];
+        io.torque_o[3 * a] = (int32_t)f.tq[0]; io.torque_o[3 * a + 1] = (int32_t)f.tq[1];
+        io.torque_o[3 * a + 2] = (int32_t)f.tq[2];
     }
     io.sk_o[a] = key_a;
     io.keys_o[a] = key_n;
@@ -633,13 +709,14 @@ __global__ __launch_bounds__(FZ_BLK) void k_contact_fused(FusedIO io, int32_t n_
             io.mo_o[r] = key_a;
         }
     }
+    CT_PROBE(threadIdx.x == 0, 3);
 }
 
 int32_t contact_fused_max() { return FZ_N; }
 
 void launch_contact_fused(const FusedIO& io, int32_t n_active, int32_t n, GridDesc g, ContactConst c, hipStream_t s) {
     if (n <= 0 || n > FZ_N) return;
-    SPH_LAUNCH(k_contact_fused, (n + FZ_BLK / 64 - 1) / (FZ_BLK / 64), FZ_BLK, 0, s, io, n_active, n, g, c);
+    SPH_LAUNCH(k_contact_fused, (n + FZ_T - 1) / FZ_T, FZ_BLK, 0, s, io, n_active, n, g, c);
 }
 
 // Lanes per target: enough teams to fill the chip (256 CUs × 8 waves × 64 lanes ≈ 131k lanes) without

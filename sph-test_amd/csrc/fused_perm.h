@@ -5,6 +5,13 @@
 #pragma once
 #include "common.h"
 
+// test-only phase clocks (contact.hip defines it in its -DSPH_CONTACT_PROBE build)
+#ifndef FZ_PROBE
+#define FZ_PROBE(slot) \
+    do {               \
+    } while (0)
+#endif
+
 namespace sph {
 
 constexpr int32_t FZ_N = 4096;
@@ -32,70 +39,74 @@ struct FusedMap {
         }
         return c + lo - A(c);   // old keys follow the old slots: movers with an old key < k = A(cs[k])
     }
-    // the previous order's slot of sorted position j; mv: it is a mover (its new key in key)
-    __device__ __forceinline__ uint32_t old_of(uint32_t j, bool& mv, uint32_t& key) const {
+    // LDS: for every sorted position its previous slot (bits 0-15) and, for a mover, 1 + its index in ms (bits 16-31)
+    const uint32_t* pm;
+    __device__ __forceinline__ uint32_t old(uint32_t j) const { return m == 0 ? j : (pm[j] & 0xffffu); }
+    // the previous order's slot of sorted position j, from the table; mv: it is a mover (its new key in key)
+    __device__ __forceinline__ uint32_t old_at(uint32_t j, bool& mv, uint32_t& key) const {
         mv = false;
         if (m == 0) return j;
-        uint32_t lo = 0, hi = m;   // movers placed below j
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (dst[mid] < j) lo = mid + 1;
-            else hi = mid;
-        }
-        if (lo < m && dst[lo] == j) {
+        const uint32_t e = pm[j];
+        if (e >> 16) {
             mv = true;
-            key = (uint32_t)(ms[lo] >> 32);
-            return (uint32_t)ms[lo];
+            key = (uint32_t)(ms[(e >> 16) - 1u] >> 32);
         }
-        const uint32_t s = j - lo;   // the s-th stayer: the smallest i with (i + 1) − A(i + 1) > s, i in [s, s + m]
-        uint32_t a = s, b = s + m;
-        while (a < b) {
-            const uint32_t mid = (a + b) >> 1;
-            if (mid + 1u - A(mid + 1u) > s) b = mid;
-            else a = mid + 1;
-        }
-        return a;
+        return e & 0xffffu;
     }
-    const uint16_t* pm;    // LDS: old_of for every sorted position (filled once per workgroup)
-    __device__ __forceinline__ uint32_t old(uint32_t j) const { return m == 0 ? j : (uint32_t)pm[j]; }
 };
 
 
 // The permutation of a step with m movers (mi: old slot, mk: new key) over n <= FZ_N slots, built by every thread of a
-// BLK-thread workgroup into LDS; also writes the workgroup's share of the new cell-start table (cs_o, ncells + 2
-// entries) and, from workgroup 0, zeroes `zero` and stores m into host_count (mapped host memory) when given.
+// BLK-thread workgroup into LDS; from workgroup 0 it also zeroes `zero` and stores m into host_count (mapped host
+// memory) when given. The caller writes the workgroup's share of the new cell-start table (fused_cs_share).
 struct FusedLds {
     uint64_t ms[FZ_N];
     uint32_t dst[FZ_N];
     uint32_t bm[FZ_WORDS], bpre[FZ_WORDS];
-    uint16_t pm[FZ_N];
+    uint32_t pm[FZ_N];
 };
 
 template <int BLK>
 __device__ FusedMap fused_build(FusedLds& L, const uint32_t* __restrict__ count, const uint32_t* __restrict__ mi,
-                                const uint32_t* __restrict__ mk, const uint32_t* __restrict__ cs, uint32_t* __restrict__ cs_o,
-                                uint32_t ncells, int32_t n, uint32_t* zero, uint32_t* host_count) {
+                                const uint32_t* __restrict__ mk, const uint32_t* __restrict__ cs, int32_t n, uint32_t* zero,
+                                uint32_t* host_count) {
     uint64_t* ms = L.ms;
     uint32_t* dst = L.dst;
     uint32_t* bm = L.bm;
     uint32_t* bpre = L.bpre;
-    uint16_t* pm = L.pm;
-    const uint32_t m = min(*count, (uint32_t)n);
+    uint32_t* pm = L.pm;
+    // the count and the first BLK movers' entries in one round trip (the lists hold n entries: in bounds)
+    const uint32_t m_raw = *count;
+    uint32_t x0 = 0u, k0 = 0u;
+    if (threadIdx.x < (uint32_t)n) {
+        x0 = mi[threadIdx.x];
+        k0 = mk[threadIdx.x];
+    }
+    const uint32_t nw = ((uint32_t)n >> 5) + 1u;
+    for (uint32_t t = threadIdx.x; t < nw; t += BLK) bm[t] = 0u;
+    const uint32_t m = min(m_raw, (uint32_t)n);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (zero) *zero = 0u;
         if (host_count) *host_count = m;
     }
-    const uint32_t nw = ((uint32_t)n >> 5) + 1u;
-    for (uint32_t t = threadIdx.x; t < nw; t += BLK) bm[t] = 0u;
     __syncthreads();
     for (uint32_t r = threadIdx.x; r < m; r += BLK) {
-        const uint32_t x = mi[r], k = mk[r];
+        const uint32_t x = r < (uint32_t)BLK ? x0 : mi[r], k = r < (uint32_t)BLK ? k0 : mk[r];
         ms[r] = (uint64_t)k << 32 | x;
         atomicOr(&bm[x >> 5], 1u << (x & 31u));
     }
+    // the old cell range of a mover's new key (its position below clamps the slot into it), loaded under the sort
+    uint32_t c0 = 0u, c1 = 0u;
+    if (threadIdx.x < m) {
+        c0 = cs[k0];
+        c1 = cs[k0 + 1u];
+    }
     __syncthreads();
-    // the movers in (new key, slot) order: up to BLK by counting, more by a bitonic sort
-    if (m <= (uint32_t)BLK) {
+    FZ_PROBE(4);
+    // the movers in (new key, slot) order: up to BLK by counting (each entry's clamped slot q rides along in dst),
+    // more by a bitonic sort
+    const bool counted = m <= (uint32_t)BLK;
+    if (counted) {
         uint64_t e = 0;
         uint32_t rk = 0;
         if (threadIdx.x < m) {
@@ -103,7 +114,10 @@ __device__ FusedMap fused_build(FusedLds& L, const uint32_t* __restrict__ count,
             for (uint32_t f = 0; f < m; ++f) rk += ms[f] < e ? 1u : 0u;
         }
         __syncthreads();
-        if (threadIdx.x < m) ms[rk] = e;
+        if (threadIdx.x < m) {
+            ms[rk] = e;
+            dst[rk] = x0 < c0 ? c0 : (x0 > c1 ? c1 : x0);
+        }
     } else {
         uint32_t P = 1;
         while (P < m) P <<= 1;
@@ -122,6 +136,7 @@ __device__ FusedMap fused_build(FusedLds& L, const uint32_t* __restrict__ count,
                 __syncthreads();
             }
     }
+    FZ_PROBE(5);
     // the bitmap's word prefix (nw <= FZ_WORDS words)
     if (threadIdx.x < 64) {
         uint32_t carry = 0;
@@ -140,27 +155,53 @@ __device__ FusedMap fused_build(FusedLds& L, const uint32_t* __restrict__ count,
     }
     __syncthreads();
     FusedMap M{cs, ms, dst, bm, bpre, m, pm};
-    for (uint32_t r = threadIdx.x; r < m; r += BLK) {   // the movers' sorted positions
-        const uint32_t k = (uint32_t)(ms[r] >> 32), x = (uint32_t)ms[r];
-        const uint32_t c0 = cs[k], c1 = cs[k + 1];
-        const uint32_t q = x < c0 ? c0 : (x > c1 ? c1 : x);
+    for (uint32_t r = threadIdx.x; r < m; r += BLK) {   // the movers' sorted positions (q − A(q)) + r
+        uint32_t q;
+        if (counted) {
+            q = dst[r];
+        } else {
+            const uint32_t k = (uint32_t)(ms[r] >> 32), x = (uint32_t)ms[r];
+            const uint32_t a0 = cs[k], a1 = cs[k + 1];
+            q = x < a0 ? a0 : (x > a1 ? a1 : x);
+        }
         dst[r] = (q - M.A(q)) + r;
     }
     __syncthreads();
+    FZ_PROBE(6);
     if (m) {   // the whole permutation: a lookup is one LDS read
-        for (uint32_t j = threadIdx.x; j < (uint32_t)n; j += BLK) {
-            bool mv;
-            uint32_t key;
-            pm[j] = (uint16_t)M.old_of(j, mv, key);
+        // movers at their positions; stayers scattered from the old order: a thread takes a run of old slots, the
+        // stayer of rank s = i − A(i) lands at s + #{r : dst[r] − r <= s} (dst[r] − r, the stayers placed before
+        // mover r, does not decrease): one search for the run's first stayer, then a walk
+        for (uint32_t r = threadIdx.x; r < m; r += BLK) pm[dst[r]] = (uint32_t)ms[r] | ((r + 1u) << 16);
+        const uint32_t per = ((uint32_t)n + BLK - 1u) / BLK;
+        const uint32_t i0 = threadIdx.x * per, i1 = min(i0 + per, (uint32_t)n);
+        if (i0 < i1) {
+            uint32_t st = i0 - M.A(i0);
+            uint32_t lo = 0, hi = m;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (dst[mid] - mid <= st) lo = mid + 1;
+                else hi = mid;
+            }
+            for (uint32_t i = i0; i < i1; ++i) {
+                if ((bm[i >> 5] >> (i & 31u)) & 1u) continue;   // a mover
+                while (lo < m && dst[lo] - lo <= st) ++lo;
+                pm[st + lo] = i;
+                ++st;
+            }
         }
         __syncthreads();
     }
-    {   // this workgroup's share of the new cell-start table (entry ncells + 1: the slot count, unchanged)
-        const uint32_t tot = ncells + 2u, G = gridDim.x;
-        const uint32_t k0 = (uint32_t)((uint64_t)tot * blockIdx.x / G), k1 = (uint32_t)((uint64_t)tot * (blockIdx.x + 1) / G);
-        for (uint32_t k = k0 + threadIdx.x; k < k1; k += BLK) cs_o[k] = k <= ncells ? M.start(k) : cs[k];
-    }
     return M;
+}
+
+// This workgroup's share of the new cell-start table (ncells + 2 entries; entry ncells + 1, the slot count, unchanged),
+// by threads t = 0..T-1 of it. The pass needs none of it, so a kernel runs it where its lanes would idle.
+__device__ __forceinline__ void fused_cs_share(const FusedMap& M, uint32_t* __restrict__ cs_o, uint32_t ncells,
+                                               uint32_t t, uint32_t T) {
+    const uint32_t tot = ncells + 2u, G = gridDim.x;
+    const uint32_t k0 = (uint32_t)((uint64_t)tot * blockIdx.x / G), k1 = (uint32_t)((uint64_t)tot * (blockIdx.x + 1) / G);
+    for (uint32_t k = k0 + t; k < k1; k += T) cs_o[k] = k <= ncells ? M.start(k) : M.cs[k];
 }
 
 }  // namespace sph

@@ -1078,16 +1078,11 @@ __global__ __launch_bounds__(256) void k_force_small(const float4* __restrict__ 
 // launches per step instead of three, bit-identical (tests/test_gpu_small.py).
 constexpr int FZS_BLK = 1024;
 template <int XS>
-__global__ __launch_bounds__(FZS_BLK) void k_density_fused(FusedIOS io, int32_t n, GridDesc g, SphConst c) {
-    __shared__ FusedLds L;
-    const FusedMap M = fused_build<FZS_BLK>(L, io.count, io.mi, io.mk, io.cs, io.cs_o, g.ncells, n, io.count_zero,
-                                            io.host_count);
-    const int lane = (int)lane_id();
-    const int32_t i = (int32_t)blockIdx.x * (FZS_BLK / 64) + (int32_t)(threadIdx.x >> 6);
-    if (i >= n) return;   // wave-uniform
+__device__ __forceinline__ void density_fused_target(const FusedIOS& io, const FusedMap& M, int32_t i, int lane,
+                                                     const GridDesc& g, const SphConst& c) {
     bool mv;
     uint32_t key;
-    const uint32_t o = M.old_of((uint32_t)i, mv, key);
+    const uint32_t o = M.old_at((uint32_t)i, mv, key);
     if (!mv) key = io.sk[o];
     const float4 pi = io.pos[o];
     const SmallRows<XS> R(g, M, pi, lane);
@@ -1107,6 +1102,19 @@ __global__ __launch_bounds__(FZS_BLK) void k_density_fused(FusedIOS io, int32_t 
     io.vel_o[i] = io.vel[o];
     io.id_o[i] = io.id[o];
     io.sk_o[i] = key;
+}
+
+template <int XS>
+__global__ __launch_bounds__(FZS_BLK) void k_density_fused(FusedIOS io, int32_t n, GridDesc g, SphConst c) {
+    __shared__ FusedLds L;
+    const FusedMap M = fused_build<FZS_BLK>(L, io.count, io.mi, io.mk, io.cs, n, io.count_zero, io.host_count);
+    const int lane = (int)lane_id();
+    const int32_t i = (int32_t)blockIdx.x * (FZS_BLK / 64) + (int32_t)(threadIdx.x >> 6);
+    if (i < n) {   // wave-uniform
+        density_fused_target<XS>(io, M, i, lane, g, c);
+    }
+    // the workgroup's share of the new cell-start table, each wave after its target
+    fused_cs_share(M, io.cs_o, g.ncells, threadIdx.x, FZS_BLK);
 }
 
 int32_t density_fused_max() { return FZ_N; }
