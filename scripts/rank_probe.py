@@ -20,12 +20,19 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="C3")
 ap.add_argument("--advance", type=int, default=5000)
 ap.add_argument("--steps", type=int, default=10)
+ap.add_argument("--slab", type=int, default=0,
+                help="C3 x N as a serialised local group of N slabs; the probe holds the last re-sort launched")
 a = ap.parse_args()
 pkg = GE.load_package()
 from importlib import import_module  # noqa: E402
 abi = import_module(pkg.__name__ + "._abi")
 L = abi.lib()
-sim = pkg.SPHSim.from_config(a.config)
+if a.slab > 1:
+    from sph_test_amd import slab  # noqa: E402
+    os.environ.setdefault("SPH_DEBUG_SERIAL_GROUP", "1")
+    sim = pkg.SPHSim(slab.weak_scenario(a.config, a.slab), ndev=a.slab, rebalance_every=0)
+else:
+    sim = pkg.SPHSim.from_config(a.config)
 done = 0
 while done < a.advance:
     k = min(1000, a.advance - done)
