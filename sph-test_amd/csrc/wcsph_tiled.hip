@@ -1013,6 +1013,41 @@ __device__ __forceinline__ float lanef(float v, uint32_t src) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)src));
 }
 
+// s + w over the wave's lanes in lane (visit) order, taking only the lanes whose w is not ±0: s starts at +0 and the
+// weights are ≥ +0, so s is never −0 and adding a zero term leaves it unchanged bit for bit (NaN terms are kept).
+__device__ __forceinline__ float visit_sum(float s, float w) {
+    for (uint64_t m = __ballot(w != 0.0f); m; m &= m - 1ull) s += lanef(w, (uint32_t)__builtin_ctzll(m));
+    return s;
+}
+
+// The force sums of a wave's hits in visit order, transposed: lane c < 6 accumulates component c (the a = cf·d and
+// s = −cx·du products of pair_add, the same fused multiply-adds in the same order), reading each hit's terms from
+// the wave's LDS row instead of eight lane reads per hit.
+struct HitTerms {
+    float4 a, b;   // (cf, dx, dy, dz), (cx, du, dv, dw)
+};
+__device__ __forceinline__ float hit_fold(float acc, const HitTerms* row, uint64_t m, int lane) {
+    const float* base = reinterpret_cast<const float*>(row);
+    const int pi = lane < 3 ? 0 : 4;                      // cf or cx
+    const int qi = lane < 3 ? 1 + lane : 5 + (lane - 3);  // dx, dy, dz or du, dv, dw
+    const float sg = lane < 3 ? 1.0f : -1.0f;
+    while (m) {
+        const int s0 = __builtin_ctzll(m);
+        m &= m - 1ull;
+        const float p0 = sg * base[8 * s0 + pi], q0 = base[8 * s0 + qi];
+        if (m) {
+            const int s1 = __builtin_ctzll(m);
+            m &= m - 1ull;
+            const float p1 = sg * base[8 * s1 + pi], q1 = base[8 * s1 + qi];
+            acc = fmaf(p0, q0, acc);
+            acc = fmaf(p1, q1, acc);
+        } else {
+            acc = fmaf(p0, q0, acc);
+        }
+    }
+    return acc;
+}
+
 template <int XS>
 __global__ __launch_bounds__(256) void k_density_small(const float4* __restrict__ pos, const uint32_t* __restrict__ cs,
                                                        int32_t n, GridDesc g, SphConst c, float2* __restrict__ rp) {
@@ -1028,8 +1063,7 @@ __global__ __launch_bounds__(256) void k_density_small(const float4* __restrict_
         float v;
         const float w4 = spline_w4(c, dist2(pi, pos[R.slot(min(f, R.total - 1u))]), v);
         const float w = f < R.total ? w4 : 0.0f;
-#pragma unroll
-        for (int t = 0; t < 64; ++t) s += lanef(w, (uint32_t)t);   // visit order; past the end +0
+        s = visit_sum(s, w);
     }
     if (lane == 0) rp[i] = density_eos(c, s);
 }
@@ -1046,26 +1080,32 @@ __global__ __launch_bounds__(256) void k_force_small(const float4* __restrict__ 
     const float4 pi = pos[i], vi = vel[i];
     const float2 ri = rp[i];
     const SmallRows<XS> R(g, cs, pi, lane);
-    ForceAcc acc{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    __shared__ HitTerms rows[4][64];
+    HitTerms* row = rows[threadIdx.x >> 6];
+    float comp = 0.0f;   // lane c < 6: component c of the sums (pair_add's ax, ay, az, sx, sy, sz)
 #pragma unroll 1
     for (uint32_t base = 0; base < R.total; base += 64u) {
         const uint32_t f = base + (uint32_t)lane;
         const uint32_t j = R.slot(min(f, R.total - 1u));
         const float4 pj = pos[j];
         const bool hit = f < R.total && is_hit(c, dist2(pi, pj));
-        PairTerms t{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         if (hit) {
             const float4 vj = vel[j];
             const float2 rj = rp[j];
-            t = pair_terms(pk, pi, vi, ri.x, ri.y, make_float4(pj.x, pj.y, pj.z, rj.x), make_float4(vj.x, vj.y, vj.z, rj.y));
+            const PairTerms t =
+                pair_terms(pk, pi, vi, ri.x, ri.y, make_float4(pj.x, pj.y, pj.z, rj.x), make_float4(vj.x, vj.y, vj.z, rj.y));
+            row[lane] = HitTerms{make_float4(t.cf, t.dx, t.dy, t.dz), make_float4(t.cx, t.du, t.dv, t.dw)};
         }
-        for (uint64_t m = __ballot(hit); m; m &= m - 1ull) {   // the hits in visit order
-            const uint32_t src = (uint32_t)__builtin_ctzll(m);
-            const PairTerms u{lanef(t.cf, src), lanef(t.dx, src), lanef(t.dy, src), lanef(t.dz, src),
-                              lanef(t.cx, src), lanef(t.du, src), lanef(t.dv, src), lanef(t.dw, src)};
-            pair_add(u, acc);
-        }
+        const uint64_t m = __ballot(hit);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < 6) comp = hit_fold(comp, row, m, lane);   // the hits in visit order
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    const ForceAcc acc{lanef(comp, 0), lanef(comp, 1), lanef(comp, 2), lanef(comp, 3), lanef(comp, 4), lanef(comp, 5)};
     if (lane != 0) return;
     const uint32_t key = integrate_target<XS>(acc, pk, c, g, pi, vi, dt, fext_x, i, pos_o, vel_o, keys_o);
     append_mover(mv, i, key);   // one lane: window_key = cell_key in a single domain
@@ -1085,6 +1125,8 @@ __device__ __forceinline__ void density_fused_target(const FusedIOS& io, const F
     const uint32_t o = M.old_at((uint32_t)i, mv, key);
     if (!mv) key = io.sk[o];
     const float4 pi = io.pos[o];
+    const float4 vi = io.vel[o];   // written at the end: loaded under the sums
+    const int32_t idi = io.id[o];
     const SmallRows<XS> R(g, M, pi, lane);
     float s = 0.0f;
 #pragma unroll 1
@@ -1093,14 +1135,13 @@ __device__ __forceinline__ void density_fused_target(const FusedIOS& io, const F
         float v;
         const float w4 = spline_w4(c, dist2(pi, io.pos[M.old(R.slot(min(f, R.total - 1u)))]), v);
         const float w = f < R.total ? w4 : 0.0f;
-#pragma unroll
-        for (int t = 0; t < 64; ++t) s += lanef(w, (uint32_t)t);   // visit order; past the end +0
+        s = visit_sum(s, w);
     }
     if (lane != 0) return;
     io.rp_o[i] = density_eos(c, s);
     io.pos_o[i] = pi;
-    io.vel_o[i] = io.vel[o];
-    io.id_o[i] = io.id[o];
+    io.vel_o[i] = vi;
+    io.id_o[i] = idi;
     io.sk_o[i] = key;
 }
 
