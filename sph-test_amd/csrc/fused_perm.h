@@ -66,6 +66,23 @@ struct FusedLds {
     uint32_t pm[FZ_N];
 };
 
+// the bitmap's exclusive word prefix (nw <= FZ_WORDS words) by one wave, lane t
+__device__ __forceinline__ void word_prefix(const uint32_t* bm, uint32_t* bpre, uint32_t nw, uint32_t lane) {
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nw; base += 64) {
+        const uint32_t t = base + lane;
+        const uint32_t v = t < nw ? (uint32_t)__popc(bm[t]) : 0u;
+        uint32_t inc = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
+            if (lane >= (uint32_t)o) inc += u;
+        }
+        if (t < nw) bpre[t] = carry + inc - v;
+        carry += (uint32_t)__shfl((int)inc, 63, 64);
+    }
+}
+
 template <int BLK>
 __device__ FusedMap fused_build(FusedLds& L, const uint32_t* __restrict__ count, const uint32_t* __restrict__ mi,
                                 const uint32_t* __restrict__ mk, const uint32_t* __restrict__ cs, int32_t n, uint32_t* zero,
@@ -106,6 +123,9 @@ __device__ FusedMap fused_build(FusedLds& L, const uint32_t* __restrict__ count,
     // the movers in (new key, slot) order: up to BLK by counting (each entry's clamped slot q rides along in dst),
     // more by a bitonic sort
     const bool counted = m <= (uint32_t)BLK;
+    // the bitmap's word prefix needs only the bitmap: the last wave takes it beside a counting sort that leaves it idle
+    const bool pre_last = m <= (uint32_t)BLK - 64u;
+    if (pre_last && threadIdx.x >= (uint32_t)BLK - 64u) word_prefix(bm, bpre, nw, threadIdx.x - ((uint32_t)BLK - 64u));
     if (counted) {
         uint64_t e = 0;
         uint32_t rk = 0;
@@ -137,22 +157,7 @@ __device__ FusedMap fused_build(FusedLds& L, const uint32_t* __restrict__ count,
             }
     }
     FZ_PROBE(5);
-    // the bitmap's word prefix (nw <= FZ_WORDS words)
-    if (threadIdx.x < 64) {
-        uint32_t carry = 0;
-        for (uint32_t base = 0; base < nw; base += 64) {
-            const uint32_t t = base + threadIdx.x;
-            const uint32_t v = t < nw ? (uint32_t)__popc(bm[t]) : 0u;
-            uint32_t inc = v;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
-                if (lane_id() >= (uint32_t)o) inc += u;
-            }
-            if (t < nw) bpre[t] = carry + inc - v;
-            carry += (uint32_t)__shfl((int)inc, 63, 64);
-        }
-    }
+    if (!pre_last && threadIdx.x < 64) word_prefix(bm, bpre, nw, threadIdx.x);
     __syncthreads();
     FusedMap M{cs, ms, dst, bm, bpre, m, pm};
     for (uint32_t r = threadIdx.x; r < m; r += BLK) {   // the movers' sorted positions (q − A(q)) + r
