@@ -1031,19 +1031,22 @@ __device__ __forceinline__ float hit_fold(float acc, const HitTerms* row, uint64
     const int pi = lane < 3 ? 0 : 4;                      // cf or cx
     const int qi = lane < 3 ? 1 + lane : 5 + (lane - 3);  // dx, dy, dz or du, dv, dw
     const float sg = lane < 3 ? 1.0f : -1.0f;
+    while (__popcll(m) >= 4) {   // four hits' reads in flight, then their four multiply-adds in order
+        float p[4], q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int su = __builtin_ctzll(m);
+            m &= m - 1ull;
+            p[u] = sg * base[8 * su + pi];
+            q[u] = base[8 * su + qi];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = fmaf(p[u], q[u], acc);
+    }
     while (m) {
         const int s0 = __builtin_ctzll(m);
         m &= m - 1ull;
-        const float p0 = sg * base[8 * s0 + pi], q0 = base[8 * s0 + qi];
-        if (m) {
-            const int s1 = __builtin_ctzll(m);
-            m &= m - 1ull;
-            const float p1 = sg * base[8 * s1 + pi], q1 = base[8 * s1 + qi];
-            acc = fmaf(p0, q0, acc);
-            acc = fmaf(p1, q1, acc);
-        } else {
-            acc = fmaf(p0, q0, acc);
-        }
+        acc = fmaf(sg * base[8 * s0 + pi], base[8 * s0 + qi], acc);
     }
     return acc;
 }
