@@ -223,6 +223,7 @@ __device__ __forceinline__ void contact_accumulate_team(const float4* __restrict
 // one at a time instead: same order, same sums.
 constexpr int CT_FLAT = 65;
 constexpr int CF_CHUNKS = 8, CF_SLOTS = 3;
+constexpr int CF_WAVES = 16;   // waves per workgroup of the kernels that run the flat form (k_contact_fused: 1,024 lanes)
 // The slot arrays as the contact pass reads them: cell starts and the slot holding sorted position j. DirectMap: the
 // arrays are in sorted order (after the re-sort); FusedMap (below): the previous step's order, read through this
 // step's permutation (the one-launch step at the reference's scale).
@@ -290,9 +291,37 @@ __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict
         if (h != 2) TA = mk(0, 0, 0);
         if (h == 0) F = mk(0, 0, 0);
     };
-    auto add_hit = [&](const f3& F, const f3& TA, int src) __attribute__((always_inline)) {
-        totalForce = add_exact(totalForce, mk(__shfl(F.x, src, 64), __shfl(F.y, src, 64), __shfl(F.z, src, 64)));
-        totalTorque = add_exact(totalTorque, mk(__shfl(TA.x, src, 64), __shfl(TA.y, src, 64), __shfl(TA.z, src, 64)));
+    // a chunk's hits into the sums in lane order, transposed: the hit lanes write (F, TA) to the wave's LDS row and
+    // lane c < 6 adds component c of each (F.x, F.y, F.z, TA.x, TA.y, TA.z), the same adds in the same order
+    __shared__ float cf_rows[CF_WAVES][64 * 6];
+    float* row = cf_rows[threadIdx.x >> 6];
+    float comp = 0.0f;
+    auto fold = [&](const f3& F, const f3& TA, bool hit) __attribute__((always_inline)) {
+        uint64_t m = __ballot(hit);
+        if (m == 0) return;   // wave-uniform
+        if (hit) {
+            float* e = row + 6 * lane;
+            e[0] = F.x; e[1] = F.y; e[2] = F.z; e[3] = TA.x; e[4] = TA.y; e[5] = TA.z;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < 6) {
+            while (__popcll(m) >= 4) {   // four reads in flight, then the four adds in order
+                float x[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    x[u] = row[6 * __builtin_ctzll(m) + lane];
+                    m &= m - 1ull;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) comp = comp + x[u];
+            }
+            for (; m; m &= m - 1ull) comp = comp + row[6 * __builtin_ctzll(m) + lane];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
 #pragma unroll 1
     for (uint32_t round = 0; round < total; round += 64u * CF_CHUNKS) {
@@ -329,7 +358,7 @@ __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict
                 f3 F = mk(0, 0, 0), TA = mk(0, 0, 0);
                 const bool hit = (touch >> ch) & 1u;
                 if (hit) body(jj[ch], F, TA);
-                for (uint64_t m = __ballot(hit); m; m &= m - 1ull) add_hit(F, TA, __builtin_ctzll(m));
+                fold(F, TA, hit);
             }
             continue;
         }
@@ -354,7 +383,7 @@ __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict
 #pragma unroll
         for (int ch = 0; ch < CF_CHUNKS; ++ch) {
             const bool hc = (touch >> ch) & 1u;
-            for (uint64_t m = __ballot(hc); m; m &= m - 1ull) add_hit(F0, T0, __builtin_ctzll(m));
+            fold(F0, T0, hc);
             if (hc) {
                 F0 = F1; T0 = T1;
                 F1 = F2; T1 = T2;
@@ -368,6 +397,8 @@ __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict
         q2 += (uint32_t)__shfl_xor((int)q2, o, 64);
     }
     tq[0] = q0; tq[1] = q1; tq[2] = q2;
+    totalForce = mk(__shfl(comp, 0, 64), __shfl(comp, 1, 64), __shfl(comp, 2, 64));
+    totalTorque = mk(__shfl(comp, 3, 64), __shfl(comp, 4, 64), __shfl(comp, 5, 64));
     v = A.vel + (totalForce / va.w) * dt;                                    // :302-306
     w = A.omg + (totalTorque / wa.w) * dt;
 }
