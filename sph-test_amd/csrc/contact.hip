@@ -458,7 +458,8 @@ __device__ __forceinline__ void contact_finish(const ContactConst& c, int32_t pi
     const float angle = len(w * dt);
     if (angle > 0.00001f) {
         const f3 axis = normalize(w);
-        const float s = sin_r(angle * 0.5f), co = cos_r(angle * 0.5f);
+        float s, co;
+        sincos_r(angle * 0.5f, s, co);
         const float4 r = quat_mul(make_float4(axis.x * s, axis.y * s, axis.z * s, co), qa);
         const float l = sqrtf(r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w);
         q = make_float4(r.x / l, r.y / l, r.z / l, r.w / l);

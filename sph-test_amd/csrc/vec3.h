@@ -44,6 +44,13 @@ __device__ __forceinline__ float pow125_r(float x) {
 __device__ __forceinline__ float exp_r(float x) { return (float)exp((double)x); }
 __device__ __forceinline__ float sin_r(float x) { return (float)sin((double)x); }
 __device__ __forceinline__ float cos_r(float x) { return (float)cos((double)x); }
+// sin_r and cos_r of one argument from one double sincos (one argument reduction; the same values)
+__device__ __forceinline__ void sincos_r(float x, float& s, float& c) {
+    double sd, cd;
+    sincos((double)x, &sd, &cd);
+    s = (float)sd;
+    c = (float)cd;
+}
 __device__ __forceinline__ float atan2_r(float y, float x) { return (float)atan2((double)y, (double)x); }
 
 __device__ __forceinline__ int32_t ftoi(float x) {   // D3D ftoi: truncate, saturate, NaN -> 0
