@@ -310,6 +310,26 @@ def per_step_ms(kstats: dict, steps: int) -> dict:
             for k, v in kstats.items() if v.get("timed", 0) > 0 and v["total_ms"] > 0}
 
 
+def resort_counts_dict(c) -> dict:
+    """sph_read_resort_counts over the timed steps: whole-list ranges and lanes must be 0 (resort.hip)."""
+    return {"whole_list_ranges": int(c[0]), "whole_list_lanes": int(c[1]), "multi_pass_ranges": int(c[2]),
+            "passes": int(c[3]), "max_range_entries": int(c[4])}
+
+
+def kernel_sum_check(ks_ms: dict, gpu_event_ms: float, every: int) -> dict:
+    """The sampled kernel scopes' sum per step against the GPU-event time of the same steps: a step whose time
+    the sampled launches do not name (a kernel slow on other steps than the sampled ones, or gaps between
+    launches) shows as a ratio away from 1 and gets a note (verdict r5: the C5 line hid a re-sort cliff)."""
+    tot = sum(ks_ms.values())
+    out = {"kernels_sum_ms_per_step": round(tot, 4),
+           "kernels_sum_over_gpu_event": round(tot / gpu_event_ms, 4) if gpu_event_ms > 0 else None}
+    if gpu_event_ms > 0 and abs(tot / gpu_event_ms - 1.0) > 0.05:
+        out["kernels_note"] = (f"the timed kernel scopes (one step in {every} sampled) sum to {tot:.4f} ms per step "
+                               f"against {gpu_event_ms:.4f} ms of GPU events: {100 * (1 - tot / gpu_event_ms):+.1f}% of "
+                               "the step is not in the sampled launches (unsampled slow steps, gaps or overlap)")
+    return out
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -498,6 +518,7 @@ def main():
     n_total = runner.total_particles()
     value = n_total * args.steps / wall
     kstats = runner.kernel_stats()
+    rcounts = runner.resort_counts() if hasattr(runner, "resort_counts") else None
 
     roofline = None
     fi = kstats.get("force_integrate")
@@ -596,7 +617,8 @@ def main():
         mid = {"ms_per_step_mid_collapse": round(mwall * 1e3 / args.mid_steps, 4),
                "value_mid_collapse": round(runner.total_particles() * args.mid_steps / mwall, 1),
                "mid_collapse_state": runner.mid_state(max(done, args.mid_at), args.mid_steps),
-               "kernels_ms_per_step_mid_collapse": per_step_ms(mks, args.mid_steps)}
+               "kernels_ms_per_step_mid_collapse": per_step_ms(mks, args.mid_steps),
+               "resort_counts_mid_collapse": runner.resort_counts()}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -648,7 +670,10 @@ def main():
             "cpu_baseline": cpu,
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
             "kernels_ms_per_step": per_step_ms(kstats, args.steps),
+            "resort_counts": rcounts,
         }
+        if prof:
+            line.update(kernel_sum_check(line["kernels_ms_per_step"], gpu_ms / args.steps, prof))
         if mid:
             line.update(mid)
         if check is not None:
@@ -875,9 +900,13 @@ class LibraryRankRunner:
 
     def reset_stats(self):
         self.ctx.reset_kernel_stats()
+        self.ctx.resort_counts(reset=True)
 
     def kernel_stats(self):
         return self.ctx.kernel_stats()
+
+    def resort_counts(self):
+        return resort_counts_dict(self.ctx.resort_counts(reset=False))
 
     def total_particles(self):
         return self.n_total
@@ -912,9 +941,13 @@ class SingleRunner:
 
     def reset_stats(self):
         self.sim.ctx.reset_kernel_stats()
+        self.sim.ctx.resort_counts(reset=True)
 
     def kernel_stats(self):
         return self.sim.ctx.kernel_stats()
+
+    def resort_counts(self):
+        return resort_counts_dict(self.sim.ctx.resort_counts(reset=False))
 
     def total_particles(self):
         return self.sim.n

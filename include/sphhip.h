@@ -256,6 +256,14 @@ int sph_read_path_counts(sph_ctx* ctx, uint32_t counts[4], int32_t reset);
  * last change of the slot order), [1] waves run (3 planes each).
  * reset != 0 zeroes them after the read. */
 int sph_read_hit_mask_counts(sph_ctx* ctx, uint32_t counts[2], int32_t reset);
+/* The incremental re-sort's path counters since the last reset (both models; always counted, no cost on the
+ * fast path): [0] key/slot ranges that counted against the whole mover list (slow: O(slots x movers); 0 in
+ * every measured scene), [1] lanes whose insertion slot lay below the staged slot window (a whole-list count
+ * each), [2] ranges whose dest entries overflowed LDS and ran in passes over key sub-intervals (a dam-break
+ * front entering empty columns), [3] their passes, [4] the largest dest-entry count of one range (recorded
+ * above a quarter of the LDS capacity; maximum, not sum, over a group), [5..7] 0. reset != 0 zeroes them
+ * after the read. Replaces no Unity call (the reference rebuilds its grid every frame, compute:196-209). */
+int sph_read_resort_counts(sph_ctx* ctx, uint32_t counts[8], int32_t reset);
 /* Model S: particles whose cell key changed in the last step (the movers the next incremental re-sort
  * places; 0 with SPH_RESORT=0). Waits for the context's stream. */
 int sph_read_mover_count(sph_ctx* ctx, uint32_t* movers);

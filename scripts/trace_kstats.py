@@ -14,4 +14,5 @@ for r in rows:
 span = int(rows[-1]["End_Timestamp"]) - int(rows[0]["Start_Timestamp"])
 print(f"dispatches {len(rows)} span {span / 1e3:.1f} us")
 for k, v in sorted(d.items(), key=lambda kv: -sum(kv[1])):
-    print(f"{k[:50]:50s} n {len(v):5d} mean {sum(v) / len(v) / 1e3:8.2f} us  total {sum(v) / 1e3:10.1f} us")
+    print(f"{k[:50]:50s} n {len(v):5d} mean {sum(v) / len(v) / 1e3:8.2f} us  max {max(v) / 1e3:8.2f} us  "
+          f"total {sum(v) / 1e3:10.1f} us")

@@ -176,6 +176,7 @@ SIGNATURES = {
     "sph_read_torque_int": ([_P, _P, _I], C.c_int),
     "sph_read_path_counts": ([_P, _P, _I], C.c_int),
     "sph_read_mover_count": ([_P, _P], C.c_int),
+    "sph_read_resort_counts": ([_P, _P, _I], C.c_int),
     "sph_read_hit_mask_counts": ([_P, _P, _I], C.c_int),
     "sph_debug_radix_sort": ([_P, _P, _I, _I, _P, _P], C.c_int),
     "sph_debug_kick": ([_P, _I, _P], C.c_int),

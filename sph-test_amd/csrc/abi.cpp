@@ -778,19 +778,21 @@ int sph_read_cell_start(sph_ctx* ctx, uint32_t* cs, int32_t count) {
 
 }  // extern "C"
 
-// counters [first, first + m) of ctx->paths (summed over a local group's slab contexts)
-static int read_paths(sph_ctx* ctx, int first, int m, uint32_t* counts, int32_t reset) {
+// counters [first, first + m) of ctx->paths (summed over a local group's slab contexts; word max_at, if any, by
+// maximum). arm: from now on the neighbour passes count (the re-sort's counters always count)
+static int read_paths(sph_ctx* ctx, int first, int m, uint32_t* counts, int32_t reset, bool arm = true,
+                      int max_at = -1) {
     const std::vector<sph_ctx*> kids = sph::multi_kids(ctx);
     if (!kids.empty()) {
         for (int k = 0; k < m; ++k) counts[k] = 0;
         for (sph_ctx* kc : kids) {
             uint32_t c[8];
-            if (int r = read_paths(kc, first, m, c, reset)) return r;
-            for (int k = 0; k < m; ++k) counts[k] += c[k];
+            if (int r = read_paths(kc, first, m, c, reset, arm, max_at)) return r;
+            for (int k = 0; k < m; ++k) counts[k] = k == max_at ? std::max(counts[k], c[k]) : counts[k] + c[k];
         }
         return SPH_OK;
     }
-    ctx->count_paths = true;   // from now on the neighbour passes count
+    if (arm) ctx->count_paths = true;
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipMemcpyAsync(counts, ctx->paths + first, m * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
     if (reset) HIPCHK(hipMemsetAsync(ctx->paths + first, 0, m * sizeof(uint32_t), ctx->stream));
@@ -803,6 +805,11 @@ extern "C" {
 int sph_read_path_counts(sph_ctx* ctx, uint32_t counts[4], int32_t reset) {
     if (!ctx || !counts) return SPH_ERR_INVALID;
     return read_paths(ctx, 0, 4, counts, reset);
+}
+
+int sph_read_resort_counts(sph_ctx* ctx, uint32_t counts[8], int32_t reset) {
+    if (!ctx || !counts) return SPH_ERR_INVALID;
+    return read_paths(ctx, 16, 8, counts, reset, false, 4);
 }
 
 int sph_read_mover_count(sph_ctx* ctx, uint32_t* movers) {

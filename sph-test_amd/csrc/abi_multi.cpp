@@ -1334,14 +1334,17 @@ int read_switches(Multi& M, sph_ctx* ctx, int* skew) {
     *skew = sk ? std::atoi(sk) : 0;
     if (M.mode != 2 || M.world < 2) return SPH_OK;
     int32_t v[6] = {M.no_early ? 1 : 0, M.msg_cap, *skew, M.no_early ? -1 : 0, -M.msg_cap, -*skew};
-    int32_t* d = nullptr;
-    HIPCHK(hipMalloc((void**)&d, sizeof v));
+    // The context's small scratch (sdev[0..6): the step's column-start picks, rewritten by the first sort), not an
+    // allocation: a rank whose allocation failed would return before the all-reduce its peers then wait in. Every
+    // rank enters the all-reduce, a failed copy included, and fails after it.
+    int32_t* d = (int32_t*)ctx->sdev;
     hipError_t he = hipMemcpy(d, v, sizeof v, hipMemcpyHostToDevice);
-    ncclResult_t nr = ncclSuccess;
-    if (he == hipSuccess) nr = ncclAllReduce(d, d, 6, ncclInt32, ncclMax, M.comm, ctx->stream);
-    if (he == hipSuccess && nr == ncclSuccess) he = hipMemcpyAsync(v, d, sizeof v, hipMemcpyDeviceToHost, ctx->stream);
-    if (he == hipSuccess && nr == ncclSuccess) he = hipStreamSynchronize(ctx->stream);
-    (void)hipFree(d);
+    const ncclResult_t nr = ncclAllReduce(d, d, 6, ncclInt32, ncclMax, M.comm, ctx->stream);
+    if (nr == ncclSuccess) {
+        const hipError_t h2 = hipMemcpyAsync(v, d, sizeof v, hipMemcpyDeviceToHost, ctx->stream);
+        const hipError_t h3 = hipStreamSynchronize(ctx->stream);
+        if (he == hipSuccess) he = h2 != hipSuccess ? h2 : h3;
+    }
     if (nr != ncclSuccess) return fail(ctx, SPH_ERR_HIP, "switch agreement: %s", ncclGetErrorString(nr));
     if (he != hipSuccess) return fail(ctx, SPH_ERR_HIP, "switch agreement: %s", hipGetErrorString(he));
     for (int k = 0; k < 3; ++k)

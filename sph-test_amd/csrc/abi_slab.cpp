@@ -325,6 +325,9 @@ int sph::slab_assemble(sph_ctx* ctx, const void* dev_left, int32_t nl, const voi
         // the sorted keys of the new slot order: the next step's old keys
         if (ctx->resort_mode != 0 && n > 0)
             HIPCHK(hipMemcpyAsync(ctx->sk_cur, sk, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+        // taken for a large mover count: the host's next choice needs the count the last force pass appended
+        // (k_mv_rank, which otherwise stores it, did not run), or the context would stay on this path for good
+        if (many) HIPCHK(hipMemcpyAsync(ctx->mv_host, ctx->mv_count + ctx->mv_par, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemsetAsync(ctx->mv_count, 0, 2 * sizeof(uint32_t), s));
         launch_pick(ctx->cs, idx, 8, ctx->sdev, s, ctx->rng_host);
     }

@@ -57,7 +57,11 @@ struct ContactConst {
     float roll_mult, repulsion_strength;
     int32_t drag_id;
     float drag_tx, drag_ty, drag_tz, drag_strength;
+    // device word: an upper bound of every radius (float bits, k_keys on the full sort after any change of the
+    // particles; +inf until then). The contact pass skips the cells of its 27 that lie beyond rA/2 + rmax/2. null: none
+    const uint32_t* rmax = nullptr;
 };
+constexpr int SDEV_RMAX = 15;   // sph_ctx::sdev word holding ContactConst::rmax (Model R)
 
 #if defined(__HIPCC__)
 __device__ __forceinline__ int32_t cell_coord(float x, float o, float inv, int32_t G) {
@@ -356,6 +360,7 @@ struct ResortScratch {
     const SlabSizes* dz = nullptr;   // non-null: mi_off = nl - o0 from the device sizes
     uint32_t* err = nullptr;         // SZ_OVF_MOVERS if a destination would pass cap (never written)
     uint32_t* host_count = nullptr;  // mapped host memory: k_mv_rank stores the mover count there (the host's sort choice)
+    uint32_t* stats = nullptr;       // [8] the re-sort's path counters (resort.hip RS_*; sph_read_resort_counts)
 };
 // a mover entry whose mi has this bit holds a slot of the assembled array (a halo record's);
 // without it, mi is the force pass's slot and the assembled slot is mi + mi_off
@@ -526,8 +531,9 @@ void launch_resort(AsmSrc src, uint32_t* cs, uint32_t* cs_new, uint32_t ncells, 
 
 // grid / data movement (grid.hip)
 // window_sentinel (slab): a particle outside the held columns gets key ncells (sorts last)
+// rmax (Model R): atomicMax of the radii's float bits into a word the caller zeroed (ContactConst::rmax)
 void launch_keys(const float4* pos, int32_t n, const int32_t* id, int32_t n_active_id,
-                 GridDesc g, uint32_t* keys, hipStream_t s, bool window_sentinel = false);
+                 GridDesc g, uint32_t* keys, hipStream_t s, bool window_sentinel = false, uint32_t* rmax = nullptr);
 // cell_start[k] = lower_bound(sorted keys, k) for k = 0..ncells, every cell written once:
 // each particle boundary fills the cells up to its key; gaps longer than CS_SHORT cells are
 // queued (gap list + counter, zeroed by the call) and filled by whole workgroups.

@@ -77,6 +77,42 @@ __device__ __forceinline__ int contact_pair(const ContactConst& c, const Body& A
 // at most the sign of a zero component differing (b - a = +0 where -(a - b) = -0), and ftoi(+-0) = 0. The oracle
 // evaluates both sides; the Model R bit-exact tests compare the int torque sums.
 
+// Cell skipping (r6). The reference scans the 27 cells of 4.0 around a target (compute:228-233), and a contact needs
+// dist < (rA + rB)/2 − 0.001 (:251-253). With every radius at most rmax (ContactConst::rmax), a cell whose nearest
+// point lies farther than rA/2 + rmax/2 holds no contact: the pass drops such rows ((x, y) cells) and each row's end z
+// cells. The candidates that remain keep their order (rows in order, slots increasing), so every sum equals the
+// oracle's bit for bit (the oracle scans all 27). Per axis, in cell units from the coordinate cell_coord rounds
+// (g = (x − o)/cell, cell c): a lower neighbour cell lies more than f = g − c below the target, an upper one more than
+// 1 − f above (f is only larger, or 1 − f only larger, for a target clamped into an edge cell). The bound keeps a
+// margin (1.001·reach + 0.001) far above the rounding of g. An rmax not yet known (+inf), negative or NaN radii, or a
+// NaN coordinate skip nothing. At the rate table's sphere (radii 1.5-2, rmax 2) a target keeps ~8 of its 27 cells.
+struct CellReach {
+    float fx, fy, fz, r2;   // r2: the squared bound in cell units (+inf: no skipping)
+};
+__device__ __forceinline__ CellReach cell_reach(const GridDesc& g, const ContactConst& c, float4 pa, int32_t cx, int32_t cy,
+                                                int32_t cz) {
+    CellReach q;
+    q.fx = (pa.x - g.ox) * g.inv_cell - (float)cx;
+    q.fy = (pa.y - g.oy) * g.inv_cell - (float)cy;
+    q.fz = (pa.z - g.oz) * g.inv_cz - (float)cz;
+    const float rm = c.rmax ? __uint_as_float(*c.rmax) : __builtin_inff();
+    const float reach = 0.5f * pa.w + 0.5f * rm;
+    const float b = (reach * 1.001f + 0.001f) * g.inv_cell;
+    q.r2 = (reach >= 0.0f && reach < 1e30f && g.inv_cell == g.inv_cz) ? b * b : __builtin_inff();
+    return q;
+}
+// Row (dx, dy): false when its (x, y) cells lie beyond reach, else its z cells [z0, z1] (of [cz − 1, cz + 1]) in reach
+__device__ __forceinline__ bool reach_row(const CellReach& q, int dx, int dy, int32_t cz, int32_t gz, int32_t& z0,
+                                          int32_t& z1) {
+    const float lx = dx < 0 ? q.fx : (dx > 0 ? 1.0f - q.fx : 0.0f);
+    const float ly = dy < 0 ? q.fy : (dy > 0 ? 1.0f - q.fy : 0.0f);
+    const float l2 = lx * lx + ly * ly, ua = q.fz, ub = 1.0f - q.fz;
+    if (l2 > q.r2) return false;
+    z0 = cz > 0 && !(l2 + ua * ua > q.r2) ? cz - 1 : cz;
+    z1 = cz < gz - 1 && !(l2 + ub * ub > q.r2) ? cz + 1 : cz;
+    return true;
+}
+
 // ApplySPHForces' neighbour loop (compute:228-300) for slot a, then its integration
 // (:302-306): v1 = v + F/m·dt, w1 = ω + T/I·dt, and the int reaction torque sums.
 __device__ __forceinline__ void contact_accumulate(const float4* __restrict__ pos, const float4* __restrict__ vel,
@@ -90,11 +126,13 @@ __device__ __forceinline__ void contact_accumulate(const float4* __restrict__ po
     const int32_t cx = cell_cx(g, pa.x);
     const int32_t cy = cell_coord(pa.y, g.oy, g.inv_cell, g.gy);
     const int32_t cz = cell_coord(pa.z, g.oz, g.inv_cz, g.gz);
-    const int32_t z0 = cz > 0 ? cz - 1 : 0, z1 = cz < g.gz - 1 ? cz + 1 : g.gz - 1;
+    const CellReach cr = cell_reach(g, c, pa, cx, cy, cz);
 #pragma unroll 1
     for (int k = 0; k < 9; ++k) {
         const int32_t xx = cx + k / 3 - 1, yy = cy + k % 3 - 1;
-        if (xx < 0 || xx >= g.gx || yy < 0 || yy >= g.gy) continue;
+        int32_t z0, z1;
+        if (xx < 0 || xx >= g.gx || yy < 0 || yy >= g.gy || !reach_row(cr, k / 3 - 1, k % 3 - 1, cz, g.gz, z0, z1))
+            continue;
         const uint32_t rowk = ((uint32_t)xx * (uint32_t)g.gy + (uint32_t)yy) * (uint32_t)g.gz;
         const uint32_t j0 = cs[rowk + (uint32_t)z0], j1 = cs[rowk + (uint32_t)z1 + 1u];
 #pragma unroll 1
@@ -150,12 +188,13 @@ __device__ __forceinline__ void contact_accumulate_team(const float4* __restrict
     const int32_t cx = cell_cx(g, pa.x);
     const int32_t cy = cell_coord(pa.y, g.oy, g.inv_cell, g.gy);
     const int32_t cz = cell_coord(pa.z, g.oz, g.inv_cz, g.gz);
-    const int32_t z0 = cz > 0 ? cz - 1 : 0, z1 = cz < g.gz - 1 ? cz + 1 : g.gz - 1;
+    const CellReach cr = cell_reach(g, c, pa, cx, cy, cz);
     // lanes 0..8 of the team fetch the nine row ranges at once; rows are read back by shuffle
     uint32_t rj0 = 0u, rj1 = 0u;
     if (t < 9) {
         const int32_t xx = cx + t / 3 - 1, yy = cy + t % 3 - 1;
-        if (xx >= 0 && xx < g.gx && yy >= 0 && yy < g.gy) {
+        int32_t z0, z1;
+        if (xx >= 0 && xx < g.gx && yy >= 0 && yy < g.gy && reach_row(cr, t / 3 - 1, t % 3 - 1, cz, g.gz, z0, z1)) {
             const uint32_t rowk = ((uint32_t)xx * (uint32_t)g.gy + (uint32_t)yy) * (uint32_t)g.gz;
             rj0 = cs[rowk + (uint32_t)z0];
             rj1 = cs[rowk + (uint32_t)z1 + 1u];
@@ -245,11 +284,12 @@ __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict
     const int32_t cx = cell_cx(g, pa.x);
     const int32_t cy = cell_coord(pa.y, g.oy, g.inv_cell, g.gy);
     const int32_t cz = cell_coord(pa.z, g.oz, g.inv_cz, g.gz);
-    const int32_t z0 = cz > 0 ? cz - 1 : 0, z1 = cz < g.gz - 1 ? cz + 1 : g.gz - 1;
+    const CellReach cr = cell_reach(g, c, pa, cx, cy, cz);
     uint32_t rj0 = 0u, rlen = 0u;
     if (lane < 9) {
         const int32_t xx = cx + lane / 3 - 1, yy = cy + lane % 3 - 1;
-        if (xx >= 0 && xx < g.gx && yy >= 0 && yy < g.gy) {
+        int32_t z0, z1;
+        if (xx >= 0 && xx < g.gx && yy >= 0 && yy < g.gy && reach_row(cr, lane / 3 - 1, lane % 3 - 1, cz, g.gz, z0, z1)) {
             const uint32_t rowk = ((uint32_t)xx * (uint32_t)g.gy + (uint32_t)yy) * (uint32_t)g.gz;
             rj0 = M.start(rowk + (uint32_t)z0);
             rlen = M.start(rowk + (uint32_t)z1 + 1u) - rj0;

@@ -17,15 +17,24 @@ namespace sph {
 constexpr int BLK = 256;
 static inline int nblk(int64_t n) { return (int)((n + BLK - 1) / BLK); }
 
+// rmax (Model R, optional): the largest radius (pos.w) as float bits, atomicMax of the waves' maxima into a word the
+// caller zeroed; a negative or NaN radius gives bits above +inf's, which the contact pass reads as "no bound".
 __global__ __launch_bounds__(BLK) void k_keys(const float4* __restrict__ pos, int32_t n,
                                               const int32_t* __restrict__ id, int32_t n_active_id,
-                                              GridDesc g, uint32_t* __restrict__ keys, bool window_sentinel) {
+                                              GridDesc g, uint32_t* __restrict__ keys, bool window_sentinel,
+                                              uint32_t* __restrict__ rmax) {
     const int32_t i = blockIdx.x * BLK + threadIdx.x;
     if (i >= n) return;
     const float4 p = pos[i];
     uint32_t k = window_sentinel ? window_key(g, p.x, p.y, p.z) : cell_key(g, p.x, p.y, p.z);
     if (id != nullptr && id[i] >= n_active_id) k = g.ncells;   // inactive: sorts last
     keys[i] = k;
+    if (rmax) {
+        uint32_t r = __float_as_uint(p.w);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) r = max(r, (uint32_t)__shfl_xor((int)r, o, 64));
+        if (lane_id() == __builtin_ctzll(__ballot(true))) atomicMax(rmax, r);
+    }
 }
 
 constexpr uint32_t CS_SHORT = 32;
@@ -219,8 +228,8 @@ __global__ __launch_bounds__(BLK) void k_iota(uint32_t* __restrict__ v, int32_t 
 
 // ---------------------------------------------------------------- launchers
 void launch_keys(const float4* pos, int32_t n, const int32_t* id, int32_t n_active_id, GridDesc g,
-                 uint32_t* keys, hipStream_t s, bool window_sentinel) {
-    if (n > 0) k_keys<<<nblk(n), BLK, 0, s>>>(pos, n, id, n_active_id, g, keys, window_sentinel);
+                 uint32_t* keys, hipStream_t s, bool window_sentinel, uint32_t* rmax) {
+    if (n > 0) k_keys<<<nblk(n), BLK, 0, s>>>(pos, n, id, n_active_id, g, keys, window_sentinel, rmax);
 }
 void launch_cell_start(const uint32_t* sk, int32_t n, uint32_t* cs, uint32_t ncells, uint4* gaps,
                        uint32_t* gap_count, int* par, hipStream_t s) {

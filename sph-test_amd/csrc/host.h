@@ -130,8 +130,9 @@ struct sph_ctx {
     std::vector<sph::Pending> pending;
     std::vector<hipEvent_t> ev_pool;
     int64_t device_bytes = 0;
-    uint32_t* paths = nullptr;   // [16] path counters of the neighbour passes (sph_read_path_counts, _mask_counts;
-                                 // [8, 16): lane-utilisation counters of -DSPH_DIAG builds)
+    uint32_t* paths = nullptr;   // [24] path counters of the neighbour passes (sph_read_path_counts, _mask_counts;
+                                 // [8, 16): lane-utilisation counters of -DSPH_DIAG builds; [16, 24): the re-sort's,
+                                 // always counted, sph_read_resort_counts)
     bool count_paths = false;    // armed by the first counter read: counted launches pay for atomics
     uint32_t* hmask = nullptr;   // Model S: HM_WORDS x capacity hit-mask words (pass 1 -> pass 2)
     bool hm_valid = false;       // hmask describes the current slot order (a density pass ran since the last sort)
@@ -144,7 +145,8 @@ struct sph_ctx {
     int32_t rng[10] = {0};
     int32_t send_counts[2] = {0, 0};
     uint32_t* sblk = nullptr;    // compaction block counts [2][nblk]
-    uint32_t* sdev = nullptr;    // small device scratch (totals, picks; [8], [9]: cell-start gap counters)
+    uint32_t* sdev = nullptr;    // small device scratch (totals, picks; [8], [9]: cell-start gap counters; [15]: Model R
+                                 // radius bound, SDEV_RMAX)
     int gap_par = 0;             // which of sdev[8], sdev[9] the next cell-start call uses
     uint32_t* rng_host = nullptr;   // pinned: column-start picks of the last assemble
     hipEvent_t rng_ev = nullptr;    // recorded after their device->host copy

@@ -44,9 +44,13 @@ int alloc_particles(sph_ctx* ctx, int32_t cap) {
     AL(id, n); AL(id2, n);
     AL(keys, n); AL(keys2, n); AL(vals, n); AL(vals2, n);
     AL(hist, radix_hist_elems((int32_t)n)); AL(bin_total, 256);
-    AL(sblk, 2 * (size_t)slab_compact_blocks(0, (int32_t)n) + 2); AL(sdev, 16); AL(paths, 16);
+    AL(sblk, 2 * (size_t)slab_compact_blocks(0, (int32_t)n) + 2); AL(sdev, 16); AL(paths, 24);
     HIPCHK(hipMemset(ctx->sdev, 0, 16 * sizeof(uint32_t)));
-    HIPCHK(hipMemset(ctx->paths, 0, 16 * sizeof(uint32_t)));
+    {   // the contact pass's radius bound: +inf (no cell skipped) until the first key pass computes it
+        const uint32_t inf = 0x7f800000u;
+        HIPCHK(hipMemcpy(ctx->sdev + SDEV_RMAX, &inf, sizeof inf, hipMemcpyHostToDevice));
+    }
+    HIPCHK(hipMemset(ctx->paths, 0, 24 * sizeof(uint32_t)));
     ctx->gap_par = 0;
     if (is_contact(ctx)) {
         AL(omg, n); AL(rot, n); AL(aux, n); AL(omg2, n); AL(rot2, n); AL(aux2, n);

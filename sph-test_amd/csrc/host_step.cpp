@@ -18,8 +18,11 @@ int sort_and_reorder(sph_ctx* ctx, int32_t n_active_id, const uint32_t** sorted_
     const int32_t n = ctx->n;
     if (!ctx->keys_valid || ctx->keys_active != n_active_id) {
         KTimer t(ctx, "keys", 20.0 * n);
+        // Model R: the radius bound of the contact pass's cell skipping, recomputed with the keys after any change
+        uint32_t* rmax = is_contact(ctx) ? ctx->sdev + SDEV_RMAX : nullptr;
+        if (rmax) HIPCHK(hipMemsetAsync(rmax, 0, sizeof(uint32_t), ctx->stream));
         launch_keys(ctx->pos, n, is_contact(ctx) ? ctx->id : nullptr, n_active_id, ctx->grid, ctx->keys,
-                    ctx->stream);
+                    ctx->stream, false, rmax);
     }
     int side;
     {
@@ -109,6 +112,7 @@ ResortScratch resort_scratch(sph_ctx* ctx) {
     ResortScratch w{ctx->mv_mi, ctx->mv_mk, ctx->mv_mo, ctx->mv_ms, ctx->mv_mx, ctx->mv_mos,
                     (uint32_t)std::max(ctx->capacity, 1), 0};
     w.host_count = ctx->mv_host_dev;
+    w.stats = ctx->paths + 16;
     return w;
 }
 
@@ -338,6 +342,7 @@ ContactConst contact_const(const sph_ctx* ctx, float dt) {
     c.drag_ty = ctx->drag.target[1];
     c.drag_tz = ctx->drag.target[2];
     c.drag_strength = ctx->drag.strength;
+    c.rmax = ctx->sdev + SDEV_RMAX;
     return c;
 }
 
@@ -389,22 +394,7 @@ int step_contact(sph_ctx* ctx, float dt) {
     int r = sort_contact(ctx, act);
     if (r != SPH_OK) return r;
     const MoverSink mv = mover_sink(ctx);
-    const sph_params& p = ctx->prm;
-    (void)p;
-    ContactConst c{};
-    c.dt = dt;
-    c.spawn_radius = p.spawn_radius;
-    c.global_drag = p.global_drag_multiplier;
-    c.torque_factor = p.torque_factor;
-    c.torque_damping = p.torque_damping;
-    c.boundary_friction = p.boundary_friction;
-    c.roll_mult = p.rolling_contact_radius_multiplier;
-    c.repulsion_strength = p.repulsion_strength;
-    c.drag_id = ctx->drag.selected_id;
-    c.drag_tx = ctx->drag.target[0];
-    c.drag_ty = ctx->drag.target[1];
-    c.drag_tz = ctx->drag.target[2];
-    c.drag_strength = ctx->drag.strength;
+    const ContactConst c = contact_const(ctx, dt);   // the one-launch step's constants, field for field
     if (ctx->nbonds == 0) {
         KTimer t(ctx, "contact_step", (double)n * (2 * 64 + 4 + 12 + 4));
         launch_contact_step(ctx->pos, ctx->vel, ctx->omg, ctx->rot, ctx->aux, ctx->id, ctx->cs, act, n, ctx->grid,

@@ -32,6 +32,10 @@ constexpr int MV_BLK = 256;
 
 static __device__ __forceinline__ uint64_t comp(uint32_t key, uint32_t idx) { return (uint64_t)key << 32 | idx; }
 
+// a workgroup-uniform value (LDS / block reductions / same-address loads) into a scalar register: the rank kernel runs
+// at 64 VGPRs (two 1,024-lane workgroups per CU), and its range bounds and counts are live across every loop
+static __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
 static __device__ __forceinline__ bool asm_rec(const AsmSrc& a, int32_t x) { return x < a.nl || x >= a.nre; }
 
 // Model R's other slot arrays (single domain: slot x is x)
@@ -114,14 +118,35 @@ static __device__ __forceinline__ uint32_t lower_bound(const T* __restrict__ a, 
 // took the kernel from ~5 to ~32 us). The dest entries are ranked by counting (LDS broadcast reads) up to RK_COUNT of
 // them, by sorting beyond. The mover is placed at dst = (q − A(q)) + rk, every stayer of the slot range at
 // (i − A(i)) + #{movers (k, y) < (k_i, i)} (k_i in [kd0, kd1]; at kd1 the kd1 movers staged apart), and the share of
-// cells written from its staged keys. A range with more entries than LDS holds (a state where most particles move,
-// only under SPH_RESORT=2) counts them against the whole list instead: slow, same result. Also zeroes the next step's
-// mover counter. Per workgroup the kernel is a chain of memory round trips (~1.5 us each; the probe build,
-// scripts/rank_probe.py): one before the stream (count, range keys and the first movers together), one for the
-// entries' and stayers' loads, one for the cells.
+// cells written from its staged keys.
+//
+// A range's key interval [kd0, kd1) can span empty cells: the last range's reaches past the fluid's last column, so
+// every particle a dam-break front carries into an empty column is one of its dest entries (C5 from step ~60: more
+// than MV_RK_CAP per step). Such a range runs in passes over key sub-intervals (multi-pass): a second stream over the
+// mover list copies its nd dest entries to ms[below_k, below_k + nd) (the ranges' key intervals are disjoint and
+// ordered, so these spans are too) and bins them by key in an LDS histogram; sub-interval p is the bins whose
+// exclusive prefix lies in [p·C, (p+1)·C), C = MP_CAP − (largest bin), so each holds < MP_CAP entries. Per pass the
+// sub-interval's entries are staged from the copy (nd/1024 loads per lane), sorted, placed with rank
+// below_k + (entries of earlier passes) + local rank, and the stayers whose old key lies in it scattered. r5 counted
+// such a range's entries against the whole mover list instead, O(slots · m): 7.75 against 4.19 ms per C5 step from
+// step ~60 on. The whole-list counts remain only for states no bin layout fits (one bin of more than
+// MP_CAP / 2 movers, more than RK_KD1_CAP movers into one cell, insertion slots below the staged window) and are
+// counted (ResortScratch.stats, sph_read_resort_counts). Also zeroes the next step's mover counter. Per workgroup the
+// kernel is a chain of memory round trips (~1.5 us each; the probe build, scripts/rank_probe.py): one before the
+// stream (count, range keys and the first movers together), one for the entries' and stayers' loads, one for the
+// cells.
 constexpr int MV_RANK_GRID = 256;   // workgroups at least (one per CU); more above 2M slots
 constexpr int RK_U = 8;             // movers per lane per streaming round
+// Test-only variant (csrc/Makefile `variants`, SPH_RK_SMALLCAP): LDS caps cut so that small scenes take the
+// multi-pass path; results must equal the product build's bit for bit (tests/test_gpu_path_independence.py).
+#ifdef SPH_RK_SMALLCAP
+constexpr int MV_RK_CAP = 32;   // (MP_CAP >= 64: lds_sort pads to 64 entries)
+#else
 constexpr int MV_RK_CAP = 2048;     // dest entries staged per workgroup (a power of two)
+#endif
+constexpr int MP_CAP = 2 * MV_RK_CAP;   // multi-pass: entries per pass (dk and ds as one array)
+constexpr int RK_HBITS = 12;
+constexpr int RK_HBINS = 1 << RK_HBITS; // multi-pass: key bins of a range
 constexpr int RK_BM_WORDS = 1024;   // slot-presence bitmap over [xw, x1): up to 32,768 slots
 constexpr int RK_WIN = 2048;        // slot entries staged below x0 (covers the cell holding x0)
 // Slots per range at most: the grid grows past MV_RANK_GRID workgroups for n > 2M (C5 single-context: 2,048 ranges;
@@ -129,13 +154,22 @@ constexpr int RK_WIN = 2048;        // slot entries staged below x0 (covers the 
 // entries within LDS (a C5 range of 65,536 slots held more old keys than RK_OK_CAP mid-run, r5).
 constexpr uint32_t RK_MAX_RANGE = 8192;
 static_assert(RK_MAX_RANGE + RK_WIN + 512u <= 32u * RK_BM_WORDS, "a range and its window fit the bitmap");
+#ifdef SPH_RK_SMALLCAP
+constexpr int RK_COUNT = 8;
+#else
 constexpr int RK_COUNT = 256;       // dest entries ranked by counting, more by sorting
+#endif
 constexpr int RK_KD1_CAP = 1024;    // movers into the cell a range ends in, staged
 constexpr int RK_SU = 2;            // stayer slots per lane in flight
 constexpr uint32_t RK_CELLS = 16384; // cells per share at most (k_mv_rank's cell workgroups)
 constexpr int RK_POOL_U64 = RK_CELLS / 2;   // the LDS pool: a share's differences, or a range's entries and bitmap
 constexpr int RK_CU = 4;            // cells per lane in flight
-static_assert(2 * MV_RK_CAP * 8 + 4 * (RK_KD1_CAP + 2 * (RK_BM_WORDS + 1)) <= RK_POOL_U64 * 8, "a range's LDS fits the pool");
+static_assert(2 * MV_RK_CAP * 8 + 4 * (RK_KD1_CAP + 2 * (RK_BM_WORDS + 1) + RK_HBINS + 1) <= RK_POOL_U64 * 8,
+              "a range's LDS fits the pool");
+// ResortScratch.stats words (sph_read_resort_counts): ranges that counted against the whole mover list, lanes whose
+// insertion slot lay below the staged window (a whole-list count each), multi-pass ranges, their passes, the largest
+// dest-entry count of a range (recorded above MV_RK_CAP / 4)
+enum { RS_WHOLE = 0, RS_WHOLE_LANES, RS_MULTI, RS_PASSES, RS_MAX_ND, RS_WORDS = 8 };
 // Test-only timing probe (scripts/rank_probe.py, a -DSPH_RANK_PROBE build): per workgroup the wall clock at its start,
 // after the mover stream, after the sorts and at its end, with its entry counts.
 #ifdef SPH_RANK_PROBE
@@ -329,15 +363,16 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
                                                     ResortExtra ex) {
     // one LDS pool, laid out per role: a range's entries and slot bitmap, or a cell share's count differences
     __shared__ uint64_t pool[RK_POOL_U64];
-    __shared__ uint32_t cnt[5], red[RK_BLK / 64];
-    uint64_t* dk = pool;                                    // dest entries (new key, slot)
+    __shared__ uint32_t cnt[8], red[RK_BLK / 64];
+    uint64_t* dk = pool;                                    // dest entries (new key, slot); multi-pass: MP_CAP of them
     uint64_t* ds = pool + MV_RK_CAP;                        // the dest entries in (key, slot) order
     uint32_t* kx1 = (uint32_t*)(pool + 2 * MV_RK_CAP);      // slots of the movers whose new key is kd1
     uint32_t* bm = kx1 + RK_KD1_CAP;                        // movers' slots in [xw, x1): bits
     uint32_t* bpre = bm + (RK_BM_WORDS + 1);                // and the words' prefix
+    uint32_t* hp = bpre + (RK_BM_WORDS + 1);                // multi-pass: key bins, then their exclusive prefix
     RK_PROBE(0, wall_clock64());
     resolve_sizes(src, w, n);
-    if (threadIdx.x < 5) cnt[threadIdx.x] = 0u;
+    if (threadIdx.x < 8) cnt[threadIdx.x] = 0u;
     if (blockIdx.x >= G) {   // a share of the cells: its own workgroup, beside the ranges
         mv_cells(blockIdx.x - G, gridDim.x - G, mtotal, cs, cs_new, ncells, pick, w, (int32_t*)pool, red);
         return;
@@ -366,7 +401,7 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
     };
     load_round(0, w.cap - 1u);
     const uint32_t m = *mtotal;
-    const uint32_t sk0 = *sk_ptr(x0), sk1 = *sk_ptr(x1);
+    const uint32_t sk0 = uni(*sk_ptr(x0)), sk1 = uni(*sk_ptr(x1));
     if (b == 0 && threadIdx.x == 0) {
         *next_count = 0u;
         if (w.host_count) *w.host_count = m;   // for the host's next sort choices (no copy launch)
@@ -403,9 +438,9 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
         }
         if (base + RK_BLK * RK_U < m) load_round(base + RK_BLK * RK_U, m - 1u);
     }
-    below_k = block_sum<RK_BLK>(below_k, red);   // (its barriers also publish the staged entries and counts)
-    below_x0 = block_sum<RK_BLK>(below_x0, red);
-    const uint32_t nd = cnt[0], n1 = cnt[2];
+    below_k = uni(block_sum<RK_BLK>(below_k, red));   // (its barriers also publish the staged entries and counts)
+    below_x0 = uni(block_sum<RK_BLK>(below_x0, red));
+    const uint32_t nd = uni(cnt[0]), n1 = uni(cnt[2]);
     const bool dest_staged = nd <= MV_RK_CAP;   // block-uniform
     RK_PROBE(1, wall_clock64());
     RK_PROBE(4, nd);
@@ -451,10 +486,75 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
         }
     if (dest_staged && !dcount) lds_sort(dk, nullptr, nd);
     __syncthreads();
-    const uint64_t* sd = dcount ? ds : dk;   // sorted dest entries (dest_staged)
     RK_PROBE(2, wall_clock64());
     RK_PROBE(7, bits_ok ? 1 : 0);
-    // ---- counts against the whole list (ranges holding more than LDS does: a state where most particles move)
+    // ---- multi-pass (more dest entries than MV_RK_CAP; block-uniform): copy them to ms[below_k, below_k + nd) and
+    // bin them by key (bin = (k − kd0) >> sh, RK_HBINS bins over the keys the range can receive; mover keys are at
+    // most ncells), then the bins' exclusive prefix and the largest bin.
+    uint32_t P = 1, Cg = 1, sh = 0;
+    bool mp = false;
+    if (!dest_staged) {
+        const uint32_t kend = min(kd1, ncells + 1u);
+        const uint32_t span = kend > kd0 ? kend - kd0 : 1u;
+        sh = span > (uint32_t)RK_HBINS ? 32u - (uint32_t)__builtin_clz((span - 1u) >> RK_HBITS) : 0u;
+        for (uint32_t t = threadIdx.x; t < (uint32_t)RK_HBINS; t += RK_BLK) hp[t] = 0u;
+        __syncthreads();
+        uint64_t* const mcopy = w.ms + below_k;   // below_k + nd <= m <= cap
+        load_round(0, m - 1u);                    // (m > MV_RK_CAP here)
+        for (uint32_t base = 0; base < m; base += RK_BLK * RK_U) {
+#pragma unroll
+            for (int u = 0; u < RK_U; ++u) {
+                const uint32_t r = base + u * RK_BLK + threadIdx.x, k = ks[u];
+                if (r < m && k >= kd0 && k < kd1) {
+                    atomicAdd(&hp[(k - kd0) >> sh], 1u);
+                    const uint32_t j = atomicAdd(&cnt[6], 1u);
+                    if (j < nd) mcopy[j] = comp(k, mv_slot(w, xs[u]));
+                }
+            }
+            if (base + RK_BLK * RK_U < m) load_round(base + RK_BLK * RK_U, m - 1u);
+        }
+        __syncthreads();
+        constexpr uint32_t HPL = RK_HBINS / RK_BLK;   // consecutive bins per lane
+        static_assert(HPL * RK_BLK == RK_HBINS, "bins per lane");
+        const uint32_t h0 = HPL * threadIdx.x;
+        uint32_t hc[HPL], inc = 0, mx = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < HPL; ++j) {
+            hc[j] = hp[h0 + j];
+            inc += hc[j];
+            mx = max(mx, hc[j]);
+        }
+        const uint32_t mine = inc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
+            if (lane_id() >= (uint32_t)o) inc += u;
+            mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+        }
+        if (lane_id() == 63) red[threadIdx.x >> 6] = inc;
+        if (lane_id() == 0) atomicMax(&cnt[5], mx);
+        __syncthreads();
+        uint32_t run = inc - mine;
+        for (uint32_t k = 0; k < (threadIdx.x >> 6); ++k) run += red[k];
+#pragma unroll
+        for (uint32_t j = 0; j < HPL; ++j) {
+            hp[h0 + j] = run;
+            run += hc[j];
+        }
+        if (threadIdx.x == RK_BLK - 1) hp[RK_HBINS] = run;   // == nd
+        __syncthreads();
+        const uint32_t maxbin = uni(cnt[5]);
+        mp = maxbin <= (uint32_t)(MP_CAP / 2);   // else no bin layout fits: the whole list
+        if (mp) {
+            Cg = (uint32_t)MP_CAP - maxbin;
+            P = (nd - 1u) / Cg + 1u;
+        }
+    }
+    const bool dest_ok = dest_staged || mp;   // block-uniform; false: every dest count takes the whole list
+    // pass state: the key sub-interval [Ka, Kb), the entries of earlier passes, this pass's sorted entries
+    uint32_t Ka = kd0, Kb = kd1, before = 0, ndp = nd;
+    const uint64_t* sd = dcount ? ds : dk;   // sorted dest entries (dest_staged)
+    // ---- counts against the whole list (a state no LDS layout fits; counted in w.stats)
     auto count_slots = [&](uint32_t y) {   // #movers with slot < y
         uint32_t c = 0;
         for (uint32_t f = 0; f < m; ++f) c += mv_slot(w, w.mi[f]) < y ? 1u : 0u;
@@ -470,13 +570,17 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
         const uint32_t d = min(y, x1) - xw, wd = d >> 5;
         return bpre[wd] + (uint32_t)__popc(bm[wd] & ((1u << (d & 31u)) - 1u));
     };
-    const uint32_t r0 = bits_ok ? rank_of(x0) : 0u;
-    auto slots_below = [&](uint32_t y) { return bits_ok && y >= xw ? below_x0 + rank_of(y) - r0 : count_slots(y); };
+    const uint32_t r0 = uni(bits_ok ? rank_of(x0) : 0u);
+    auto slots_below = [&](uint32_t y) {
+        if (bits_ok && y >= xw) return below_x0 + rank_of(y) - r0;
+        if (w.stats) atomicAdd(w.stats + RS_WHOLE_LANES, 1u);
+        return count_slots(y);
+    };
     // #movers with (new key, slot) < (k, i) for k in [kd0, kd1]: below the key range plus the dest entries before it;
     // at kd1 all of those plus the kd1 movers with a smaller slot
     auto dest_below = [&](uint32_t k, uint32_t i) {
-        if (!dest_staged) return count_dest(comp(k, i));
-        if (k < kd1) return below_k + lower_bound(sd, nd, comp(k, i));
+        if (!dest_ok) return count_dest(comp(k, i));
+        if (k < kd1) return below_k + before + lower_bound(sd, ndp, comp(k, i));
         if (n1 > (uint32_t)RK_KD1_CAP) return count_dest(comp(k, i));
         uint32_t c = below_k + nd;
         for (uint32_t f = 0; f < n1; ++f) c += kx1[f] < i ? 1u : 0u;
@@ -503,42 +607,81 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
         sk_o[dst] = k;
         store_extra(ex, e, dst);
     };
-    if (dest_staged) {
-        for (uint32_t t = threadIdx.x; t < nd; t += RK_BLK) place(dk[t]);
-    } else {
-        for (uint32_t r = threadIdx.x; r < m; r += RK_BLK) {
-            const uint32_t k = w.mk[r];
-            if (k >= kd0 && k < kd1) place(comp(k, mv_slot(w, w.mi[r])));
-        }
-    }
-    // ---- the stayers of [x0, x1): dst = (i − A(i)) + #{movers (k, y) < (k_i, i)}, k_i in [kd0, kd1]. Every load
-    // of a round of slots issues before its stores.
-    for (uint32_t base = x0; base < x1; base += RK_BLK * RK_SU) {
-        uint32_t ko[RK_SU], kn[RK_SU];
-        float4 p[RK_SU], v[RK_SU];
-        int32_t pid[RK_SU];
+    for (uint32_t pass = 0; pass < P; ++pass) {
+        const bool last = pass + 1u == P;
+        if (mp) {   // stage the entries of bins [ba, bb) from the copy and sort them
+            const uint32_t ba = pass == 0 ? 0u : lower_bound(hp, (uint32_t)RK_HBINS, pass * Cg);
+            const uint32_t bb = last ? (uint32_t)RK_HBINS : lower_bound(hp, (uint32_t)RK_HBINS, (pass + 1u) * Cg);
+            Ka = uni(kd0 + (ba << sh));
+            Kb = uni(last ? kd1 : kd0 + (bb << sh));
+            before = uni(hp[ba]);
+            ndp = uni(min(hp[bb] - before, (uint32_t)MP_CAP));
+            const uint64_t* const mcopy = w.ms + below_k;
+            for (uint32_t t0 = 0; t0 < nd; t0 += RK_BLK * RK_U) {
+                uint64_t e[RK_U];
 #pragma unroll
-        for (int u = 0; u < RK_SU; ++u) {
-            const uint32_t i = min(base + u * RK_BLK + threadIdx.x, x1 - 1u);
-            ko[u] = asm_sk(src, (int32_t)i);
-            kn[u] = asm_key(src, (int32_t)i);
-            asm_load(src, (int32_t)i, p[u], v[u], pid[u]);
-        }
+                for (int u = 0; u < RK_U; ++u) e[u] = mcopy[min(t0 + u * RK_BLK + threadIdx.x, nd - 1u)];
 #pragma unroll
-        for (int u = 0; u < RK_SU; ++u) {
-            const uint32_t i = base + u * RK_BLK + threadIdx.x;
-            if (i >= x1 || kn[u] != ko[u]) continue;
-            const uint32_t dst = (i - slots_below(i)) + dest_below(ko[u], i);
-            if (dst >= w.cap) {
-                if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
-                continue;
+                for (int u = 0; u < RK_U; ++u) {
+                    const uint32_t k = (uint32_t)(e[u] >> 32);
+                    if (t0 + u * RK_BLK + threadIdx.x < nd && k >= Ka && k < Kb) {
+                        const uint32_t j = atomicAdd(&cnt[3 + (pass & 1u)], 1u);
+                        if (j < (uint32_t)MP_CAP) dk[j] = e[u];
+                    }
+                }
             }
-            pos_o[dst] = p[u];
-            vel_o[dst] = v[u];
-            id_o[dst] = pid[u];
-            sk_o[dst] = ko[u];
-            move_extra(ex, i, dst);   // Model R's further arrays (the reference's scale: not prefetched)
+            if (threadIdx.x == 0) cnt[3 + ((pass + 1u) & 1u)] = 0u;   // the next pass's counter (read before the last barrier)
+            lds_sort(dk, nullptr, ndp);   // (its first barrier publishes the staged entries; it ends on a barrier)
+            sd = dk;
         }
+        if (dest_ok) {
+            for (uint32_t t = threadIdx.x; t < ndp; t += RK_BLK) place(dk[t]);   // (multi-pass: sorted)
+        } else {
+            for (uint32_t r = threadIdx.x; r < m; r += RK_BLK) {
+                const uint32_t k = w.mk[r];
+                if (k >= kd0 && k < kd1) place(comp(k, mv_slot(w, w.mi[r])));
+            }
+        }
+        // ---- the stayers of [x0, x1): dst = (i − A(i)) + #{movers (k, y) < (k_i, i)}, k_i in [kd0, kd1] (multi-pass:
+        // those with k_i in this pass's sub-interval, kd1 in the last). Every load of a round of slots issues before
+        // its stores.
+        for (uint32_t base = x0; base < x1; base += RK_BLK * RK_SU) {
+            uint32_t ko[RK_SU], kn[RK_SU];
+            float4 p[RK_SU], v[RK_SU];
+            int32_t pid[RK_SU];
+#pragma unroll
+            for (int u = 0; u < RK_SU; ++u) {
+                const uint32_t i = min(base + u * RK_BLK + threadIdx.x, x1 - 1u);
+                ko[u] = asm_sk(src, (int32_t)i);
+                kn[u] = asm_key(src, (int32_t)i);
+                asm_load(src, (int32_t)i, p[u], v[u], pid[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < RK_SU; ++u) {
+                const uint32_t i = base + u * RK_BLK + threadIdx.x;
+                if (i >= x1 || kn[u] != ko[u]) continue;
+                if (mp && !((ko[u] >= Ka && ko[u] < Kb) || (last && ko[u] == kd1))) continue;
+                const uint32_t dst = (i - slots_below(i)) + dest_below(ko[u], i);
+                if (dst >= w.cap) {
+                    if (w.err) atomicOr(w.err, SZ_OVF_MOVERS);
+                    continue;
+                }
+                pos_o[dst] = p[u];
+                vel_o[dst] = v[u];
+                id_o[dst] = pid[u];
+                sk_o[dst] = ko[u];
+                move_extra(ex, i, dst);   // Model R's further arrays (the reference's scale: not prefetched)
+            }
+        }
+        if (mp && !last) __syncthreads();   // this pass's entries are read until here
+    }
+    if (threadIdx.x == 0 && w.stats) {   // block-uniform facts: no barrier needed
+        if (!dest_ok || n1 > (uint32_t)RK_KD1_CAP || !bits_ok) atomicAdd(w.stats + RS_WHOLE, 1u);
+        if (mp) {
+            atomicAdd(w.stats + RS_MULTI, 1u);
+            atomicAdd(w.stats + RS_PASSES, P);
+        }
+        if (nd > (uint32_t)(MV_RK_CAP / 4)) atomicMax(w.stats + RS_MAX_ND, nd);
     }
 #ifdef SPH_RANK_PROBE
     __syncthreads();
