@@ -313,7 +313,7 @@ def per_step_ms(kstats: dict, steps: int) -> dict:
 def resort_counts_dict(c) -> dict:
     """sph_read_resort_counts over the timed steps: whole-list ranges and lanes must be 0 (resort.hip)."""
     return {"whole_list_ranges": int(c[0]), "whole_list_lanes": int(c[1]), "multi_pass_ranges": int(c[2]),
-            "passes": int(c[3]), "max_range_entries": int(c[4])}
+            "passes": int(c[3]), "max_range_entries": int(c[4]), "share_restreams": int(c[5])}
 
 
 def kernel_sum_check(ks_ms: dict, gpu_event_ms: float, every: int) -> dict:

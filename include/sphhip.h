@@ -261,7 +261,8 @@ int sph_read_hit_mask_counts(sph_ctx* ctx, uint32_t counts[2], int32_t reset);
  * every measured scene), [1] lanes whose insertion slot lay below the staged slot window (a whole-list count
  * each), [2] ranges whose dest entries overflowed LDS and ran in passes over key sub-intervals (a dam-break
  * front entering empty columns), [3] their passes, [4] the largest dest-entry count of one range (recorded
- * above a quarter of the LDS capacity; maximum, not sum, over a group), [5..7] 0. reset != 0 zeroes them
+ * above a quarter of the LDS capacity; maximum, not sum, over a group), [5] cell shares whose mover keys
+ * overflowed LDS (one stream of the mover list per pass instead of one in all), [6..7] 0. reset != 0 zeroes them
  * after the read. Replaces no Unity call (the reference rebuilds its grid every frame, compute:196-209). */
 int sph_read_resort_counts(sph_ctx* ctx, uint32_t counts[8], int32_t reset);
 /* Model S: particles whose cell key changed in the last step (the movers the next incremental re-sort

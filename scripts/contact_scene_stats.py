@@ -3,7 +3,7 @@ state after K steps: candidates per target (the 27 cells of the reference's 4.0 
 candidates, chunks a round scans, and the body passes a wave runs, as the kernel schedules them now (a lane's touches
 in up to three slots, the wave running max-per-lane passes; chunk by chunk when a lane has more) and with the touches
 compacted over the wave's lanes (ceil(touches / 64) passes). CPU only (the oracle restatement, test infrastructure).
-    python scripts/contact_scene_stats.py [--steps K] [--n 4096]"""
+    python scripts/contact_scene_stats.py [--steps K] [--n 4096] [--trim]"""
 import argparse
 import sys
 from pathlib import Path
@@ -35,10 +35,14 @@ def sphere(pkg, n):   # scripts/small_n_timing.py, bench.py --table
     return parts
 
 
-def stats(parts, spawn=15.0):
+def stats(parts, spawn=15.0, trim=False):
+    """trim: the rows and end z cells contact.hip's cell_reach / reach_row drop (beyond rA/2 + rmax/2)."""
     x = parts["position"].astype(np.float32)
     r = parts["radius"].astype(np.float32)
-    c = np.clip(np.floor((x + np.float32(spawn)) * np.float32(0.25)).astype(np.int64), 0, 31)
+    gq = (x + np.float32(spawn)) * np.float32(0.25)
+    c = np.clip(np.floor(gq).astype(np.int64), 0, 31)
+    fr = gq - c.astype(np.float32)
+    rmax = float(r.max())
     key = (c[:, 0] * 32 + c[:, 1]) * 32 + c[:, 2]
     order = np.argsort(key, kind="stable")
     ks = key[order]
@@ -47,11 +51,20 @@ def stats(parts, spawn=15.0):
     for a in range(len(x)):
         cx, cy, cz = c[a]
         z0, z1 = max(cz - 1, 0), min(cz + 1, 31)
+        b = ((0.5 * r[a] + 0.5 * rmax) * 1.001 + 0.001) * 0.25
         flat = []
         for k in range(9):
             xx, yy = cx + k // 3 - 1, cy + k % 3 - 1
             if not (0 <= xx < 32 and 0 <= yy < 32):
                 continue
+            if trim:
+                lx = fr[a, 0] if k // 3 == 0 else (1 - fr[a, 0] if k // 3 == 2 else 0.0)
+                ly = fr[a, 1] if k % 3 == 0 else (1 - fr[a, 1] if k % 3 == 2 else 0.0)
+                l2 = lx * lx + ly * ly
+                if l2 > b * b:
+                    continue
+                z0 = cz - 1 if cz > 0 and not (l2 + fr[a, 2] ** 2 > b * b) else cz
+                z1 = cz + 1 if cz < 31 and not (l2 + (1 - fr[a, 2]) ** 2 > b * b) else cz
             row = (xx * 32 + yy) * 32
             flat.extend(order[cs[row + z0]:cs[row + z1 + 1]])
         flat = np.asarray(flat, np.int64)
@@ -82,6 +95,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", default="0,20,300")
     ap.add_argument("--n", type=int, default=4096)
+    ap.add_argument("--trim", action="store_true", help="count the candidates after contact.hip's cell skipping")
     args = ap.parse_args()
     pkg = GE.load_package()
     O = GE.load_oracle()
@@ -93,7 +107,8 @@ def main():
         while done < k:
             p, _ = O.contact_step(cp, p, nthreads=8)
             done += 1
-        print({"scene": "sphere R=15", "n": args.n, "step": k, **stats(p)}, flush=True)
+        print({"scene": "sphere R=15", "n": args.n, "step": k, "trim": args.trim, **stats(p, trim=args.trim)},
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -239,10 +239,10 @@ class Context:
 
     def resort_counts(self, reset: bool = True) -> np.ndarray:
         """The incremental re-sort's path counters (sph_read_resort_counts): whole-list ranges, whole-list lanes,
-        multi-pass ranges, their passes, the largest dest-entry count of a range."""
+        multi-pass ranges, their passes, the largest dest-entry count of a range, cell shares that re-streamed."""
         out = np.zeros(8, np.uint32)
         self._chk("sph_read_resort_counts", self._L.sph_read_resort_counts(self._h, A.ptr(out), 1 if reset else 0))
-        return out[:5]
+        return out[:6]
 
     def mover_count(self) -> int:
         """Particles whose cell key changed in the last step (sph_read_mover_count; Model S, single context)."""

@@ -253,16 +253,18 @@ __device__ __forceinline__ void contact_accumulate_team(const float4* __restrict
 
 // Flat form (team code CT_FLAT): one wave per target over the target's candidates flattened across the nine rows
 // (candidate f = row k's j = rj0_k + f − P_k, P the rows' exclusive length prefix), for the reference's scale where a
-// target has ~500 candidates in ~9 rows of ~56: the team form walks the rows one after another, a dependent global
+// target has ~100-800 candidates in up to 9 rows: the team form walks the rows one after another, a dependent global
 // load of positions, then of the touching candidates' velocities, per row. Here one round prefetches the positions of
-// CF_CHUNKS x 64 candidates, finds the touching ones (the reject test of :253, the same expressions), loads the
-// velocities of a lane's (at most CF_SLOTS) touching candidates together, evaluates both pair bodies, and adds the
-// hits' F and TA in flattened order, i.e. rows in order and j increasing within a row: the serial order, bit for bit.
-// A round where a lane touches more than CF_SLOTS candidates (never at the reference's packing) takes its chunks
-// one at a time instead: same order, same sums.
+// CF_CHUNKS x 64 candidates and finds the touching ones (the reject test of :253, the same expressions); the touching
+// candidates are then compacted over the wave's lanes in flattened order (chunk-major, lane-minor: rows in order and j
+// increasing within a row, the serial order) through a per-wave LDS list, and each batch of 64 evaluates its pair
+// bodies on all lanes and adds the hits' F and TA in list order: the serial order, bit for bit. r5 gave each lane its
+// own touching candidates (up to three slots), so a round took as many body passes as its busiest lane touched
+// candidates: 3.9 passes per wave at the rate table's 32,768-particle sphere against 1.85 compacted
+// (scripts/contact_scene_stats.py), at ~280 VALU per pass.
 constexpr int CT_FLAT = 65;
-constexpr int CF_CHUNKS = 8, CF_SLOTS = 3;
-constexpr int CF_WAVES = 16;   // waves per workgroup of the kernels that run the flat form (k_contact_fused: 1,024 lanes)
+constexpr int CF_CHUNKS = 8;
+constexpr int CF_WAVES = 16;   // waves per workgroup of k_contact_fused (1,024 lanes)
 // The slot arrays as the contact pass reads them: cell starts and the slot holding sorted position j. DirectMap: the
 // arrays are in sorted order (after the re-sort); FusedMap (below): the previous step's order, read through this
 // step's permutation (the one-launch step at the reference's scale).
@@ -271,7 +273,7 @@ struct DirectMap {
     __device__ __forceinline__ uint32_t start(uint32_t k) const { return cs[k]; }
     __device__ __forceinline__ uint32_t old(uint32_t j) const { return j; }
 };
-template <class Map>
+template <int WAVES, class Map>
 __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict__ pos, const float4* __restrict__ vel,
                                                         const float4* __restrict__ omg, const Map& M,
                                                         const GridDesc& g, const ContactConst& c, int32_t a, float4 pa,
@@ -331,10 +333,12 @@ __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict
         if (h != 2) TA = mk(0, 0, 0);
         if (h == 0) F = mk(0, 0, 0);
     };
-    // a chunk's hits into the sums in lane order, transposed: the hit lanes write (F, TA) to the wave's LDS row and
+    // a batch's hits into the sums in lane order, transposed: the hit lanes write (F, TA) to the wave's LDS row and
     // lane c < 6 adds component c of each (F.x, F.y, F.z, TA.x, TA.y, TA.z), the same adds in the same order
-    __shared__ float cf_rows[CF_WAVES][64 * 6];
+    __shared__ float cf_rows[WAVES][64 * 6];
+    __shared__ uint32_t cf_list[WAVES][64 * CF_CHUNKS];   // a round's touching candidates (sorted slots), in order
     float* row = cf_rows[threadIdx.x >> 6];
+    uint32_t* list = cf_list[threadIdx.x >> 6];
     float comp = 0.0f;
     auto fold = [&](const f3& F, const f3& TA, bool hit) __attribute__((always_inline)) {
         uint64_t m = __ballot(hit);
@@ -392,42 +396,27 @@ __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict
             const float t = (reff - 0.0009f) + reff * 1e-5f;
             if (f < total && (int32_t)jj[ch] != a && t > 0.0f && dot(d, d) < t * t) touch |= 1u << ch;
         }
-        if (__any(__popc(touch) > CF_SLOTS)) {   // wave-uniform: chunk by chunk
-#pragma unroll
-            for (int ch = 0; ch < CF_CHUNKS; ++ch) {
-                f3 F = mk(0, 0, 0), TA = mk(0, 0, 0);
-                const bool hit = (touch >> ch) & 1u;
-                if (hit) body(jj[ch], F, TA);
-                fold(F, TA, hit);
-            }
-            continue;
-        }
-        // this lane's touching candidates in chunk order into three slots, then their bodies (loads in flight
-        // together). Named registers throughout: an array indexed by a lane's running count (or a select chain
-        // over one) compiles to a scratch-memory table.
-        uint32_t j0 = 0u, j1 = 0u, j2 = 0u;
-        int cnt = 0;
-#pragma unroll
-        for (int ch = 0; ch < CF_CHUNKS; ++ch)
-            if ((touch >> ch) & 1u) {
-                j2 = cnt == 2 ? jj[ch] : j2;
-                j1 = cnt == 1 ? jj[ch] : j1;
-                j0 = cnt == 0 ? jj[ch] : j0;
-                ++cnt;
-            }
-        f3 F0 = mk(0, 0, 0), T0 = F0, F1 = F0, T1 = F0, F2 = F0, T2 = F0;
-        if (cnt > 0) body(j0, F0, T0);
-        if (cnt > 1) body(j1, F1, T1);
-        if (cnt > 2) body(j2, F2, T2);
-        // the hits in flattened order: chunk by chunk, lowest lane first; a lane's next hit is always slot 0
+        // compaction: candidate (ch, lane) goes to list position (touches of the chunks before) + (touching lanes
+        // below it in its chunk); the rounds' positions are wave-uniform running counts
+        uint32_t T = 0;
 #pragma unroll
         for (int ch = 0; ch < CF_CHUNKS; ++ch) {
-            const bool hc = (touch >> ch) & 1u;
-            fold(F0, T0, hc);
-            if (hc) {
-                F0 = F1; T0 = T1;
-                F1 = F2; T1 = T2;
-            }
+            if ((uint32_t)ch >= nch) break;
+            const bool t = (touch >> ch) & 1u;
+            const uint64_t b = __ballot(t);
+            if (t) list[T + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = jj[ch];
+            T += (uint32_t)__popcll(b);
+        }
+        if (T == 0) continue;   // wave-uniform
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+        for (uint32_t b0 = 0; b0 < T; b0 += 64u) {   // a batch: every lane one body, then the adds in list order
+            const bool hit = b0 + (uint32_t)lane < T;
+            f3 F = mk(0, 0, 0), TA = mk(0, 0, 0);
+            if (hit) body(list[b0 + (uint32_t)lane], F, TA);
+            fold(F, TA, hit);
         }
     }
 #pragma unroll
@@ -451,7 +440,7 @@ __device__ __forceinline__ void contact_accumulate_lanes(const float4* __restric
                                                          const GridDesc& g, const ContactConst& c, int32_t a, float4 pa,
                                                          float4 va, float4 wa, f3& v, f3& w, uint32_t tq[3]) {
     if constexpr (T == CT_FLAT)
-        contact_accumulate_flat(pos, vel, omg, DirectMap{cs}, g, c, a, pa, va, wa, v, w, tq);
+        contact_accumulate_flat<CT_BLK / 64>(pos, vel, omg, DirectMap{cs}, g, c, a, pa, va, wa, v, w, tq);
     else
         contact_accumulate_team<T>(pos, vel, omg, cs, g, c, a, pa, va, wa, v, w, tq);
 }
@@ -722,7 +711,7 @@ __global__ __launch_bounds__(FZ_BLK) void k_contact_fused(FusedIO io, int32_t n_
             const int32_t id = io.id[o], mode = io.mode[o];
             f3 v = xyz(va), w = xyz(wa);
             uint32_t tq[3] = {0u, 0u, 0u};
-            if (a < n_active) contact_accumulate_flat(io.pos, io.vel, io.omg, M, g, c, a, pa, va, wa, v, w, tq);
+            if (a < n_active) contact_accumulate_flat<CF_WAVES>(io.pos, io.vel, io.omg, M, g, c, a, pa, va, wa, v, w, tq);
             if ((threadIdx.x & 63u) == 0) {
                 FusedFin& f = fin[threadIdx.x >> 6];
                 f.pa = pa; f.va = va; f.wa = wa; f.v = v; f.w = w;

@@ -145,14 +145,15 @@ constexpr int MV_RK_CAP = 32;   // (MP_CAP >= 64: lds_sort pads to 64 entries)
 constexpr int MV_RK_CAP = 2048;     // dest entries staged per workgroup (a power of two)
 #endif
 constexpr int MP_CAP = 2 * MV_RK_CAP;   // multi-pass: entries per pass (dk and ds as one array)
-constexpr int RK_HBITS = 12;
+constexpr int RK_HBITS = 11;
 constexpr int RK_HBINS = 1 << RK_HBITS; // multi-pass: key bins of a range
-constexpr int RK_BM_WORDS = 1024;   // slot-presence bitmap over [xw, x1): up to 32,768 slots
+constexpr int RK_BM_WORDS = 2048;   // slot-presence bitmap over [xw, x1): up to 65,536 slots
 constexpr int RK_WIN = 2048;        // slot entries staged below x0 (covers the cell holding x0)
-// Slots per range at most: the grid grows past MV_RANK_GRID workgroups for n > 2M (C5 single-context: 2,048 ranges;
-// every workgroup streams the whole mover list, so that costs ~G·m, small against such a step), which keeps a range's
-// entries within LDS (a C5 range of 65,536 slots held more old keys than RK_OK_CAP mid-run, r5).
-constexpr uint32_t RK_MAX_RANGE = 8192;
+// Slots per range at most: the grid grows past MV_RANK_GRID workgroups for n > 8M (C5 single-context: 512 ranges).
+// Every workgroup streams the whole mover list, so the grid costs ~(ranges + shares)·m of L2 reads: r5's 8,192-slot
+// ranges and 16,384-cell shares made 5,627 workgroups at C5 (4.5 GB of mover reads per step, k_mv_rank 0.55 ms);
+// a range's dest entries beyond LDS now take the multi-pass path, so ranges can be 4x longer.
+constexpr uint32_t RK_MAX_RANGE = 32768;
 static_assert(RK_MAX_RANGE + RK_WIN + 512u <= 32u * RK_BM_WORDS, "a range and its window fit the bitmap");
 #ifdef SPH_RK_SMALLCAP
 constexpr int RK_COUNT = 8;
@@ -161,15 +162,26 @@ constexpr int RK_COUNT = 256;       // dest entries ranked by counting, more by 
 #endif
 constexpr int RK_KD1_CAP = 1024;    // movers into the cell a range ends in, staged
 constexpr int RK_SU = 2;            // stayer slots per lane in flight
-constexpr uint32_t RK_CELLS = 16384; // cells per share at most (k_mv_rank's cell workgroups)
-constexpr int RK_POOL_U64 = RK_CELLS / 2;   // the LDS pool: a share's differences, or a range's entries and bitmap
+#ifdef SPH_RK_SMALLCAP   // (the variant: shares of several passes whose keys overflow LDS)
+constexpr uint32_t RK_SUB = 1024;
+constexpr uint32_t RK_SHARE_KEYS = 48;
+#else
+constexpr uint32_t RK_SUB = 8192;    // cells per LDS pass of a share (its difference array)
+constexpr uint32_t RK_SHARE_KEYS = 16384;  // a share's mover keys staged in LDS, 16 bits each (beyond: a stream per pass)
+#endif
+constexpr uint32_t RK_SUBS = 8;      // passes per share at most
+constexpr uint32_t RK_CELLS = RK_SUB * RK_SUBS;   // cells per share at most (k_mv_rank's cell workgroups)
+constexpr int RK_POOL_U64 = 8192;   // the LDS pool (64 KB): a share's differences and keys, or a range's entries and bitmap
+static_assert(4 * RK_SUB + 2 * RK_SHARE_KEYS <= 8 * RK_POOL_U64 && RK_SUB * RK_SUBS <= 65536u,
+              "a share's LDS fits the pool; its cell offsets fit 16 bits");
 constexpr int RK_CU = 4;            // cells per lane in flight
 static_assert(2 * MV_RK_CAP * 8 + 4 * (RK_KD1_CAP + 2 * (RK_BM_WORDS + 1) + RK_HBINS + 1) <= RK_POOL_U64 * 8,
               "a range's LDS fits the pool");
 // ResortScratch.stats words (sph_read_resort_counts): ranges that counted against the whole mover list, lanes whose
 // insertion slot lay below the staged window (a whole-list count each), multi-pass ranges, their passes, the largest
-// dest-entry count of a range (recorded above MV_RK_CAP / 4)
-enum { RS_WHOLE = 0, RS_WHOLE_LANES, RS_MULTI, RS_PASSES, RS_MAX_ND, RS_WORDS = 8 };
+// dest-entry count of a range (recorded above MV_RK_CAP / 4), cell shares whose mover keys overflowed LDS (a stream
+// of the mover list per pass instead of one)
+enum { RS_WHOLE = 0, RS_WHOLE_LANES, RS_MULTI, RS_PASSES, RS_MAX_ND, RS_SHARE_RESTREAM, RS_WORDS = 8 };
 // Test-only timing probe (scripts/rank_probe.py, a -DSPH_RANK_PROBE build): per workgroup the wall clock at its start,
 // after the mover stream, after the sorts and at its end, with its entry counts.
 #ifdef SPH_RANK_PROBE
@@ -271,13 +283,16 @@ __device__ void lds_sort(uint64_t* a, uint32_t* b, uint32_t len) {
 }
 
 // A share of the cells [c0, c1) of [0, ncells] (workgroups G.. of k_mv_rank): cs_new[k] = cs[k] + #{movers: new key
-// < k} − #{movers: old key < k}. One stream over the movers' keys counts those below c0 and adds +1 (new key) / −1 (old
-// key) at key + 1 into a difference array over the share; its prefix sum is each cell's change. The old table is only
-// read (every workgroup's movers read their insertion cells from it), the new one written whole; the cell starts read
-// back (picks) come from here.
+// < k} − #{movers: old key < k}. One stream over the movers' keys counts those below c0 and stages the others that
+// change a cell of the share (key k in [c0, c1 − 1): cell k + 1 on) in LDS, as j − 1 = k − c0 in 16 bits, new keys
+// from the front of the list and old keys from its back. Then per pass of RK_SUB cells: the staged keys of the pass add
+// ±1 at j into a difference array, whose prefix (plus the passes before) is each cell's change. A share holds up to RK_SUBS passes, so that at C5 (58.6M cells) 895 shares
+// stream the mover list instead of r5's 3,578 16,384-cell ones; a share whose keys overflow LDS streams the list once
+// per pass (counted). The old table is only read (every workgroup's movers read their insertion cells from it), the new
+// one written whole; the cell starts read back (picks) come from here.
 __device__ void mv_cells(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ mtotal, const uint32_t* __restrict__ cs,
                          uint32_t* __restrict__ cs_new, uint32_t ncells, const CsPick& pick, const ResortScratch& w,
-                         int32_t* diff, uint32_t* red) {
+                         int32_t* diff, uint16_t* kl, uint32_t* cnt, uint32_t* red) {
     const uint32_t c0 = (uint32_t)((uint64_t)(ncells + 1u) * cb / Gc), c1 = (uint32_t)((uint64_t)(ncells + 1u) * (cb + 1) / Gc);
     const uint32_t L = c1 - c0;   // <= RK_CELLS (the launcher's share count)
     uint32_t ks[RK_U], os[RK_U];
@@ -290,9 +305,10 @@ __device__ void mv_cells(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ 
         }
     };
     load_round(0, w.cap - 1u);
-    const uint32_t m = *mtotal;
-    for (uint32_t t = threadIdx.x; t < L; t += RK_BLK) diff[t] = 0;
-    __syncthreads();
+    const uint32_t m = uni(*mtotal);
+    __syncthreads();   // cnt zeroed
+    // cells [c0 + a, c0 + b) of the share changed by key k: k + 1 − c0 in [a, b)
+    auto in_share = [&](uint32_t k, uint32_t a, uint32_t b) { return k >= c0 && k + 1u < c1 && k + 1u - c0 >= a && k + 1u - c0 < b; };
     uint32_t bn_c = 0, bo_c = 0;
     for (uint32_t base = 0; base < m; base += RK_BLK * RK_U) {
 #pragma unroll
@@ -302,56 +318,92 @@ __device__ void mv_cells(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ 
             const uint32_t k = ks[u], o = os[u];
             bn_c += okr && k < c0 ? 1u : 0u;
             bo_c += okr && o < c0 ? 1u : 0u;
-            if (okr && k >= c0 && k + 1u < c1) atomicAdd(&diff[k + 1u - c0], 1);
-            if (okr && o >= c0 && o + 1u < c1) atomicAdd(&diff[o + 1u - c0], -1);
+            if (okr && in_share(k, 0u, L)) {
+                const uint32_t p = atomicAdd(&cnt[0], 1u);
+                if (p < RK_SHARE_KEYS) kl[p] = (uint16_t)(k - c0);
+            }
+            if (okr && in_share(o, 0u, L)) {
+                const uint32_t p = atomicAdd(&cnt[1], 1u);
+                if (p < RK_SHARE_KEYS) kl[RK_SHARE_KEYS - 1u - p] = (uint16_t)(o - c0);
+            }
         }
         if (base + RK_BLK * RK_U < m) load_round(base + RK_BLK * RK_U, m - 1u);
     }
-    bn_c = block_sum<RK_BLK>(bn_c, red);   // (its barriers also publish the differences)
-    bo_c = block_sum<RK_BLK>(bo_c, red);
-    // inclusive prefix of diff[0, L): RK_CELLS / RK_BLK consecutive entries per lane
-    constexpr uint32_t EPL = RK_CELLS / RK_BLK;
-    const uint32_t e0 = EPL * threadIdx.x;
-    int32_t tot = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < EPL; ++j) tot += e0 + j < L ? diff[e0 + j] : 0;
-    int32_t inc = tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int32_t u = __shfl_up(inc, o, 64);
-        if (lane_id() >= (uint32_t)o) inc += u;
-    }
-    __syncthreads();   // block_sum's last reads of red
-    if (lane_id() == 63) red[threadIdx.x >> 6] = (uint32_t)inc;
-    __syncthreads();
-    int32_t pre = (int32_t)bn_c - (int32_t)bo_c + inc - tot;
-    for (uint32_t k = 0; k < (threadIdx.x >> 6); ++k) pre += (int32_t)red[k];
-#pragma unroll
-    for (uint32_t j = 0; j < EPL; ++j)   // now the change of cell c0 + e0 + j (each lane rewrites only its own entries)
-        if (e0 + j < L) {
-            pre += diff[e0 + j];
-            diff[e0 + j] = pre;
+    bn_c = uni(block_sum<RK_BLK>(bn_c, red));   // (its barriers also publish the staged keys)
+    bo_c = uni(block_sum<RK_BLK>(bo_c, red));
+    const uint32_t nn = uni(cnt[0]), no = uni(cnt[1]);
+    const bool staged = nn + no <= RK_SHARE_KEYS;   // block-uniform
+    if (!staged && threadIdx.x == 0 && w.stats) atomicAdd(w.stats + RS_SHARE_RESTREAM, 1u);
+    int32_t carry = (int32_t)uni((uint32_t)((int32_t)bn_c - (int32_t)bo_c));   // the change below the pass's first cell
+    for (uint32_t s0 = 0; s0 < L; s0 += RK_SUB) {
+        const uint32_t Ls = min(RK_SUB, L - s0);
+        __syncthreads();   // the previous pass's reads of diff and red
+        for (uint32_t t = threadIdx.x; t < RK_SUB; t += RK_BLK) diff[t] = 0;
+        __syncthreads();
+        if (staged) {
+            for (uint32_t t = threadIdx.x; t < nn + no; t += RK_BLK) {
+                const bool nw = t < nn;
+                const uint32_t j = (uint32_t)kl[nw ? t : RK_SHARE_KEYS - 1u - (t - nn)] + 1u;
+                if (j >= s0 && j < s0 + Ls) atomicAdd(&diff[j - s0], nw ? 1 : -1);
+            }
+        } else {   // the keys did not fit: this pass's from the whole list (rare: a plain loop, few registers)
+            for (uint32_t r = threadIdx.x; r < m; r += RK_BLK) {
+                const uint32_t k = w.mk[r], o = w.mo[r];
+                if (in_share(k, s0, s0 + Ls)) atomicAdd(&diff[k + 1u - c0 - s0], 1);
+                if (in_share(o, s0, s0 + Ls)) atomicAdd(&diff[o + 1u - c0 - s0], -1);
+            }
         }
-    __syncthreads();
-    for (uint32_t base = 0; base < L; base += RK_BLK * RK_CU) {
-        uint32_t cv[RK_CU];
+        __syncthreads();
+        // inclusive prefix of diff[0, Ls): RK_SUB / RK_BLK consecutive entries per lane, from carry
+        constexpr uint32_t EPL = RK_SUB / RK_BLK;
+        static_assert(EPL * RK_BLK == RK_SUB, "cells per lane");
+        const uint32_t e0 = EPL * threadIdx.x;
+        int32_t tot = 0;
 #pragma unroll
-        for (int u = 0; u < RK_CU; ++u) cv[u] = cs[c0 + min(base + u * RK_BLK + threadIdx.x, L - 1u)];
+        for (uint32_t j = 0; j < EPL; ++j) tot += e0 + j < Ls ? diff[e0 + j] : 0;
+        int32_t inc = tot;
 #pragma unroll
-        for (int u = 0; u < RK_CU; ++u) {
-            const uint32_t t = base + u * RK_BLK + threadIdx.x;
-            if (t < L) cs_new[c0 + t] = (uint32_t)((int32_t)cv[u] + diff[t]);
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t u = __shfl_up(inc, o, 64);
+            if (lane_id() >= (uint32_t)o) inc += u;
+        }
+        if (lane_id() == 63) red[threadIdx.x >> 6] = (uint32_t)inc;
+        __syncthreads();
+        int32_t pre = carry + inc - tot, all = 0;
+        for (uint32_t k = 0; k < RK_BLK / 64; ++k) {
+            const int32_t rk = (int32_t)red[k];
+            pre += k < (threadIdx.x >> 6) ? rk : 0;
+            all += rk;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < EPL; ++j)   // now the change of cell c0 + s0 + e0 + j (each lane rewrites its own entries)
+            if (e0 + j < Ls) {
+                pre += diff[e0 + j];
+                diff[e0 + j] = pre;
+            }
+        carry = (int32_t)uni((uint32_t)(carry + all));
+        __syncthreads();
+        const uint32_t cb0 = c0 + s0;
+        for (uint32_t base = 0; base < Ls; base += RK_BLK * RK_CU) {
+            uint32_t cv[RK_CU];
+#pragma unroll
+            for (int u = 0; u < RK_CU; ++u) cv[u] = cs[cb0 + min(base + u * RK_BLK + threadIdx.x, Ls - 1u)];
+#pragma unroll
+            for (int u = 0; u < RK_CU; ++u) {
+                const uint32_t t = base + u * RK_BLK + threadIdx.x;
+                if (t < Ls) cs_new[cb0 + t] = (uint32_t)((int32_t)cv[u] + diff[t]);
+            }
+        }
+        if ((int32_t)threadIdx.x < pick.m) {   // cell starts read back: the ones in this pass
+            const uint32_t k = (uint32_t)pick.idx[threadIdx.x];
+            if (k >= cb0 && k < cb0 + Ls) {
+                const uint32_t v = (uint32_t)((int32_t)cs[k] + diff[k - cb0]);
+                pick.out[threadIdx.x] = v;
+                if (pick.out_host) pick.out_host[threadIdx.x] = v;
+            }
         }
     }
     if (c1 == ncells + 1u && threadIdx.x == 0) cs_new[ncells + 1u] = cs[ncells + 1u];
-    if ((int32_t)threadIdx.x < pick.m) {   // cell starts read back: the ones in this share
-        const uint32_t k = (uint32_t)pick.idx[threadIdx.x];
-        if (k >= c0 && k < c1) {
-            const uint32_t v = (uint32_t)((int32_t)cs[k] + diff[k - c0]);
-            pick.out[threadIdx.x] = v;
-            if (pick.out_host) pick.out_host[threadIdx.x] = v;
-        }
-    }
 }
 
 __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restrict__ mtotal, uint32_t* __restrict__ next_count,
@@ -363,7 +415,7 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
                                                     ResortExtra ex) {
     // one LDS pool, laid out per role: a range's entries and slot bitmap, or a cell share's count differences
     __shared__ uint64_t pool[RK_POOL_U64];
-    __shared__ uint32_t cnt[8], red[RK_BLK / 64];
+    __shared__ uint32_t cnt[10], red[RK_BLK / 64];
     uint64_t* dk = pool;                                    // dest entries (new key, slot); multi-pass: MP_CAP of them
     uint64_t* ds = pool + MV_RK_CAP;                        // the dest entries in (key, slot) order
     uint32_t* kx1 = (uint32_t*)(pool + 2 * MV_RK_CAP);      // slots of the movers whose new key is kd1
@@ -372,9 +424,10 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
     uint32_t* hp = bpre + (RK_BM_WORDS + 1);                // multi-pass: key bins, then their exclusive prefix
     RK_PROBE(0, wall_clock64());
     resolve_sizes(src, w, n);
-    if (threadIdx.x < 8) cnt[threadIdx.x] = 0u;
+    if (threadIdx.x < 10) cnt[threadIdx.x] = 0u;
     if (blockIdx.x >= G) {   // a share of the cells: its own workgroup, beside the ranges
-        mv_cells(blockIdx.x - G, gridDim.x - G, mtotal, cs, cs_new, ncells, pick, w, (int32_t*)pool, red);
+        mv_cells(blockIdx.x - G, gridDim.x - G, mtotal, cs, cs_new, ncells, pick, w, (int32_t*)pool,
+                 (uint16_t*)((int32_t*)pool + RK_SUB), cnt, red);
         return;
     }
     for (uint32_t t = threadIdx.x; t <= (uint32_t)RK_BM_WORDS; t += RK_BLK) bm[t] = 0u;
@@ -493,12 +546,8 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
     // most ncells), then the bins' exclusive prefix and the largest bin.
     uint32_t P = 1, Cg = 1, sh = 0;
     bool mp = false;
+    uint32_t kb0 = kd0;   // the bins' first key
     if (!dest_staged) {
-        const uint32_t kend = min(kd1, ncells + 1u);
-        const uint32_t span = kend > kd0 ? kend - kd0 : 1u;
-        sh = span > (uint32_t)RK_HBINS ? 32u - (uint32_t)__builtin_clz((span - 1u) >> RK_HBITS) : 0u;
-        for (uint32_t t = threadIdx.x; t < (uint32_t)RK_HBINS; t += RK_BLK) hp[t] = 0u;
-        __syncthreads();
         uint64_t* const mcopy = w.ms + below_k;   // below_k + nd <= m <= cap
         load_round(0, m - 1u);                    // (m > MV_RK_CAP here)
         for (uint32_t base = 0; base < m; base += RK_BLK * RK_U) {
@@ -506,13 +555,22 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
             for (int u = 0; u < RK_U; ++u) {
                 const uint32_t r = base + u * RK_BLK + threadIdx.x, k = ks[u];
                 if (r < m && k >= kd0 && k < kd1) {
-                    atomicAdd(&hp[(k - kd0) >> sh], 1u);
                     const uint32_t j = atomicAdd(&cnt[6], 1u);
                     if (j < nd) mcopy[j] = comp(k, mv_slot(w, xs[u]));
+                    atomicMax(&cnt[7], k);    // the entries' key span [kmin, kmax]
+                    atomicMax(&cnt[8], ~k);
                 }
             }
             if (base + RK_BLK * RK_U < m) load_round(base + RK_BLK * RK_U, m - 1u);
         }
+        for (uint32_t t = threadIdx.x; t < (uint32_t)RK_HBINS; t += RK_BLK) hp[t] = 0u;
+        __syncthreads();
+        // bins over the entries' own key span (a front's movers fill a few columns of a range whose key interval can
+        // span every empty column of the tank: bins over [kd0, kd1) put thousands in one bin at C5, r6)
+        kb0 = uni(~cnt[8]);
+        const uint32_t span = uni(cnt[7]) - kb0 + 1u;
+        sh = span > (uint32_t)RK_HBINS ? 32u - (uint32_t)__builtin_clz((span - 1u) >> RK_HBITS) : 0u;
+        for (uint32_t t = threadIdx.x; t < nd; t += RK_BLK) atomicAdd(&hp[((uint32_t)(mcopy[t] >> 32) - kb0) >> sh], 1u);
         __syncthreads();
         constexpr uint32_t HPL = RK_HBINS / RK_BLK;   // consecutive bins per lane
         static_assert(HPL * RK_BLK == RK_HBINS, "bins per lane");
@@ -612,8 +670,8 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
         if (mp) {   // stage the entries of bins [ba, bb) from the copy and sort them
             const uint32_t ba = pass == 0 ? 0u : lower_bound(hp, (uint32_t)RK_HBINS, pass * Cg);
             const uint32_t bb = last ? (uint32_t)RK_HBINS : lower_bound(hp, (uint32_t)RK_HBINS, (pass + 1u) * Cg);
-            Ka = uni(kd0 + (ba << sh));
-            Kb = uni(last ? kd1 : kd0 + (bb << sh));
+            Ka = uni(pass == 0 ? kd0 : kb0 + (ba << sh));
+            Kb = uni(last ? kd1 : kb0 + (bb << sh));
             before = uni(hp[ba]);
             ndp = uni(min(hp[bb] - before, (uint32_t)MP_CAP));
             const uint64_t* const mcopy = w.ms + below_k;
@@ -832,7 +890,7 @@ void launch_resort(AsmSrc src, uint32_t* cs, uint32_t* cs_new, uint32_t ncells, 
     if (n <= 0) return;
     // n is an upper bound of the slots on device-sized steps: the rank kernel's ranges split the device count
     const uint32_t G = resort_ranges(n);
-    // the cell shares: as many workgroups, and at most RK_CELLS cells each (C3: 224 would do)
+    // the cell shares: as many workgroups as ranges, and at most RK_CELLS cells each (C3: 256 of ~14,300 cells; C5: 895)
     const uint32_t Gc = std::max(G, (ncells + RK_CELLS) / RK_CELLS);
     SPH_LAUNCH(k_mv_rank, G + Gc, RK_BLK, 0, s, count, count_other, cs, cs_new, ncells, pick, G, w, src, n, pos_o, vel_o,
                id_o, sk_o, ex);

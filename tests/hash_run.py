@@ -3,7 +3,7 @@ steps a Model S scenario and writes, as JSON, a sha1 of the positions and veloci
 sparse-path counters summed over the run (sph_read_path_counts: density chunked, density global, force
 chunked, force global), the hit-mask counters (wave-planes scanned by distance, waves) and the incremental
 re-sort's counters (sph_read_resort_counts: whole-list ranges, whole-list lanes, multi-pass ranges, passes,
-largest range). `violent`: tests/test_gpu_resort.py's many-movers state (random velocities of up to a z
+largest range, cell shares that re-streamed). `violent`: tests/test_gpu_resort.py's many-movers state (random velocities of up to a z
 sub-cell per step), where most ranges take the re-sort's multi-pass path in the small-cap variant library.
 
   python tests/hash_run.py OUT.json STEPS {slab|violent|C1|C2|C3}
@@ -38,7 +38,7 @@ def main() -> None:
         paths = np.zeros(4, np.int64)
         hm = np.zeros(2, np.int64)
         sim.ctx.resort_counts(reset=True)
-        rs = np.zeros(5, np.int64)
+        rs = np.zeros(6, np.int64)
         hs = []
         for _ in range(steps):
             sim.step(1)
@@ -47,6 +47,7 @@ def main() -> None:
             c = sim.ctx.resort_counts(reset=True).astype(np.int64)
             rs[:4] += c[:4]
             rs[4] = max(rs[4], c[4])
+            rs[5] += c[5]
             x, v = sim.positions(), sim.velocities()
             hs.append(hashlib.sha1(x.tobytes() + v.tobytes()).hexdigest()[:16])
         lib = str(pkg._abi.lib_path()) if hasattr(pkg, "_abi") else ""

@@ -15,8 +15,9 @@ The product library runs against libsphhip_smallplanes.so, the same sources with
 the variant's counters must show that its planes really took the chunked and global-gather paths. The
 violent state (most particles change sub-cell every step) runs both libraries on the incremental re-sort
 (SPH_RESORT=2) against the product's full sort (SPH_RESORT=0), so the variant's ranges take the re-sort's
-multi-pass path (resort.hip: dest entries beyond LDS, staged per key sub-interval) and must still give the
-full sort's permutation. The analogue in the reference is its
+multi-pass path (resort.hip: dest entries beyond LDS, staged per key sub-interval) and its cell shares the
+path for keys beyond LDS (a stream per pass); C3 gives the variant's shares several passes of 1,024 cells.
+All must still give the full sort's permutation and cell starts. The analogue in the reference is its
 contact test `SimulateParticles.compute:249-253`, evaluated the same way for every candidate.
 """
 import json
@@ -68,8 +69,9 @@ def test_resort_multi_pass_matches_the_full_sort(tmp_path):
     prod = _run(tmp_path, None, 12, "violent", "product", resort="2")
     small = _run(tmp_path, SMALL, 12, "violent", "small", resort="2")
     print({"product_resort": prod["resort"], "small_resort": small["resort"]})
-    whole, whole_lanes, multi, passes, _ = small["resort"]
+    whole, whole_lanes, multi, passes, _, restream = small["resort"]
     assert multi > 0 and passes > multi, small["resort"]     # ranges ran in several passes
+    assert restream > 0, small["resort"]                     # cell shares whose keys overflowed LDS
     assert whole == 0 and whole_lanes == 0, small["resort"]  # and none counted against the whole list
     assert prod["resort"][0] == 0 and prod["resort"][1] == 0, prod["resort"]
     for name, run in (("product", prod), ("small", small)):

@@ -146,15 +146,16 @@ def test_resort_ranges_never_count_against_the_whole_list(pkg, shape):
                                            seed=1234), profile=True)
     try:
         sim.ctx.resort_counts(reset=True)
-        tot = np.zeros(5, np.int64)
+        tot = np.zeros(6, np.int64)
         for _ in range(6):
             sim.step(50)
             c = sim.ctx.resort_counts(reset=True).astype(np.int64)
             tot[:4] += c[:4]
             tot[4] = max(tot[4], c[4])
+            tot[5] += c[5]
         ks = sim.ctx.kernel_stats()
         print({"shape": shape, "whole": int(tot[0]), "whole_lanes": int(tot[1]), "multi_pass_ranges": int(tot[2]),
-               "passes": int(tot[3]), "max_range_entries": int(tot[4]),
+               "passes": int(tot[3]), "max_range_entries": int(tot[4]), "share_restreams": int(tot[5]),
                "resort_launches": ks.get("resort", {}).get("launches", 0),
                "radix_sort_launches": ks.get("radix_sort", {}).get("launches", 0)})
         assert tot[0] == 0 and tot[1] == 0, tot
