@@ -15,12 +15,15 @@ for r in csv.DictReader(open(f)):
 ev.sort()
 dens = [i for i, e in enumerate(ev) if e[2] == "k_density_tiled"]
 main = ev[dens[-1]][3]   # the compute stream (every density pass runs there)
+# the comm streams: those running the halo kernels (an interior pass on its own CU-masked stream, SPH_INTERIOR_CU_EXCLUDE,
+# is neither the compute stream nor a comm stream)
+comm_streams = {e[3] for e in ev if e[2] in ("k_slab_unpack_rho2", "k_slab_pack2", "k_slab_rec", "k_slab_lag")} - {main}
 starts = dens[::nsl]     # the first density pass of each group step
 slack, bnd = [], []
 for a, b in zip(starts[-steps - 1:-1], starts[-steps:]):
     w = ev[a:b]
-    inter = [e for e in w if e[2] == "k_force_tiled" and e[3] == main]
-    comm = [e for e in w if e[3] != main]
+    inter = [e for e in w if e[2] == "k_force_tiled" and e[3] not in comm_streams]
+    comm = [e for e in w if e[3] in comm_streams]
     if not inter or not comm:
         continue
     slack.append((max(e[1] for e in inter) - max(e[1] for e in comm)) / 1e3)

@@ -145,15 +145,24 @@ constexpr int MV_RK_CAP = 32;   // (MP_CAP >= 64: lds_sort pads to 64 entries)
 constexpr int MV_RK_CAP = 2048;     // dest entries staged per workgroup (a power of two)
 #endif
 constexpr int MP_CAP = 2 * MV_RK_CAP;   // multi-pass: entries per pass (dk and ds as one array)
+#ifdef SPH_RK_RANGE8K   // A/B: r5's 8,192-slot ranges
+constexpr int RK_HBITS = 12;
+constexpr int RK_BM_WORDS = 1024;
+#else
 constexpr int RK_HBITS = 11;
-constexpr int RK_HBINS = 1 << RK_HBITS; // multi-pass: key bins of a range
 constexpr int RK_BM_WORDS = 2048;   // slot-presence bitmap over [xw, x1): up to 65,536 slots
+#endif
+constexpr int RK_HBINS = 1 << RK_HBITS; // multi-pass: key bins of a range
 constexpr int RK_WIN = 2048;        // slot entries staged below x0 (covers the cell holding x0)
 // Slots per range at most: the grid grows past MV_RANK_GRID workgroups for n > 8M (C5 single-context: 512 ranges).
 // Every workgroup streams the whole mover list, so the grid costs ~(ranges + shares)·m of L2 reads: r5's 8,192-slot
 // ranges and 16,384-cell shares made 5,627 workgroups at C5 (4.5 GB of mover reads per step, k_mv_rank 0.55 ms);
 // a range's dest entries beyond LDS now take the multi-pass path, so ranges can be 4x longer.
+#ifdef SPH_RK_RANGE8K
+constexpr uint32_t RK_MAX_RANGE = 8192;
+#else
 constexpr uint32_t RK_MAX_RANGE = 32768;
+#endif
 static_assert(RK_MAX_RANGE + RK_WIN + 512u <= 32u * RK_BM_WORDS, "a range and its window fit the bitmap");
 #ifdef SPH_RK_SMALLCAP
 constexpr int RK_COUNT = 8;
@@ -162,18 +171,21 @@ constexpr int RK_COUNT = 256;       // dest entries ranked by counting, more by 
 #endif
 constexpr int RK_KD1_CAP = 1024;    // movers into the cell a range ends in, staged
 constexpr int RK_SU = 2;            // stayer slots per lane in flight
-#ifdef SPH_RK_SMALLCAP   // (the variant: shares of several passes whose keys overflow LDS)
+#ifdef SPH_RK_SMALLCAP   // (the variant: shares of several passes whose keys overflow LDS; no direct shares)
 constexpr uint32_t RK_SUB = 1024;
 constexpr uint32_t RK_SHARE_KEYS = 48;
+constexpr uint32_t RK_DIRECT = 0;
 #else
 constexpr uint32_t RK_SUB = 8192;    // cells per LDS pass of a share (its difference array)
 constexpr uint32_t RK_SHARE_KEYS = 16384;  // a share's mover keys staged in LDS, 16 bits each (beyond: a stream per pass)
+constexpr uint32_t RK_DIRECT = 16384;      // a share of at most this many cells: one pass, the stream adding into LDS
 #endif
 constexpr uint32_t RK_SUBS = 8;      // passes per share at most
 constexpr uint32_t RK_CELLS = RK_SUB * RK_SUBS;   // cells per share at most (k_mv_rank's cell workgroups)
 constexpr int RK_POOL_U64 = 8192;   // the LDS pool (64 KB): a share's differences and keys, or a range's entries and bitmap
-static_assert(4 * RK_SUB + 2 * RK_SHARE_KEYS <= 8 * RK_POOL_U64 && RK_SUB * RK_SUBS <= 65536u,
-              "a share's LDS fits the pool; its cell offsets fit 16 bits");
+static_assert(4 * RK_SUB + 2 * RK_SHARE_KEYS <= 8 * RK_POOL_U64 && RK_SUB * RK_SUBS <= 65536u &&
+              4 * RK_DIRECT <= 8 * RK_POOL_U64 && RK_DIRECT <= 16u * 1024u,
+              "a share's LDS fits the pool; its cell offsets fit 16 bits; a direct share's prefix fits 16 cells per lane");
 constexpr int RK_CU = 4;            // cells per lane in flight
 static_assert(2 * MV_RK_CAP * 8 + 4 * (RK_KD1_CAP + 2 * (RK_BM_WORDS + 1) + RK_HBINS + 1) <= RK_POOL_U64 * 8,
               "a range's LDS fits the pool");
@@ -290,7 +302,91 @@ __device__ void lds_sort(uint64_t* a, uint32_t* b, uint32_t len) {
 // stream the mover list instead of r5's 3,578 16,384-cell ones; a share whose keys overflow LDS streams the list once
 // per pass (counted). The old table is only read (every workgroup's movers read their insertion cells from it), the new
 // one written whole; the cell starts read back (picks) come from here.
-__device__ void mv_cells(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ mtotal, const uint32_t* __restrict__ cs,
+// A share of up to RK_DIRECT cells (C3: 256 shares of ~14,300) in one pass, r5's form: the stream adds +1 (new key) / −1
+// (old key) at key + 1 straight into an LDS difference array over the whole share. Larger shares (C5: 895 of 65,536
+// cells) take the staged form below (mv_cells_staged); two functions, so that the staged form's registers do not
+// reach the direct form's code (a kernel with both measured the C3 re-sort 29 → 34 µs, profiles/r06_resort_ab.log).
+__device__ void mv_cells_direct(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ mtotal, const uint32_t* __restrict__ cs,
+                         uint32_t* __restrict__ cs_new, uint32_t ncells, const CsPick& pick, const ResortScratch& w,
+                         int32_t* diff, uint32_t* red) {
+    const uint32_t c0 = (uint32_t)((uint64_t)(ncells + 1u) * cb / Gc), c1 = (uint32_t)((uint64_t)(ncells + 1u) * (cb + 1) / Gc);
+    const uint32_t L = c1 - c0;   // <= RK_DIRECT (the caller's choice)
+    uint32_t ks[RK_U], os[RK_U];
+    auto load_round = [&](uint32_t base, uint32_t last) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < RK_U; ++u) {
+            const uint32_t r = min(base + u * RK_BLK + threadIdx.x, last);
+            ks[u] = w.mk[r];
+            os[u] = w.mo[r];
+        }
+    };
+    load_round(0, w.cap - 1u);
+    const uint32_t m = uni(*mtotal);
+    for (uint32_t t = threadIdx.x; t < L; t += RK_BLK) diff[t] = 0;
+    __syncthreads();
+    uint32_t bn_c = 0, bo_c = 0;
+    for (uint32_t base = 0; base < m; base += RK_BLK * RK_U) {
+#pragma unroll
+        for (int u = 0; u < RK_U; ++u) {
+            const uint32_t r = base + u * RK_BLK + threadIdx.x;
+            const bool okr = r < m;
+            const uint32_t k = ks[u], o = os[u];
+            bn_c += okr && k < c0 ? 1u : 0u;
+            bo_c += okr && o < c0 ? 1u : 0u;
+            if (okr && k >= c0 && k + 1u < c1) atomicAdd(&diff[k + 1u - c0], 1);
+            if (okr && o >= c0 && o + 1u < c1) atomicAdd(&diff[o + 1u - c0], -1);
+        }
+        if (base + RK_BLK * RK_U < m) load_round(base + RK_BLK * RK_U, m - 1u);
+    }
+    bn_c = block_sum<RK_BLK>(bn_c, red);   // (its barriers also publish the differences)
+    bo_c = block_sum<RK_BLK>(bo_c, red);
+    // inclusive prefix of diff[0, L): RK_DIRECT / RK_BLK consecutive entries per lane
+    constexpr uint32_t EPL = RK_DIRECT >= (uint32_t)RK_BLK ? RK_DIRECT / RK_BLK : 1u;
+    const uint32_t e0 = EPL * threadIdx.x;
+    int32_t tot = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < EPL; ++j) tot += e0 + j < L ? diff[e0 + j] : 0;
+    int32_t inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t u = __shfl_up(inc, o, 64);
+        if (lane_id() >= (uint32_t)o) inc += u;
+    }
+    __syncthreads();   // block_sum's last reads of red
+    if (lane_id() == 63) red[threadIdx.x >> 6] = (uint32_t)inc;
+    __syncthreads();
+    int32_t pre = (int32_t)bn_c - (int32_t)bo_c + inc - tot;
+    for (uint32_t k = 0; k < (threadIdx.x >> 6); ++k) pre += (int32_t)red[k];
+#pragma unroll
+    for (uint32_t j = 0; j < EPL; ++j)   // now the change of cell c0 + e0 + j (each lane rewrites only its own entries)
+        if (e0 + j < L) {
+            pre += diff[e0 + j];
+            diff[e0 + j] = pre;
+        }
+    __syncthreads();
+    for (uint32_t base = 0; base < L; base += RK_BLK * RK_CU) {
+        uint32_t cv[RK_CU];
+#pragma unroll
+        for (int u = 0; u < RK_CU; ++u) cv[u] = cs[c0 + min(base + u * RK_BLK + threadIdx.x, L - 1u)];
+#pragma unroll
+        for (int u = 0; u < RK_CU; ++u) {
+            const uint32_t t = base + u * RK_BLK + threadIdx.x;
+            if (t < L) cs_new[c0 + t] = (uint32_t)((int32_t)cv[u] + diff[t]);
+        }
+    }
+    if (c1 == ncells + 1u && threadIdx.x == 0) cs_new[ncells + 1u] = cs[ncells + 1u];
+    if ((int32_t)threadIdx.x < pick.m) {   // cell starts read back: the ones in this share
+        const uint32_t k = (uint32_t)pick.idx[threadIdx.x];
+        if (k >= c0 && k < c1) {
+            const uint32_t v = (uint32_t)((int32_t)cs[k] + diff[k - c0]);
+            pick.out[threadIdx.x] = v;
+            if (pick.out_host) pick.out_host[threadIdx.x] = v;
+        }
+    }
+}
+
+
+__device__ void mv_cells_staged(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ mtotal, const uint32_t* __restrict__ cs,
                          uint32_t* __restrict__ cs_new, uint32_t ncells, const CsPick& pick, const ResortScratch& w,
                          int32_t* diff, uint16_t* kl, uint32_t* cnt, uint32_t* red) {
     const uint32_t c0 = (uint32_t)((uint64_t)(ncells + 1u) * cb / Gc), c1 = (uint32_t)((uint64_t)(ncells + 1u) * (cb + 1) / Gc);
@@ -337,24 +433,26 @@ __device__ void mv_cells(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ 
     int32_t carry = (int32_t)uni((uint32_t)((int32_t)bn_c - (int32_t)bo_c));   // the change below the pass's first cell
     for (uint32_t s0 = 0; s0 < L; s0 += RK_SUB) {
         const uint32_t Ls = min(RK_SUB, L - s0);
-        __syncthreads();   // the previous pass's reads of diff and red
-        for (uint32_t t = threadIdx.x; t < RK_SUB; t += RK_BLK) diff[t] = 0;
-        __syncthreads();
-        if (staged) {
-            for (uint32_t t = threadIdx.x; t < nn + no; t += RK_BLK) {
-                const bool nw = t < nn;
-                const uint32_t j = (uint32_t)kl[nw ? t : RK_SHARE_KEYS - 1u - (t - nn)] + 1u;
-                if (j >= s0 && j < s0 + Ls) atomicAdd(&diff[j - s0], nw ? 1 : -1);
+        {
+            __syncthreads();   // the previous pass's reads of diff and red
+            for (uint32_t t = threadIdx.x; t < RK_SUB; t += RK_BLK) diff[t] = 0;
+            __syncthreads();
+            if (staged) {
+                for (uint32_t t = threadIdx.x; t < nn + no; t += RK_BLK) {
+                    const bool nw = t < nn;
+                    const uint32_t j = (uint32_t)kl[nw ? t : RK_SHARE_KEYS - 1u - (t - nn)] + 1u;
+                    if (j >= s0 && j < s0 + Ls) atomicAdd(&diff[j - s0], nw ? 1 : -1);
+                }
+            } else {   // the keys did not fit: this pass's from the whole list (rare: a plain loop, few registers)
+                for (uint32_t r = threadIdx.x; r < m; r += RK_BLK) {
+                    const uint32_t k = w.mk[r], o = w.mo[r];
+                    if (in_share(k, s0, s0 + Ls)) atomicAdd(&diff[k + 1u - c0 - s0], 1);
+                    if (in_share(o, s0, s0 + Ls)) atomicAdd(&diff[o + 1u - c0 - s0], -1);
+                }
             }
-        } else {   // the keys did not fit: this pass's from the whole list (rare: a plain loop, few registers)
-            for (uint32_t r = threadIdx.x; r < m; r += RK_BLK) {
-                const uint32_t k = w.mk[r], o = w.mo[r];
-                if (in_share(k, s0, s0 + Ls)) atomicAdd(&diff[k + 1u - c0 - s0], 1);
-                if (in_share(o, s0, s0 + Ls)) atomicAdd(&diff[o + 1u - c0 - s0], -1);
-            }
+            __syncthreads();
         }
-        __syncthreads();
-        // inclusive prefix of diff[0, Ls): RK_SUB / RK_BLK consecutive entries per lane, from carry
+        // inclusive prefix of diff[0, Ls): EPL consecutive entries per lane, from carry
         constexpr uint32_t EPL = RK_SUB / RK_BLK;
         static_assert(EPL * RK_BLK == RK_SUB, "cells per lane");
         const uint32_t e0 = EPL * threadIdx.x;
@@ -406,6 +504,10 @@ __device__ void mv_cells(uint32_t cb, uint32_t Gc, const uint32_t* __restrict__ 
     if (c1 == ncells + 1u && threadIdx.x == 0) cs_new[ncells + 1u] = cs[ncells + 1u];
 }
 
+// STAGED: the cell shares exceed RK_DIRECT cells (mv_cells_staged), else mv_cells_direct; one form per instantiation, so
+// that the C3 kernel carries only the direct form's registers (60 VGPRs, nothing spilled; both forms in one kernel
+// spilled 22)
+template <bool STAGED>
 __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restrict__ mtotal, uint32_t* __restrict__ next_count,
                                                     const uint32_t* __restrict__ cs, uint32_t* __restrict__ cs_new,
                                                     uint32_t ncells, CsPick pick, uint32_t G, ResortScratch w,
@@ -426,8 +528,11 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
     resolve_sizes(src, w, n);
     if (threadIdx.x < 10) cnt[threadIdx.x] = 0u;
     if (blockIdx.x >= G) {   // a share of the cells: its own workgroup, beside the ranges
-        mv_cells(blockIdx.x - G, gridDim.x - G, mtotal, cs, cs_new, ncells, pick, w, (int32_t*)pool,
-                 (uint16_t*)((int32_t*)pool + RK_SUB), cnt, red);
+        if constexpr (STAGED)
+            mv_cells_staged(blockIdx.x - G, gridDim.x - G, mtotal, cs, cs_new, ncells, pick, w, (int32_t*)pool,
+                            (uint16_t*)((int32_t*)pool + RK_SUB), cnt, red);
+        else
+            mv_cells_direct(blockIdx.x - G, gridDim.x - G, mtotal, cs, cs_new, ncells, pick, w, (int32_t*)pool, red);
         return;
     }
     for (uint32_t t = threadIdx.x; t <= (uint32_t)RK_BM_WORDS; t += RK_BLK) bm[t] = 0u;
@@ -892,8 +997,12 @@ void launch_resort(AsmSrc src, uint32_t* cs, uint32_t* cs_new, uint32_t ncells, 
     const uint32_t G = resort_ranges(n);
     // the cell shares: as many workgroups as ranges, and at most RK_CELLS cells each (C3: 256 of ~14,300 cells; C5: 895)
     const uint32_t Gc = std::max(G, (ncells + RK_CELLS) / RK_CELLS);
-    SPH_LAUNCH(k_mv_rank, G + Gc, RK_BLK, 0, s, count, count_other, cs, cs_new, ncells, pick, G, w, src, n, pos_o, vel_o,
-               id_o, sk_o, ex);
+    if ((ncells + Gc) / Gc > RK_DIRECT)   // the largest share's cells (ncells + 1 split in Gc)
+        SPH_LAUNCH(k_mv_rank<true>, G + Gc, RK_BLK, 0, s, count, count_other, cs, cs_new, ncells, pick, G, w, src, n, pos_o,
+                   vel_o, id_o, sk_o, ex);
+    else
+        SPH_LAUNCH(k_mv_rank<false>, G + Gc, RK_BLK, 0, s, count, count_other, cs, cs_new, ncells, pick, G, w, src, n,
+                   pos_o, vel_o, id_o, sk_o, ex);
 }
 
 }  // namespace sph
