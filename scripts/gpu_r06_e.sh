@@ -8,6 +8,6 @@ trap "kill $HB" EXIT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_resort.py tests/test_gpu_path_independence.py -m gpu -v -s -p no:cacheprovider --timeout=300 --timeout-method thread -x > $O/pytest.log 2>&1; rc=$?
 echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|Error|'shape'|_resort" $O/pytest.log | tail -6
 [ $rc -ne 0 ] && exit $rc
-bash scripts/variant_ab.sh "head2 head r5rs" 3 > $O/ab.log 2>&1; rc=$?
+bash scripts/variant_ab.sh "${AB_VARIANTS:-head2 head r5rs}" 3 > $O/ab.log 2>&1; rc=$?
 cat $O/ab.log
 exit $rc

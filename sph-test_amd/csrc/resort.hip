@@ -535,7 +535,6 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
             mv_cells_direct(blockIdx.x - G, gridDim.x - G, mtotal, cs, cs_new, ncells, pick, w, (int32_t*)pool, red);
         return;
     }
-    for (uint32_t t = threadIdx.x; t <= (uint32_t)RK_BM_WORDS; t += RK_BLK) bm[t] = 0u;
     const uint32_t b = blockIdx.x;
     // the ranges are whole blocks of 256 slots
     const uint32_t nbk = ((uint32_t)n + 255u) / 256u;
@@ -571,6 +570,9 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
     // in cells of more than RK_WIN particles; such an entry counts its A(q) against the whole list instead.
     const uint32_t xw = x0 > (uint32_t)RK_WIN ? x0 - (uint32_t)RK_WIN : 0u;
     const bool bits_ok = x1 - xw <= 32u * RK_BM_WORDS;   // block-uniform
+    // the bitmap's words over [xw, x1) only (C3: 192 of 2,048)
+    const uint32_t nbw = min((x1 - xw + 31u) >> 5, (uint32_t)RK_BM_WORDS);
+    for (uint32_t t = threadIdx.x; t <= nbw; t += RK_BLK) bm[t] = 0u;
     __syncthreads();
     uint32_t below_k = 0, below_x0 = 0;
     for (uint32_t base = 0; base < m; base += RK_BLK * RK_U) {
@@ -642,7 +644,6 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
             for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < dk[e] ? 1u : 0u;
             ds[lr] = dk[e];
         }
-    if (dest_staged && !dcount) lds_sort(dk, nullptr, nd);
     __syncthreads();
     RK_PROBE(2, wall_clock64());
     RK_PROBE(7, bits_ok ? 1 : 0);
@@ -654,19 +655,15 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
     uint32_t kb0 = kd0;   // the bins' first key
     if (!dest_staged) {
         uint64_t* const mcopy = w.ms + below_k;   // below_k + nd <= m <= cap
-        load_round(0, m - 1u);                    // (m > MV_RK_CAP here)
-        for (uint32_t base = 0; base < m; base += RK_BLK * RK_U) {
-#pragma unroll
-            for (int u = 0; u < RK_U; ++u) {
-                const uint32_t r = base + u * RK_BLK + threadIdx.x, k = ks[u];
-                if (r < m && k >= kd0 && k < kd1) {
-                    const uint32_t j = atomicAdd(&cnt[6], 1u);
-                    if (j < nd) mcopy[j] = comp(k, mv_slot(w, xs[u]));
-                    atomicMax(&cnt[7], k);    // the entries' key span [kmin, kmax]
-                    atomicMax(&cnt[8], ~k);
-                }
+        // (a rare path: plain loops, little code; the kernel's instruction footprint is shared by two CUs)
+        for (uint32_t r = threadIdx.x; r < m; r += RK_BLK) {
+            const uint32_t k = w.mk[r];
+            if (k >= kd0 && k < kd1) {
+                const uint32_t j = atomicAdd(&cnt[6], 1u);
+                if (j < nd) mcopy[j] = comp(k, mv_slot(w, w.mi[r]));
+                atomicMax(&cnt[7], k);    // the entries' key span [kmin, kmax]
+                atomicMax(&cnt[8], ~k);
             }
-            if (base + RK_BLK * RK_U < m) load_round(base + RK_BLK * RK_U, m - 1u);
         }
         for (uint32_t t = threadIdx.x; t < (uint32_t)RK_HBINS; t += RK_BLK) hp[t] = 0u;
         __syncthreads();
@@ -780,23 +777,19 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
             before = uni(hp[ba]);
             ndp = uni(min(hp[bb] - before, (uint32_t)MP_CAP));
             const uint64_t* const mcopy = w.ms + below_k;
-            for (uint32_t t0 = 0; t0 < nd; t0 += RK_BLK * RK_U) {
-                uint64_t e[RK_U];
-#pragma unroll
-                for (int u = 0; u < RK_U; ++u) e[u] = mcopy[min(t0 + u * RK_BLK + threadIdx.x, nd - 1u)];
-#pragma unroll
-                for (int u = 0; u < RK_U; ++u) {
-                    const uint32_t k = (uint32_t)(e[u] >> 32);
-                    if (t0 + u * RK_BLK + threadIdx.x < nd && k >= Ka && k < Kb) {
-                        const uint32_t j = atomicAdd(&cnt[3 + (pass & 1u)], 1u);
-                        if (j < (uint32_t)MP_CAP) dk[j] = e[u];
-                    }
+            for (uint32_t t = threadIdx.x; t < nd; t += RK_BLK) {
+                const uint64_t e = mcopy[t];
+                const uint32_t k = (uint32_t)(e >> 32);
+                if (k >= Ka && k < Kb) {
+                    const uint32_t j = atomicAdd(&cnt[3 + (pass & 1u)], 1u);
+                    if (j < (uint32_t)MP_CAP) dk[j] = e;
                 }
             }
             if (threadIdx.x == 0) cnt[3 + ((pass + 1u) & 1u)] = 0u;   // the next pass's counter (read before the last barrier)
-            lds_sort(dk, nullptr, ndp);   // (its first barrier publishes the staged entries; it ends on a barrier)
             sd = dk;
         }
+        // the sort of the range's entries (more than RK_COUNT) or of this pass's: one call site (its code is long)
+        if (mp || (dest_staged && !dcount)) lds_sort(dk, nullptr, ndp);   // (its first barrier publishes the staged entries)
         if (dest_ok) {
             for (uint32_t t = threadIdx.x; t < ndp; t += RK_BLK) place(dk[t]);   // (multi-pass: sorted)
         } else {
