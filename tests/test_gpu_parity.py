@@ -239,6 +239,53 @@ def test_contact_bit_exact(pkg, oracle, n, steps):
     ctl.OnDestroy()
 
 
+@pytest.mark.parametrize("case", ["outside", "big_radius", "shrink"])
+def test_contact_cell_skipping_edge_states(pkg, oracle, case):
+    """The contact pass skips the cells of its 27 that lie beyond rA/2 + rmax/2 (contact.hip cell_reach / reach_row, r6);
+    the oracle scans all 27 (SimulateParticles.compute:228-233), so any wrongly skipped contact shows as a bit difference.
+    The states where the bound could go wrong: particles far outside the 128-unit grid, clamped into its edge cells
+    (there the per-axis bound only grows), a few of them touching each other there; one radius far above the rest (the
+    bound then skips little); radii shrunk between steps by a range write (the bound must follow on the full sort the
+    write forces, and a too-small stale bound would drop contacts of the grown ones: here the first 1,000 shrink and
+    the next 200 grow). Bit-exact over several steps, the oracle fed in the GPU's slot order."""
+    n = 4096
+    parts = random_sphere(pkg.PARTICLE84, n, seed=77)
+    if case == "outside":
+        rng = np.random.default_rng(3)
+        parts["position"][:200] *= 6.0                                                   # spread far outside the grid
+        parts["position"][200:260] = (-40.0, -40.0, -40.0) + rng.uniform(-1.5, 1.5, (60, 3))   # a clamped cluster
+        parts["position"][260:320] = (60.0, 9.0, -1.0) + rng.uniform(-1.5, 1.5, (60, 3))      # beyond +x, in contact
+    if case == "big_radius":
+        parts["radius"][5] = 12.0
+        parts["mass"][5] = 0.1 * 4.0 / 3.0 * 3.1415926 * 12.0 ** 3
+        parts["momentOfInertia"][5] = 0.4 * parts["mass"][5] * 144.0
+    dt = 0.01
+    ctl = pkg.ParticleSystemController(particleCount=n)
+    ctl.Start(parts)
+    ref = parts.view(oracle.PARTICLE84).copy()
+    order = np.arange(n)
+    for s in range(6):
+        if case == "shrink" and s == 3:
+            cur = ctl.context.get_particles(0, 1200)
+            cur["radius"][:1000] *= np.float32(0.5)
+            cur["radius"][1000:1200] *= np.float32(1.6)
+            ctl.context.set_particles(0, cur)
+            ref_idx = ref.copy()
+            ref_idx["radius"][:1000] *= np.float32(0.5)
+            ref_idx["radius"][1000:1200] *= np.float32(1.6)
+            ref = ref_idx
+        out, tq_slot = oracle.contact_step(oracle.contact_params(dt), ref[order])
+        ref[order] = out
+        tq_ref = np.empty_like(tq_slot)
+        tq_ref[order] = tq_slot
+        ctl.Update(dt)
+        order = ctl.context.sorted_ids()
+    got = ctl.GetParticles()
+    assert np.array_equal(ctl.context.torque_int(), tq_ref), case
+    assert got.tobytes() == ref.tobytes(), case
+    ctl.OnDestroy()
+
+
 def test_contact_drag_and_inactive(pkg, oracle):
     n = 2000
     parts = random_sphere(pkg.PARTICLE84, n, seed=5)
