@@ -58,12 +58,18 @@ int or_sph_step(const or_sph_params* p, int n, float* pos3, float* vel3, int32_t
                 float dt, float t, float* rho, float* prho, uint32_t* cell_start,
                 int nthreads);
 /* or_sph_step plus diagnostics in the sorted order (each optional): acc3 = the pair sum
- * a_i = -Σ m(Pρ_i + Pρ_j + Π_ij)F(r)x_ij (no gravity / forcing); mag3 = the error scales the GPU parity
+ * a_i = -Σ m(Pρ_i + Pρ_j + Π_ij)F(r)x_ij (no gravity / forcing); mag5 = the error scales the GPU parity
  * tests normalise by: Σ m|F|r(|Pρ_i| + |Pρ_j| + |Π_ij|) (the acceleration terms before they cancel),
  * Σ|pair XSPH term|, and Σ m|F|r(E_i + E_j) with E = (B/ρ²)(5(ρ/ρ0)^7 + 2) (the acceleration's change
- * per unit relative error of the densities: the stiff Tait EOS amplifies pass-1 rounding). */
+ * per unit relative error of the densities: the stiff Tait EOS amplifies pass-1 rounding); then the two support-edge
+ * conditioning terms OR_DIAG_DQ bounds: Σ_{q>=1} 2·m|F|r(|Pρ_i| + |Pρ_j| + |Π_ij|)·δq/(2 − q) and
+ * Σ_{q>=1} 3|pair XSPH term|·δq/(2 − q). For q >= 1 a pair's F·r is ∝ (2 − q)² and its W ∝ (2 − q)³, so two
+ * evaluations whose q differ by δq (r² by an fma chain or by plain products, r by rsq or sqrt: a few ulp of q) differ
+ * in the term by 2δq/(2 − q), 3δq/(2 − q) of it, which grows without bound at the support edge.
+ * mag5 holds five floats per particle. */
+#define OR_DIAG_DQ (1.0 / 2097152.0) /* δq = 2^-21: four ulp of q in [1, 2) */
 int or_sph_step_diag(const or_sph_params* p, int n, float* pos3, float* vel3, int32_t* id, float dt, float t,
-                     float* rho, float* prho, uint32_t* cell_start, float* acc3, float* mag3, int nthreads);
+                     float* rho, float* prho, uint32_t* cell_start, float* acc3, float* mag5, int nthreads);
 /* Phases of or_sph_step over sorted arrays (sk = sorted keys, cs = cell start), used by the
  * slab-decomposition tests: targets [i0, i1); neighbours may be any sorted slot (ghosts). */
 void or_sph_density_range(const or_sph_params* p, const float* pos3, const uint32_t* sk, const uint32_t* cs,
@@ -71,10 +77,10 @@ void or_sph_density_range(const or_sph_params* p, const float* pos3, const uint3
 void or_sph_force_range(const or_sph_params* p, const float* pos3, const float* vel3, const float* rho,
                         const float* prho, const uint32_t* sk, const uint32_t* cs, int i0, int i1, float dt,
                         float t, float* pos_out, float* vel_out, int nthreads);
-/* or_sph_force_range with the diagnostics of or_sph_step_diag (acc3, mag3 at the target's slot) */
+/* or_sph_force_range with the diagnostics of or_sph_step_diag (acc3, mag5 at the target's slot) */
 void or_sph_force_range_diag(const or_sph_params* p, const float* pos3, const float* vel3, const float* rho,
                              const float* prho, const uint32_t* sk, const uint32_t* cs, int i0, int i1, float dt,
-                             float t, float* pos_out, float* vel_out, float* acc3, float* mag3, int nthreads);
+                             float t, float* pos_out, float* vel_out, float* acc3, float* mag5, int nthreads);
 /* Dam-break lattice init (SPEC_SPH.md; the same integer hash as the device init). */
 void or_sph_lattice(int dim, int nx, int ny, int nz, float dx, float x0, float y0, float z0,
                     uint32_t seed, float jitter, float* pos3);

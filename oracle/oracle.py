@@ -147,7 +147,8 @@ def sph_step(p: OrSphParams, pos, vel, ids, dt, t=0.0, nthreads=0):
 
 def sph_step_diag(p: OrSphParams, pos, vel, ids, dt, t=0.0, nthreads=0):
     """sph_step plus, in the same sorted order, acc (n,3): the pair sum a_i without gravity or
-    forcing, and mag (n,2): Σ|pair acceleration term| and Σ|pair XSPH term| (error scales).
+    forcing, and mag (n,5): Σ|pair acceleration term|, Σ|pair XSPH term|, the EOS sensitivity and the
+    two support-edge conditioning terms (error scales, oracle.h or_sph_step_diag).
     Returns (pos, vel, ids, rho, prho, cell_start, acc, mag)."""
     pos = np.ascontiguousarray(pos, dtype=np.float32).copy()
     vel = np.ascontiguousarray(vel, dtype=np.float32).copy()
@@ -157,7 +158,7 @@ def sph_step_diag(p: OrSphParams, pos, vel, ids, dt, t=0.0, nthreads=0):
     prho = np.empty(n, np.float32)
     cs = np.empty(ncells(p) + 1, np.uint32)
     acc = np.empty((n, 3), np.float32)
-    mag = np.empty((n, 3), np.float32)
+    mag = np.empty((n, 5), np.float32)
     lib().or_sph_step_diag(C.byref(p), n, _ptr(pos), _ptr(vel), _ptr(ids), dt, t, _ptr(rho), _ptr(prho),
                            _ptr(cs), _ptr(acc), _ptr(mag), nthreads)
     return pos, vel, ids, rho, prho, cs, acc, mag
@@ -175,7 +176,7 @@ def force_range_diag(p: OrSphParams, pos, vel, rho, prho, sk, cs, dt, t=0.0, nth
     n = pos.shape[0]
     po, vo = np.empty_like(pos), np.empty_like(vel)
     acc = np.empty((n, 3), np.float32)
-    mag = np.empty((n, 3), np.float32)
+    mag = np.empty((n, 5), np.float32)
     lib().or_sph_force_range_diag(C.byref(p), _ptr(pos), _ptr(vel), _ptr(rho), _ptr(prho), _ptr(sk), _ptr(cs), 0, n,
                                   dt, t, _ptr(po), _ptr(vo), _ptr(acc), _ptr(mag), nthreads)
     return po, vo, acc, mag

@@ -197,7 +197,7 @@ static inline double eos_sens(const or_sph_params* p, float rho) {
  * Reads p2/v2/rho/prho (all sorted slots, ghosts included), writes pos_out/vel_out[i]. */
 static void force_range_impl(const or_sph_params* p, const float* p2, const float* v2, const float* rho,
                              const float* prho, const uint32_t* sk, const uint32_t* cs, int i0, int i1, float dt,
-                             float t, float* pos_out, float* vel_out, float* acc3, float* mag3, int nthreads) {
+                             float t, float* pos_out, float* vel_out, float* acc3, float* mag5, int nthreads) {
     const or_grid* g = &p->grid;
     const float m = p->mass, four_h2 = p->four_h2;
     const float h = p->h, eta2 = 0.01f * h * h, ac0 = p->alpha * p->c0, eps = p->eps_xsph;
@@ -217,9 +217,10 @@ static void force_range_impl(const or_sph_params* p, const float* p2, const floa
         float ax = 0, ay = 0, az = 0, sx = 0, sy = 0, sz = 0;
         /* diagnostics: am = Σ m|F|r(|Pρ_i| + |Pρ_j| + |Π_ij|), the pressure and viscous pair terms before they
          * cancel; sm = Σ|pair XSPH term|; em = Σ m|F|r(E_i + E_j), E = |dPρ/dρ|·ρ = (B/ρ²)(5(ρ/ρ0)^7 + 2): the
-         * acceleration change per unit relative density error of both ends (Tait EOS sensitivity) */
-        double am = 0.0, sm = 0.0, em = 0.0;
-        const double Ei = mag3 ? eos_sens(p, rhoi) : 0.0;
+         * acceleration change per unit relative density error of both ends (Tait EOS sensitivity); qa, qs: the
+         * support-edge conditioning of am's and sm's terms (oracle.h, OR_DIAG_DQ) */
+        double am = 0.0, sm = 0.0, em = 0.0, qa = 0.0, qs = 0.0;
+        const double Ei = mag5 ? eos_sens(p, rhoi) : 0.0;
         for (int r = 0; r < nr; ++r)
             for (uint32_t j = rg[r][0]; j < rg[r][1]; ++j) {
                 if ((int)j == i) continue;
@@ -240,15 +241,26 @@ static void force_range_impl(const or_sph_params* p, const float* p2, const floa
                 ax += c * ddx; ay += c * ddy; az += c * ddz;
                 float cx = eps * m / rbar * W;
                 sx -= cx * du; sy -= cx * dv; sz -= cx * dw;
-                if (mag3) {
+                if (mag5) {
                     const double mfr = (double)m * fabs((double)F) * sqrt((double)r2);
-                    am += mfr * (fabs((double)pri) + fabs((double)prho[j]) + fabs((double)pi_ij));
-                    sm += fabs((double)cx) * sqrt((double)du * du + (double)dv * dv + (double)dw * dw);
+                    const double ta = mfr * (fabs((double)pri) + fabs((double)prho[j]) + fabs((double)pi_ij));
+                    const double ts = fabs((double)cx) * sqrt((double)du * du + (double)dv * dv + (double)dw * dw);
+                    am += ta;
+                    sm += ts;
                     em += mfr * (Ei + eos_sens(p, rho[j]));
+                    const double qd = sqrt((double)r2) * (double)p->inv_h;
+                    if (qd >= 1.0) {
+                        const double te = fmax(2.0 - qd, 1e-12);
+                        qa += 2.0 * ta * OR_DIAG_DQ / te;
+                        qs += 3.0 * ts * OR_DIAG_DQ / te;
+                    }
                 }
             }
         if (acc3) { acc3[3 * (size_t)i] = ax; acc3[3 * (size_t)i + 1] = ay; acc3[3 * (size_t)i + 2] = az; }
-        if (mag3) { mag3[3 * (size_t)i] = (float)am; mag3[3 * (size_t)i + 1] = (float)sm; mag3[3 * (size_t)i + 2] = (float)em; }
+        if (mag5) {
+            float* o = mag5 + 5 * (size_t)i;
+            o[0] = (float)am; o[1] = (float)sm; o[2] = (float)em; o[3] = (float)qa; o[4] = (float)qs;
+        }
         float nu = ui + (ax + p->g[0] + fx) * dt;
         float nv = vi + (ay + p->g[1]) * dt;
         float nw = wi + (az + p->g[2]) * dt;
@@ -272,8 +284,8 @@ void or_sph_force_range(const or_sph_params* p, const float* p2, const float* v2
 
 void or_sph_force_range_diag(const or_sph_params* p, const float* p2, const float* v2, const float* rho,
                              const float* prho, const uint32_t* sk, const uint32_t* cs, int i0, int i1, float dt,
-                             float t, float* pos_out, float* vel_out, float* acc3, float* mag3, int nthreads) {
-    force_range_impl(p, p2, v2, rho, prho, sk, cs, i0, i1, dt, t, pos_out, vel_out, acc3, mag3, nthreads);
+                             float t, float* pos_out, float* vel_out, float* acc3, float* mag5, int nthreads) {
+    force_range_impl(p, p2, v2, rho, prho, sk, cs, i0, i1, dt, t, pos_out, vel_out, acc3, mag5, nthreads);
 }
 
 int or_sph_step(const or_sph_params* p, int n, float* pos, float* vel, int32_t* id,
@@ -282,7 +294,7 @@ int or_sph_step(const or_sph_params* p, int n, float* pos, float* vel, int32_t* 
 }
 
 int or_sph_step_diag(const or_sph_params* p, int n, float* pos, float* vel, int32_t* id, float dt, float t,
-                     float* rho_out, float* prho_out, uint32_t* cs_out, float* acc3, float* mag3, int nthreads) {
+                     float* rho_out, float* prho_out, uint32_t* cs_out, float* acc3, float* mag5, int nthreads) {
     const or_grid* g = &p->grid;
     uint32_t nk = (uint32_t)g->G[0] * (uint32_t)g->xsub * (uint32_t)g->G[1] * (uint32_t)g->G[2];
     size_t nn = (size_t)(n > 0 ? n : 1);
@@ -307,7 +319,7 @@ int or_sph_step_diag(const or_sph_params* p, int n, float* pos, float* vel, int3
     }
     or_cell_start(n, sk, nk, cs);
     or_sph_density_range(p, p2, sk, cs, 0, n, rho, prho, nthreads);
-    force_range_impl(p, p2, v2, rho, prho, sk, cs, 0, n, dt, t, pos, vel, acc3, mag3, nthreads);
+    force_range_impl(p, p2, v2, rho, prho, sk, cs, 0, n, dt, t, pos, vel, acc3, mag5, nthreads);
     memcpy(id, id2, sizeof(int32_t) * (size_t)n);
     if (rho_out) memcpy(rho_out, rho, sizeof(float) * (size_t)n);
     if (prho_out) memcpy(prho_out, prho, sizeof(float) * (size_t)n);

@@ -187,6 +187,32 @@ def test_sph_pair_momentum_and_kernel(oracle):
     assert vo[order][0][0] == pytest.approx(a0 * dt, rel=1e-4)
 
 
+def test_sph_diag_support_edge_conditioning(oracle):
+    """The diagnostics' conditioning columns (oracle.h or_sph_step_diag): a pair at q = 1.99 has
+    Q = 2·S·δq/(2 − q) and Q_x = 3·(XSPH scale)·δq/(2 − q) with δq = 2^-21, and a pair at q < 1 has none; the
+    rounding of q by that δq moves the pair's acceleration term by at most Q (finite difference, float64)."""
+    O = oracle
+    p = _sph(O)
+    p.g[1] = 0.0
+    h = 0.012
+    dq = 2.0 ** -21
+    for q, cond in ((1.99, True), (0.7, False)):
+        x = np.array([[0.5, 0.5, 0.5], [0.5 + q * h, 0.5, 0.5]], np.float32)
+        v = np.array([[0.0, 0.0, 0.0], [0.0, 0.3, 0.0]], np.float32)
+        *_, mag = O.sph_step_diag(p, x, v, np.array([0, 1], np.int32), 1e-5)
+        assert mag.shape == (2, 5)
+        for k in range(2):
+            S, Sx, _, Q, Qx = (float(c) for c in mag[k])
+            if cond:
+                t = 2.0 - float(np.sqrt(np.float64((x[1, 0] - x[0, 0]) ** 2))) / float(np.float32(h))
+                assert Q == pytest.approx(2 * S * dq / t, rel=1e-5)
+                assert Qx == pytest.approx(3 * Sx * dq / t, rel=1e-5)
+                # the pair term is ∝ t²: a q moved by dq moves it by ≈ 2·dq/t of itself
+                assert abs((t - dq) ** 2 - t ** 2) / t ** 2 * S <= Q * (1 + 1e-3)
+            else:
+                assert Q == 0.0 and Qx == 0.0
+
+
 def test_sph_walls_clamp_and_restitution(oracle):
     O = oracle
     p = _sph(O, L=(1.0, 1.0, 1.0))
