@@ -29,7 +29,7 @@ ctl = pkg.ParticleSystemController(particleCount=a.n)
 ctl.Start(sphere(pkg, a.n))
 ctl.context.step(0.01, 20)
 ctl.context.synchronize()
-W = 24
+W = 32
 buf = (C.c_uint64 * (256 * W))()
 acc = []
 L_count = []
@@ -47,11 +47,13 @@ for s in range(a.steps):
     wv = p[:, 8:24].max(1)
     acc.append([(p[:, 1] - p[:, 0]).mean(), (wv - p[:, 1]).mean(), (p[:, 2] - wv).mean(), (p[:, 3] - p[:, 2]).mean(),
                 p[:, 3].max() - t0, (p[:, 0] - t0).max(), (p[:, 8:24] - p[:, 1:2]).mean(),
-                (p[:, 4] - p[:, 0]).mean(), (p[:, 5] - p[:, 4]).mean(), (p[:, 6] - p[:, 5]).mean(), (p[:, 1] - p[:, 6]).mean()])
+                (p[:, 4] - p[:, 0]).mean(), (p[:, 5] - p[:, 4]).mean(), (p[:, 6] - p[:, 5]).mean(), (p[:, 1] - p[:, 6]).mean(),
+                (p[:, 24] - p[:, 2]).mean(), (p[:, 25] - p[:, 24]).mean(), (p[:, 3] - p[:, 25]).mean()])
 m = np.mean(acc, 0) / 100.0   # 100 MHz ticks -> us
 print({"n": a.n, "steps": a.steps, "build_us": round(m[0], 2), "sums_slowest_wave_us": round(m[1], 2),
        "sums_mean_wave_us": round(m[6], 2), "barrier_us": round(m[2], 2), "finish_us": round(m[3], 2),
        "span_us": round(m[4], 2), "last_start_us": round(m[5], 2), "build_loads_us": round(m[7], 2),
        "build_sort_us": round(m[8], 2), "build_prefix_dst_us": round(m[9], 2), "build_table_us": round(m[10], 2),
+       "finish_math_us": round(m[11], 2), "finish_stores_us": round(m[12], 2), "finish_append_us": round(m[13], 2),
        "movers_mean": round(float(np.mean(L_count)), 1) if L_count else None}, flush=True)
 ctl.OnDestroy()

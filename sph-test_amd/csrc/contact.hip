@@ -20,7 +20,7 @@
 #ifdef SPH_CONTACT_PROBE
 namespace sph { extern __device__ uint64_t g_ct_probe[]; }
 #define FZ_PROBE(slot) \
-    do { if (threadIdx.x == 0 && blockIdx.x < 256) sph::g_ct_probe[blockIdx.x * 24 + (slot)] = wall_clock64(); } while (0)
+    do { if (threadIdx.x == 0 && blockIdx.x < 256) sph::g_ct_probe[blockIdx.x * 32 + (slot)] = wall_clock64(); } while (0)
 #endif
 #include "bonds.h"
 #include "common.h"
@@ -664,11 +664,12 @@ constexpr int FZ_BLK = 1024;   // 16 targets (one per wave) per workgroup: the p
 constexpr int FZ_T = FZ_BLK / 64;
 
 // Test-only timing probe (scripts/contact_probe.py, a -DSPH_CONTACT_PROBE build): per workgroup the wall clock (100 MHz)
-// at its start, after the permutation build, after the barrier and at its end, and each wave's end of its neighbour sums.
+// at its start, after the permutation build, after the barrier and at its end, each wave's end of its neighbour sums
+// (8-23), and in the finish: after its arithmetic (24) and after its plain stores, before the mover append (25).
 #ifdef SPH_CONTACT_PROBE
-constexpr int CT_PROBE_W = 24;
-__device__ uint64_t g_ct_probe[256 * 24];
-static_assert(CT_PROBE_W == 24, "FZ_PROBE's stride");
+constexpr int CT_PROBE_W = 32;
+__device__ uint64_t g_ct_probe[256 * 32];
+static_assert(CT_PROBE_W == 32, "FZ_PROBE's stride");
 #define CT_PROBE(cond, slot)                                                                               \
     do {                                                                                                   \
         if ((cond) && blockIdx.x < 256) g_ct_probe[blockIdx.x * CT_PROBE_W + (slot)] = wall_clock64();    \
@@ -749,6 +750,7 @@ __global__ __launch_bounds__(FZ_BLK) void k_contact_fused(FusedIO io, int32_t n_
         contact_finish(c, f.id, pa, f.v, f.w, va.w, wa.w, f.aux.x, f.rot, f.tq, p, v, w, q);
         key_n = cell_key(g, p.x, p.y, p.z);
     }
+    CT_PROBE(threadIdx.x == 0, 24);
     io.pos_o[a] = a >= n_active ? pa : make_float4(p.x, p.y, p.z, pa.w);
     io.vel_o[a] = make_float4(v.x, v.y, v.z, va.w);
     io.omg_o[a] = a >= n_active ? wa : make_float4(w.x, w.y, w.z, wa.w);
@@ -762,6 +764,7 @@ __global__ __launch_bounds__(FZ_BLK) void k_contact_fused(FusedIO io, int32_t n_
     }
     io.sk_o[a] = key_a;
     io.keys_o[a] = key_n;
+    CT_PROBE(threadIdx.x == 0, 25);
     if (key_n != key_a) {   // a mover of the next step's re-sort
         const uint32_t r = atomicAdd(io.count_o, 1u);
         if (r < io.cap) {
