@@ -167,3 +167,28 @@ def test_launcher_reports_a_failed_rank(tmp_path):
     assert r.returncode == 5, (r.stdout, r.stderr)
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["value"] is None and line["n_gpus"] == 2 and [1, 5] in line["failed_ranks"]
+
+
+def test_kernel_sum_check_flags_a_step_the_samples_miss():
+    """verdict r5 item 2: the sampled kernels' sum against the GPU events; within 5% no note, beyond it a note that
+    names the gap (the r5 C5 line read 4.37 ms of kernels against 7.75 ms of events)."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    ok = bench.kernel_sum_check({"density": 0.115, "force_integrate": 0.165, "resort": 0.030}, 0.3125, 16)
+    assert ok["kernels_sum_ms_per_step"] == pytest.approx(0.31) and "kernels_note" not in ok
+    assert ok["kernels_sum_over_gpu_event"] == pytest.approx(0.31 / 0.3125, abs=1e-4)
+    bad = bench.kernel_sum_check({"density": 1.55, "force_integrate": 2.27, "resort": 0.55}, 7.75, 16)
+    assert bad["kernels_sum_over_gpu_event"] == pytest.approx(4.37 / 7.75, abs=1e-4)
+    assert "+43.6%" in bad["kernels_note"] and "one step in 16" in bad["kernels_note"]
+    assert bench.kernel_sum_check({"a": 1.0}, 0.0, 16)["kernels_sum_over_gpu_event"] is None
+
+
+def test_resort_counts_dict_names_the_library_words():
+    """sph_read_resort_counts' eight words (include/sphhip.h) into the bench line's names, in the ABI's order."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    d = bench.resort_counts_dict([3, 5, 7, 11, 13, 17, 0, 0])
+    assert d == {"whole_list_ranges": 3, "whole_list_lanes": 5, "multi_pass_ranges": 7, "passes": 11,
+                 "max_range_entries": 13, "share_restreams": 17}
+    hdr = (ROOT / "include" / "sphhip.h").read_text()
+    assert "sph_read_resort_counts" in hdr
