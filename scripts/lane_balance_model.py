@@ -14,7 +14,9 @@ the target itself included, as the mask walk visits them) and prices the walk's 
       result does not depend on the block partition): 32 targets per wave, trips = max over lanes of the halves;
   S3  the wave's hits dealt out as 4-hit chunks of one target each (chunk boundaries fixed by the target alone, chunk
       sums added in order by the owner): trips = ceil(chunks / 64) per wave and plane, before any cost of the
-      hand-out (target state by ds_bpermute, the k-th set bit, the chunk sums through LDS).
+      hand-out (target state by ds_bpermute, the k-th set bit, the chunk sums through LDS);
+  S4  (r6) the workgroup's 256 targets dealt to its four waves in order of their hit counts (total, centre plane, or
+      4-hit trips), so a wave's lanes need similar trip counts; a target's sums stay on one lane in visit order.
 
 busy = useful hit-slots / issued lane-slots (64 x 4 per trip). The product's measured figure (SPH_DIAG counters,
 scripts/pass_util.py) is 66-71 % from rest; S0 should reproduce it.
@@ -77,6 +79,18 @@ def main():
     s2 = 64 * 4 * c4(h2).max(axis=1).sum()
     chunks = c4(w).sum(axis=1)                             # [wave, plane] 4-hit chunks
     s3 = 64 * 4 * (-(-chunks // 64)).sum()
+    # S4: the block's 256 targets re-dealt to lanes by hit count (a permutation inside the workgroup; each target's sums
+    # stay on one lane in visit order, so the results keep every bit): waves of 64 consecutive in the sorted order
+    nb = n // 256
+    blk = hp[: nb * 256].reshape(nb, 256, 3)
+    def s4(key):
+        o = np.argsort(key(blk), axis=1, kind="stable")
+        srt = np.take_along_axis(blk, o[:, :, None], axis=1).reshape(nb * 4, 64, 3)
+        return 64 * 4 * c4(srt).max(axis=1).sum(), int(srt.sum())
+    s4t, u4 = s4(lambda b: b.sum(axis=2))
+    s4c, _ = s4(lambda b: b[:, :, 1] * 1000 + b[:, :, 0] + b[:, :, 2])
+    s4q, _ = s4(lambda b: c4(b).sum(axis=2) * 1000 + b[:, :, 1])
+    s0b = 64 * 4 * c4(blk.reshape(nb * 4, 64, 3)).max(axis=1).sum()
     per_t = hp.sum(axis=1)
     out = {"config": args.config, "state": args.npz or "lattice", "particles": n, "h": h,
            "hits_per_target_mean": round(float(per_t.mean()), 2),
@@ -84,6 +98,8 @@ def main():
            "busy_S0_product": round(float(useful) / s0, 4), "busy_S1_three_planes": round(float(useful) / s1, 4),
            "busy_S1b_side_planes_together": round(float(useful) / s1b, 4),
            "busy_S2_two_lanes_per_target": round(float(useful) / s2, 4), "busy_S3_chunks_before_overhead": round(float(useful) / s3, 4),
+           "busy_S4_sorted_by_hits": round(u4 / s4t, 4), "busy_S4_sorted_by_centre_plane": round(u4 / s4c, 4),
+           "busy_S4_sorted_by_trips": round(u4 / s4q, 4), "walk_slots_S4_vs_S0": round(float(min(s4t, s4c, s4q)) / s0b, 4),
            "walk_slots_vs_S0": {"S1": round(float(s1) / s0, 4), "S1b": round(float(s1b) / s0, 4), "S2": round(float(s2) / s0, 4), "S3": round(float(s3) / s0, 4)}}
     print(out, flush=True)
 
