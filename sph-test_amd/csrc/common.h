@@ -64,6 +64,17 @@ struct ContactConst {
 constexpr int SDEV_RMAX = 15;   // sph_ctx::sdev word holding ContactConst::rmax (Model R)
 
 #if defined(__HIPCC__)
+// A word another launch wrote (a count, a range key), read through the vector memory path with the default cache policy.
+// A uniform address otherwise becomes a scalar load, and the wait for the kernel arguments' scalar loads (lgkmcnt,
+// which cannot tell them apart) then also waits for it: the loads that follow issued one memory round trip late.
+// The zero offset comes from a VGPR the compiler cannot see through (vzero; one for several loads keeps them together).
+__device__ __forceinline__ uint32_t vzero() {
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
+__device__ __forceinline__ uint32_t ld_vec(const uint32_t* p) { return p[vzero()]; }
+
 __device__ __forceinline__ int32_t cell_coord(float x, float o, float inv, int32_t G) {
     // GetGridCoord (compute:102-105): (uint)((p - origin) * inv) with ftou (neg/NaN -> 0), clamp
     float g = (x - o) * inv;
@@ -732,6 +743,10 @@ struct FusedIO {
     uint32_t *sk_o, *keys_o, *cs_o;
     uint32_t *mi_o, *mk_o, *mo_o, *count_o, *count_zero, *host_count;
     uint32_t cap;
+    // (cs[k], cs[k + 1]) of each mover's new key k as the step before computed it, or ~0: that step's own table (null:
+    // the build loads them); mc_o: this step's, for the next (fused_perm.h)
+    const uint32_t* mc;
+    uint32_t* mc_o;
 };
 int32_t contact_fused_max();
 // Model S's counterpart (wcsph_tiled.hip k_density_fused): re-sort + pass 1 in one launch, then k_force_small

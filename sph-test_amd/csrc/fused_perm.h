@@ -66,20 +66,29 @@ struct FusedLds {
     uint32_t pm[FZ_N];
 };
 
-// the bitmap's exclusive word prefix (nw <= FZ_WORDS words) by one wave, lane t
+// the bitmap's exclusive word prefix (nw <= FZ_WORDS words) by one wave, lane t: WPW consecutive words per lane and one
+// scan over the wave (each shuffle step is a cross-lane round trip; r6: three dependent 64-word scans took ~0.4 us)
+constexpr uint32_t WPW = (FZ_WORDS + 63) / 64;
 __device__ __forceinline__ void word_prefix(const uint32_t* bm, uint32_t* bpre, uint32_t nw, uint32_t lane) {
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < nw; base += 64) {
-        const uint32_t t = base + lane;
-        const uint32_t v = t < nw ? (uint32_t)__popc(bm[t]) : 0u;
-        uint32_t inc = v;
+    uint32_t c[WPW], mine = 0;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
-            if (lane >= (uint32_t)o) inc += u;
-        }
-        if (t < nw) bpre[t] = carry + inc - v;
-        carry += (uint32_t)__shfl((int)inc, 63, 64);
+    for (uint32_t j = 0; j < WPW; ++j) {
+        const uint32_t t = lane * WPW + j;
+        c[j] = t < nw ? (uint32_t)__popc(bm[t]) : 0u;
+        mine += c[j];
+    }
+    uint32_t inc = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
+        if (lane >= (uint32_t)o) inc += u;
+    }
+    uint32_t run = inc - mine;
+#pragma unroll
+    for (uint32_t j = 0; j < WPW; ++j) {
+        const uint32_t t = lane * WPW + j;
+        if (t < nw) bpre[t] = run;
+        run += c[j];
     }
 }
 
@@ -92,13 +101,15 @@ __device__ FusedMap fused_build(FusedLds& L, const uint32_t* __restrict__ count,
     uint32_t* bm = L.bm;
     uint32_t* bpre = L.bpre;
     uint32_t* pm = L.pm;
-    // the count and the first BLK movers' entries in one round trip (the lists hold n entries: in bounds)
-    const uint32_t m_raw = *count;
+    // the count and the first BLK movers' entries in one round trip (the lists hold n entries: in bounds). The entries
+    // are loaded first and the count after them through the vector path (ld_vec): as a scalar load, the count held the
+    // entries' loads back by one round trip
     uint32_t x0 = 0u, k0 = 0u;
     if (threadIdx.x < (uint32_t)n) {
         x0 = mi[threadIdx.x];
         k0 = mk[threadIdx.x];
     }
+    const uint32_t m_raw = ld_vec(count);
     const uint32_t nw = ((uint32_t)n >> 5) + 1u;
     for (uint32_t t = threadIdx.x; t < nw; t += BLK) bm[t] = 0u;
     const uint32_t m = min(m_raw, (uint32_t)n);
@@ -131,7 +142,16 @@ __device__ FusedMap fused_build(FusedLds& L, const uint32_t* __restrict__ count,
         uint32_t rk = 0;
         if (threadIdx.x < m) {
             e = ms[threadIdx.x];
-            for (uint32_t f = 0; f < m; ++f) rk += ms[f] < e ? 1u : 0u;
+            // eight LDS reads in flight per round: one at a time, the count waited on LDS latency (~m x 70 cycles)
+            uint32_t f = 0;
+            for (; f + 8u <= m; f += 8u) {
+                uint64_t t[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) t[u] = ms[f + (uint32_t)u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) rk += t[u] < e ? 1u : 0u;
+            }
+            for (; f < m; ++f) rk += ms[f] < e ? 1u : 0u;
         }
         __syncthreads();
         if (threadIdx.x < m) {

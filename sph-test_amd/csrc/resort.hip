@@ -187,6 +187,7 @@ static_assert(4 * RK_SUB + 2 * RK_SHARE_KEYS <= 8 * RK_POOL_U64 && RK_SUB * RK_S
               4 * RK_DIRECT <= 8 * RK_POOL_U64 && RK_DIRECT <= 16u * 1024u,
               "a share's LDS fits the pool; its cell offsets fit 16 bits; a direct share's prefix fits 16 cells per lane");
 constexpr int RK_CU = 4;            // cells per lane in flight
+constexpr int RK_CNT_U = 4;         // dest entries per counting round in flight (LDS reads)
 static_assert(2 * MV_RK_CAP * 8 + 4 * (RK_KD1_CAP + 2 * (RK_BM_WORDS + 1) + RK_HBINS + 1) <= RK_POOL_U64 * 8,
               "a range's LDS fits the pool");
 // ResortScratch.stats words (sph_read_resort_counts): ranges that counted against the whole mover list, lanes whose
@@ -321,7 +322,7 @@ __device__ void mv_cells_direct(uint32_t cb, uint32_t Gc, const uint32_t* __rest
         }
     };
     load_round(0, w.cap - 1u);
-    const uint32_t m = uni(*mtotal);
+    const uint32_t m = uni(ld_vec(mtotal));
     for (uint32_t t = threadIdx.x; t < L; t += RK_BLK) diff[t] = 0;
     __syncthreads();
     uint32_t bn_c = 0, bo_c = 0;
@@ -401,7 +402,7 @@ __device__ void mv_cells_staged(uint32_t cb, uint32_t Gc, const uint32_t* __rest
         }
     };
     load_round(0, w.cap - 1u);
-    const uint32_t m = uni(*mtotal);
+    const uint32_t m = uni(ld_vec(mtotal));
     __syncthreads();   // cnt zeroed
     // cells [c0 + a, c0 + b) of the share changed by key k: k + 1 − c0 in [a, b)
     auto in_share = [&](uint32_t k, uint32_t a, uint32_t b) { return k >= c0 && k + 1u < c1 && k + 1u - c0 >= a && k + 1u - c0 < b; };
@@ -557,8 +558,12 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
         }
     };
     load_round(0, w.cap - 1u);
-    const uint32_t m = *mtotal;
-    const uint32_t sk0 = uni(*sk_ptr(x0)), sk1 = uni(*sk_ptr(x1));
+    // the count and the range keys through the vector path behind the movers' loads (ld_vec), all in one round trip
+    // (as scalar loads, the wait for the kernel arguments also waited for them before the movers' loads could issue)
+    const uint32_t z = vzero();
+    const uint32_t skv0 = sk_ptr(x0)[z], skv1 = sk_ptr(x1)[z], mv = mtotal[z];
+    asm volatile("" ::"v"(skv0), "v"(skv1), "v"(mv));   // issued here, not sunk into the blocks that use them
+    const uint32_t m = uni(mv), sk0 = uni(skv0), sk1 = uni(skv1);
     if (b == 0 && threadIdx.x == 0) {
         *next_count = 0u;
         if (w.host_count) *w.host_count = m;   // for the host's next sort choices (no copy launch)
@@ -640,9 +645,18 @@ __global__ __launch_bounds__(RK_BLK, 8) void k_mv_rank(const uint32_t* __restric
     const bool dcount = nd <= (uint32_t)RK_COUNT;
     if (dest_staged && dcount)
         for (uint32_t e = threadIdx.x; e < nd; e += RK_BLK) {
-            uint32_t lr = 0;
-            for (uint32_t f = 0; f < nd; ++f) lr += dk[f] < dk[e] ? 1u : 0u;
-            ds[lr] = dk[e];
+            const uint64_t me = dk[e];
+            uint32_t lr = 0, f = 0;
+            // RK_CNT_U reads in flight per round (one at a time, the count waited on LDS latency per entry)
+            for (; f + (uint32_t)RK_CNT_U <= nd; f += (uint32_t)RK_CNT_U) {
+                uint64_t t[RK_CNT_U];
+#pragma unroll
+                for (int u = 0; u < RK_CNT_U; ++u) t[u] = dk[f + (uint32_t)u];
+#pragma unroll
+                for (int u = 0; u < RK_CNT_U; ++u) lr += t[u] < me ? 1u : 0u;
+            }
+            for (; f < nd; ++f) lr += dk[f] < me ? 1u : 0u;
+            ds[lr] = me;
         }
     __syncthreads();
     RK_PROBE(2, wall_clock64());
