@@ -60,6 +60,9 @@ struct ContactConst {
     // device word: an upper bound of every radius (float bits, k_keys on the full sort after any change of the
     // particles; +inf until then). The contact pass skips the cells of its 27 that lie beyond rA/2 + rmax/2. null: none
     const uint32_t* rmax = nullptr;
+    // its value, read by each contact kernel at its start with its first loads (contact.hip rmax_load): read where the
+    // cell reach is computed, the load waited one more memory round trip in every target's chain
+    float rmv = __builtin_inff();
 };
 constexpr int SDEV_RMAX = 15;   // sph_ctx::sdev word holding ContactConst::rmax (Model R)
 

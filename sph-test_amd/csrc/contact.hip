@@ -89,14 +89,17 @@ __device__ __forceinline__ int contact_pair(const ContactConst& c, const Body& A
 struct CellReach {
     float fx, fy, fz, r2;   // r2: the squared bound in cell units (+inf: no skipping)
 };
+// ContactConst::rmv from the device word (a contact kernel's first statement, so the load joins its first round trip)
+__device__ __forceinline__ void rmax_load(ContactConst& c) {
+    c.rmv = c.rmax ? __uint_as_float(ld_vec(c.rmax)) : __builtin_inff();
+}
 __device__ __forceinline__ CellReach cell_reach(const GridDesc& g, const ContactConst& c, float4 pa, int32_t cx, int32_t cy,
                                                 int32_t cz) {
     CellReach q;
     q.fx = (pa.x - g.ox) * g.inv_cell - (float)cx;
     q.fy = (pa.y - g.oy) * g.inv_cell - (float)cy;
     q.fz = (pa.z - g.oz) * g.inv_cz - (float)cz;
-    const float rm = c.rmax ? __uint_as_float(*c.rmax) : __builtin_inff();
-    const float reach = 0.5f * pa.w + 0.5f * rm;
+    const float reach = 0.5f * pa.w + 0.5f * c.rmv;
     const float b = (reach * 1.001f + 0.001f) * g.inv_cell;
     q.r2 = (reach >= 0.0f && reach < 1e30f && g.inv_cell == g.inv_cz) ? b * b : __builtin_inff();
     return q;
@@ -505,6 +508,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step(
     float4* __restrict__ rot_o, int32_t* __restrict__ torque_o, uint32_t* __restrict__ keys_o, MoverSink mv) {
     const int32_t a = blockIdx.x * CT_BLK + threadIdx.x;
     if (a >= n) return;
+    rmax_load(c);
     const float4 pa = pos[a], va = vel[a], wa = omg[a], qa = rot[a];
     if (a >= n_active) {   // inactive slots (id >= activeParticleCount): drag only
         const f3 v = apply_drag(c, id[a], xyz(pa), xyz(va), va.w);
@@ -543,6 +547,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_step_team(
     const int32_t a = blockIdx.x * (CT_BLK / L) + (int32_t)(threadIdx.x / L);
     const bool lead = (threadIdx.x & (L - 1)) == 0;
     if (a >= n) return;                                                      // team-uniform
+    rmax_load(c);
     const float4 pa = pos[a], va = vel[a], wa = omg[a];
     if (a >= n_active) {
         if (!lead) return;
@@ -583,6 +588,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_forces_team(
     const int32_t a = blockIdx.x * (CT_BLK / L) + (int32_t)(threadIdx.x / L);
     const bool lead = (threadIdx.x & (L - 1)) == 0;
     if (a >= n) return;                                                      // team-uniform
+    rmax_load(c);
     const float4 pa = pos[a], va = vel[a], wa = omg[a];
     f3 v = xyz(va), w = xyz(wa);
     uint32_t tq[3] = {0u, 0u, 0u};
@@ -604,6 +610,7 @@ __global__ __launch_bounds__(CT_BLK) void k_contact_forces(
     int32_t* __restrict__ slot_of) {
     const int32_t a = blockIdx.x * CT_BLK + threadIdx.x;
     if (a >= n) return;
+    rmax_load(c);
     const float4 pa = pos[a], va = vel[a], wa = omg[a];
     const int32_t pid = id[a];
     if ((uint32_t)pid < (uint32_t)n) slot_of[pid] = a;
@@ -697,19 +704,22 @@ __global__ __launch_bounds__(FZ_BLK) void k_contact_fused(FusedIO io, int32_t n_
     __shared__ FusedLds L;
     __shared__ FusedFin fin[FZ_T];
     CT_PROBE(threadIdx.x == 0, 0);
+    rmax_load(c);   // with the build's first loads
     const FusedMap M = fused_build<FZ_BLK>(L, io.count, io.mi, io.mk, io.cs, n, io.count_zero, io.host_count);
     CT_PROBE(threadIdx.x == 0, 1);
     {   // one target per wave: sorted position a, read from the previous order's slot o
         const int32_t a = blockIdx.x * FZ_T + (int32_t)(threadIdx.x >> 6);
         if (a < n) {   // wave-uniform
             bool mv;
-            uint32_t key_a;
-            const uint32_t o = M.old_at((uint32_t)a, mv, key_a);
-            if (!mv) key_a = io.sk[o];
+            uint32_t key_mv;
+            const uint32_t o = M.old_at((uint32_t)a, mv, key_mv);
             const float4 pa = io.pos[o], va = io.vel[o], wa = io.omg[o];
-            // the finishing lane's inputs, loaded under the neighbour sums
+            // the finishing lane's inputs, loaded under the neighbour sums; the old key loaded whether or not the
+            // target moved (a load under a branch had the compiler wait for it before issuing the others)
             const float4 rot = io.rot[o], aux = io.aux[o];
             const int32_t id = io.id[o], mode = io.mode[o];
+            const uint32_t sko = io.sk[o];
+            const uint32_t key_a = mv ? key_mv : sko;
             f3 v = xyz(va), w = xyz(wa);
             uint32_t tq[3] = {0u, 0u, 0u};
             if (a < n_active) contact_accumulate_flat<CF_WAVES>(io.pos, io.vel, io.omg, M, g, c, a, pa, va, wa, v, w, tq);
