@@ -28,8 +28,9 @@ struct FusedMap {
         const uint32_t wd = y >> 5;
         return bpre[wd] + (uint32_t)__popc(bm[wd] & ((1u << (y & 31u)) - 1u));
     }
-    __device__ __forceinline__ uint32_t start(uint32_t k) const {   // cs_new[k]
-        const uint32_t c = cs[k];
+    __device__ __forceinline__ uint32_t start(uint32_t k) const { return start_c(k, cs[k]); }   // cs_new[k]
+    // the same from c = cs[k] loaded by the caller (several keys' loads in flight before any search)
+    __device__ __forceinline__ uint32_t start_c(uint32_t k, uint32_t c) const {
         if (m == 0) return c;
         uint32_t lo = 0, hi = m;   // movers with new key < k
         while (lo < hi) {

@@ -973,7 +973,9 @@ struct SmallRows {
         b.cx = cell_cxs<XS>(g, pi.x);
         b.cy = cell_coord(pi.y, g.oy, g.inv_cell, g.gy);
         cell_fracs<XS>(g, pi.x, pi.y, pi.z, b.cx, b.cy, b.fx, b.fy, b.gzf);
-        uint32_t len = 0u;
+        // both table reads of a row first, then the map's searches: one memory round trip, not two
+        uint32_t len = 0u, ka = 0u, kb = 0u;
+        bool in_row = false;
         if (lane < NR) {
             const int32_t dxk = lane / 3 - XS, dyk = lane % 3 - 1;
             const int32_t xx = b.cx + dxk, yy = b.cy + dyk;
@@ -981,9 +983,15 @@ struct SmallRows {
             if (xx >= 0 && xx < g.gx * XS && yy >= 0 && yy < g.gy &&
                 row_window<XS>(g, b.fx, b.fy, b.gzf, dxk, dyk, zlo, zhi)) {
                 const uint32_t rowk = ((uint32_t)xx * (uint32_t)g.gy + (uint32_t)yy) * (uint32_t)g.gz;
-                rj0 = M.start(rowk + (uint32_t)zlo);
-                len = M.start(rowk + (uint32_t)zhi + 1u) - rj0;
+                ka = rowk + (uint32_t)zlo;
+                kb = rowk + (uint32_t)zhi + 1u;
+                in_row = true;
             }
+        }
+        const uint32_t ca = M.cs[ka], cb = M.cs[kb];   // (key 0 for lanes without a row: in bounds, unused)
+        if (in_row) {
+            rj0 = M.start_c(ka, ca);
+            len = M.start_c(kb, cb) - rj0;
         }
         prefix(len, lane);
     }
@@ -1090,11 +1098,12 @@ __global__ __launch_bounds__(256) void k_force_small(const float4* __restrict__ 
     for (uint32_t base = 0; base < R.total; base += 64u) {
         const uint32_t f = base + (uint32_t)lane;
         const uint32_t j = R.slot(min(f, R.total - 1u));
-        const float4 pj = pos[j];
+        // a candidate's velocity and pass-1 terms load with its position whether or not it is a hit: one memory round
+        // trip per round instead of two (the hit test waited for the position before the others issued)
+        const float4 pj = pos[j], vj = vel[j];
+        const float2 rj = rp[j];
         const bool hit = f < R.total && is_hit(c, dist2(pi, pj));
         if (hit) {
-            const float4 vj = vel[j];
-            const float2 rj = rp[j];
             const PairTerms t =
                 pair_terms(pk, pi, vi, ri.x, ri.y, make_float4(pj.x, pj.y, pj.z, rj.x), make_float4(vj.x, vj.y, vj.z, rj.y));
             row[lane] = HitTerms{make_float4(t.cf, t.dx, t.dy, t.dz), make_float4(t.cx, t.du, t.dv, t.dw)};
@@ -1124,12 +1133,13 @@ template <int XS>
 __device__ __forceinline__ void density_fused_target(const FusedIOS& io, const FusedMap& M, int32_t i, int lane,
                                                      const GridDesc& g, const SphConst& c) {
     bool mv;
-    uint32_t key;
-    const uint32_t o = M.old_at((uint32_t)i, mv, key);
-    if (!mv) key = io.sk[o];
+    uint32_t key_mv;
+    const uint32_t o = M.old_at((uint32_t)i, mv, key_mv);
     const float4 pi = io.pos[o];
     const float4 vi = io.vel[o];   // written at the end: loaded under the sums
     const int32_t idi = io.id[o];
+    const uint32_t sko = io.sk[o];   // whether or not a mover: a load under a branch was waited before the others issued
+    const uint32_t key = mv ? key_mv : sko;
     const SmallRows<XS> R(g, M, pi, lane);
     float s = 0.0f;
 #pragma unroll 1
