@@ -186,6 +186,40 @@ __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
+// Inclusive sum inside each row of 16 lanes by DPP row shifts (lanes 0-15: the scan of lanes 0-15)
+__device__ __forceinline__ uint32_t row_scan_incl(uint32_t x) {
+    const uint32_t rl = lane_id() & 15u;
+    uint32_t t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    if (rl >= 1u) x += t;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x112, 0xf, 0xf, false);            // row_shr:2
+    if (rl >= 2u) x += t;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x114, 0xf, 0xf, false);            // row_shr:4
+    if (rl >= 4u) x += t;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x118, 0xf, 0xf, false);            // row_shr:8
+    if (rl >= 8u) x += t;
+    return x;
+}
+
+// Inclusive sum over the wave's 64 lanes by DPP moves (row shifts by 1, 2, 4, 8 inside rows of 16, then the row
+// broadcasts of lanes 15 and 31): six VALU-latency steps, where a shuffle scan (ds_bpermute) waits an LDS round trip
+// at each of its six steps
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+    const uint32_t lane = lane_id(), rl = lane & 15u;
+    uint32_t t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    if (rl >= 1u) x += t;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x112, 0xf, 0xf, false);            // row_shr:2
+    if (rl >= 2u) x += t;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x114, 0xf, 0xf, false);            // row_shr:4
+    if (rl >= 4u) x += t;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x118, 0xf, 0xf, false);            // row_shr:8
+    if (rl >= 8u) x += t;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x142, 0xf, 0xf, false);            // row_bcast:15
+    if ((lane & 31u) >= 16u) x += t;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x143, 0xf, 0xf, false);            // row_bcast:31
+    if (lane >= 32u) x += t;
+    return x;
+}
+
 // Per-kernel timing without extra packets in the stream. While a timing scope (host.h KTimer,
 // profiling on) is open, the launches inside it carry the scope's events in their own dispatch
 // packets (hipExtLaunchKernel): the first launch the start event, every launch the stop event (the last

@@ -300,12 +300,7 @@ __device__ __forceinline__ void contact_accumulate_flat(const float4* __restrict
             rlen = M.start(rowk + (uint32_t)z1 + 1u) - rj0;
         }
     }
-    uint32_t incl = rlen;   // inclusive prefix over lanes 0..8 (lanes >= 9 hold 0)
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
-        if (lane >= o) incl += t;
-    }
+    const uint32_t incl = row_scan_incl(rlen);   // inclusive prefix over lanes 0..8 (lanes >= 9 hold 0)
     const uint32_t excl = incl - rlen;
     // the rows' flattened starts, wave-uniform (scalar registers)
     uint32_t P[9];

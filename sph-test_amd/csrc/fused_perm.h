@@ -68,7 +68,7 @@ struct FusedLds {
 };
 
 // the bitmap's exclusive word prefix (nw <= FZ_WORDS words) by one wave, lane t: WPW consecutive words per lane and one
-// scan over the wave (each shuffle step is a cross-lane round trip; r6: three dependent 64-word scans took ~0.4 us)
+// DPP scan over the wave (r6: three dependent 64-word shuffle scans took ~0.4 us)
 constexpr uint32_t WPW = (FZ_WORDS + 63) / 64;
 __device__ __forceinline__ void word_prefix(const uint32_t* bm, uint32_t* bpre, uint32_t nw, uint32_t lane) {
     uint32_t c[WPW], mine = 0;
@@ -78,12 +78,7 @@ __device__ __forceinline__ void word_prefix(const uint32_t* bm, uint32_t* bpre, 
         c[j] = t < nw ? (uint32_t)__popc(bm[t]) : 0u;
         mine += c[j];
     }
-    uint32_t inc = mine;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
-        if (lane >= (uint32_t)o) inc += u;
-    }
+    const uint32_t inc = wave_scan_incl(mine);
     uint32_t run = inc - mine;
 #pragma unroll
     for (uint32_t j = 0; j < WPW; ++j) {

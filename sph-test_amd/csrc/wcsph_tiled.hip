@@ -995,13 +995,8 @@ struct SmallRows {
         }
         prefix(len, lane);
     }
-    __device__ __forceinline__ void prefix(uint32_t len, int lane) {
-        uint32_t incl = len;
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-            const uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
-            if (lane >= o) incl += t;
-        }
+    __device__ __forceinline__ void prefix(uint32_t len, int) {
+        const uint32_t incl = row_scan_incl(len);   // rows on lanes 0..NR-1 (NR <= 15)
         excl = incl - len;
 #pragma unroll
         for (int k = 0; k < NR; ++k) P[k] = (uint32_t)__builtin_amdgcn_readlane((int)excl, k);
